@@ -1,0 +1,149 @@
+"""ctypes binding of the oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.om_load.restype = ctypes.c_void_p
+        L.om_load.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.POINTER(ctypes.c_int)]
+        L.om_free.argtypes = [ctypes.c_void_p]
+        L.om_find_func.restype = ctypes.c_int
+        L.om_find_func.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p,
+                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p]
+        L.om_instantiate.restype = ctypes.c_void_p
+        L.om_instantiate.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.om_inst_free.argtypes = [ctypes.c_void_p]
+        L.om_invoke.restype = ctypes.c_int
+        L.om_invoke.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.om_mem_pages.restype = ctypes.c_uint32
+        L.om_mem_pages.argtypes = [ctypes.c_void_p]
+        L.om_mem_data.restype = ctypes.c_void_p
+        L.om_mem_data.argtypes = [ctypes.c_void_p]
+        L.om_mem_hash.restype = ctypes.c_uint64
+        L.om_mem_hash.argtypes = [ctypes.c_void_p]
+        L.om_hash_bytes.restype = ctypes.c_uint64
+        L.om_hash_bytes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+        L.om_run_batch.restype = ctypes.c_double
+        L.om_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class OracleError(Exception):
+    def __init__(self, code):
+        super().__init__("oracle error 0x%02x" % code)
+        self.code = code
+
+
+def _split(v):
+    v &= (1 << 128) - 1
+    return v & 0xFFFFFFFFFFFFFFFF, v >> 64
+
+
+class Module:
+    """A loaded + validated module in the oracle (one per wasm binary)."""
+
+    def __init__(self, wasm, page_limit=65536):
+        L = lib()
+        err = ctypes.c_int(0)
+        self._h = L.om_load(wasm, len(wasm), page_limit, ctypes.byref(err))
+        if not self._h:
+            raise OracleError(err.value)
+        self.wasm = wasm
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().om_free(self._h)
+            self._h = None
+
+    def func(self, name):
+        np_, nr = ctypes.c_uint32(), ctypes.c_uint32()
+        pt, rt = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
+        idx = lib().om_find_func(self._h, name.encode(), ctypes.byref(np_), pt,
+                                 ctypes.byref(nr), rt)
+        if idx < 0:
+            raise KeyError(name)
+        return idx, list(pt.raw[:np_.value]), list(rt.raw[:nr.value])
+
+    def run(self, name, args):
+        """Fresh instance, invoke, return (code, results(int list), count, memhash)."""
+        L = lib()
+        idx, pt, rt = self.func(name)
+        err = ctypes.c_int(0)
+        inst = L.om_instantiate(self._h, ctypes.byref(err))
+        if not inst:
+            return err.value, [], 0, 0
+        try:
+            params = (ctypes.c_uint64 * (2 * max(1, len(pt))))()
+            for k, a in enumerate(args):
+                params[2 * k], params[2 * k + 1] = _split(a)
+            res = (ctypes.c_uint64 * (2 * max(1, len(rt))))()
+            cnt = ctypes.c_uint64(0)
+            code = L.om_invoke(inst, idx, params, res, ctypes.byref(cnt))
+            vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
+            return code, vals, cnt.value, L.om_mem_hash(inst)
+        finally:
+            L.om_inst_free(inst)
+
+    def run_with_memory(self, name, args):
+        L = lib()
+        idx, pt, rt = self.func(name)
+        err = ctypes.c_int(0)
+        inst = L.om_instantiate(self._h, ctypes.byref(err))
+        if not inst:
+            return err.value, [], 0, b""
+        try:
+            params = (ctypes.c_uint64 * (2 * max(1, len(pt))))()
+            for k, a in enumerate(args):
+                params[2 * k], params[2 * k + 1] = _split(a)
+            res = (ctypes.c_uint64 * (2 * max(1, len(rt))))()
+            cnt = ctypes.c_uint64(0)
+            code = L.om_invoke(inst, idx, params, res, ctypes.byref(cnt))
+            vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
+            n = L.om_mem_pages(inst) * 65536
+            mem = ctypes.string_at(L.om_mem_data(inst), n) if n else b""
+            return code, vals, cnt.value, mem
+        finally:
+            L.om_inst_free(inst)
+
+    def run_batch(self, name, params_u64, n, threads=1):
+        """params_u64: numpy uint64 array shape [n, nparams, 2]. Returns dict of arrays."""
+        import numpy as np
+        L = lib()
+        idx, pt, rt = self.func(name)
+        params = np.ascontiguousarray(params_u64, dtype=np.uint64).reshape(n, len(pt), 2)
+        results = np.zeros((n, max(1, len(rt)), 2), dtype=np.uint64)
+        codes = np.zeros(n, dtype=np.uint8)
+        counts = np.zeros(n, dtype=np.uint64)
+        hashes = np.zeros(n, dtype=np.uint64)
+        secs = L.om_run_batch(self._h, idx, n, params.ctypes.data, results.ctypes.data,
+                              codes.ctypes.data, counts.ctypes.data, hashes.ctypes.data, threads)
+        return {"results": results[:, :len(rt), :], "codes": codes, "counts": counts,
+                "hashes": hashes, "seconds": secs}
+
+
+def hash_bytes(data, pages):
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    return lib().om_hash_bytes(buf, len(data), pages)

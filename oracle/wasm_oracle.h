@@ -1,0 +1,63 @@
+/*
+ * wasm_oracle.h -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * A plain-C restatement of the reference interpreter path (WasmEdge 0.9.1):
+ *   loader      lib/loader/ast/instruction.cpp:35-116   (JumpEnd/JumpElse/IsLast)
+ *   validator   lib/validator/formchecker.cpp:202-1423  (Jump descriptors, StackOffset)
+ *   executor    lib/executor/engine/engine.cpp:68-1638   (dispatch loop + counting)
+ *   stack       include/runtime/stackmgr.h:25-148        (16-byte ValVariant slots)
+ *   memory      include/runtime/instance/memory.h:34-332 (bounds, grow, page limit)
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * The product (libwasmedge_batch.so) never links or calls it.
+ *
+ * Parity pins (see DESIGN.md "Oracle"): fib/fac example KATs (tools/wasmedge/examples),
+ * mt19937 KATs (test/thread/ThreadTest.cpp:158-163), fib(30) instruction count
+ * 28,271,634 (measured on the reference), node/V8 cross-checks.
+ */
+#ifndef WASM_ORACLE_H
+#define WASM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct OMod OMod;
+typedef struct OInst OInst;
+
+/* Load + validate a module. page_limit mirrors RuntimeConfigure::MaxMemPage
+ * (include/common/configure.h:123). Returns NULL and an ErrCode in *err on failure. */
+OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err);
+void om_free(OMod *m);
+
+/* Function lookup by export name. Types use the wasm valtype bytes (0x7F i32 ...). */
+int om_find_func(const OMod *m, const char *name, uint32_t *nparams, uint8_t *ptypes,
+                 uint32_t *nresults, uint8_t *rtypes);
+
+/* Instantiate (memory, globals, tables, elem/data init, start function). */
+OInst *om_instantiate(OMod *m, int *err);
+void om_inst_free(OInst *i);
+
+/* Invoke function index fidx. Values are 16 bytes each (lo,hi u64 pairs), as
+ * WasmEdge_Value's uint128 (include/api/wasmedge/wasmedge.h:39-46). Returns ErrCode
+ * (0 success, 0x84.. traps). *count receives the reference-rule instruction count. */
+int om_invoke(OInst *i, uint32_t fidx, const uint64_t *params, uint64_t *results,
+              uint64_t *count);
+
+/* Linear memory 0 view and hash (hash defined in DESIGN.md, shared with the GPU). */
+uint32_t om_mem_pages(const OInst *i);
+const uint8_t *om_mem_data(const OInst *i);
+uint64_t om_mem_hash(const OInst *i);
+uint64_t om_hash_bytes(const uint8_t *data, uint64_t nbytes, uint32_t pages);
+
+/* Batch driver (CPU baseline): one fresh instance per invocation, `threads` host
+ * threads, contiguous instance-id blocks per thread. params: [n][nparams][2] u64.
+ * results: [n][nresults][2]; codes/counts/hashes may be NULL. Returns wall seconds. */
+double om_run_batch(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
+                    uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
+                    int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

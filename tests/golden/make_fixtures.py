@@ -1,0 +1,43 @@
+"""Regenerate tests/golden/ fixtures from the reference's own test data (run in the
+build container, where /root/reference exists; the GPU box only reads the outputs).
+
+Fixtures are data only (wasm binaries the reference's tests hold, and their expected
+answers):
+  mt19937.wasm      bytes of test/thread/ThreadTest.cpp:31-150 (MersenneTwister19937)
+  mt19937.json      answers test/thread/ThreadTest.cpp:152-157, args :168-169
+  fibonacci.wasm    tools/wasmedge/examples/fibonacci.wasm (README: fib 8 -> 34)
+  factorial.wasm    tools/wasmedge/examples/factorial.wasm (README: fac 12 -> 479001600)
+  apitest.wasm      test/api/apiTestData/test.wasm
+"""
+import json
+import os
+import re
+import shutil
+import sys
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def main():
+    src = open(os.path.join(REF, "test/thread/ThreadTest.cpp")).read()
+    m = re.search(r"MersenneTwister19937\{(.*?)\};", src, re.S)
+    data = bytes(int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]{2}", m.group(1)))
+    assert len(data) == 1481, len(data)
+    open(os.path.join(OUT, "mt19937.wasm"), "wb").write(data)
+    a = re.search(r"Answers\{(.*?)\};", src, re.S)
+    answers = [int(x) for x in re.findall(r"UINT64_C\((\d+)\)", a.group(1))]
+    json.dump({"source": "test/thread/ThreadTest.cpp:31-163",
+               "func": "mt19937",
+               "args": [[2504 * i, 5489, 100000 + i] for i in range(len(answers))],
+               "answers": answers}, open(os.path.join(OUT, "mt19937.json"), "w"), indent=1)
+    for name in ("fibonacci", "factorial"):
+        shutil.copy(os.path.join(REF, "tools/wasmedge/examples/%s.wasm" % name),
+                    os.path.join(OUT, name + ".wasm"))
+    shutil.copy(os.path.join(REF, "test/api/apiTestData/test.wasm"),
+                os.path.join(OUT, "apitest.wasm"))
+    print("ok", len(answers))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
