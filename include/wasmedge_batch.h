@@ -1,0 +1,138 @@
+/*
+ * wasmedge_batch.h -- C ABI of the MI355X batched WebAssembly interpreter.
+ *
+ * A batched entry placed BESIDE the reference's WasmEdge_VMExecute
+ * (include/api/wasmedge/wasmedge.h:3301-3303, lib/api/wasmedge.cpp:2687-2698): one
+ * validated module, N independent instances, one GPU lane each.  Conventions follow the
+ * reference C API (include/api/wasmedge/wasmedge.h:39-60):
+ *   - values are WasmEdge_Value {uint128_t Value; enum WasmEdge_ValType Type};
+ *   - errors are returned by value as WasmEdge_Result{uint8_t Code} holding the
+ *     reference ErrCode byte (include/common/enum.inc:573-749);
+ *   - buffers are caller-owned; surplus returns are dropped, a ReturnLen shortfall is
+ *     silent (lib/api/wasmedge.cpp:245-255 fillWasmEdge_ValueArr);
+ *   - a NULL context gives WrongVMWorkflow (0x04) (lib/api/wasmedge.cpp:266-277);
+ *   - contexts returned by *Create are owned by the caller and freed by *Delete.
+ * Per-instance outcomes (traps) are reported per lane with the reference trap codes
+ * (0x84..0x8E), never through the call-level result.
+ *
+ * Plain C types only; no torch/HIP types cross this boundary.
+ */
+#ifndef WASMEDGE_BATCH_H
+#define WASMEDGE_BATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef WASMEDGE_C_API_H /* use the reference's definitions when its header is included */
+typedef unsigned __int128 uint128_t;
+enum WasmEdge_ValType {
+  WasmEdge_ValType_I32 = 0x7FU,
+  WasmEdge_ValType_I64 = 0x7EU,
+  WasmEdge_ValType_F32 = 0x7DU,
+  WasmEdge_ValType_F64 = 0x7CU,
+  WasmEdge_ValType_V128 = 0x7BU,
+  WasmEdge_ValType_FuncRef = 0x70U,
+  WasmEdge_ValType_ExternRef = 0x6FU
+};
+typedef struct WasmEdge_Value {
+  uint128_t Value;
+  enum WasmEdge_ValType Type;
+} WasmEdge_Value;
+typedef struct WasmEdge_String {
+  uint32_t Length;
+  const char *Buf;
+} WasmEdge_String;
+typedef struct WasmEdge_Result {
+  uint8_t Code;
+} WasmEdge_Result;
+#endif
+
+#define WASMEDGE_BATCH_API __attribute__((visibility("default")))
+
+/* Per-instance status byte (PerInstance[i]) beyond the reference trap codes. */
+#define WASMEDGE_BATCH_OK 0x00u
+#define WASMEDGE_BATCH_INTERRUPTED 0x07u      /* ErrCode::Interrupted: step/time limit */
+#define WASMEDGE_BATCH_STACK_EXHAUSTED 0xB0u  /* device call stack full */
+#define WASMEDGE_BATCH_HOST_CALL 0xB1u        /* reached a host import (yield: not yet) */
+
+typedef struct WasmEdge_BatchConfigure {
+  /* Page budget per instance; plays RuntimeConfigure::MaxMemPage
+   * (include/common/configure.h:123). 0 = the module's declared maximum, else its
+   * initial size. memory.grow beyond it returns -1 exactly like the reference. */
+  uint32_t MaxMemoryPage;
+  /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
+  uint32_t CallStackCells;
+  /* Dispatch budget per wavefront (0 = unlimited) and wall-clock limit per launch in
+   * seconds (0 = 600); exceeding either marks running instances Interrupted (0x07),
+   * mirroring the reference's StopToken / --time-limit (helper.cpp:24-27). */
+  uint64_t MaxSteps;
+  double TimeLimitSeconds;
+  /* HIP device ordinal (-1 = the current device). */
+  int32_t DeviceOrdinal;
+} WasmEdge_BatchConfigure;
+
+typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
+
+/* Load + validate + lower `WasmBuf` and allocate device state for NumInstances
+ * instances. Replaces VM::loadWasm/validate/instantiate (lib/vm/vm.cpp) for the batch.
+ * Returns NULL on failure with the ErrCode in *Res (may be NULL). */
+WASMEDGE_BATCH_API WasmEdge_BatchContext *
+WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf, const uint8_t *WasmBuf,
+                     uint32_t WasmLen, uint32_t NumInstances, WasmEdge_Result *Res);
+
+/* Run `FuncName` on every instance from a fresh instantiation (one instance per lane).
+ * Params: [NumInstances][ParamLen] row-major; Returns: [NumInstances][ReturnLen].
+ * PerInstance[i]: 0 ok, else trap/status code. InstrCounts[i]: the reference's
+ * instruction count (include/common/statistics.h:44). Either may be NULL.
+ * Mirrors WasmEdge_VMExecute (wasmedge.h:3301) per instance. */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName,
+                      const WasmEdge_Value *Params, const uint32_t ParamLen,
+                      WasmEdge_Value *Returns, const uint32_t ReturnLen,
+                      uint8_t *PerInstance, uint64_t *InstrCounts);
+
+/* Staged form of BatchExecute, for callers that keep inputs resident on the device
+ * and time the interpreter alone (bench.py):
+ *   SetArgs  -> resolve FuncName, check types (FuncSigMismatch), upload params
+ *   Reset    -> fresh instances: memory image + globals (instantiate/*.cpp)
+ *   Run      -> launch the interpreter; *KernelSeconds = HIP-event time on the
+ *               library's stream (may be NULL)
+ *   Results  -> copy returns / statuses / counts back. */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchSetArgs(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName,
+                      const WasmEdge_Value *Params, const uint32_t ParamLen);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *Cxt,
+                                                       double *KernelSeconds);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *Cxt,
+                                                     double *KernelSeconds);
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchResults(WasmEdge_BatchContext *Cxt, WasmEdge_Value *Returns,
+                      const uint32_t ReturnLen, uint8_t *PerInstance, uint64_t *InstrCounts);
+
+/* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
+ * computes the same function). Hashes: [NumInstances]. */
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *Cxt,
+                                                            uint64_t *Hashes);
+/* Copy Len bytes of instance Inst's linear memory starting at Off into Dst
+ * (MemoryOutOfBounds 0x88 if outside its current size). */
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *Cxt,
+                                                           uint32_t Inst, uint32_t Off,
+                                                           uint8_t *Dst, uint32_t Len);
+/* Current page count of instance Inst's memory (after the last Run). */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *Cxt,
+                                                         uint32_t Inst);
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *Cxt);
+/* Human-readable description of the last failure on this context (or of the last
+ * failed BatchCreate when Cxt is NULL). */
+WASMEDGE_BATCH_API const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *Cxt);
+/* Number of device instructions and max wasm instructions folded into one dispatch. */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetCodeSize(const WasmEdge_BatchContext *Cxt);
+WASMEDGE_BATCH_API void WasmEdge_BatchDelete(WasmEdge_BatchContext *Cxt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

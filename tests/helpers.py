@@ -1,0 +1,123 @@
+"""Shared test helpers: run a module on the oracle and on the device/emulator and
+compare return bits, trap codes, instruction counts and memory hashes."""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU_PATH = os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch_emu.so")
+_emu = None
+
+CELLS = {0x7F: 1, 0x7E: 2, 0x7D: 1, 0x7C: 2, 0x7B: 4, 0x70: 1, 0x6F: 1}
+
+
+def emu_lib():
+    global _emu
+    if _emu is None:
+        E = ctypes.CDLL(EMU_PATH)
+        E.wb_emu_last_error.restype = ctypes.c_char_p
+        E.wb_emu_execute.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                     ctypes.c_uint32] + [ctypes.c_void_p] * 5 + \
+            [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        E.wb_emu_disasm.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                    ctypes.c_uint32]
+        _emu = E
+    return _emu
+
+
+def to_cells(args, types):
+    out = []
+    for a, t in zip(args, types):
+        v = int(a) & ((1 << 128) - 1)
+        for q in range(CELLS[t]):
+            out.append((v >> (32 * q)) & 0xFFFFFFFF)
+    return out
+
+
+def from_cells(cells, types):
+    vals, at = [], 0
+    for t in types:
+        v = 0
+        for q in range(CELLS[t]):
+            v |= int(cells[at]) << (32 * q)
+            at += 1
+        vals.append(v)
+    return vals
+
+
+def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0):
+    E = emu_lib()
+    n = len(arg_rows)
+    pc = sum(CELLS[t] for t in ptypes)
+    rc = sum(CELLS[t] for t in rtypes)
+    params = np.zeros((n, max(pc, 1)), np.uint32)
+    for i, row in enumerate(arg_rows):
+        params[i, :pc] = to_cells(row, ptypes)
+    res = np.zeros((n, max(rc, 1)), np.uint32)
+    st = np.zeros(n, np.uint8)
+    cnt = np.zeros(n, np.uint64)
+    h = np.zeros(n, np.uint64)
+    e = E.wb_emu_execute(wasm, len(wasm), func.encode(), n, params.ctypes.data,
+                         res.ctypes.data, st.ctypes.data, cnt.ctypes.data, h.ctypes.data,
+                         max_pages, gs_depth, max_steps)
+    if e:
+        raise RuntimeError("emu error 0x%x: %s" % (e, E.wb_emu_last_error().decode()))
+    rets = [from_cells(res[i], rtypes) if st[i] == 0 else [] for i in range(n)]
+    return rets, st, cnt, h
+
+
+def disasm(wasm):
+    E = emu_lib()
+    buf = ctypes.create_string_buffer(1 << 22)
+    E.wb_emu_disasm(wasm, len(wasm), buf, len(buf))
+    return buf.value.decode()
+
+
+def canon(v, t):
+    """Canonicalise NaN payloads as the spec permits (f32/f64 results only)."""
+    if t == 0x7D and (v & 0x7FFFFFFF) > 0x7F800000:
+        return "nan32"
+    if t == 0x7C and (v & 0x7FFFFFFFFFFFFFFF) > 0x7FF0000000000000:
+        return "nan64"
+    return v
+
+
+def oracle_run(mod, func, arg_rows):
+    out = []
+    for row in arg_rows:
+        code, vals, cnt, h = mod.run(func, row)
+        out.append((code, vals, cnt, h))
+    return out
+
+
+def gpu_run(wasm, func, arg_rows, ptypes, rtypes, **kw):
+    from wasmedge_amd import batch
+    ctx = batch.BatchContext(wasm, len(arg_rows), **kw)
+    try:
+        vals = batch.make_values(arg_rows, ptypes)
+        rets, st, cnt = ctx.execute(func, vals, len(rtypes))
+        h = ctx.memory_hash()
+        ints = batch.ret_ints(rets)
+        rows = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(arg_rows))]
+        return rows, st, cnt, h
+    finally:
+        ctx.close()
+
+
+def compare(oracle_rows, rets, st, cnt, h, rtypes, check_hash=True):
+    bad = []
+    for i, (code, vals, ocnt, oh) in enumerate(oracle_rows):
+        if int(st[i]) != code:
+            bad.append((i, "status", code, int(st[i])))
+            continue
+        if int(cnt[i]) != ocnt:
+            bad.append((i, "count", ocnt, int(cnt[i])))
+        if code == 0:
+            a = [canon(v, t) for v, t in zip(vals, rtypes)]
+            b = [canon(v, t) for v, t in zip(rets[i], rtypes)]
+            if a != b:
+                bad.append((i, "ret", vals, rets[i]))
+        if check_hash and code == 0 and int(h[i]) != oh:
+            bad.append((i, "memhash", oh, int(h[i])))
+    return bad

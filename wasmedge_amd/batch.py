@@ -1,0 +1,208 @@
+"""Python host mirror of the batched C ABI (include/wasmedge_batch.h) over ctypes.
+
+Mirrors the reference VM/C-API flow (lib/vm/vm.cpp, include/api/wasmedge/wasmedge.h):
+load -> validate -> instantiate -> execute, but for N instances at once.  The product
+path is the HIP library `libwasmedge_batch.so`; there is no CPU fallback -- if the library
+or a GPU is missing, construction raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwasmedge_batch.so")
+
+# valtypes (include/api/wasmedge/enum_types.h)
+I32, I64, F32, F64, V128, FUNCREF, EXTERNREF = 0x7F, 0x7E, 0x7D, 0x7C, 0x7B, 0x70, 0x6F
+
+# WasmEdge_Value: {uint128_t Value; enum WasmEdge_ValType Type;} -> 32 bytes (16-aligned)
+VALUE_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8"), ("type", "<u4"), ("pad", "<u4", (3,))])
+
+# per-instance status codes (reference ErrCodes, include/common/enum.inc:717-745)
+STATUS_NAMES = {0x00: "ok", 0x07: "interrupted", 0x84: "integer divide by zero",
+                0x85: "integer overflow", 0x86: "invalid conversion to integer",
+                0x87: "out of bounds table access", 0x88: "out of bounds memory access",
+                0x89: "unreachable", 0x8A: "uninitialized element", 0x8B: "undefined element",
+                0x8C: "indirect call type mismatch", 0xB0: "call stack exhausted",
+                0xB1: "host call (yield path not implemented)"}
+
+
+class WasmEdgeError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("WasmEdge_Result 0x%02x %s" % (code, msg))
+        self.code = code
+
+
+class _Conf(ctypes.Structure):
+    _fields_ = [("MaxMemoryPage", ctypes.c_uint32), ("CallStackCells", ctypes.c_uint32),
+                ("MaxSteps", ctypes.c_uint64), ("TimeLimitSeconds", ctypes.c_double),
+                ("DeviceOrdinal", ctypes.c_int32)]
+
+
+class _String(ctypes.Structure):
+    _fields_ = [("Length", ctypes.c_uint32), ("Buf", ctypes.c_char_p)]
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("Code", ctypes.c_uint8)]
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (raises if it was not built -- no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError("libwasmedge_batch.so not built: run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.WasmEdge_BatchCreate.restype = vp
+        L.WasmEdge_BatchCreate.argtypes = [ctypes.POINTER(_Conf), ctypes.c_char_p, u32, u32,
+                                           ctypes.POINTER(_Result)]
+        for name, args in [
+            ("WasmEdge_BatchExecute", [vp, _String, vp, u32, vp, u32, vp, vp]),
+            ("WasmEdge_BatchSetArgs", [vp, _String, vp, u32]),
+            ("WasmEdge_BatchReset", [vp, ctypes.POINTER(ctypes.c_double)]),
+            ("WasmEdge_BatchRun", [vp, ctypes.POINTER(ctypes.c_double)]),
+            ("WasmEdge_BatchResults", [vp, vp, u32, vp, vp]),
+            ("WasmEdge_BatchMemoryHash", [vp, vp]),
+            ("WasmEdge_BatchGetMemory", [vp, u32, u32, vp, u32]),
+        ]:
+            f = getattr(L, name)
+            f.restype = _Result
+            f.argtypes = args
+        L.WasmEdge_BatchGetMemoryPages.restype = u32
+        L.WasmEdge_BatchGetMemoryPages.argtypes = [vp, u32]
+        L.WasmEdge_BatchGetInstanceCount.restype = u32
+        L.WasmEdge_BatchGetInstanceCount.argtypes = [vp]
+        L.WasmEdge_BatchGetCodeSize.restype = u32
+        L.WasmEdge_BatchGetCodeSize.argtypes = [vp]
+        L.WasmEdge_BatchGetLastError.restype = ctypes.c_char_p
+        L.WasmEdge_BatchGetLastError.argtypes = [vp]
+        L.WasmEdge_BatchDelete.restype = None
+        L.WasmEdge_BatchDelete.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def make_values(rows, types):
+    """rows: iterable of per-instance argument tuples (python ints, bit patterns for
+    floats) or a numpy integer array [n, nparams]; types: list of valtypes."""
+    if isinstance(rows, np.ndarray):
+        arr = rows.reshape(rows.shape[0], -1)
+        n = arr.shape[0]
+        out = np.zeros((n, len(types)), VALUE_DTYPE)
+        for k, t in enumerate(types):
+            col = arr[:, k].astype(np.uint64) if arr.dtype.kind == "u" else \
+                arr[:, k].astype(np.int64).view(np.uint64)
+            if t in (I32, F32, FUNCREF, EXTERNREF):
+                col = col & np.uint64(0xFFFFFFFF)
+            out["lo"][:, k] = col
+            out["type"][:, k] = t
+        return out
+    rows = list(rows)
+    out = np.zeros((len(rows), len(types)), VALUE_DTYPE)
+    for i, r in enumerate(rows):
+        for k, t in enumerate(types):
+            v = int(r[k]) & ((1 << 128) - 1)
+            if t in (I32, F32, FUNCREF, EXTERNREF):
+                v &= 0xFFFFFFFF
+            elif t in (I64, F64):
+                v &= (1 << 64) - 1
+            out["lo"][i, k] = v & 0xFFFFFFFFFFFFFFFF
+            out["hi"][i, k] = v >> 64
+            out["type"][i, k] = t
+    return out
+
+
+class BatchContext:
+    """N instances of one module on one GPU (WasmEdge_BatchContext)."""
+
+    def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
+                 time_limit=0.0, device=-1):
+        L = lib()
+        conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device)
+        res = _Result(0)
+        self._h = L.WasmEdge_BatchCreate(ctypes.byref(conf), bytes(wasm), len(wasm), n,
+                                         ctypes.byref(res))
+        if not self._h:
+            raise WasmEdgeError(res.Code, L.WasmEdge_BatchGetLastError(None).decode())
+        self.n = n
+        self.func = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().WasmEdge_BatchDelete(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, r):
+        if r.Code:
+            raise WasmEdgeError(r.Code, lib().WasmEdge_BatchGetLastError(self._h).decode())
+
+    @staticmethod
+    def _name(func):
+        b = func.encode()
+        return _String(len(b), b)
+
+    def set_args(self, func, values):
+        values = np.ascontiguousarray(values, VALUE_DTYPE)
+        nparams = values.shape[1] if values.ndim == 2 else 0
+        self._check(lib().WasmEdge_BatchSetArgs(self._h, self._name(func),
+                                                values.ctypes.data if values.size else None,
+                                                nparams))
+        self.func = func
+        self._keep = values
+
+    def reset(self):
+        t = ctypes.c_double(0)
+        self._check(lib().WasmEdge_BatchReset(self._h, ctypes.byref(t)))
+        return t.value
+
+    def run(self):
+        t = ctypes.c_double(0)
+        self._check(lib().WasmEdge_BatchRun(self._h, ctypes.byref(t)))
+        return t.value
+
+    def results(self, nret):
+        rets = np.zeros((self.n, max(nret, 1)), VALUE_DTYPE)
+        status = np.zeros(self.n, np.uint8)
+        counts = np.zeros(self.n, np.uint64)
+        self._check(lib().WasmEdge_BatchResults(self._h, rets.ctypes.data, nret,
+                                                status.ctypes.data, counts.ctypes.data))
+        return rets[:, :nret], status, counts
+
+    def execute(self, func, values, nret):
+        """Fresh instantiation + run. Returns (returns[n, nret] VALUE_DTYPE, status, counts)."""
+        self.set_args(func, values)
+        self.reset()
+        self.run()
+        return self.results(nret)
+
+    def memory_hash(self):
+        h = np.zeros(self.n, np.uint64)
+        self._check(lib().WasmEdge_BatchMemoryHash(self._h, h.ctypes.data))
+        return h
+
+    def memory(self, inst, off, length):
+        buf = ctypes.create_string_buffer(length)
+        self._check(lib().WasmEdge_BatchGetMemory(self._h, inst, off, buf, length))
+        return buf.raw
+
+    def memory_pages(self, inst):
+        return lib().WasmEdge_BatchGetMemoryPages(self._h, inst)
+
+    def code_size(self):
+        return lib().WasmEdge_BatchGetCodeSize(self._h)
+
+
+def ret_ints(rets):
+    """Return values (VALUE_DTYPE array) as python ints (uint128)."""
+    lo = rets["lo"].astype(object)
+    hi = rets["hi"].astype(object)
+    return lo + hi * (1 << 64)

@@ -1,0 +1,406 @@
+// batch_api.cpp -- implementation of include/wasmedge_batch.h (the drop-in C ABI).
+// Owns the lowered Program, device buffers, one HIP stream per context, and the
+// per-instance result buffers.  See the header for the reference interfaces mirrored.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/wasmedge_batch.h"
+#include "frontend.h"
+#include "kparams.h"
+
+extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
+                                     size_t lds_bytes, hipStream_t s);
+extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
+                                         uint32_t image_words, uint32_t init_words,
+                                         uint32_t mem_words, uint32_t nwaves, hipStream_t s);
+extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *pages,
+                                         uint64_t *hashes, uint32_t mem_words, uint32_t n,
+                                         hipStream_t s);
+
+namespace {
+
+// ErrCodes (include/common/enum.inc)
+constexpr uint8_t kRuntimeError = 0x02, kWrongVMWorkflow = 0x04, kFuncNotFound = 0x05,
+                  kFuncSigMismatch = 0x83, kMemoryOutOfBounds = 0x88;
+
+std::string g_last_create_error;
+
+WasmEdge_Result R(uint8_t c) { return WasmEdge_Result{c}; }
+
+template <typename T>
+struct DevBuf {
+  T *ptr = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (ptr) (void)hipFree(ptr); }
+  bool alloc(size_t count) {
+    if (ptr) { (void)hipFree(ptr); ptr = nullptr; }
+    n = count;
+    if (count == 0) return true;
+    return hipMalloc(&ptr, sizeof(T) * count) == hipSuccess;
+  }
+  bool upload(const std::vector<T> &v, hipStream_t s) {
+    if (!alloc(v.size() ? v.size() : 1)) return false;
+    if (v.empty()) return true;
+    return hipMemcpyAsync(ptr, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  }
+};
+
+}  // namespace
+
+struct WasmEdge_BatchContext {
+  wb::Program prog;
+  WasmEdge_BatchConfigure conf{};
+  uint32_t n = 0, nwaves = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string last_error;
+  // module buffers
+  DevBuf<DInstr> code;
+  DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
+  DevBuf<DFunc> funcs;
+  DevBuf<uint8_t> data_pool;
+  // instance state
+  DevBuf<uint32_t> mem, gstack, params, results, pages;
+  DevBuf<uint8_t> status;
+  DevBuf<uint64_t> counts, hashes;
+  uint32_t image_words = 0, init_dropped = 0;
+  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0;
+  // current invocation
+  int func = -1;
+  uint32_t param_cells = 0, result_cells = 0;
+  std::vector<uint8_t> result_types;
+  bool ran = false;
+
+  uint8_t fail(uint8_t code, const std::string &m) {
+    last_error = m;
+    return code;
+  }
+  bool hip_ok(hipError_t e, const char *what) {
+    if (e == hipSuccess) return true;
+    last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return false;
+  }
+};
+
+namespace {
+
+uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
+  uint8_t ec = 0;
+  std::string err = wb::load_program(wasm, len, C->prog, &ec);
+  if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
+  const wb::Program &P = C->prog;
+  if (C->conf.DeviceOrdinal >= 0) {
+    if (!C->hip_ok(hipSetDevice(C->conf.DeviceOrdinal), "hipSetDevice")) return kRuntimeError;
+  }
+  (void)hipGetDevice(&C->device);
+  if (!C->hip_ok(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking), "stream"))
+    return kRuntimeError;
+  (void)hipEventCreate(&C->ev0);
+  (void)hipEventCreate(&C->ev1);
+  hipStream_t s = C->stream;
+  // memory budget (RuntimeConfigure::MaxMemPage analogue)
+  uint32_t budget = C->conf.MaxMemoryPage;
+  if (budget == 0) budget = P.mem_has_max ? P.mem_max : P.mem_min;
+  if (P.mem_has_max && budget > P.mem_max) budget = P.mem_max;
+  if (budget < P.mem_min) budget = P.mem_min;
+  if (!P.has_mem) budget = 0;
+  C->mem_max_pages = budget;
+  C->mem_words = budget << 14;
+  C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
+  C->nwaves = (C->n + 63) / 64;
+  // module image: active data segments over the initial pages
+  std::vector<uint32_t> img;
+  std::vector<uint8_t> pool;
+  std::vector<uint32_t> doff, dlen;
+  uint32_t dropped = 0;
+  for (size_t k = 0; k < P.datas.size(); k++) {
+    const auto &d = P.datas[k];
+    doff.push_back(uint32_t(pool.size()));
+    dlen.push_back(uint32_t(d.bytes.size()));
+    pool.insert(pool.end(), d.bytes.begin(), d.bytes.end());
+    if (d.active) {
+      if (k < 32) dropped |= 1u << k;   // active segments are dropped after init
+      uint64_t end = uint64_t(d.offset) + d.bytes.size();
+      if (img.size() * 4 < end) img.resize((end + 3) / 4, 0);
+      for (size_t b = 0; b < d.bytes.size(); b++) {
+        uint32_t a = d.offset + uint32_t(b);
+        img[a >> 2] = (img[a >> 2] & ~(0xFFu << (8 * (a & 3)))) | (uint32_t(d.bytes[b]) << (8 * (a & 3)));
+      }
+    }
+  }
+  C->image_words = uint32_t(img.size());
+  C->init_dropped = dropped;
+  std::vector<DFunc> fv;
+  for (const auto &f : P.funcs)
+    fv.push_back(DFunc{f.imported ? 0xFFFFFFFFu : f.entry_pc, P.type_canon[f.type]});
+  bool ok = C->code.upload(P.code, s) && C->brtab.upload(P.brtab, s) &&
+            C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
+            C->global_init.upload(P.global_init, s) && C->image.upload(img, s) &&
+            C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
+            C->data_off.upload(doff, s) && C->data_len.upload(dlen, s);
+  if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
+  size_t nw = C->nwaves;
+  if (!C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64) ||
+      !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) || !C->status.alloc(C->n + 1) ||
+      !C->counts.alloc(C->n + 1) || !C->pages.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1))
+    return C->fail(kRuntimeError, "device allocation of instance state failed (" +
+                                      std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
+                                      " MiB linear memory)");
+  if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
+  return 0;
+}
+
+uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
+
+}  // namespace
+
+extern "C" {
+
+WasmEdge_BatchContext *WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf,
+                                            const uint8_t *WasmBuf, uint32_t WasmLen,
+                                            uint32_t NumInstances, WasmEdge_Result *Res) {
+  if (!WasmBuf || NumInstances == 0) {
+    g_last_create_error = "null buffer or zero instances";
+    if (Res) *Res = R(kWrongVMWorkflow);
+    return nullptr;
+  }
+  auto *C = new WasmEdge_BatchContext();
+  if (Conf) C->conf = *Conf;
+  else C->conf.DeviceOrdinal = -1;
+  C->n = NumInstances;
+  uint8_t e = setup(C, WasmBuf, WasmLen);
+  if (e) {
+    g_last_create_error = C->last_error;
+    if (Res) *Res = R(e);
+    WasmEdge_BatchDelete(C);
+    return nullptr;
+  }
+  if (Res) *Res = R(0);
+  return C;
+}
+
+WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_String FuncName,
+                                      const WasmEdge_Value *Params, const uint32_t ParamLen) {
+  if (!C) return R(kWrongVMWorkflow);
+  std::string name(FuncName.Buf ? FuncName.Buf : "", FuncName.Length);
+  int f = wb::find_export(C->prog, name);
+  if (f < 0) return R(C->fail(kFuncNotFound, "function '" + name + "' not found"));
+  const wb::FuncType &t = C->prog.types[C->prog.funcs[f].type];
+  // executor.cpp:88-100: parameter count and types must match
+  if (ParamLen != t.params.size()) return R(C->fail(kFuncSigMismatch, "parameter count mismatch"));
+  uint32_t pc = 0;
+  for (uint8_t ty : t.params) pc += cells_of_value(ty);
+  std::vector<uint32_t> cells(size_t(C->n) * (pc ? pc : 1));
+  for (uint32_t i = 0; i < C->n; i++) {
+    uint32_t at = 0;
+    for (uint32_t k = 0; k < ParamLen; k++) {
+      const WasmEdge_Value &v = Params[size_t(i) * ParamLen + k];
+      if (uint8_t(v.Type) != t.params[k])
+        return R(C->fail(kFuncSigMismatch, "parameter type mismatch"));
+      uint128_t x = v.Value;
+      for (uint32_t q = 0; q < cells_of_value(t.params[k]); q++)
+        cells[size_t(i) * pc + at++] = uint32_t(x >> (32 * q));
+    }
+  }
+  uint32_t rc = 0;
+  for (uint8_t ty : t.results) rc += cells_of_value(ty);
+  if (!C->params.alloc(cells.size()) ||
+      !C->results.alloc(size_t(C->n) * (rc ? rc : 1)))
+    return R(C->fail(kRuntimeError, "device allocation failed"));
+  if (!C->hip_ok(hipMemcpyAsync(C->params.ptr, cells.data(), cells.size() * 4,
+                                hipMemcpyHostToDevice, C->stream), "params upload"))
+    return R(kRuntimeError);
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "params upload")) return R(kRuntimeError);
+  C->func = f;
+  C->param_cells = pc;
+  C->result_cells = rc;
+  C->result_types = t.results;
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeconds) {
+  if (!C) return R(kWrongVMWorkflow);
+  const wb::Program &P = C->prog;
+  uint32_t init_words = P.mem_min << 14;
+  (void)hipEventRecord(C->ev0, C->stream);
+  if (P.has_mem &&
+      !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
+                                    C->mem_words, C->nwaves, C->stream), "mem init"))
+    return R(kRuntimeError);
+  (void)hipEventRecord(C->ev1, C->stream);
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
+  if (KernelSeconds) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
+    *KernelSeconds = ms * 1e-3;
+  }
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSeconds) {
+  if (!C) return R(kWrongVMWorkflow);
+  if (C->func < 0) return R(C->fail(kWrongVMWorkflow, "BatchSetArgs not called"));
+  const wb::Program &P = C->prog;
+  const wb::FuncInfo &F = P.funcs[C->func];
+  if (F.imported) return R(C->fail(kRuntimeError, "exported function is a host import"));
+  KParams k{};
+  k.code = C->code.ptr; k.brtab = C->brtab.ptr; k.vconst = C->vconst.ptr;
+  k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
+  k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
+  k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.params = C->params.ptr;
+  k.results = C->results.ptr; k.status = C->status.ptr; k.counts = C->counts.ptr;
+  k.pages_out = C->pages.ptr;
+  k.n = C->n;
+  k.entry_pc = F.entry_pc;
+  k.param_cells = C->param_cells;
+  k.result_cells = C->result_cells;
+  k.global_cells = P.global_cells;
+  k.total_cells = P.total_cells() ? P.total_cells() : 1;
+  k.table_size = uint32_t(P.table0.size());
+  k.mem_words = C->mem_words;
+  k.init_pages = P.mem_min;
+  k.mem_max_pages = C->mem_max_pages;
+  k.gs_depth = C->gs_depth;
+  k.init_dropped = C->init_dropped;
+  k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
+  double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
+  k.max_ticks = uint64_t(tl * 1e8);
+  // launch geometry: 4 waves per block when the frames fit, 1 otherwise
+  size_t wave_lds = size_t(k.total_cells) * 64 * 4;
+  if (wave_lds > 160 * 1024)
+    return R(C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
+                                        " cells exceeds LDS (global-frame mode: next)"));
+  uint32_t wpb = 4;
+  while (wpb > 1 && wave_lds * wpb > 160 * 1024) wpb >>= 1;
+  uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
+  (void)hipEventRecord(C->ev0, C->stream);
+  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb, C->stream), "launch"))
+    return R(kRuntimeError);
+  (void)hipEventRecord(C->ev1, C->stream);
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return R(kRuntimeError);
+  if (KernelSeconds) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
+    *KernelSeconds = ms * 1e-3;
+  }
+  C->ran = true;
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchResults(WasmEdge_BatchContext *C, WasmEdge_Value *Returns,
+                                      const uint32_t ReturnLen, uint8_t *PerInstance,
+                                      uint64_t *InstrCounts) {
+  if (!C) return R(kWrongVMWorkflow);
+  if (!C->ran) return R(C->fail(kWrongVMWorkflow, "BatchRun not called"));
+  std::vector<uint8_t> st(C->n);
+  if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, C->n, hipMemcpyDeviceToHost), "status"))
+    return R(kRuntimeError);
+  if (PerInstance) memcpy(PerInstance, st.data(), C->n);
+  if (InstrCounts &&
+      !C->hip_ok(hipMemcpy(InstrCounts, C->counts.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "counts"))
+    return R(kRuntimeError);
+  if (Returns && ReturnLen) {
+    uint32_t rc = C->result_cells;
+    std::vector<uint32_t> cells(size_t(C->n) * (rc ? rc : 1));
+    if (rc && !C->hip_ok(hipMemcpy(cells.data(), C->results.ptr, cells.size() * 4,
+                                   hipMemcpyDeviceToHost), "results"))
+      return R(kRuntimeError);
+    for (uint32_t i = 0; i < C->n; i++) {
+      uint32_t at = 0;
+      for (uint32_t k = 0; k < C->result_types.size(); k++) {
+        uint8_t ty = C->result_types[k];
+        uint128_t v = 0;
+        for (uint32_t q = 0; q < cells_of_value(ty); q++)
+          v |= uint128_t(cells[size_t(i) * rc + at++]) << (32 * q);
+        if (k < ReturnLen) {
+          WasmEdge_Value &out = Returns[size_t(i) * ReturnLen + k];
+          out.Value = st[i] == 0 ? v : 0;
+          out.Type = static_cast<enum WasmEdge_ValType>(ty);
+        }
+      }
+    }
+  }
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_String FuncName,
+                                      const WasmEdge_Value *Params, const uint32_t ParamLen,
+                                      WasmEdge_Value *Returns, const uint32_t ReturnLen,
+                                      uint8_t *PerInstance, uint64_t *InstrCounts) {
+  if (!C) return R(kWrongVMWorkflow);
+  WasmEdge_Result r = WasmEdge_BatchSetArgs(C, FuncName, Params, ParamLen);
+  if (r.Code) return r;
+  r = WasmEdge_BatchReset(C, nullptr);
+  if (r.Code) return r;
+  r = WasmEdge_BatchRun(C, nullptr);
+  if (r.Code) return r;
+  return WasmEdge_BatchResults(C, Returns, ReturnLen, PerInstance, InstrCounts);
+}
+
+WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Hashes) {
+  if (!C) return R(kWrongVMWorkflow);
+  if (!C->ran) return R(C->fail(kWrongVMWorkflow, "BatchRun not called"));
+  if (!C->hip_ok(wb_launch_mem_hash(C->mem.ptr, C->pages.ptr, C->hashes.ptr, C->mem_words,
+                                    C->n, C->stream), "hash"))
+    return R(kRuntimeError);
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "hash")) return R(kRuntimeError);
+  if (!C->hip_ok(hipMemcpy(Hashes, C->hashes.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "hash"))
+    return R(kRuntimeError);
+  return R(0);
+}
+
+uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
+  if (!C || Inst >= C->n || !C->ran) return 0;
+  uint32_t p = 0;
+  (void)hipMemcpy(&p, C->pages.ptr + Inst, 4, hipMemcpyDeviceToHost);
+  return p;
+}
+
+WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off,
+                                        uint8_t *Dst, uint32_t Len) {
+  if (!C) return R(kWrongVMWorkflow);
+  if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
+  uint32_t pages = C->ran ? WasmEdge_BatchGetMemoryPages(C, Inst) : C->prog.mem_min;
+  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return R(kMemoryOutOfBounds);
+  if (Len == 0) return R(0);
+  // gather the lane's interleaved words: word w at ((wave*W + w)*64 + lane)
+  uint32_t wave = Inst / 64, lane = Inst % 64;
+  uint32_t w0 = Off / 4, w1 = (Off + Len + 3) / 4;
+  std::vector<uint32_t> rows(size_t(w1 - w0) * 64);
+  const uint32_t *src = C->mem.ptr + (size_t(wave) * C->mem_words + w0) * 64;
+  if (!C->hip_ok(hipMemcpy(rows.data(), src, rows.size() * 4, hipMemcpyDeviceToHost), "memory"))
+    return R(kRuntimeError);
+  for (uint32_t b = 0; b < Len; b++) {
+    uint32_t a = Off + b;
+    uint32_t w = rows[size_t(a / 4 - w0) * 64 + lane];
+    Dst[b] = uint8_t(w >> (8 * (a & 3)));
+  }
+  return R(0);
+}
+
+uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *C) { return C ? C->n : 0; }
+
+uint32_t WasmEdge_BatchGetCodeSize(const WasmEdge_BatchContext *C) {
+  return C ? uint32_t(C->prog.code.size()) : 0;
+}
+
+const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
+  return C ? C->last_error.c_str() : g_last_create_error.c_str();
+}
+
+void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
+  if (!C) return;
+  if (C->stream) (void)hipStreamSynchronize(C->stream);
+  if (C->ev0) (void)hipEventDestroy(C->ev0);
+  if (C->ev1) (void)hipEventDestroy(C->ev1);
+  hipStream_t s = C->stream;
+  delete C;
+  if (s) (void)hipStreamDestroy(s);
+}
+
+}  // extern "C"

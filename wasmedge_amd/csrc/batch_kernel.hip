@@ -1,0 +1,184 @@
+// batch_kernel.hip -- CDNA4 (gfx950) batched WebAssembly interpreter.
+//
+// One lane = one wasm instance; one wave = 64 instances executing the same module.
+// Replaces the reference's Executor::execute dispatch loop (lib/executor/engine/
+// engine.cpp:68-1638), StackManager (include/runtime/stackmgr.h) and MemoryInstance
+// (include/runtime/instance/memory.h) for the batched path.
+//
+// Execution model
+//  * wave-coherent dispatch: the wave fetches ONE 16-byte DBC instruction per step with
+//    a scalar load (uniform pc), and executes it for the lanes whose pc matches.  When
+//    all running lanes share a pc (the common, converged case) that costs one readlane +
+//    one ballot; after divergence the wave picks the minimum pc over running lanes, which
+//    reconverges structured control flow (join points sit at higher pcs than both arms).
+//  * frames: the CURRENT frame of every lane (globals + params + locals + operand cells)
+//    lives in LDS, cell-major / lane-minor, so a cell access is one conflict-free
+//    ds_read_b32/ds_write_b32 for the whole wave.  call spills the caller's live cells
+//    to a lane-interleaved HBM call stack; return restores them (POST_CALL).
+//  * linear memory: HBM, 4-byte words interleaved across the 64 lanes of a wave:
+//    word w of lane l is at mem[(wave*W + w)*64 + l], so lanes touching the same address
+//    coalesce into one 256-byte transaction.  Bounds and traps are per lane.
+//  * counting: every dispatch adds its `cnt` (wasm instructions retired) to a per-lane
+//    64-bit counter -- the reference's Statistics instruction count, exactly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dbc.h"
+#include "kparams.h"
+
+
+#include "dbc_ops.h"
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
+    v = o < v ? o : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+
+// ======================================================================= interpreter
+extern "C" __global__ void __launch_bounds__(256)
+wb_exec_kernel(const KParams p) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wib = threadIdx.x >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t inst = wave * 64u + lane;
+  uint32_t *const fr = lds + ((wib * p.total_cells) << 6) + lane;
+  uint32_t *const gs = p.gstack + (size_t)wave * p.gs_depth * 64u + lane;
+  uint32_t *const mem = p.mem + (size_t)wave * p.mem_words * 64u + lane;
+  const DInstr *__restrict__ code = p.code;
+
+#define CELL(x) fr[(uint32_t)(x) << 6]
+#define R32(x) CELL(x)
+#define W32(x, v) (CELL(x) = (uint32_t)(v))
+#define R64(x) ((uint64_t)CELL(x) | ((uint64_t)CELL((x) + 1) << 32))
+#define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
+#define GS(slot) gs[(size_t)(slot) << 6]
+#define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+
+  uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
+  uint32_t pc = p.entry_pc, gsp = 0, pages = p.init_pages, dropped = p.init_dropped;
+  uint64_t count = 0;
+  if (status == WB_STATUS_RUNNING) {
+    for (uint32_t c = 0; c < p.global_cells; c++) W32(c, p.global_init[c]);
+    const uint32_t *prm = p.params + (size_t)inst * p.param_cells;
+    for (uint32_t c = 0; c < p.param_cells; c++) W32(p.global_cells + c, prm[c]);
+    GS(0) = DBC_EXIT_PC;   // return record of the entry frame: L = 0, pc = EXIT
+    gsp = 1;
+  }
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t steps = 0;
+
+  for (;;) {
+    const uint64_t amask = __ballot(status == WB_STATUS_RUNNING);
+    if (amask == 0) break;
+    // ---- wave-coherent pc selection
+    const uint32_t first = (uint32_t)__builtin_ctzll(amask);
+    uint32_t pcs = __builtin_amdgcn_readlane(pc, first);
+    if (__ballot(status == WB_STATUS_RUNNING && pc == pcs) != amask)
+      pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
+    // ---- safety: fuel / wall-clock limit (ErrCode::Interrupted, mirrors StopToken)
+    if ((++steps & 1023u) == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (steps >= p.max_steps || now - t0 > p.max_ticks) {
+        if (status == WB_STATUS_RUNNING) status = WB_ERR_INTERRUPTED;
+        break;
+      }
+    }
+    const DInstr I = code[pcs];
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(I.w0);
+    const uint32_t w1 = __builtin_amdgcn_readfirstlane(I.w1);
+    const uint32_t w2 = __builtin_amdgcn_readfirstlane(I.w2);
+    const uint32_t w3 = __builtin_amdgcn_readfirstlane(I.w3);
+    if (status != WB_STATUS_RUNNING || pc != pcs) continue;
+
+    const uint32_t op = w0 & 0xFFFFu;
+    const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = w0 >> 24;
+    int32_t add = (int32_t)cnt8;
+    uint32_t npc = pcs + 1;
+    const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+
+    switch (op) {
+#include "dbc_step.inc"
+    }
+    count += (int64_t)add;
+    pc = npc;
+  }
+#undef CELL
+  if (inst < p.n) {
+    p.status[inst] = (uint8_t)status;
+    p.counts[inst] = count;
+    p.pages_out[inst] = pages;
+  }
+}
+
+// ======================================================================= helpers
+// Instantiation image broadcast (instantiate/memory.cpp + data.cpp): every lane's
+// pages [0, init_pages) = the module image (data segments), rest of those pages zero.
+extern "C" __global__ void __launch_bounds__(256)
+wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
+                   uint32_t init_words, uint32_t mem_words, uint32_t nwaves) {
+  const size_t total = (size_t)nwaves * init_words * 64u;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t wave = i / ((size_t)init_words * 64u);
+    const uint32_t rem = (uint32_t)(i - wave * (size_t)init_words * 64u);
+    const uint32_t word = rem >> 6, lane = rem & 63u;
+    mem[(wave * mem_words + word) * 64u + lane] = word < image_words ? image[word] : 0u;
+  }
+}
+
+// Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
+extern "C" __global__ void __launch_bounds__(256)
+wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *pages_of, uint64_t *hashes,
+                   uint32_t mem_words, uint32_t n) {
+  const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
+  if (inst >= n) return;
+  const uint32_t wave = inst >> 6, lane = inst & 63u;
+  const uint32_t *m = mem + (size_t)wave * mem_words * 64u + lane;
+  const uint32_t pages = pages_of ? pages_of[inst] : 0;
+  const uint64_t nw = (uint64_t)pages << 13;
+  uint64_t h = 0;
+  for (uint64_t i = 0; i < nw; i++) {
+    const uint64_t w = (uint64_t)m[(2 * i) << 6] | ((uint64_t)m[(2 * i + 1) << 6] << 32);
+    h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
+  }
+  hashes[inst] = h ^ fmix64((uint64_t)pages + 0x1234567ull);
+}
+
+// ======================================================================= launchers
+// (host stubs live in this translation unit; the C-ABI layer calls these)
+extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
+                                     size_t lds_bytes, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
+  return hipGetLastError();
+}
+extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
+                                         uint32_t image_words, uint32_t init_words,
+                                         uint32_t mem_words, uint32_t nwaves, hipStream_t s) {
+  const size_t total = (size_t)nwaves * init_words * 64u;
+  if (total == 0) return hipSuccess;
+  size_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(wb_mem_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, mem, image,
+                     image_words, init_words, mem_words, nwaves);
+  return hipGetLastError();
+}
+extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *pages,
+                                         uint64_t *hashes, uint32_t mem_words, uint32_t n,
+                                         hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mem, pages,
+                     hashes, mem_words, n);
+  return hipGetLastError();
+}

@@ -1,0 +1,142 @@
+// emu.cpp -- TEST-ONLY host emulator of the DBC interpreter. It compiles the very same
+// dbc_step.inc the gfx950 kernel runs (one lane at a time, contiguous per-lane memory)
+// so tests can check the lowering and the per-op code against the oracle on a CPU.
+// It is built into a separate library (libwasmedge_batch_emu.so) that the product never
+// loads; the product path (libwasmedge_batch.so) has no CPU execution path.
+#define WB_MSHIFT 0
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dbc_ops.h"
+#include "frontend.h"
+#include "kparams.h"
+
+static std::string g_err;
+
+extern "C" {
+
+__attribute__((visibility("default"))) const char *wb_emu_last_error() { return g_err.c_str(); }
+
+// Returns ErrCode of the call; per-instance outputs like WasmEdge_BatchExecute.
+// params: [n][param cells] u32; results: [n][result cells] u32.
+__attribute__((visibility("default"))) int wb_emu_execute(
+    const uint8_t *wasm, uint32_t len, const char *func, uint32_t n, const uint32_t *params,
+    uint32_t *results, uint8_t *statuses, uint64_t *counts, uint64_t *hashes,
+    uint32_t max_pages, uint32_t gs_depth, uint64_t max_steps) {
+  wb::Program P;
+  uint8_t ec = 0;
+  g_err = wb::load_program(wasm, len, P, &ec);
+  if (!g_err.empty()) return ec ? ec : 2;
+  int f = wb::find_export(P, func);
+  if (f < 0) { g_err = "function not found"; return 0x05; }
+  const wb::FuncInfo &F = P.funcs[f];
+  const wb::FuncType &T = P.types[F.type];
+  uint32_t pcells = 0, rcells = 0;
+  for (uint8_t t : T.params) pcells += wb::cells_of(t);
+  for (uint8_t t : T.results) rcells += wb::cells_of(t);
+  uint32_t budget = max_pages ? max_pages : (P.mem_has_max ? P.mem_max : P.mem_min);
+  if (P.mem_has_max && budget > P.mem_max) budget = P.mem_max;
+  if (budget < P.mem_min) budget = P.mem_min;
+  if (!P.has_mem) budget = 0;
+  if (!gs_depth) gs_depth = 4096;
+  std::vector<DFunc> fv;
+  for (const auto &fi : P.funcs) fv.push_back(DFunc{fi.imported ? 0xFFFFFFFFu : fi.entry_pc, P.type_canon[fi.type]});
+  std::vector<uint8_t> pool;
+  std::vector<uint32_t> doff, dlen;
+  uint32_t init_dropped = 0;
+  for (size_t k = 0; k < P.datas.size(); k++) {
+    doff.push_back(uint32_t(pool.size()));
+    dlen.push_back(uint32_t(P.datas[k].bytes.size()));
+    pool.insert(pool.end(), P.datas[k].bytes.begin(), P.datas[k].bytes.end());
+    if (P.datas[k].active && k < 32) init_dropped |= 1u << k;
+  }
+  KParams p{};
+  p.code = P.code.data(); p.brtab = P.brtab.data(); p.vconst = P.vconst.data();
+  p.funcs = fv.data(); p.table = P.table0.data(); p.global_init = P.global_init.data();
+  p.data_pool = pool.data(); p.data_off = doff.data(); p.data_len = dlen.data();
+  p.results = results; p.param_cells = pcells; p.result_cells = rcells;
+  p.global_cells = P.global_cells; p.total_cells = P.total_cells();
+  p.table_size = uint32_t(P.table0.size()); p.mem_max_pages = budget;
+  p.gs_depth = gs_depth;
+  std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
+  std::vector<uint32_t> memv;
+  for (uint32_t inst = 0; inst < n; inst++) {
+    // instantiate: memory image + globals
+    memv.assign(size_t(budget) << 14, 0u);
+    uint8_t *mb = reinterpret_cast<uint8_t *>(memv.data());
+    for (const auto &d : P.datas)
+      if (d.active) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
+    uint32_t *fr = frame.data(), *gs = gstack.data(), *mem = memv.data();
+#define CELL(x) fr[(uint32_t)(x)]
+#define R32(x) CELL(x)
+#define W32(x, v) (CELL(x) = (uint32_t)(v))
+#define R64(x) ((uint64_t)CELL(x) | ((uint64_t)CELL((x) + 1) << 32))
+#define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
+#define GS(slot) gs[(size_t)(slot)]
+#define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+    uint32_t status = WB_STATUS_RUNNING, pc = F.entry_pc, gsp = 0, pages = P.mem_min;
+    uint32_t dropped = init_dropped;
+    uint64_t count = 0, steps = 0;
+    for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
+    for (uint32_t c = 0; c < pcells; c++) W32(P.global_cells + c, params[size_t(inst) * pcells + c]);
+    GS(0) = DBC_EXIT_PC;
+    gsp = 1;
+    while (status == WB_STATUS_RUNNING) {
+      if (max_steps && ++steps > max_steps) { status = 0x07; break; }
+      const uint32_t pcs = pc;
+      const DInstr I = P.code[pcs];
+      const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
+      const uint32_t op = w0 & 0xFFFFu;
+      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = w0 >> 24;
+      int32_t add = (int32_t)cnt8;
+      uint32_t npc = pcs + 1;
+      const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+      switch (op) {
+#include "dbc_step.inc"
+      }
+      count += (int64_t)add;
+      pc = npc;
+    }
+    statuses[inst] = uint8_t(status);
+    counts[inst] = count;
+    if (hashes) {
+      uint64_t h = 0, nw = uint64_t(pages) << 13;
+      for (uint64_t i = 0; i < nw; i++) {
+        uint64_t w = uint64_t(mem[2 * i]) | (uint64_t(mem[2 * i + 1]) << 32);
+        h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
+      }
+      hashes[inst] = h ^ fmix64(uint64_t(pages) + 0x1234567ull);
+    }
+  }
+  return 0;
+}
+
+// Disassemble the lowered program (debugging / tests of the lowering).
+__attribute__((visibility("default"))) int wb_emu_disasm(const uint8_t *wasm, uint32_t len,
+                                                         char *out, uint32_t outlen) {
+  wb::Program P;
+  uint8_t ec = 0;
+  g_err = wb::load_program(wasm, len, P, &ec);
+  if (!g_err.empty()) return ec ? ec : 2;
+  std::string s;
+  char buf[160];
+  for (size_t k = 0; k < P.code.size(); k++) {
+    const DInstr &I = P.code[k];
+    snprintf(buf, sizeof buf, "%5zu %-18s cnt=%u post=%u a=%u b=%u c=%u d=%d imm=%u\n", k,
+             wb::dop_name(I.w0 & 0xFFFF), (I.w0 >> 16) & 0xFF, I.w0 >> 24, I.w1 & 0xFFFF,
+             I.w1 >> 16, I.w2 & 0xFFFF, int(int16_t(I.w2 >> 16)), I.w3);
+    s += buf;
+  }
+  snprintf(buf, sizeof buf, "; globals=%u frame=%u code=%zu\n", P.global_cells, P.frame_cells,
+           P.code.size());
+  s += buf;
+  if (out && outlen) {
+    strncpy(out, s.c_str(), outlen - 1);
+    out[outlen - 1] = 0;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1393 @@
+// frontend.cpp -- decode + validate + lower a wasm module to the register-form DBC.
+// See frontend.h / dbc.h. Reference behaviour restated (with file:line) where it
+// determines results or instruction counts.
+#include "frontend.h"
+
+#include <cstring>
+#include <map>
+#include <unordered_map>
+
+namespace wb {
+
+namespace {
+
+// ErrCodes (include/common/enum.inc:573-749)
+enum : uint8_t { E_MALFORMED = 0x21, E_ILLEGAL_OPCODE = 0x37, E_TYPECHECK = 0x41,
+                 E_UNSUPPORTED = 0x02 /* RuntimeError: outside the batched subset */ };
+
+struct Err {
+  uint8_t code;
+  std::string msg;
+};
+
+struct Reader {
+  const uint8_t *p, *end;
+  uint8_t u8() {
+    if (p >= end) throw Err{E_MALFORMED, "unexpected end"};
+    return *p++;
+  }
+  uint64_t uleb(int bits = 32) {
+    uint64_t v = 0;
+    int sh = 0;
+    for (;;) {
+      uint8_t b = u8();
+      v |= uint64_t(b & 0x7F) << sh;
+      sh += 7;
+      if (!(b & 0x80)) break;
+      if (sh >= bits + 7) throw Err{E_MALFORMED, "integer representation too long"};
+    }
+    return v;
+  }
+  int64_t sleb(int bits) {
+    int64_t v = 0;
+    int sh = 0;
+    uint8_t b;
+    do {
+      b = u8();
+      v |= int64_t(b & 0x7F) << sh;
+      sh += 7;
+      if (sh >= bits + 7) throw Err{E_MALFORMED, "integer representation too long"};
+    } while (b & 0x80);
+    if (sh < 64 && (b & 0x40)) v |= -(int64_t(1) << sh);
+    return v;
+  }
+  uint32_t u32() { return uint32_t(uleb(32)); }
+  std::string name() {
+    uint32_t n = u32();
+    if (uint64_t(end - p) < n) throw Err{E_MALFORMED, "name"};
+    std::string s(reinterpret_cast<const char *>(p), n);
+    p += n;
+    return s;
+  }
+};
+
+// ------------------------------------------------------------------ op tables
+struct SimpleOp {
+  uint16_t dop;
+  int16_t dop_imm;     // register-immediate variant, -1 if none
+  const char *sig;     // "pops:pushes", i=i32 l=i64 f=f32 d=f64 v=v128
+  bool commutative;
+};
+
+std::unordered_map<uint16_t, SimpleOp> build_simple() {
+  std::unordered_map<uint16_t, SimpleOp> t;
+  auto add = [&](uint16_t w, uint16_t d, int16_t di, const char *s, bool c = false) {
+    t[w] = SimpleOp{d, di, s, c};
+  };
+  // i32 compare / arithmetic (wasm 0x46-0x4F, 0x6A-0x78)
+  const uint16_t i32cmp[] = {OP_I32_EQ, OP_I32_NE, OP_I32_LT_S, OP_I32_LT_U, OP_I32_GT_S,
+                             OP_I32_GT_U, OP_I32_LE_S, OP_I32_LE_U, OP_I32_GE_S, OP_I32_GE_U};
+  for (int k = 0; k < 10; k++)
+    add(0x46 + k, i32cmp[k], int16_t(i32cmp[k] - OP_I32_ADD + OP_I32_ADD_I), "ii:i", k < 2);
+  const uint16_t i32ar[] = {OP_I32_ADD, OP_I32_SUB, OP_I32_MUL, OP_I32_DIV_S, OP_I32_DIV_U,
+                            OP_I32_REM_S, OP_I32_REM_U, OP_I32_AND, OP_I32_OR, OP_I32_XOR,
+                            OP_I32_SHL, OP_I32_SHR_S, OP_I32_SHR_U, OP_I32_ROTL, OP_I32_ROTR};
+  const bool i32c[] = {1, 0, 1, 0, 0, 0, 0, 1, 1, 1, 0, 0, 0, 0, 0};
+  for (int k = 0; k < 15; k++)
+    add(0x6A + k, i32ar[k], int16_t(i32ar[k] - OP_I32_ADD + OP_I32_ADD_I), "ii:i", i32c[k]);
+  const uint16_t i64cmp[] = {OP_I64_EQ, OP_I64_NE, OP_I64_LT_S, OP_I64_LT_U, OP_I64_GT_S,
+                             OP_I64_GT_U, OP_I64_LE_S, OP_I64_LE_U, OP_I64_GE_S, OP_I64_GE_U};
+  for (int k = 0; k < 10; k++)
+    add(0x51 + k, i64cmp[k], int16_t(i64cmp[k] - OP_I64_ADD + OP_I64_ADD_I), "ll:i", k < 2);
+  const uint16_t i64ar[] = {OP_I64_ADD, OP_I64_SUB, OP_I64_MUL, OP_I64_DIV_S, OP_I64_DIV_U,
+                            OP_I64_REM_S, OP_I64_REM_U, OP_I64_AND, OP_I64_OR, OP_I64_XOR,
+                            OP_I64_SHL, OP_I64_SHR_S, OP_I64_SHR_U, OP_I64_ROTL, OP_I64_ROTR};
+  for (int k = 0; k < 15; k++)
+    add(0x7C + k, i64ar[k], int16_t(i64ar[k] - OP_I64_ADD + OP_I64_ADD_I), "ll:l", i32c[k]);
+  add(0x45, OP_I32_EQZ, -1, "i:i");
+  add(0x50, OP_I64_EQZ, -1, "l:i");
+  add(0x67, OP_I32_CLZ, -1, "i:i"); add(0x68, OP_I32_CTZ, -1, "i:i");
+  add(0x69, OP_I32_POPCNT, -1, "i:i");
+  add(0x79, OP_I64_CLZ, -1, "l:l"); add(0x7A, OP_I64_CTZ, -1, "l:l");
+  add(0x7B, OP_I64_POPCNT, -1, "l:l");
+  const uint16_t f32cmp[] = {OP_F32_EQ, OP_F32_NE, OP_F32_LT, OP_F32_GT, OP_F32_LE, OP_F32_GE};
+  const uint16_t f64cmp[] = {OP_F64_EQ, OP_F64_NE, OP_F64_LT, OP_F64_GT, OP_F64_LE, OP_F64_GE};
+  for (int k = 0; k < 6; k++) { add(0x5B + k, f32cmp[k], -1, "ff:i"); add(0x61 + k, f64cmp[k], -1, "dd:i"); }
+  const uint16_t f32un[] = {OP_F32_ABS, OP_F32_NEG, OP_F32_CEIL, OP_F32_FLOOR, OP_F32_TRUNC,
+                            OP_F32_NEAREST, OP_F32_SQRT};
+  const uint16_t f64un[] = {OP_F64_ABS, OP_F64_NEG, OP_F64_CEIL, OP_F64_FLOOR, OP_F64_TRUNC,
+                            OP_F64_NEAREST, OP_F64_SQRT};
+  for (int k = 0; k < 7; k++) { add(0x8B + k, f32un[k], -1, "f:f"); add(0x99 + k, f64un[k], -1, "d:d"); }
+  const uint16_t f32bin[] = {OP_F32_ADD, OP_F32_SUB, OP_F32_MUL, OP_F32_DIV, OP_F32_MIN,
+                             OP_F32_MAX, OP_F32_COPYSIGN};
+  const uint16_t f64bin[] = {OP_F64_ADD, OP_F64_SUB, OP_F64_MUL, OP_F64_DIV, OP_F64_MIN,
+                             OP_F64_MAX, OP_F64_COPYSIGN};
+  for (int k = 0; k < 7; k++) { add(0x92 + k, f32bin[k], -1, "ff:f"); add(0xA0 + k, f64bin[k], -1, "dd:d"); }
+  add(0xA8, OP_I32_TRUNC_F32_S, -1, "f:i"); add(0xA9, OP_I32_TRUNC_F32_U, -1, "f:i");
+  add(0xAA, OP_I32_TRUNC_F64_S, -1, "d:i"); add(0xAB, OP_I32_TRUNC_F64_U, -1, "d:i");
+  add(0xAC, OP_I64_EXTEND_I32_S, -1, "i:l"); add(0xAD, OP_I64_EXTEND_I32_U, -1, "i:l");
+  add(0xAE, OP_I64_TRUNC_F32_S, -1, "f:l"); add(0xAF, OP_I64_TRUNC_F32_U, -1, "f:l");
+  add(0xB0, OP_I64_TRUNC_F64_S, -1, "d:l"); add(0xB1, OP_I64_TRUNC_F64_U, -1, "d:l");
+  add(0xB2, OP_F32_CONVERT_I32_S, -1, "i:f"); add(0xB3, OP_F32_CONVERT_I32_U, -1, "i:f");
+  add(0xB4, OP_F32_CONVERT_I64_S, -1, "l:f"); add(0xB5, OP_F32_CONVERT_I64_U, -1, "l:f");
+  add(0xB6, OP_F32_DEMOTE_F64, -1, "d:f");
+  add(0xB7, OP_F64_CONVERT_I32_S, -1, "i:d"); add(0xB8, OP_F64_CONVERT_I32_U, -1, "i:d");
+  add(0xB9, OP_F64_CONVERT_I64_S, -1, "l:d"); add(0xBA, OP_F64_CONVERT_I64_U, -1, "l:d");
+  add(0xBB, OP_F64_PROMOTE_F32, -1, "f:d");
+  add(0xC0, OP_I32_EXT8S, -1, "i:i"); add(0xC1, OP_I32_EXT16S, -1, "i:i");
+  add(0xC2, OP_I64_EXT8S, -1, "l:l"); add(0xC3, OP_I64_EXT16S, -1, "l:l");
+  add(0xC4, OP_I64_EXT32S, -1, "l:l");
+  const uint16_t sat[] = {OP_I32_TRUNC_SAT_F32_S, OP_I32_TRUNC_SAT_F32_U, OP_I32_TRUNC_SAT_F64_S,
+                          OP_I32_TRUNC_SAT_F64_U, OP_I64_TRUNC_SAT_F32_S, OP_I64_TRUNC_SAT_F32_U,
+                          OP_I64_TRUNC_SAT_F64_S, OP_I64_TRUNC_SAT_F64_U};
+  const char *satsig[] = {"f:i", "f:i", "d:i", "d:i", "f:l", "f:l", "d:l", "d:l"};
+  for (int k = 0; k < 8; k++) add(0xFC00 + k, sat[k], -1, satsig[k]);
+  // SIMD subset lowered in this round (the rest are rejected at load time)
+  add(0xFD4D, OP_V_NOT, -1, "v:v"); add(0xFD4E, OP_V_AND, -1, "vv:v", true);
+  add(0xFD4F, OP_V_ANDNOT, -1, "vv:v"); add(0xFD50, OP_V_OR, -1, "vv:v", true);
+  add(0xFD51, OP_V_XOR, -1, "vv:v", true); add(0xFD52, OP_V_BITSELECT, -1, "vvv:v");
+  add(0xFD53, OP_V_ANY_TRUE, -1, "v:i");
+  add(0xFD0F, OP_V_I8X16_SPLAT, -1, "i:v"); add(0xFD10, OP_V_I16X8_SPLAT, -1, "i:v");
+  add(0xFD11, OP_V_I32X4_SPLAT, -1, "i:v"); add(0xFD12, OP_V_I64X2_SPLAT, -1, "l:v");
+  add(0xFD13, OP_V_F32X4_SPLAT, -1, "f:v"); add(0xFD14, OP_V_F64X2_SPLAT, -1, "d:v");
+  add(0xFD0E, OP_V_SWIZZLE, -1, "vv:v");
+  add(0xFD6E, OP_V_I8X16_ADD, -1, "vv:v"); add(0xFD71, OP_V_I8X16_SUB, -1, "vv:v");
+  add(0xFD8E, OP_V_I16X8_ADD, -1, "vv:v"); add(0xFD91, OP_V_I16X8_SUB, -1, "vv:v");
+  add(0xFD95, OP_V_I16X8_MUL, -1, "vv:v");
+  add(0xFDAE, OP_V_I32X4_ADD, -1, "vv:v"); add(0xFDB1, OP_V_I32X4_SUB, -1, "vv:v");
+  add(0xFDB5, OP_V_I32X4_MUL, -1, "vv:v");
+  add(0xFDCE, OP_V_I64X2_ADD, -1, "vv:v"); add(0xFDD1, OP_V_I64X2_SUB, -1, "vv:v");
+  add(0xFDD5, OP_V_I64X2_MUL, -1, "vv:v");
+  add(0xFD23, OP_V_I8X16_EQ, -1, "vv:v"); add(0xFD24, OP_V_I8X16_NE, -1, "vv:v");
+  add(0xFD2D, OP_V_I16X8_EQ, -1, "vv:v"); add(0xFD2E, OP_V_I16X8_NE, -1, "vv:v");
+  const uint16_t i32x4cmp[] = {OP_V_I32X4_EQ, OP_V_I32X4_NE, OP_V_I32X4_LT_S, OP_V_I32X4_LT_U,
+                               OP_V_I32X4_GT_S, OP_V_I32X4_GT_U, OP_V_I32X4_LE_S,
+                               OP_V_I32X4_LE_U, OP_V_I32X4_GE_S, OP_V_I32X4_GE_U};
+  for (int k = 0; k < 10; k++) add(0xFD37 + k, i32x4cmp[k], -1, "vv:v");
+  const uint16_t i64x2cmp[] = {OP_V_I64X2_EQ, OP_V_I64X2_NE, OP_V_I64X2_LT_S, OP_V_I64X2_GT_S,
+                               OP_V_I64X2_LE_S, OP_V_I64X2_GE_S};
+  for (int k = 0; k < 6; k++) add(0xFDD6 + k, i64x2cmp[k], -1, "vv:v");
+  const uint16_t shifts[] = {OP_V_I8X16_SHL, OP_V_I8X16_SHR_S, OP_V_I8X16_SHR_U};
+  for (int k = 0; k < 3; k++) add(0xFD6B + k, shifts[k], -1, "vi:v");
+  add(0xFD8B, OP_V_I16X8_SHL, -1, "vi:v"); add(0xFD8C, OP_V_I16X8_SHR_S, -1, "vi:v");
+  add(0xFD8D, OP_V_I16X8_SHR_U, -1, "vi:v");
+  add(0xFDAB, OP_V_I32X4_SHL, -1, "vi:v"); add(0xFDAC, OP_V_I32X4_SHR_S, -1, "vi:v");
+  add(0xFDAD, OP_V_I32X4_SHR_U, -1, "vi:v");
+  add(0xFDCB, OP_V_I64X2_SHL, -1, "vi:v"); add(0xFDCC, OP_V_I64X2_SHR_S, -1, "vi:v");
+  add(0xFDCD, OP_V_I64X2_SHR_U, -1, "vi:v");
+  add(0xFD63, OP_V_I8X16_ALL_TRUE, -1, "v:i"); add(0xFD83, OP_V_I16X8_ALL_TRUE, -1, "v:i");
+  add(0xFDA3, OP_V_I32X4_ALL_TRUE, -1, "v:i"); add(0xFDC3, OP_V_I64X2_ALL_TRUE, -1, "v:i");
+  add(0xFD64, OP_V_I8X16_BITMASK, -1, "v:i"); add(0xFD84, OP_V_I16X8_BITMASK, -1, "v:i");
+  add(0xFDA4, OP_V_I32X4_BITMASK, -1, "v:i"); add(0xFDC4, OP_V_I64X2_BITMASK, -1, "v:i");
+  add(0xFDA1, OP_V_I32X4_NEG, -1, "v:v"); add(0xFDC1, OP_V_I64X2_NEG, -1, "v:v");
+  add(0xFDA0, OP_V_I32X4_ABS, -1, "v:v"); add(0xFDC0, OP_V_I64X2_ABS, -1, "v:v");
+  const uint16_t f32x4b[] = {OP_V_F32X4_ADD, OP_V_F32X4_SUB, OP_V_F32X4_MUL, OP_V_F32X4_DIV,
+                             OP_V_F32X4_MIN, OP_V_F32X4_MAX, OP_V_F32X4_PMIN, OP_V_F32X4_PMAX};
+  const uint16_t f64x2b[] = {OP_V_F64X2_ADD, OP_V_F64X2_SUB, OP_V_F64X2_MUL, OP_V_F64X2_DIV,
+                             OP_V_F64X2_MIN, OP_V_F64X2_MAX, OP_V_F64X2_PMIN, OP_V_F64X2_PMAX};
+  for (int k = 0; k < 8; k++) { add(0xFDE4 + k, f32x4b[k], -1, "vv:v"); add(0xFDF0 + k, f64x2b[k], -1, "vv:v"); }
+  const uint16_t f32x4c[] = {OP_V_F32X4_EQ, OP_V_F32X4_NE, OP_V_F32X4_LT, OP_V_F32X4_GT,
+                             OP_V_F32X4_LE, OP_V_F32X4_GE};
+  const uint16_t f64x2c[] = {OP_V_F64X2_EQ, OP_V_F64X2_NE, OP_V_F64X2_LT, OP_V_F64X2_GT,
+                             OP_V_F64X2_LE, OP_V_F64X2_GE};
+  for (int k = 0; k < 6; k++) { add(0xFD41 + k, f32x4c[k], -1, "vv:v"); add(0xFD47 + k, f64x2c[k], -1, "vv:v"); }
+  add(0xFDE0, OP_V_F32X4_ABS, -1, "v:v"); add(0xFDE1, OP_V_F32X4_NEG, -1, "v:v");
+  add(0xFDE3, OP_V_F32X4_SQRT, -1, "v:v");
+  add(0xFDEC, OP_V_F64X2_ABS, -1, "v:v"); add(0xFDED, OP_V_F64X2_NEG, -1, "v:v");
+  add(0xFDEF, OP_V_F64X2_SQRT, -1, "v:v");
+  return t;
+}
+
+const std::unordered_map<uint16_t, SimpleOp> &simple_ops() {
+  static const auto t = build_simple();
+  return t;
+}
+
+uint8_t sigt(char c) {
+  switch (c) {
+    case 'i': return I32; case 'l': return I64; case 'f': return F32; case 'd': return F64;
+    default: return V128;
+  }
+}
+
+bool is_numtype(uint8_t t) {
+  return t == I32 || t == I64 || t == F32 || t == F64 || t == V128 || t == FUNCREF ||
+         t == EXTERNREF;
+}
+
+// ------------------------------------------------------------------ lowering
+enum Kind : uint8_t { K_CELL, K_CONST, K_LOCAL };
+
+struct Entry {
+  uint8_t type;
+  Kind kind;
+  uint32_t cell;        // canonical cell of this stack slot
+  uint32_t local;       // K_LOCAL: local index
+  uint32_t k[4];        // K_CONST: value words
+  int64_t producer;     // index of the DInstr that wrote this cell as `c`, -1 if none
+};
+
+struct Fixup {
+  bool brtab;           // patch brtab entry (else DInstr imm/d)
+  uint32_t index;
+  int32_t extra;
+};
+
+enum CtrlKind : uint8_t { C_BLOCK, C_LOOP, C_IF, C_FUNC };
+
+struct Ctrl {
+  CtrlKind kind;
+  std::vector<uint8_t> in, out;
+  uint32_t height;       // stack entries below the frame's values
+  uint32_t cell_base;    // canonical cell at height
+  bool unreachable = false;
+  bool dead = false;     // pushed inside unreachable code
+  bool label_known = false;
+  uint32_t label_pc = 0;
+  int32_t label_tcnt = 0;
+  std::vector<Fixup> fixups;
+  int64_t else_br = -1;  // BR_UNLESS of an `if`, patched at else/end
+  bool has_else = false;
+};
+
+struct CallFix {
+  uint32_t instr;
+  uint32_t callee;
+};
+
+class Lowerer {
+ public:
+  Lowerer(Program &P, const uint8_t *bin) : P(P), bin(bin) {}
+
+  void lower_function(uint32_t fi, std::vector<CallFix> &callfix);
+
+ private:
+  Program &P;
+  const uint8_t *bin;
+  // per function
+  const FuncType *ft = nullptr;
+  std::vector<uint8_t> ltypes;
+  std::vector<uint32_t> lcell;
+  uint32_t frame_base = 0, opnd_base = 0, max_cell = 0;
+  std::vector<Entry> st;
+  std::vector<Ctrl> ctrl;
+  uint32_t pending = 0;
+  int64_t last_emit = -1;
+  bool can_retarget = false;
+  std::vector<CallFix> *callfix = nullptr;
+
+  [[noreturn]] void fail(uint8_t code, const std::string &m) { throw Err{code, m}; }
+
+  bool live() const { return !ctrl.back().unreachable; }
+
+  uint32_t top_cell() const {
+    if (st.empty()) return opnd_base;
+    return st.back().cell + cells_of(st.back().type);
+  }
+
+  DInstr &emit(uint16_t op, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0, uint32_t d = 0,
+               uint32_t imm = 0) {
+    if (a > 0xFFFF || b > 0xFFFF || c > 0xFFFF)
+      fail(E_UNSUPPORTED, "cell index out of range for the DBC encoding");
+    while (pending > 255) {                  // cnt is 8 bits: spill into NOP_CNT
+      P.code.push_back(DInstr{uint32_t(OP_NOP_CNT) | (255u << 16), 0, 0, 0});
+      pending -= 255;
+    }
+    DInstr I;
+    I.w0 = uint32_t(op) | (pending << 16);
+    I.w1 = (a & 0xFFFF) | (b << 16);
+    I.w2 = (c & 0xFFFF) | (d << 16);
+    I.w3 = imm;
+    if (pending > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = pending;
+    pending = 0;
+    P.code.push_back(I);
+    last_emit = int64_t(P.code.size()) - 1;
+    can_retarget = true;
+    return P.code.back();
+  }
+
+  void place_label() { can_retarget = false; }
+
+  // ---------------- stack
+  Entry &push_cell(uint8_t t, int64_t producer = -1) {
+    Entry e{};
+    e.type = t;
+    e.kind = K_CELL;
+    e.cell = top_cell();
+    e.producer = producer;
+    st.push_back(e);
+    uint32_t hi = e.cell + cells_of(t);
+    if (hi > max_cell) max_cell = hi;
+    return st.back();
+  }
+  void push_const(uint8_t t, const uint32_t *k) {
+    Entry &e = push_cell(t);
+    e.kind = K_CONST;
+    memcpy(e.k, k, sizeof e.k);
+  }
+  void push_local(uint32_t li) {
+    Entry &e = push_cell(ltypes[li]);
+    e.kind = K_LOCAL;
+    e.local = li;
+  }
+  Entry pop_any() {
+    Ctrl &f = ctrl.back();
+    if (st.size() == f.height) {
+      if (f.unreachable) {
+        Entry e{};
+        e.type = UNKNOWN;
+        e.kind = K_CELL;
+        e.cell = top_cell();
+        e.producer = -1;
+        return e;
+      }
+      fail(E_TYPECHECK, "type mismatch: operand stack underflow");
+    }
+    Entry e = st.back();
+    st.pop_back();
+    return e;
+  }
+  Entry pop_t(uint8_t t) {
+    Entry e = pop_any();
+    if (e.type != UNKNOWN && t != UNKNOWN && e.type != t) fail(E_TYPECHECK, "type mismatch");
+    if (e.type == UNKNOWN) e.type = t;
+    return e;
+  }
+  void pop_types(const std::vector<uint8_t> &ts) {
+    for (size_t k = ts.size(); k > 0; k--) pop_t(ts[k - 1]);
+  }
+
+  // ---------------- materialisation
+  void materialize_into(const Entry &e, uint32_t dst) {
+    uint32_t w = cells_of(e.type);
+    if (e.kind == K_CONST) {
+      if (w == 1) emit(OP_CONST32, 0, 0, dst, 0, e.k[0]);
+      else if (w == 2) emit(OP_CONST64, e.k[1] & 0xFFFF, e.k[1] >> 16, dst, 0, e.k[0]);
+      else {
+        uint32_t idx = uint32_t(P.vconst.size() / 4);
+        P.vconst.insert(P.vconst.end(), e.k, e.k + 4);
+        emit(OP_CONST128, 0, 0, dst, 0, idx);
+      }
+    } else {
+      uint32_t src = e.kind == K_LOCAL ? lcell[e.local] : e.cell;
+      if (src == dst) return;
+      emit(w == 1 ? OP_MOV32 : w == 2 ? OP_MOV64 : OP_MOV128, src, 0, dst);
+    }
+  }
+  void materialize(size_t idx) {
+    Entry &e = st[idx];
+    if (e.kind == K_CELL) return;
+    if (live()) materialize_into(e, e.cell);
+    e.kind = K_CELL;
+    e.producer = -1;
+  }
+  void materialize_locals(int64_t local = -1) {
+    for (size_t k = 0; k < st.size(); k++)
+      if (st[k].kind == K_LOCAL && (local < 0 || st[k].local == uint32_t(local))) materialize(k);
+  }
+  void materialize_top(size_t n) {
+    for (size_t k = st.size() - n; k < st.size(); k++) materialize(k);
+  }
+  // source cell for an operand (materialising constants into their own slot)
+  uint32_t src(Entry &e) {
+    if (e.kind == K_LOCAL) return lcell[e.local];
+    if (e.kind == K_CONST) {
+      if (live()) materialize_into(e, e.cell);
+      e.kind = K_CELL;
+    }
+    return e.cell;
+  }
+
+  // ---------------- control
+  void block_type(Reader &r, std::vector<uint8_t> &in, std::vector<uint8_t> &out) {
+    uint8_t b = *r.p;
+    if (b == 0x40) { r.p++; return; }
+    if (is_numtype(b)) { r.p++; out.push_back(b); return; }
+    int64_t ti = r.sleb(33);
+    if (ti < 0 || uint64_t(ti) >= P.types.size()) fail(E_TYPECHECK, "unknown type");
+    in = P.types[ti].params;
+    out = P.types[ti].results;
+  }
+
+  void push_ctrl(CtrlKind k, std::vector<uint8_t> in, std::vector<uint8_t> out) {
+    Ctrl c;
+    c.kind = k;
+    c.height = uint32_t(st.size() - in.size());
+    c.cell_base = st.size() - in.size() < st.size() ? st[st.size() - in.size()].cell
+                                                    : top_cell();
+    if (in.empty()) c.cell_base = top_cell();
+    c.in = std::move(in);
+    c.out = std::move(out);
+    c.dead = c.unreachable = !ctrl.empty() && ctrl.back().unreachable;
+    ctrl.push_back(std::move(c));
+  }
+
+  const std::vector<uint8_t> &label_types(const Ctrl &c) const {
+    return c.kind == C_LOOP ? c.in : c.out;
+  }
+
+  // Move the top `n` stack values into the canonical cells starting at dst_base.
+  void move_top_to(size_t n, uint32_t dst_base) {
+    uint32_t dst = dst_base;
+    for (size_t k = st.size() - n; k < st.size(); k++) {
+      materialize_into(st[k], dst);
+      dst += cells_of(st[k].type);
+    }
+  }
+
+  bool top_in_place(size_t n, uint32_t dst_base) const {
+    uint32_t dst = dst_base;
+    for (size_t k = st.size() - n; k < st.size(); k++) {
+      if (st[k].kind != K_CELL || st[k].cell != dst) return false;
+      dst += cells_of(st[k].type);
+    }
+    return true;
+  }
+
+  void branch_fixup(Ctrl &f, bool brtab, uint32_t index, int32_t extra) {
+    if (f.label_known) {
+      int32_t t = f.label_tcnt + extra;
+      if (brtab) {
+        P.brtab[2 * index] = f.label_pc;
+        P.brtab[2 * index + 1] = uint32_t(t);
+      } else {
+        P.code[index].w3 = f.label_pc;
+        P.code[index].w2 = (P.code[index].w2 & 0xFFFF) | (uint32_t(uint16_t(int16_t(t))) << 16);
+      }
+    } else {
+      f.fixups.push_back(Fixup{brtab, index, extra});
+    }
+  }
+
+  void resolve_label(Ctrl &f, uint32_t pc, int32_t tcnt) {
+    f.label_known = true;
+    f.label_pc = pc;
+    f.label_tcnt = tcnt;
+    for (const Fixup &x : f.fixups) {
+      int32_t t = tcnt + x.extra;
+      if (t < -32768 || t > 32767) fail(E_UNSUPPORTED, "tcnt overflow");
+      if (x.brtab) {
+        P.brtab[2 * x.index] = pc;
+        P.brtab[2 * x.index + 1] = uint32_t(t);
+      } else {
+        P.code[x.index].w3 = pc;
+        P.code[x.index].w2 = (P.code[x.index].w2 & 0xFFFF) | (uint32_t(uint16_t(int16_t(t))) << 16);
+      }
+    }
+    f.fixups.clear();
+  }
+
+  void set_unreachable() {
+    Ctrl &f = ctrl.back();
+    st.resize(f.height);
+    f.unreachable = true;
+  }
+
+  // retarget the last producer of the top entry to write `dst`; true on success
+  bool try_retarget(const Entry &top, uint32_t dst) {
+    if (!can_retarget || top.kind != K_CELL || top.producer < 0 || top.producer != last_emit)
+      return false;
+    DInstr &I = P.code[last_emit];
+    if ((I.w2 & 0xFFFF) != top.cell) return false;
+    uint32_t cnt = (I.w0 >> 16) & 0xFF, post = I.w0 >> 24;
+    if (cnt + pending > 255 || post + pending > 255) return false;
+    I.w2 = (I.w2 & 0xFFFF0000u) | dst;
+    I.w0 = (I.w0 & 0xFFFF) | ((cnt + pending) << 16) | ((post + pending) << 24);
+    pending = 0;
+    return true;
+  }
+
+  void do_simple(const SimpleOp &s);
+  void do_load(uint16_t dop, uint8_t rtype, Reader &r);
+  void do_store(uint16_t dop, uint8_t vtype, Reader &r);
+  void do_call(uint32_t callee);
+};
+
+void Lowerer::do_simple(const SimpleOp &s) {
+  const char *colon = strchr(s.sig, ':');
+  int npop = int(colon - s.sig);
+  Entry ops[3];
+  for (int q = npop - 1; q >= 0; q--) ops[q] = pop_t(sigt(s.sig[q]));
+  uint8_t rt = colon[1] ? sigt(colon[1]) : 0;
+  if (!live()) {
+    if (rt) push_cell(rt);
+    return;
+  }
+  uint32_t c = top_cell();  // result lands where the first operand was
+  if (npop >= 1) c = ops[0].cell;
+  if (npop == 2 && s.dop_imm >= 0) {
+    int which = -1;
+    if (ops[1].kind == K_CONST) which = 1;
+    else if (s.commutative && ops[0].kind == K_CONST) which = 0;
+    if (which >= 0) {
+      bool fits = true;
+      uint32_t imm = ops[which].k[0];
+      if (ops[which].type == I64) {
+        int64_t v = int64_t(uint64_t(ops[which].k[0]) | (uint64_t(ops[which].k[1]) << 32));
+        fits = v >= INT32_MIN && v <= INT32_MAX;
+      }
+      if (fits) {
+        uint32_t a = src(ops[1 - which]);
+        emit(uint16_t(s.dop_imm), a, 0, c, 0, imm);
+        push_cell(rt, last_emit);
+        return;
+      }
+    }
+  }
+  uint32_t a = npop >= 1 ? src(ops[0]) : 0;
+  uint32_t b = npop >= 2 ? src(ops[1]) : 0;
+  uint32_t d = npop >= 3 ? src(ops[2]) : 0;
+  emit(s.dop, a, b, c, d);
+  if (rt) push_cell(rt, last_emit);
+}
+
+void Lowerer::do_load(uint16_t dop, uint8_t rtype, Reader &r) {
+  r.u32();
+  uint32_t off = r.u32();
+  if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
+  Entry a = pop_t(I32);
+  if (!live()) { push_cell(rtype); return; }
+  uint32_t ac = src(a);
+  emit(dop, ac, 0, a.cell, 0, off);
+  push_cell(rtype, last_emit);
+}
+
+void Lowerer::do_store(uint16_t dop, uint8_t vtype, Reader &r) {
+  r.u32();
+  uint32_t off = r.u32();
+  if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
+  Entry v = pop_t(vtype);
+  Entry a = pop_t(I32);
+  if (!live()) return;
+  uint32_t ac = src(a), vc = src(v);
+  emit(dop, ac, vc, 0, 0, off);
+}
+
+void Lowerer::do_call(uint32_t callee) {
+  if (callee >= P.funcs.size()) fail(E_TYPECHECK, "unknown function");
+  const FuncType &t = P.types[P.funcs[callee].type];
+  size_t np = t.params.size();
+  // type-check args
+  std::vector<Entry> args(np);
+  for (size_t k = np; k > 0; k--) args[k - 1] = pop_t(t.params[k - 1]);
+  if (!live()) {
+    for (uint8_t r : t.results) push_cell(r);
+    return;
+  }
+  for (auto &e : args) st.push_back(e);
+  materialize_top(np);
+  uint32_t argcells = 0;
+  for (auto &e : args) argcells += cells_of(e.type);
+  uint32_t L = top_cell() - argcells;
+  st.resize(st.size() - np);
+  if (P.funcs[callee].imported) {
+    emit(OP_UNREACHABLE, 0, 0, 0, 0, WB_ERR_HOST_CALL);
+  } else {
+    emit(OP_CALL, L, argcells, P.funcs[callee].local_cells, 0, 0);
+    callfix->push_back(CallFix{uint32_t(last_emit), callee});
+    emit(OP_POST_CALL, L);
+  }
+  for (uint8_t r : t.results) push_cell(r);
+  uint32_t hi = L + argcells;
+  if (hi > max_cell) max_cell = hi;
+}
+
+
+// ------------------------------------------------------------------ lower one function
+void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
+  callfix = &cf;
+  FuncInfo &F = P.funcs[fi];
+  ft = &P.types[F.type];
+  ltypes = ft->params;
+  ltypes.insert(ltypes.end(), F.local_types.begin(), F.local_types.end());
+  frame_base = P.global_cells;
+  lcell.clear();
+  uint32_t cc = frame_base;
+  for (uint8_t t : ltypes) { lcell.push_back(cc); cc += cells_of(t); }
+  F.param_cells = 0;
+  for (uint8_t t : ft->params) F.param_cells += cells_of(t);
+  F.local_cells = cc - frame_base - F.param_cells;
+  opnd_base = cc;
+  max_cell = cc;
+  st.clear();
+  ctrl.clear();
+  pending = 0;
+  last_emit = -1;
+  can_retarget = false;
+
+  F.entry_pc = uint32_t(P.code.size());
+  if (F.local_cells)   // prologue used by call_indirect / the kernel's first frame
+    P.code.push_back(DInstr{OP_ZERO_LOCALS, (frame_base + F.param_cells) | (F.local_cells << 16), 0, 0});
+  F.body_pc = uint32_t(P.code.size());
+  push_ctrl(C_FUNC, {}, ft->results);
+
+  Reader r{bin + F.code_off, bin + F.code_off + F.code_len};
+  const auto &simple = simple_ops();
+  while (!ctrl.empty()) {
+    uint16_t op = r.u8();
+    if (op == 0xFC || op == 0xFD) {
+      uint32_t sub = r.u32();
+      if (sub > 0xFF) fail(E_ILLEGAL_OPCODE, "illegal opcode");
+      op = uint16_t(op << 8 | sub);
+    }
+    if (op != 0x0B && op != 0x05 && op != 0x03) pending++;  // else/end/loop: at their labels
+    auto it = simple.find(op);
+    if (it != simple.end()) { do_simple(it->second); continue; }
+    switch (op) {
+      case 0x00:  // unreachable (engine.cpp:79-83)
+        if (live()) emit(OP_UNREACHABLE, 0, 0, 0, 0, 0x89);
+        set_unreachable();
+        break;
+      case 0x01: break;  // nop: counted, folded
+      case 0x02: case 0x03: case 0x04: {
+        std::vector<uint8_t> in, out;
+        block_type(r, in, out);
+        Entry cond{};
+        if (op == 0x04) cond = pop_t(I32);
+        std::vector<Entry> ps(in.size());
+        for (size_t k = in.size(); k > 0; k--) ps[k - 1] = pop_t(in[k - 1]);
+        for (auto &e : ps) st.push_back(e);
+        if (live()) {           // locals may change inside: no lazy local refs across
+          materialize_locals();
+          materialize_top(in.size());
+        }
+        if (op == 0x02) {
+          push_ctrl(C_BLOCK, in, out);
+        } else if (op == 0x03) {
+          // br to a loop lands on (and re-counts) the `loop` instruction
+          place_label();
+          int32_t tcnt = -int32_t(pending);
+          uint32_t lpc = uint32_t(P.code.size());
+          pending++;
+          push_ctrl(C_LOOP, in, out);
+          if (!ctrl.back().dead) resolve_label(ctrl.back(), lpc, tcnt);
+        } else {
+          int64_t br = -1;
+          if (live()) {
+            uint32_t c;
+            if (cond.kind == K_LOCAL) c = lcell[cond.local];
+            else {
+              if (cond.kind == K_CONST) materialize_into(cond, cond.cell);
+              c = cond.cell;
+            }
+            emit(OP_BR_UNLESS, c, 0, 0, 0, 0);
+            br = last_emit;
+          }
+          push_ctrl(C_IF, in, out);
+          ctrl.back().else_br = br;
+        }
+        break;
+      }
+      case 0x05: {  // else (controlInstr.cpp:11-34, engine.cpp:92-110)
+        Ctrl &f = ctrl.back();
+        if (f.kind != C_IF || f.has_else) fail(E_ILLEGAL_OPCODE, "else outside if");
+        if (!f.unreachable) {
+          std::vector<Entry> vals(f.out.size());
+          for (size_t k = f.out.size(); k > 0; k--) vals[k - 1] = pop_t(f.out[k - 1]);
+          if (st.size() != f.height) fail(E_TYPECHECK, "type mismatch at else");
+          for (auto &e : vals) st.push_back(e);
+          move_top_to(f.out.size(), f.cell_base);
+          pending++;                        // the `else` dispatch on the then-path
+          emit(OP_JMP);
+          branch_fixup(f, false, uint32_t(last_emit), -1);  // end is not re-counted
+        } else {
+          pending = 0;
+        }
+        st.resize(f.height);
+        for (uint8_t t : f.in) push_cell(t);
+        f.unreachable = f.dead;
+        place_label();
+        if (f.else_br >= 0) {               // if-false path: counts `else` manually (+1)
+          P.code[f.else_br].w3 = uint32_t(P.code.size());
+          P.code[f.else_br].w2 = (P.code[f.else_br].w2 & 0xFFFF) | (1u << 16);
+          f.else_br = -1;
+        }
+        f.has_else = true;
+        break;
+      }
+      case 0x0B: {  // end
+        Ctrl &f = ctrl.back();
+        if (!f.unreachable) {
+          std::vector<Entry> vals(f.out.size());
+          for (size_t k = f.out.size(); k > 0; k--) vals[k - 1] = pop_t(f.out[k - 1]);
+          if (st.size() != f.height) fail(E_TYPECHECK, "type mismatch at end");
+          for (auto &e : vals) st.push_back(e);
+          move_top_to(f.out.size(), f.cell_base);
+        } else {
+          pending = 0;
+        }
+        if (f.kind == C_IF && !f.has_else) {
+          if (f.in != f.out) fail(E_TYPECHECK, "if without else must not change the stack");
+          if (f.else_br >= 0) branch_fixup(f, false, uint32_t(f.else_br), 0);
+        }
+        place_label();
+        int32_t tcnt = -int32_t(pending);
+        uint32_t lpc = uint32_t(P.code.size());
+        pending++;                          // the `end` itself
+        if (f.kind != C_LOOP && !f.dead) resolve_label(f, lpc, tcnt);
+        if (f.kind == C_FUNC) {
+          uint32_t rc = 0;
+          for (uint8_t t : f.out) rc += cells_of(t);
+          emit(OP_RET, opnd_base, rc);
+          ctrl.pop_back();
+          break;
+        }
+        Ctrl done = std::move(ctrl.back());
+        ctrl.pop_back();
+        st.resize(done.height);
+        for (uint8_t t : done.out) push_cell(t);
+        break;
+      }
+      case 0x0C: case 0x0D: {  // br / br_if (controlInstr.cpp:36-51, helper.cpp:179-193)
+        uint32_t depth = r.u32();
+        if (depth >= ctrl.size()) fail(E_TYPECHECK, "unknown label");
+        Entry cond{};
+        if (op == 0x0D) cond = pop_t(I32);
+        Ctrl &f = ctrl[ctrl.size() - 1 - depth];
+        const std::vector<uint8_t> lt = label_types(f);
+        std::vector<Entry> vals(lt.size());
+        for (size_t k = lt.size(); k > 0; k--) vals[k - 1] = pop_t(lt[k - 1]);
+        for (auto &e : vals) st.push_back(e);
+        if (!live()) { if (op == 0x0C) set_unreachable(); break; }
+        size_t n = lt.size();
+        if (op == 0x0C) {
+          move_top_to(n, f.cell_base);
+          emit(OP_JMP);
+          branch_fixup(f, false, uint32_t(last_emit), 0);
+          set_unreachable();
+          break;
+        }
+        uint32_t c;
+        if (cond.kind == K_LOCAL) c = lcell[cond.local];
+        else {
+          if (cond.kind == K_CONST) materialize_into(cond, cond.cell);
+          c = cond.cell;
+        }
+        if (n == 0 || top_in_place(n, f.cell_base)) {
+          emit(OP_BR_IF, c);
+          branch_fixup(f, false, uint32_t(last_emit), 0);
+        } else if (n == 1 && cells_of(st.back().type) <= 2) {
+          Entry &e = st.back();
+          if (e.kind == K_CONST) materialize(st.size() - 1);
+          uint32_t s = e.kind == K_LOCAL ? lcell[e.local] : e.cell;
+          emit(cells_of(e.type) == 1 ? OP_BR_IF_MOV1 : OP_BR_IF_MOV2, c, s, f.cell_base);
+          branch_fixup(f, false, uint32_t(last_emit), 0);
+        } else {
+          emit(OP_BR_UNLESS, c);
+          uint32_t skip = uint32_t(last_emit);
+          move_top_to(n, f.cell_base);
+          emit(OP_JMP);
+          branch_fixup(f, false, uint32_t(last_emit), 0);
+          place_label();
+          P.code[skip].w3 = uint32_t(P.code.size());
+        }
+        break;
+      }
+      case 0x0E: {  // br_table (controlInstr.cpp:53-70)
+        uint32_t n = r.u32();
+        std::vector<uint32_t> depths(n + 1);
+        for (uint32_t k = 0; k <= n; k++) {
+          depths[k] = r.u32();
+          if (depths[k] >= ctrl.size()) fail(E_TYPECHECK, "unknown label");
+        }
+        Entry idx = pop_t(I32);
+        const std::vector<uint8_t> lt = label_types(ctrl[ctrl.size() - 1 - depths[n]]);
+        for (uint32_t k = 0; k < n; k++)
+          if (label_types(ctrl[ctrl.size() - 1 - depths[k]]).size() != lt.size())
+            fail(E_TYPECHECK, "br_table arity mismatch");
+        std::vector<Entry> vals(lt.size());
+        for (size_t k = lt.size(); k > 0; k--) vals[k - 1] = pop_t(lt[k - 1]);
+        for (auto &e : vals) st.push_back(e);
+        if (live()) {
+          uint32_t ic = src(idx);
+          uint32_t base = uint32_t(P.brtab.size() / 2);
+          P.brtab.resize(P.brtab.size() + 2 * (n + 1), 0);
+          emit(OP_BR_TABLE, ic, n, 0, 0, base);
+          for (uint32_t k = 0; k <= n; k++) {
+            Ctrl &f = ctrl[ctrl.size() - 1 - depths[k]];
+            if (lt.empty() || top_in_place(lt.size(), f.cell_base)) {
+              branch_fixup(f, true, base + k, 0);
+            } else {                       // trampoline: move values, jump
+              place_label();
+              P.brtab[2 * (base + k)] = uint32_t(P.code.size());
+              P.brtab[2 * (base + k) + 1] = 0;
+              move_top_to(lt.size(), f.cell_base);
+              emit(OP_JMP);
+              branch_fixup(f, false, uint32_t(last_emit), 0);
+            }
+          }
+        }
+        set_unreachable();
+        break;
+      }
+      case 0x0F: {  // return (controlInstr.cpp:72-81): the function `end` is not counted
+        std::vector<Entry> vals(ft->results.size());
+        for (size_t k = ft->results.size(); k > 0; k--) vals[k - 1] = pop_t(ft->results[k - 1]);
+        if (live()) {
+          for (auto &e : vals) st.push_back(e);
+          materialize_top(vals.size());
+          uint32_t rc = 0;
+          for (auto &e : vals) rc += cells_of(e.type);
+          emit(OP_RET, top_cell() - rc, rc);
+        }
+        set_unreachable();
+        break;
+      }
+      case 0x10: do_call(r.u32()); break;
+      case 0x11: {  // call_indirect (controlInstr.cpp:101-158)
+        uint32_t ti = r.u32();
+        uint32_t tab = r.u32();
+        if (ti >= P.types.size() || tab >= P.ntables) fail(E_TYPECHECK, "unknown type/table");
+        Entry idx = pop_t(I32);
+        const FuncType &t = P.types[ti];
+        std::vector<Entry> args(t.params.size());
+        for (size_t k = args.size(); k > 0; k--) args[k - 1] = pop_t(t.params[k - 1]);
+        if (live()) {
+          for (auto &e : args) st.push_back(e);
+          materialize_top(args.size());
+          uint32_t argcells = 0;
+          for (auto &e : args) argcells += cells_of(e.type);
+          uint32_t L = top_cell() - argcells;
+          uint32_t ic = src(idx);
+          if (ic + 1 > max_cell) max_cell = ic + 1;
+          st.resize(st.size() - args.size());
+          emit(OP_CALL_INDIRECT, L, argcells, ic, tab, P.type_canon[ti]);
+          emit(OP_POST_CALL, L);
+        }
+        for (uint8_t rt : t.results) push_cell(rt);
+        break;
+      }
+      case 0x1A: pop_any(); break;  // drop
+      case 0x1B: case 0x1C: {       // select (engine.cpp:152-166)
+        uint8_t want = UNKNOWN;
+        if (op == 0x1C) {
+          uint32_t n = r.u32();
+          if (n != 1) fail(E_TYPECHECK, "invalid result arity");
+          want = r.u8();
+        }
+        Entry cnd = pop_t(I32);
+        Entry v2 = pop_t(want), v1 = pop_t(want);
+        if (v1.type != v2.type && v1.type != UNKNOWN && v2.type != UNKNOWN)
+          fail(E_TYPECHECK, "type mismatch");
+        uint8_t t = v1.type != UNKNOWN ? v1.type : v2.type;
+        if (!live()) { push_cell(t == UNKNOWN ? I32 : t); break; }
+        uint32_t w = cells_of(t);
+        uint32_t a = src(v1), b = src(v2), d = src(cnd);
+        emit(w == 1 ? OP_SELECT32 : w == 2 ? OP_SELECT64 : OP_SELECT128, a, b, v1.cell, d);
+        push_cell(t, last_emit);
+        break;
+      }
+      case 0x20: {  // local.get (variableInstr.cpp:11-15): a lazy reference
+        uint32_t li = r.u32();
+        if (li >= ltypes.size()) fail(E_TYPECHECK, "unknown local");
+        push_local(li);
+        break;
+      }
+      case 0x21: case 0x22: {  // local.set / local.tee (variableInstr.cpp:17-30)
+        uint32_t li = r.u32();
+        if (li >= ltypes.size()) fail(E_TYPECHECK, "unknown local");
+        Entry v = pop_t(ltypes[li]);
+        if (!live()) { if (op == 0x22) push_cell(ltypes[li]); break; }
+        if (v.kind == K_LOCAL && v.local == li) { if (op == 0x22) st.push_back(v); break; }
+        materialize_locals(li);
+        if (try_retarget(v, lcell[li])) {
+          if (op == 0x22) push_local(li);
+        } else {
+          materialize_into(v, lcell[li]);
+          if (op == 0x22) st.push_back(v);
+        }
+        break;
+      }
+      case 0x23: case 0x24: {  // global.get / global.set (variableInstr.cpp:32-44)
+        uint32_t gi = r.u32();
+        if (gi >= P.global_types.size()) fail(E_TYPECHECK, "unknown global");
+        uint8_t t = P.global_types[gi];
+        uint32_t w = cells_of(t);
+        if (op == 0x23) {
+          if (live()) {
+            uint32_t dst = top_cell();
+            emit(w == 1 ? OP_MOV32 : w == 2 ? OP_MOV64 : OP_MOV128, P.global_cell[gi], 0, dst);
+            push_cell(t, last_emit);
+          } else push_cell(t);
+        } else {
+          if (!P.global_mut[gi]) fail(E_TYPECHECK, "global is immutable");
+          Entry v = pop_t(t);
+          if (!live()) break;
+          if (!try_retarget(v, P.global_cell[gi])) materialize_into(v, P.global_cell[gi]);
+        }
+        break;
+      }
+      case 0x25: {  // table.get (immutable funcref table)
+        uint32_t tab = r.u32();
+        if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        Entry idx = pop_t(I32);
+        if (!live()) { push_cell(FUNCREF); break; }
+        uint32_t ic = src(idx);
+        emit(OP_TABLE_GET, ic, 0, idx.cell, tab);
+        push_cell(FUNCREF, last_emit);
+        break;
+      }
+      // ---- memory (memory.ipp:12-68)
+      case 0x28: do_load(OP_LD32, I32, r); break;
+      case 0x29: do_load(OP_LD64, I64, r); break;
+      case 0x2A: do_load(OP_LD32, F32, r); break;
+      case 0x2B: do_load(OP_LD64, F64, r); break;
+      case 0x2C: do_load(OP_LD8S32, I32, r); break;
+      case 0x2D: do_load(OP_LD8U32, I32, r); break;
+      case 0x2E: do_load(OP_LD16S32, I32, r); break;
+      case 0x2F: do_load(OP_LD16U32, I32, r); break;
+      case 0x30: do_load(OP_LD8S64, I64, r); break;
+      case 0x31: do_load(OP_LD8U64, I64, r); break;
+      case 0x32: do_load(OP_LD16S64, I64, r); break;
+      case 0x33: do_load(OP_LD16U64, I64, r); break;
+      case 0x34: do_load(OP_LD32S64, I64, r); break;
+      case 0x35: do_load(OP_LD32U64, I64, r); break;
+      case 0x36: do_store(OP_ST32, I32, r); break;
+      case 0x37: do_store(OP_ST64, I64, r); break;
+      case 0x38: do_store(OP_ST32, F32, r); break;
+      case 0x39: do_store(OP_ST64, F64, r); break;
+      case 0x3A: do_store(OP_ST8, I32, r); break;
+      case 0x3B: do_store(OP_ST16, I32, r); break;
+      case 0x3C: do_store(OP_ST8, I64, r); break;
+      case 0x3D: do_store(OP_ST16, I64, r); break;
+      case 0x3E: do_store(OP_ST32, I64, r); break;
+      case 0x3F: {  // memory.size (memoryInstr.cpp:9-15)
+        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        if (live()) { emit(OP_MEM_SIZE, 0, 0, top_cell()); push_cell(I32, last_emit); }
+        else push_cell(I32);
+        break;
+      }
+      case 0x40: {  // memory.grow (memoryInstr.cpp:17-31)
+        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        Entry n = pop_t(I32);
+        if (!live()) { push_cell(I32); break; }
+        uint32_t a = src(n);
+        emit(OP_MEM_GROW, a, 0, n.cell);
+        push_cell(I32, last_emit);
+        break;
+      }
+      case 0x41: { uint32_t k[4] = {uint32_t(int32_t(r.sleb(32))), 0, 0, 0}; push_const(I32, k); break; }
+      case 0x42: { uint64_t v = uint64_t(r.sleb(64)); uint32_t k[4] = {uint32_t(v), uint32_t(v >> 32), 0, 0}; push_const(I64, k); break; }
+      case 0x43: { uint32_t k[4] = {0, 0, 0, 0}; for (int q = 0; q < 4; q++) k[0] |= uint32_t(r.u8()) << (8 * q); push_const(F32, k); break; }
+      case 0x44: { uint64_t v = 0; for (int q = 0; q < 8; q++) v |= uint64_t(r.u8()) << (8 * q);
+                   uint32_t k[4] = {uint32_t(v), uint32_t(v >> 32), 0, 0}; push_const(F64, k); break; }
+      case 0xA7: {  // i32.wrap_i64: the low cell of an i64 slot already is the i32
+        Entry v = pop_t(I64);
+        if (!live()) { push_cell(I32); break; }
+        if (v.kind == K_CONST) { uint32_t k[4] = {v.k[0], 0, 0, 0}; push_const(I32, k); }
+        else if (v.kind == K_LOCAL) { emit(OP_MOV32, lcell[v.local], 0, v.cell); push_cell(I32, last_emit); }
+        else push_cell(I32);
+        break;
+      }
+      case 0xBC: case 0xBD: case 0xBE: case 0xBF: {  // reinterpret: same bits, retype
+        static const uint8_t from[] = {F32, F64, I32, I64}, to[] = {I32, I64, F32, F64};
+        Entry v = pop_t(from[op - 0xBC]);
+        v.type = to[op - 0xBC];
+        if (v.kind == K_LOCAL) {  // keep lazily, but the entry's type differs from the local's
+          if (live()) { emit(cells_of(v.type) == 1 ? OP_MOV32 : OP_MOV64, lcell[v.local], 0, v.cell); }
+          v.kind = K_CELL;
+          v.producer = live() ? last_emit : -1;
+        }
+        st.push_back(v);
+        break;
+      }
+      case 0xD0: { uint8_t t = r.u8(); uint32_t k[4] = {0xFFFFFFFFu, 0, 0, 0}; push_const(t, k); break; }
+      case 0xD1: {  // ref.is_null
+        Entry v = pop_any();
+        if (v.type != FUNCREF && v.type != EXTERNREF && v.type != UNKNOWN) fail(E_TYPECHECK, "type mismatch");
+        if (!live()) { push_cell(I32); break; }
+        uint32_t a = src(v);
+        emit(OP_I32_EQ_I, a, 0, v.cell, 0, 0xFFFFFFFFu);
+        push_cell(I32, last_emit);
+        break;
+      }
+      case 0xD2: { uint32_t f = r.u32(); if (f >= P.funcs.size()) fail(E_TYPECHECK, "unknown function");
+                   uint32_t k[4] = {f, 0, 0, 0}; push_const(FUNCREF, k); break; }
+      case 0xFC08: {  // memory.init (memoryInstr.cpp:33-49)
+        uint32_t di = r.u32();
+        if (r.u8() != 0 || !P.has_mem || di >= P.datas.size()) fail(E_TYPECHECK, "unknown data");
+        Entry n = pop_t(I32), s = pop_t(I32), d = pop_t(I32);
+        if (!live()) break;
+        uint32_t dc = src(d), sc = src(s), nc = src(n);
+        emit(OP_MEM_INIT, dc, sc, nc, 0, di);
+        break;
+      }
+      case 0xFC09: {
+        uint32_t di = r.u32();
+        if (di >= P.datas.size()) fail(E_TYPECHECK, "unknown data");
+        if (di >= 32) fail(E_UNSUPPORTED, "more than 32 data segments");
+        if (live()) emit(OP_DATA_DROP, 0, 0, 0, 0, di);
+        break;
+      }
+      case 0xFC0A: case 0xFC0B: {  // memory.copy / memory.fill (memoryInstr.cpp:59-101)
+        if (op == 0xFC0A) { r.u8(); }
+        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        Entry n = pop_t(I32), s = pop_t(I32), d = pop_t(I32);
+        if (!live()) break;
+        uint32_t dc = src(d), sc = src(s), nc = src(n);
+        emit(op == 0xFC0A ? OP_MEM_COPY : OP_MEM_FILL, dc, sc, nc);
+        break;
+      }
+      case 0xFC10: {  // table.size of an immutable table is a constant
+        uint32_t tab = r.u32();
+        if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        uint32_t k[4] = {uint32_t(P.table0.size()), 0, 0, 0};
+        push_const(I32, k);
+        break;
+      }
+      // ---- SIMD memory
+      case 0xFD00: do_load(OP_LD128, V128, r); break;
+      case 0xFD01: do_load(OP_V_LD8X8S, V128, r); break;
+      case 0xFD02: do_load(OP_V_LD8X8U, V128, r); break;
+      case 0xFD03: do_load(OP_V_LD16X4S, V128, r); break;
+      case 0xFD04: do_load(OP_V_LD16X4U, V128, r); break;
+      case 0xFD05: do_load(OP_V_LD32X2S, V128, r); break;
+      case 0xFD06: do_load(OP_V_LD32X2U, V128, r); break;
+      case 0xFD07: do_load(OP_V_LD8SPLAT, V128, r); break;
+      case 0xFD08: do_load(OP_V_LD16SPLAT, V128, r); break;
+      case 0xFD09: do_load(OP_V_LD32SPLAT, V128, r); break;
+      case 0xFD0A: do_load(OP_V_LD64SPLAT, V128, r); break;
+      case 0xFD5C: do_load(OP_V_LD32ZERO, V128, r); break;
+      case 0xFD5D: do_load(OP_V_LD64ZERO, V128, r); break;
+      case 0xFD0B: do_store(OP_ST128, V128, r); break;
+      case 0xFD0C: {
+        uint32_t k[4];
+        for (int q = 0; q < 4; q++) {
+          k[q] = 0;
+          for (int b = 0; b < 4; b++) k[q] |= uint32_t(r.u8()) << (8 * b);
+        }
+        push_const(V128, k);
+        break;
+      }
+      case 0xFD0D: {  // i8x16.shuffle: mask in the v128 pool
+        uint32_t k[4];
+        for (int q = 0; q < 4; q++) {
+          k[q] = 0;
+          for (int b = 0; b < 4; b++) {
+            uint8_t lane = r.u8();
+            if (lane >= 32) fail(E_TYPECHECK, "invalid lane index");
+            k[q] |= uint32_t(lane) << (8 * b);
+          }
+        }
+        Entry y = pop_t(V128), x = pop_t(V128);
+        if (!live()) { push_cell(V128); break; }
+        uint32_t idx = uint32_t(P.vconst.size() / 4);
+        P.vconst.insert(P.vconst.end(), k, k + 4);
+        uint32_t a = src(x), b = src(y);
+        emit(OP_V_SHUFFLE, a, b, x.cell, 0, idx);
+        push_cell(V128, last_emit);
+        break;
+      }
+      case 0xFD15: case 0xFD16: case 0xFD18: case 0xFD19: case 0xFD1B: case 0xFD1D:
+      case 0xFD1F: case 0xFD21: {  // extract_lane
+        uint8_t lane = r.u8();
+        static const std::map<uint16_t, std::pair<uint16_t, uint8_t>> m = {
+            {0xFD15, {OP_V_EXTRACT8S, I32}}, {0xFD16, {OP_V_EXTRACT8U, I32}},
+            {0xFD18, {OP_V_EXTRACT16S, I32}}, {0xFD19, {OP_V_EXTRACT16U, I32}},
+            {0xFD1B, {OP_V_EXTRACT32, I32}}, {0xFD1D, {OP_V_EXTRACT64, I64}},
+            {0xFD1F, {OP_V_EXTRACT32, F32}}, {0xFD21, {OP_V_EXTRACT64, F64}}};
+        auto e = m.at(op);
+        uint32_t lanes = e.first == OP_V_EXTRACT8S || e.first == OP_V_EXTRACT8U ? 16
+                         : e.first == OP_V_EXTRACT16S || e.first == OP_V_EXTRACT16U ? 8
+                         : e.first == OP_V_EXTRACT32 ? 4 : 2;
+        if (lane >= lanes) fail(E_TYPECHECK, "invalid lane index");
+        Entry v = pop_t(V128);
+        if (!live()) { push_cell(e.second); break; }
+        uint32_t a = src(v);
+        emit(e.first, a, 0, v.cell, lane);
+        push_cell(e.second, last_emit);
+        break;
+      }
+      case 0xFD17: case 0xFD1A: case 0xFD1C: case 0xFD1E: case 0xFD20: case 0xFD22: {
+        uint8_t lane = r.u8();
+        static const std::map<uint16_t, std::pair<uint16_t, uint8_t>> m = {
+            {0xFD17, {OP_V_REPLACE8, I32}}, {0xFD1A, {OP_V_REPLACE16, I32}},
+            {0xFD1C, {OP_V_REPLACE32, I32}}, {0xFD1E, {OP_V_REPLACE64, I64}},
+            {0xFD20, {OP_V_REPLACE32, F32}}, {0xFD22, {OP_V_REPLACE64, F64}}};
+        auto e = m.at(op);
+        uint32_t lanes = e.first == OP_V_REPLACE8 ? 16 : e.first == OP_V_REPLACE16 ? 8
+                         : e.first == OP_V_REPLACE32 ? 4 : 2;
+        if (lane >= lanes) fail(E_TYPECHECK, "invalid lane index");
+        Entry s = pop_t(e.second), v = pop_t(V128);
+        if (!live()) { push_cell(V128); break; }
+        uint32_t a = src(v), b = src(s);
+        emit(e.first, a, b, v.cell, lane);
+        push_cell(V128, last_emit);
+        break;
+      }
+      default: {
+        char buf[96];
+        snprintf(buf, sizeof buf, "opcode 0x%X not supported by the batched path", op);
+        fail(E_UNSUPPORTED, buf);
+      }
+    }
+  }
+  if (r.p != r.end) fail(E_MALFORMED, "junk after function end");
+  F.frame_cells = max_cell - frame_base;
+  if (F.frame_cells > P.frame_cells) P.frame_cells = F.frame_cells;
+}
+
+// ------------------------------------------------------------------ module parsing
+struct ConstVal {
+  uint8_t type;
+  uint32_t k[4];
+};
+
+ConstVal eval_const(Reader &r, const Program &P, const std::vector<ConstVal> &globals) {
+  ConstVal v{UNKNOWN, {0, 0, 0, 0}};
+  for (;;) {
+    uint8_t op = r.u8();
+    if (op == 0x0B) break;
+    switch (op) {
+      case 0x41: v.type = I32; v.k[0] = uint32_t(int32_t(r.sleb(32))); break;
+      case 0x42: { uint64_t x = uint64_t(r.sleb(64)); v.type = I64; v.k[0] = uint32_t(x); v.k[1] = uint32_t(x >> 32); break; }
+      case 0x43: v.type = F32; for (int q = 0; q < 4; q++) v.k[0] |= uint32_t(r.u8()) << (8 * q); break;
+      case 0x44: { uint64_t x = 0; for (int q = 0; q < 8; q++) x |= uint64_t(r.u8()) << (8 * q);
+                   v.type = F64; v.k[0] = uint32_t(x); v.k[1] = uint32_t(x >> 32); break; }
+      case 0xD0: v.type = r.u8(); v.k[0] = 0xFFFFFFFFu; break;
+      case 0xD2: v.type = FUNCREF; v.k[0] = r.u32(); break;
+      case 0x23: { uint32_t g = r.u32(); if (g >= globals.size()) throw Err{E_TYPECHECK, "unknown global"}; v = globals[g]; break; }
+      case 0xFD: {
+        if (r.u32() != 0x0C) throw Err{E_TYPECHECK, "constant expression required"};
+        v.type = V128;
+        for (int q = 0; q < 4; q++) for (int b = 0; b < 4; b++) v.k[q] |= uint32_t(r.u8()) << (8 * b);
+        break;
+      }
+      default: throw Err{E_TYPECHECK, "constant expression required"};
+    }
+  }
+  (void)P;
+  return v;
+}
+
+void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
+  if (len < 8 || memcmp(wasm, "\0asm\1\0\0\0", 8)) throw Err{0x23, "magic header not detected"};
+  Reader r{wasm + 8, wasm + len};
+  std::vector<uint32_t> decl_types;
+  std::vector<ConstVal> gvals;
+  struct ElemSeg { bool active; uint32_t table, offset; std::vector<uint32_t> funcs; };
+  std::vector<ElemSeg> elems;
+  std::vector<uint32_t> table_min;
+  uint32_t ncode = 0;
+  while (r.p < r.end) {
+    uint8_t sid = r.u8();
+    uint32_t slen = r.u32();
+    if (uint64_t(r.end - r.p) < slen) throw Err{E_MALFORMED, "section size mismatch"};
+    Reader s{r.p, r.p + slen};
+    switch (sid) {
+      case 0: break;
+      case 1: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          if (s.u8() != 0x60) throw Err{E_MALFORMED, "malformed function type"};
+          FuncType t;
+          uint32_t np = s.u32();
+          for (uint32_t q = 0; q < np; q++) t.params.push_back(s.u8());
+          uint32_t nr = s.u32();
+          for (uint32_t q = 0; q < nr; q++) t.results.push_back(s.u8());
+          P.types.push_back(t);
+        }
+        break;
+      }
+      case 2: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          std::string mod = s.name(), nm = s.name();
+          uint8_t kind = s.u8();
+          if (kind != 0) throw Err{E_UNSUPPORTED, "only function imports are supported"};
+          FuncInfo f;
+          f.type = s.u32();
+          if (f.type >= P.types.size()) throw Err{E_TYPECHECK, "unknown type"};
+          f.imported = true;
+          f.import_module = mod;
+          f.import_name = nm;
+          P.funcs.push_back(f);
+          P.n_imported++;
+        }
+        break;
+      }
+      case 3: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          uint32_t t = s.u32();
+          if (t >= P.types.size()) throw Err{E_TYPECHECK, "unknown type"};
+          decl_types.push_back(t);
+        }
+        break;
+      }
+      case 4: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          uint8_t rt = s.u8();
+          uint8_t fl = s.u8();
+          uint32_t mn = s.u32();
+          if (fl & 1) s.u32();
+          if (rt != FUNCREF) throw Err{E_UNSUPPORTED, "externref tables not supported"};
+          table_min.push_back(mn);
+        }
+        P.ntables = n;
+        break;
+      }
+      case 5: {
+        uint32_t n = s.u32();
+        if (n > 1) throw Err{0x51, "multiple memories"};
+        if (n) {
+          uint8_t fl = s.u8();
+          P.has_mem = true;
+          P.mem_min = s.u32();
+          if (fl & 1) { P.mem_has_max = true; P.mem_max = s.u32(); }
+          if (P.mem_min > 65536 || (P.mem_has_max && P.mem_max > 65536))
+            throw Err{0x53, "memory size must be at most 65536 pages (4GiB)"};
+        }
+        break;
+      }
+      case 6: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          uint8_t t = s.u8();
+          uint8_t mut = s.u8();
+          ConstVal v = eval_const(s, P, gvals);
+          if (v.type != t) throw Err{E_TYPECHECK, "type mismatch in global init"};
+          gvals.push_back(v);
+          P.global_types.push_back(t);
+          P.global_mut.push_back(mut);
+        }
+        break;
+      }
+      case 7: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          std::string nm = s.name();
+          uint8_t kind = s.u8();
+          uint32_t idx = s.u32();
+          if (kind == 0) P.exports.push_back(ExportFunc{nm, idx});
+        }
+        break;
+      }
+      case 8: P.start_func = s.u32(); break;
+      case 9: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          uint32_t flags = s.u32();
+          ElemSeg e{!(flags & 1), 0, 0, {}};
+          if (!(flags & 1)) {
+            if (flags & 2) e.table = s.u32();
+            ConstVal off = eval_const(s, P, gvals);
+            e.offset = off.k[0];
+          }
+          if (flags & 3) s.u8();
+          uint32_t m = s.u32();
+          for (uint32_t q = 0; q < m; q++) {
+            if (flags & 4) e.funcs.push_back(eval_const(s, P, gvals).k[0]);
+            else e.funcs.push_back(s.u32());
+          }
+          elems.push_back(e);
+        }
+        break;
+      }
+      case 10: {
+        ncode = s.u32();
+        if (ncode != decl_types.size())
+          throw Err{0x29, "function and code section have inconsistent lengths"};
+        for (uint32_t k = 0; k < ncode; k++) {
+          uint32_t blen = s.u32();
+          const uint8_t *bend = s.p + blen;
+          FuncInfo f;
+          f.type = decl_types[k];
+          uint32_t ng = s.u32();
+          uint64_t total = 0;
+          for (uint32_t g = 0; g < ng; g++) {
+            uint32_t c = s.u32();
+            uint8_t t = s.u8();
+            total += c;
+            if (total > 50000) throw Err{0x30, "too many locals"};
+            f.local_types.insert(f.local_types.end(), c, t);
+          }
+          f.code_off = uint32_t(s.p - wasm);
+          f.code_len = uint32_t(bend - s.p);
+          s.p = bend;
+          P.funcs.push_back(f);
+        }
+        break;
+      }
+      case 11: {
+        uint32_t n = s.u32();
+        for (uint32_t k = 0; k < n; k++) {
+          uint32_t flags = s.u32();
+          DataSeg d;
+          d.active = !(flags & 1);
+          if (flags == 2) s.u32();
+          if (d.active) d.offset = eval_const(s, P, gvals).k[0];
+          uint32_t m = s.u32();
+          if (uint64_t(s.end - s.p) < m) throw Err{E_MALFORMED, "length out of bounds"};
+          d.bytes.assign(s.p, s.p + m);
+          s.p += m;
+          P.datas.push_back(d);
+        }
+        break;
+      }
+      case 12: s.u32(); break;
+      default: throw Err{0x25, "malformed section id"};
+    }
+    r.p += slen;
+  }
+  if (decl_types.size() != ncode) throw Err{0x29, "function and code section have inconsistent lengths"};
+  // canonical structural type ids (call_indirect compares FunctionTypes by value)
+  for (size_t k = 0; k < P.types.size(); k++) {
+    uint32_t id = uint32_t(k);
+    for (size_t q = 0; q < k; q++)
+      if (P.types[q] == P.types[k]) { id = P.type_canon[q]; break; }
+    P.type_canon.push_back(id);
+  }
+  // globals -> cells [0, G)
+  uint32_t gc = 0;
+  for (size_t k = 0; k < gvals.size(); k++) {
+    P.global_cell.push_back(gc);
+    uint32_t w = cells_of(gvals[k].type);
+    for (uint32_t q = 0; q < w; q++) P.global_init.push_back(gvals[k].k[q]);
+    gc += w;
+  }
+  P.global_cells = gc;
+  // table 0 image from active element segments (elem.cpp), immutable in this path
+  if (P.ntables > 1) throw Err{E_UNSUPPORTED, "multiple tables"};
+  if (P.ntables) {
+    P.table0.assign(table_min[0], 0xFFFFFFFFu);
+    for (auto &e : elems) {
+      if (!e.active) continue;
+      if (uint64_t(e.offset) + e.funcs.size() > P.table0.size())
+        throw Err{0x64, "elements segment does not fit"};
+      for (size_t q = 0; q < e.funcs.size(); q++) P.table0[e.offset + q] = e.funcs[q];
+    }
+  }
+  for (auto &d : P.datas)
+    if (d.active && uint64_t(d.offset) + d.bytes.size() > uint64_t(P.mem_min) * 65536)
+      throw Err{0x63, "data segment does not fit"};
+  if (P.start_func >= 0) throw Err{E_UNSUPPORTED, "start function not supported by the batched path"};
+  // lower
+  Lowerer L(P, wasm);
+  std::vector<CallFix> callfix;
+  for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
+  for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
+  if (P.code.size() >= DBC_MAX_PC) throw Err{E_UNSUPPORTED, "module too large for 20-bit pcs"};
+}
+
+}  // namespace
+
+std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode) {
+  try {
+    out = Program();
+    parse_and_lower(wasm, len, out);
+    *errcode = 0;
+    return "";
+  } catch (const Err &e) {
+    *errcode = e.code;
+    return e.msg;
+  }
+}
+
+int find_export(const Program &p, const std::string &name) {
+  for (auto &e : p.exports)
+    if (e.name == name) return int(e.func);
+  return -1;
+}
+
+const char *dop_name(uint16_t op) {
+  static const char *names[] = {
+#define DBC_NAME(n) #n,
+      DBC_OPS(DBC_NAME)
+#undef DBC_NAME
+  };
+  return op < OP_DBC_NUM_OPS ? names[op] : "?";
+}
+
+}  // namespace wb

@@ -1,0 +1,85 @@
+// frontend.h -- host-side module decoder, validator and DBC lowering.
+//
+// Replaces, for the batched path, what the reference does in
+//   lib/loader/loader.cpp:64-163 + lib/loader/ast/*.cpp   (decode, JumpEnd/JumpElse)
+//   lib/validator/validator.cpp:19-117 + formchecker.cpp   (type check, branch resolution)
+//   lib/executor/instantiate/module.cpp:16-172              (per-instance initial state)
+// producing a Program: register-form device bytecode + the module image every lane
+// starts from (memory pages, data segments, globals, tables).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "dbc.h"
+
+namespace wb {
+
+enum ValT : uint8_t { I32 = 0x7F, I64 = 0x7E, F32 = 0x7D, F64 = 0x7C, V128 = 0x7B,
+                      FUNCREF = 0x70, EXTERNREF = 0x6F, UNKNOWN = 0 };
+
+inline uint32_t cells_of(uint8_t t) { return t == I64 || t == F64 ? 2 : (t == V128 ? 4 : 1); }
+
+struct FuncType {
+  std::vector<uint8_t> params, results;
+  bool operator==(const FuncType &o) const { return params == o.params && results == o.results; }
+};
+
+struct DataSeg {
+  bool active = true;
+  uint32_t offset = 0;
+  std::vector<uint8_t> bytes;
+};
+
+struct ExportFunc {
+  std::string name;
+  uint32_t func;
+};
+
+struct FuncInfo {
+  uint32_t type = 0;
+  bool imported = false;
+  std::string import_module, import_name;
+  uint32_t entry_pc = 0, body_pc = 0;
+  uint32_t param_cells = 0, local_cells = 0, frame_cells = 0;
+  std::vector<uint8_t> local_types;   // declared locals (not params)
+  uint32_t code_off = 0, code_len = 0; // byte range of the body in the binary
+};
+
+struct Program {
+  // module
+  std::vector<FuncType> types;
+  std::vector<uint32_t> type_canon;    // type index -> canonical structural id
+  std::vector<FuncInfo> funcs;
+  uint32_t n_imported = 0;
+  std::vector<ExportFunc> exports;
+  bool has_mem = false;
+  uint32_t mem_min = 0, mem_max = 65536;
+  bool mem_has_max = false;
+  std::vector<DataSeg> datas;
+  std::vector<uint8_t> global_types;
+  std::vector<uint8_t> global_mut;
+  std::vector<uint32_t> global_cell;   // first cell of each global
+  std::vector<uint32_t> global_init;   // initial cell values, G cells
+  uint32_t global_cells = 0;           // G = frame base
+  std::vector<uint32_t> table0;        // funcref table 0 (immutable), 0xFFFFFFFF = null
+  uint32_t ntables = 0;
+  int64_t start_func = -1;
+  // lowered code
+  std::vector<DInstr> code;
+  std::vector<uint32_t> brtab;         // pairs (target pc, tcnt as int32)
+  std::vector<uint32_t> vconst;        // v128 pool, 4 words per entry
+  uint32_t frame_cells = 0;            // max over functions (excluding globals)
+  uint32_t total_cells() const { return global_cells + frame_cells; }
+  uint32_t max_wasm_instrs_per_dispatch = 0;
+};
+
+// Load + validate + lower. Returns empty string on success, else an error message;
+// *errcode receives the reference ErrCode byte (include/common/enum.inc).
+std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode);
+
+int find_export(const Program &p, const std::string &name);
+
+const char *dop_name(uint16_t op);
+
+}  // namespace wb

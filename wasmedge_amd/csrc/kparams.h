@@ -1,0 +1,39 @@
+// kparams.h -- launch parameters of the batched interpreter kernel (by value).
+#pragma once
+#include <stdint.h>
+
+#include "dbc.h"
+
+struct KParams {
+  // module (read-only, shared by every lane)
+  const DInstr *code;
+  const uint32_t *brtab;        // (target pc, tcnt) pairs
+  const uint32_t *vconst;       // v128 pool
+  const DFunc *funcs;           // call_indirect targets
+  const uint32_t *table;        // funcref table 0 (function indices, ~0 = null)
+  const uint32_t *global_init;  // initial global cells
+  const uint8_t *data_pool;     // passive/active data bytes (memory.init)
+  const uint32_t *data_off;
+  const uint32_t *data_len;
+  // per-lane state (lane-interleaved per wave)
+  uint32_t *mem;                // linear memory, [wave][word][64]
+  uint32_t *gstack;             // spilled frames, [wave][slot][64]
+  // per-instance inputs / outputs
+  const uint32_t *params;       // [n][param_cells]
+  uint32_t *results;            // [n][result_cells]
+  uint8_t *status;              // [n]
+  uint64_t *counts;             // [n]
+  uint32_t *pages_out;          // [n]
+  // sizes
+  uint32_t n;                   // instances in this launch
+  uint32_t entry_pc;
+  uint32_t param_cells, result_cells;
+  uint32_t global_cells, total_cells;
+  uint32_t table_size;
+  uint32_t mem_words;           // words per lane reserved (= mem_max_pages * 16384)
+  uint32_t init_pages, mem_max_pages;
+  uint32_t gs_depth;            // call-stack cells per lane
+  uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
+  uint64_t max_steps;           // dispatch budget per wave (fuel)
+  uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
+};
