@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: aggregate Wasm instructions/sec of the batched MI355X interpreter.
+
+Metric (BASELINE.json): "aggregate Wasm instrs/sec at 64K instances, 1/2/4/8 GPUs vs
+host-core interp".  A step = one pass of the hot path over one batch: fresh instantiation
+of 65,536 instances (memory image reset) + the interpreter kernel running every instance
+to completion.  Instruction counts are the reference's Statistics counts
+(include/common/statistics.h:44) produced per lane by the kernel itself.
+
+Workload at N=1 (configs[1]): C2 -- 64K instances of the BLAKE3 compression loop
+(wasmedge_amd/workloads.py), per-instance input.  Multi-GPU: one process per GPU
+(torch.distributed.run), each rank runs its own 64K-instance shard (instance ids
+[rank*64K, (rank+1)*64K)), no data-path collective -> "scaling": "weak"; a CPU-side
+(gloo) barrier + max-over-ranks brackets the timed region.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "aggregate Wasm instrs/sec at 64K instances, 1/2/4/8 GPUs vs host-core interp"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip-level parameters
+INSTANCES = 65536
+ITERS = 1000                   # chained compressions per instance
+
+
+def c2_mem_bytes(iters):
+    """Algorithmic linear-memory bytes of one C2 instance: 12 x i64.store fill (96 B),
+    per compression 16+8 i32.load + 8 i32.store (128 B), final i32.load (4 B)."""
+    return 96 + 128 * iters + 4
+
+
+class Dist:
+    """Barrier + max over ranks. torch.distributed (gloo, CPU-side) only when
+    WORLD_SIZE > 1, imported after the HIP library so the two HIP runtimes never mix
+    on the GPU."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.td = None
+
+    def init(self):
+        if self.world > 1:
+            import torch.distributed as td
+            td.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.td = td
+
+    def barrier(self):
+        if self.td:
+            self.td.barrier()
+
+    def max(self, x):
+        if not self.td:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if not self.td:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.SUM)
+        return float(t.item())
+
+
+def cpu_baseline(wasm, iters, sample, threads):
+    """The oracle (C restatement of the reference interpreter, oracle/) timed on the
+    box's host cores over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+    m = oracle_py.Module(wasm)
+    params = np.zeros((sample, 2, 2), np.uint64)
+    params[:, 0, 0] = np.arange(sample, dtype=np.uint64)
+    params[:, 1, 0] = iters
+    out = m.run_batch("run", params, sample, threads=threads)
+    instrs = float(out["counts"].sum())
+    return {"value": instrs / out["seconds"], "unit": "instr/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d C2 instances x %d compressions (%.3g instrs) in %.2fs on %d threads"
+                      % (sample, iters, instrs, out["seconds"], threads)}
+
+
+def load_profile_traffic():
+    """HBM bytes per interpreter launch from the committed rocprofv3 PMC summary
+    (profiles/), when present (see DESIGN.md 'Measurement')."""
+    p = os.path.join(ROOT, "profiles", "traffic_c2.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("iters") == ITERS and d.get("instances") == INSTANCES:
+            return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=ITERS)
+    ap.add_argument("--instances", type=int, default=INSTANCES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1024)
+    args = ap.parse_args()
+
+    dist = Dist()
+    from wasmedge_amd import batch, workloads
+    wasm = workloads.blake3_wasm()
+    n = args.instances
+    base_id = dist.rank * n
+    ctx = batch.BatchContext(wasm, n, device=dist.local_rank)
+    rows = np.zeros((n, 2), np.int64)
+    rows[:, 0] = base_id + np.arange(n)
+    rows[:, 1] = args.iters
+    ctx.set_args("run", batch.make_values(rows, [batch.I32, batch.I32]))
+    dist.init()
+
+    for _ in range(args.warmup):
+        ctx.reset()
+        ctx.run()
+    _, st, cnt = ctx.results(1)
+    if int((st != 0).sum()):
+        raise SystemExit("C2 instances trapped: %s" % np.unique(st))
+    instrs_per_step = float(cnt.sum())
+
+    dist.barrier()
+    t0 = time.perf_counter()
+    ksum = 0.0
+    for _ in range(args.steps):
+        ctx.reset()
+        ksum += ctx.run()        # HIP-event time of the interpreter kernel (its stream)
+    elapsed = time.perf_counter() - t0   # BatchRun synchronises its stream
+    dist.barrier()
+    elapsed = dist.max(elapsed)
+    total_instrs = dist.sum(instrs_per_step) * args.steps
+    _, st, cnt = ctx.results(1)
+    assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == 0
+
+    kernel_avg = ksum / args.steps
+    bytes_launch = float(c2_mem_bytes(args.iters)) * n
+    achieved = bytes_launch / kernel_avg / 1e9
+    traffic = load_profile_traffic()
+    out = {
+        "metric": METRIC,
+        "value": total_instrs / elapsed,
+        "unit": "instr/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "i32",
+        "data": "synthetic: per-instance BLAKE3 input from splitmix64(instance id), "
+                "generated inside the wasm module",
+        "config": {"workload": "C2 BLAKE3 compression loop (configs[1])",
+                   "instances_per_gpu": n, "iters": args.iters,
+                   "instrs_per_instance": instrs_per_step / n,
+                   "parallelism": "instance-sharded, 1 process per GPU"},
+        "kernel_instr_per_s": total_instrs / (dist.max(kernel_avg) * args.steps),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "note": "algorithmic = linear-memory bytes the wasm program moves; the "
+                             "path is dispatch-issue bound, see issue_roofline"},
+        "issue_roofline": {"achieved": total_instrs / elapsed / dist.world,
+                           "unit": "wasm instr/s per GPU",
+                           "dispatch_bound": "see DESIGN.md 'Roofline'"},
+    }
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(wasm, args.iters, args.cpu_sample, threads)
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

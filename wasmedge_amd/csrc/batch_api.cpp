@@ -138,7 +138,9 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   std::vector<DFunc> fv;
   for (const auto &f : P.funcs)
     fv.push_back(DFunc{f.imported ? 0xFFFFFFFFu : f.entry_pc, P.type_canon[f.type]});
-  bool ok = C->code.upload(P.code, s) && C->brtab.upload(P.brtab, s) &&
+  std::vector<DInstr> codepad = P.code;   // +1: the kernel prefetches pc+1
+  codepad.push_back(DInstr{0, 0, 0, 0});
+  bool ok = C->code.upload(codepad, s) && C->brtab.upload(P.brtab, s) &&
             C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
             C->global_init.upload(P.global_init, s) && C->image.upload(img, s) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&

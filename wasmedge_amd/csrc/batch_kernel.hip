@@ -50,7 +50,11 @@ wb_exec_kernel(const KParams p) {
   uint32_t *const fr = lds + ((wib * p.total_cells) << 6) + lane;
   uint32_t *const gs = p.gstack + (size_t)wave * p.gs_depth * 64u + lane;
   uint32_t *const mem = p.mem + (size_t)wave * p.mem_words * 64u + lane;
-  const DInstr *__restrict__ code = p.code;
+  // the bytecode is read through the constant address space so every fetch is one
+  // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
+  typedef uint32_t w4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(4))) const w4 *cptr;
+  const cptr code = (cptr)p.code;
 
 #define CELL(x) fr[(uint32_t)(x) << 6]
 #define R32(x) CELL(x)
@@ -72,16 +76,28 @@ wb_exec_kernel(const KParams p) {
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t steps = 0;
+  // Wave-uniform dispatch state (SGPRs): pcs = the pc being dispatched; conv = every
+  // running lane is at pcs (per-lane `pc` is then stale and not maintained).
+  uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
+  uint32_t pcs = p.entry_pc;
+  bool conv = true;
+  w4 I = code[pcs];
 
-  for (;;) {
-    const uint64_t amask = __ballot(status == WB_STATUS_RUNNING);
-    if (amask == 0) break;
-    // ---- wave-coherent pc selection
-    const uint32_t first = (uint32_t)__builtin_ctzll(amask);
-    uint32_t pcs = __builtin_amdgcn_readlane(pc, first);
-    if (__ballot(status == WB_STATUS_RUNNING && pc == pcs) != amask)
-      pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
-    // ---- safety: fuel / wall-clock limit (ErrCode::Interrupted, mirrors StopToken)
+  while (runmask) {
+    if (!conv) {
+      // reconverge: the minimum pc over running lanes (structured control flow puts
+      // join points above both arms, so min-pc scheduling re-joins divergent lanes)
+      const uint32_t first = (uint32_t)__builtin_ctzll(runmask);
+      pcs = __builtin_amdgcn_readlane(pc, first);
+      uint64_t m = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
+      if (m != runmask) {
+        pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
+        m = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
+      }
+      conv = m == runmask;
+      I = code[pcs];
+    }
+    // safety: fuel / wall-clock limit (ErrCode::Interrupted, mirrors StopToken)
     if ((++steps & 1023u) == 0) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (steps >= p.max_steps || now - t0 > p.max_ticks) {
@@ -89,24 +105,41 @@ wb_exec_kernel(const KParams p) {
         break;
       }
     }
-    const DInstr I = code[pcs];
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(I.w0);
-    const uint32_t w1 = __builtin_amdgcn_readfirstlane(I.w1);
-    const uint32_t w2 = __builtin_amdgcn_readfirstlane(I.w2);
-    const uint32_t w3 = __builtin_amdgcn_readfirstlane(I.w3);
-    if (status != WB_STATUS_RUNNING || pc != pcs) continue;
-
-    const uint32_t op = w0 & 0xFFFFu;
-    const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = w0 >> 24;
-    int32_t add = (int32_t)cnt8;
+    const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
+    const w4 In = code[pcs + 1];          // prefetch the fall-through successor
+    const bool ex = status == WB_STATUS_RUNNING && (conv || pc == pcs);
     uint32_t npc = pcs + 1;
-    const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
-
-    switch (op) {
+    if (ex) {
+      const uint32_t op = w0 & 0xFFFFu;
+      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
+      int32_t add = (int32_t)cnt8;
+      const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+      switch (op) {
 #include "dbc_step.inc"
+      }
+      count += (int64_t)add;
     }
-    count += (int64_t)add;
-    pc = npc;
+    if (!(w0 & DBC_CTL)) {               // falls through, cannot trap
+      if (!conv && ex) pc = npc;
+      pcs += 1;
+      I = In;
+      continue;
+    }
+    runmask = __ballot(status == WB_STATUS_RUNNING);
+    if (conv) {
+      if (!runmask) break;
+      const uint32_t first = (uint32_t)__builtin_ctzll(runmask);
+      const uint32_t n0 = __builtin_amdgcn_readlane(npc, first);
+      if (__ballot(status == WB_STATUS_RUNNING && npc == n0) == runmask) {
+        I = n0 == pcs + 1 ? In : code[n0];  // uniform branch: stay converged
+        pcs = n0;
+        continue;
+      }
+      pc = npc;
+      conv = false;
+    } else if (ex) {
+      pc = npc;
+    }
   }
 #undef CELL
   if (inst < p.n) {

@@ -12,13 +12,16 @@
 //
 // Encoding: 16 bytes, one s_load_dwordx4 per dispatch.
 //   w0: op (bits 0-15) | cnt (16-23: wasm instrs retired by this dispatch) |
-//       post (24-31: trailing folded instrs not counted when this instruction traps)
+//       post (24-30: trailing folded instrs not counted when this instruction traps) |
+//       bit 31 = CTL: the op may branch, call, return or trap (the kernel re-checks
+//       wave convergence only after such ops)
 //   w1: a (0-15) | b (16-31)       source cells / counts
 //   w2: c (0-15) | d (16-31)       destination cell / extra (d = signed tcnt on branches)
 //   w3: imm                        immediate / branch target / memarg offset
 #pragma once
 #include <stdint.h>
 
+#define DBC_CTL 0x80000000u      // w0 flag: control transfer / trap possible
 #define DBC_EXIT_PC 0xFFFFFu      // 20-bit return-pc field value that ends the lane
 #define DBC_MAX_PC 0xFFFF0u
 #define DBC_CELL_BYTES 4
@@ -31,6 +34,11 @@ struct DInstr {
 #define DBC_OPS(X)                                                                     \
   /* control: imm = target pc, d = tcnt (signed, added when taken) */                 \
   X(NOP_CNT) X(JMP) X(BR_IF) X(BR_UNLESS) X(BR_IF_MOV1) X(BR_IF_MOV2)                 \
+  /* fused compare-and-branch: taken when (a CMP b); _I: b field is a signed imm16     */ \
+  X(BR_EQ) X(BR_NE) X(BR_LT_S) X(BR_LT_U) X(BR_GT_S) X(BR_GT_U) X(BR_LE_S) X(BR_LE_U)   \
+  X(BR_GE_S) X(BR_GE_U)                                                                \
+  X(BR_EQ_I) X(BR_NE_I) X(BR_LT_S_I) X(BR_LT_U_I) X(BR_GT_S_I) X(BR_GT_U_I) X(BR_LE_S_I)\
+  X(BR_LE_U_I) X(BR_GE_S_I) X(BR_GE_U_I)                                               \
   X(BR_TABLE)     /* a = index cell, b = #labels-1, imm = brtab offset              */ \
   X(CALL)         /* a = L (caller live cells), b = arg cells, c = local cells       */ \
   X(CALL_INDIRECT)/* a = L, b = arg cells, c = index cell, d = table, imm = type id  */ \
@@ -58,6 +66,8 @@ struct DInstr {
   X(I32_LT_U_I) X(I32_GT_S_I) X(I32_GT_U_I) X(I32_LE_S_I) X(I32_LE_U_I) X(I32_GE_S_I)  \
   X(I32_GE_U_I)                                                                        \
   X(I32_EQZ) X(I32_CLZ) X(I32_CTZ) X(I32_POPCNT) X(I32_EXT8S) X(I32_EXT16S)            \
+  /* superinstructions: c = a + b + d ; c = rot(a ^ b, imm)                           */ \
+  X(I32_ADD3) X(I32_XOR_ROTR_I) X(I32_XOR_ROTL_I)                                      \
   /* i64 binary (compares write an i32 cell)                                          */ \
   X(I64_ADD) X(I64_SUB) X(I64_MUL) X(I64_DIV_S) X(I64_DIV_U) X(I64_REM_S) X(I64_REM_U) \
   X(I64_AND) X(I64_OR) X(I64_XOR) X(I64_SHL) X(I64_SHR_S) X(I64_SHR_U) X(I64_ROTL)     \

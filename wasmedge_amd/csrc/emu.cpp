@@ -89,7 +89,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
       const DInstr I = P.code[pcs];
       const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
       const uint32_t op = w0 & 0xFFFFu;
-      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = w0 >> 24;
+      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
       int32_t add = (int32_t)cnt8;
       uint32_t npc = pcs + 1;
       const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);

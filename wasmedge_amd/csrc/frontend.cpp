@@ -275,6 +275,31 @@ class Lowerer {
     return st.back().cell + cells_of(st.back().type);
   }
 
+  static bool is_ctl(uint16_t op) {
+    switch (op) {
+      case OP_JMP: case OP_BR_IF: case OP_BR_UNLESS: case OP_BR_IF_MOV1: case OP_BR_IF_MOV2:
+      case OP_BR_TABLE: case OP_CALL: case OP_CALL_INDIRECT: case OP_RET: case OP_UNREACHABLE:
+      case OP_I32_DIV_S: case OP_I32_DIV_U: case OP_I32_REM_S: case OP_I32_REM_U:
+      case OP_I32_DIV_S_I: case OP_I32_DIV_U_I: case OP_I32_REM_S_I: case OP_I32_REM_U_I:
+      case OP_I64_DIV_S: case OP_I64_DIV_U: case OP_I64_REM_S: case OP_I64_REM_U:
+      case OP_I64_DIV_S_I: case OP_I64_DIV_U_I: case OP_I64_REM_S_I: case OP_I64_REM_U_I:
+      case OP_I32_TRUNC_F32_S: case OP_I32_TRUNC_F32_U: case OP_I32_TRUNC_F64_S:
+      case OP_I32_TRUNC_F64_U: case OP_I64_TRUNC_F32_S: case OP_I64_TRUNC_F32_U:
+      case OP_I64_TRUNC_F64_S: case OP_I64_TRUNC_F64_U:
+      case OP_LD8S32: case OP_LD8U32: case OP_LD16S32: case OP_LD16U32: case OP_LD32:
+      case OP_LD8S64: case OP_LD8U64: case OP_LD16S64: case OP_LD16U64: case OP_LD32S64:
+      case OP_LD32U64: case OP_LD64: case OP_LD128: case OP_ST8: case OP_ST16: case OP_ST32:
+      case OP_ST64: case OP_ST128: case OP_MEM_FILL: case OP_MEM_COPY: case OP_MEM_INIT:
+      case OP_TABLE_GET: case OP_V_LD8X8S: case OP_V_LD8X8U: case OP_V_LD16X4S:
+      case OP_V_LD16X4U: case OP_V_LD32X2S: case OP_V_LD32X2U: case OP_V_LD8SPLAT:
+      case OP_V_LD16SPLAT: case OP_V_LD32SPLAT: case OP_V_LD64SPLAT: case OP_V_LD32ZERO:
+      case OP_V_LD64ZERO:
+        return true;
+      default:
+        return op >= OP_BR_EQ && op <= OP_BR_GE_U_I;
+    }
+  }
+
   DInstr &emit(uint16_t op, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0, uint32_t d = 0,
                uint32_t imm = 0) {
     if (a > 0xFFFF || b > 0xFFFF || c > 0xFFFF)
@@ -284,7 +309,7 @@ class Lowerer {
       pending -= 255;
     }
     DInstr I;
-    I.w0 = uint32_t(op) | (pending << 16);
+    I.w0 = uint32_t(op) | (pending << 16) | (is_ctl(op) ? DBC_CTL : 0u);
     I.w1 = (a & 0xFFFF) | (b << 16);
     I.w2 = (c & 0xFFFF) | (d << 16);
     I.w3 = imm;
@@ -479,13 +504,33 @@ class Lowerer {
       return false;
     DInstr &I = P.code[last_emit];
     if ((I.w2 & 0xFFFF) != top.cell) return false;
-    uint32_t cnt = (I.w0 >> 16) & 0xFF, post = I.w0 >> 24;
-    if (cnt + pending > 255 || post + pending > 255) return false;
+    uint32_t cnt = (I.w0 >> 16) & 0xFF, post = (I.w0 >> 24) & 0x7F;
+    if (cnt + pending > 255 || post + pending > 127) return false;
     I.w2 = (I.w2 & 0xFFFF0000u) | dst;
-    I.w0 = (I.w0 & 0xFFFF) | ((cnt + pending) << 16) | ((post + pending) << 24);
+    I.w0 = (I.w0 & (0xFFFFu | DBC_CTL)) | ((cnt + pending) << 16) | ((post + pending) << 24);
     pending = 0;
     return true;
   }
+
+  // The instruction that produced stack entry `e` if it is the last one emitted, writes
+  // e's canonical cell and no label intervened (so it can be merged with the consumer).
+  DInstr *fusable_producer(const Entry &e, uint16_t op) {
+    if (!can_retarget || e.kind != K_CELL || e.producer < 0 || e.producer != last_emit)
+      return nullptr;
+    DInstr &I = P.code[last_emit];
+    if ((I.w0 & 0xFFFF) != op || (I.w2 & 0xFFFF) != e.cell) return nullptr;
+    if (((I.w0 >> 16) & 0xFF) + pending > 255) return nullptr;
+    return &I;
+  }
+  // merge the pending count into an already emitted instruction and retype it
+  void fuse_into(DInstr &I, uint16_t op) {
+    uint32_t cnt = ((I.w0 >> 16) & 0xFF) + pending;
+    I.w0 = uint32_t(op) | (cnt << 16) | (is_ctl(op) ? DBC_CTL : 0u);
+    pending = 0;
+    if (cnt > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = cnt;
+  }
+  bool try_fuse_simple(const SimpleOp &s, Entry *ops);
+  bool try_fuse_branch(const Entry &cond, bool branch_if_true, Ctrl &f);
 
   void do_simple(const SimpleOp &s);
   void do_load(uint16_t dop, uint8_t rtype, Reader &r);
@@ -503,6 +548,7 @@ void Lowerer::do_simple(const SimpleOp &s) {
     if (rt) push_cell(rt);
     return;
   }
+  if (try_fuse_simple(s, ops)) { push_cell(rt, last_emit); return; }
   uint32_t c = top_cell();  // result lands where the first operand was
   if (npop >= 1) c = ops[0].cell;
   if (npop == 2 && s.dop_imm >= 0) {
@@ -529,6 +575,73 @@ void Lowerer::do_simple(const SimpleOp &s) {
   uint32_t d = npop >= 3 ? src(ops[2]) : 0;
   emit(s.dop, a, b, c, d);
   if (rt) push_cell(rt, last_emit);
+}
+
+// Superinstructions (merged into the previous DInstr; no label can intervene):
+//   i32.add(i32.add(a, b), m)       -> I32_ADD3       (BLAKE3 G: a = a + b + m)
+//   i32.rot{r,l}(i32.xor(a, b), k)  -> I32_XOR_ROT*_I (BLAKE3 G: d = rotr(d ^ a, k))
+bool Lowerer::try_fuse_simple(const SimpleOp &s, Entry *ops) {
+  if (s.dop == OP_I32_ADD) {
+    for (int t = 0; t < 2; t++) {
+      Entry &tmp = ops[t], &other = ops[1 - t];
+      if (other.kind == K_CONST) continue;
+      DInstr *I = fusable_producer(tmp, OP_I32_ADD);
+      if (!I) continue;
+      uint32_t oc = other.kind == K_LOCAL ? lcell[other.local] : other.cell;
+      I->w2 = (I->w2 & 0xFFFF0000u) | ops[0].cell;      // result in the first operand's slot
+      I->w2 = (I->w2 & 0xFFFFu) | (oc << 16);          // d = third addend
+      fuse_into(*I, OP_I32_ADD3);
+      return true;
+    }
+  }
+  if ((s.dop == OP_I32_ROTR || s.dop == OP_I32_ROTL) && ops[1].kind == K_CONST) {
+    DInstr *I = fusable_producer(ops[0], OP_I32_XOR);
+    if (I) {
+      I->w3 = ops[1].k[0];
+      fuse_into(*I, s.dop == OP_I32_ROTR ? OP_I32_XOR_ROTR_I : OP_I32_XOR_ROTL_I);
+      return true;
+    }
+  }
+  return false;
+}
+
+// i32 compare feeding br_if / if -> one fused compare-and-branch (target/tcnt patched by
+// the caller through the usual fixups). branch_if_true=false for `if` (branch when 0).
+bool Lowerer::try_fuse_branch(const Entry &cond, bool branch_if_true, Ctrl &f) {
+  (void)f;
+  static const uint16_t cmp_rr[] = {OP_I32_EQ, OP_I32_NE, OP_I32_LT_S, OP_I32_LT_U, OP_I32_GT_S,
+                                    OP_I32_GT_U, OP_I32_LE_S, OP_I32_LE_U, OP_I32_GE_S, OP_I32_GE_U};
+  // negation: eq<->ne, lt_s<->ge_s, lt_u<->ge_u, gt_s<->le_s, gt_u<->le_u
+  static const int neg[] = {1, 0, 8, 9, 6, 7, 4, 5, 2, 3};
+  if (!can_retarget || cond.kind != K_CELL || cond.producer < 0 || cond.producer != last_emit)
+    return false;
+  DInstr &I = P.code[last_emit];
+  uint16_t op = I.w0 & 0xFFFF;
+  if ((I.w2 & 0xFFFF) != cond.cell) return false;
+  if (((I.w0 >> 16) & 0xFF) + pending > 255) return false;
+  if (op == OP_I32_EQZ) {      // eqz + br_if -> BR_UNLESS ; eqz + if -> BR_IF
+    I.w2 = 0;
+    fuse_into(I, branch_if_true ? OP_BR_UNLESS : OP_BR_IF);
+    return true;
+  }
+  for (int k = 0; k < 10; k++) {
+    int kk = branch_if_true ? k : neg[k];
+    if (op == cmp_rr[k]) {
+      I.w2 = 0;
+      fuse_into(I, uint16_t(OP_BR_EQ + kk));
+      return true;
+    }
+    if (op == cmp_rr[k] - OP_I32_ADD + OP_I32_ADD_I) {
+      int32_t v = int32_t(I.w3);
+      if (v < -32768 || v > 32767) return false;
+      I.w1 = (I.w1 & 0xFFFF) | (uint32_t(uint16_t(int16_t(v))) << 16);
+      I.w2 = 0;
+      I.w3 = 0;
+      fuse_into(I, uint16_t(OP_BR_EQ_I + kk));
+      return true;
+    }
+  }
+  return false;
 }
 
 void Lowerer::do_load(uint16_t dop, uint8_t rtype, Reader &r) {
@@ -654,14 +767,18 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         } else {
           int64_t br = -1;
           if (live()) {
-            uint32_t c;
-            if (cond.kind == K_LOCAL) c = lcell[cond.local];
-            else {
-              if (cond.kind == K_CONST) materialize_into(cond, cond.cell);
-              c = cond.cell;
+            if (in.empty() && try_fuse_branch(cond, false, ctrl.back())) {
+              br = last_emit;
+            } else {
+              uint32_t c;
+              if (cond.kind == K_LOCAL) c = lcell[cond.local];
+              else {
+                if (cond.kind == K_CONST) materialize_into(cond, cond.cell);
+                c = cond.cell;
+              }
+              emit(OP_BR_UNLESS, c, 0, 0, 0, 0);
+              br = last_emit;
             }
-            emit(OP_BR_UNLESS, c, 0, 0, 0, 0);
-            br = last_emit;
           }
           push_ctrl(C_IF, in, out);
           ctrl.back().else_br = br;
@@ -754,7 +871,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           c = cond.cell;
         }
         if (n == 0 || top_in_place(n, f.cell_base)) {
-          emit(OP_BR_IF, c);
+          if (!try_fuse_branch(cond, true, f)) emit(OP_BR_IF, c);
           branch_fixup(f, false, uint32_t(last_emit), 0);
         } else if (n == 1 && cells_of(st.back().type) <= 2) {
           Entry &e = st.back();
