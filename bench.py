@@ -76,21 +76,44 @@ class Dist:
         return float(t.item())
 
 
-def cpu_baseline(wasm, iters, sample, threads):
+def shard_ids(rank, n):
+    """Instance ids of this rank's shard: [rank*n, (rank+1)*n) -- every rank runs
+    different instances, so N GPUs process N*n distinct instances (weak scaling)."""
+    return np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+
+
+def cpu_baseline(wasm, iters, budget_s, threads, gpu):
     """The oracle (C restatement of the reference interpreter, oracle/) timed on the
-    box's host cores over a bounded sample of the same workload."""
+    box's host cores over a bounded sample of the same workload: chunks of C2 instances
+    (ids 0, 1, 2, ...) until about `budget_s` seconds of CPU work or n_max instances."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     m = oracle_py.Module(wasm)
-    params = np.zeros((sample, 2, 2), np.uint64)
-    params[:, 0, 0] = np.arange(sample, dtype=np.uint64)
-    params[:, 1, 0] = iters
-    out = m.run_batch("run", params, sample, threads=threads)
-    instrs = float(out["counts"].sum())
-    return {"value": instrs / out["seconds"], "unit": "instr/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d C2 instances x %d compressions (%.3g instrs) in %.2fs on %d threads"
-                      % (sample, iters, instrs, out["seconds"], threads)}
+    chunk = 64 * threads
+    n_max = len(gpu["counts"])
+    done, instrs, secs = 0, 0.0, 0.0
+    while secs < budget_s and done < n_max:
+        k = min(chunk, n_max - done)
+        params = np.zeros((k, 2, 2), np.uint64)
+        params[:, 0, 0] = np.arange(done, done + k, dtype=np.uint64)
+        params[:, 1, 0] = iters
+        out = m.run_batch("run", params, k, threads=threads)
+        if int((out["codes"] != 0).sum()):
+            raise SystemExit("oracle C2 sample trapped")
+        # the oracle is the checker here too: the GPU's final state for the same
+        # instances must match bit for bit (return value, count, memory hash)
+        lo = slice(done, done + k)
+        if not (np.array_equal(out["counts"], gpu["counts"][lo])
+                and np.array_equal(out["hashes"], gpu["hashes"][lo])
+                and np.array_equal(out["results"][:, 0, 0] & 0xFFFFFFFF, gpu["ret"][lo])):
+            raise SystemExit("GPU/oracle mismatch in C2 instances [%d, %d)" % (done, done + k))
+        instrs += float(out["counts"].sum())
+        secs += out["seconds"]
+        done += k
+    return {"value": instrs / secs, "unit": "instr/s", "cores": threads, "kind": "port",
+            "sample": "%d C2 instances x %d compressions (%.3g instrs) in %.2fs on %d threads;"
+                      " bit-exact vs the GPU run on those instances" % (done, iters, instrs,
+                                                                        secs, threads)}
 
 
 def load_profile_traffic():
@@ -113,17 +136,16 @@ def main():
     ap.add_argument("--iters", type=int, default=ITERS)
     ap.add_argument("--instances", type=int, default=INSTANCES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
     dist = Dist()
     from wasmedge_amd import batch, workloads
     wasm = workloads.blake3_wasm()
     n = args.instances
-    base_id = dist.rank * n
     ctx = batch.BatchContext(wasm, n, device=dist.local_rank)
     rows = np.zeros((n, 2), np.int64)
-    rows[:, 0] = base_id + np.arange(n)
+    rows[:, 0] = shard_ids(dist.rank, n)
     rows[:, 1] = args.iters
     ctx.set_args("run", batch.make_values(rows, [batch.I32, batch.I32]))
     dist.init()
@@ -146,8 +168,13 @@ def main():
     dist.barrier()
     elapsed = dist.max(elapsed)
     total_instrs = dist.sum(instrs_per_step) * args.steps
-    _, st, cnt = ctx.results(1)
+    rets, st, cnt = ctx.results(1)
     assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == 0
+    # checksum of checksums over every instance's final linear memory (hash kernel, after
+    # the timed region)
+    hashes = ctx.memory_hash()
+    checksum = int(hashes.sum(dtype=np.uint64))
+    gpu = {"counts": cnt, "hashes": hashes, "ret": rets["lo"][:, 0] & 0xFFFFFFFF}
 
     kernel_avg = ksum / args.steps
     bytes_launch = float(c2_mem_bytes(args.iters)) * n
@@ -171,6 +198,7 @@ def main():
                    "instances_per_gpu": n, "iters": args.iters,
                    "instrs_per_instance": instrs_per_step / n,
                    "parallelism": "instance-sharded, 1 process per GPU"},
+        "memory_checksum": "%016x" % checksum,
         "kernel_instr_per_s": total_instrs / (dist.max(kernel_avg) * args.steps),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -183,7 +211,7 @@ def main():
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(wasm, args.iters, args.cpu_sample, threads)
+        out["cpu_baseline"] = cpu_baseline(wasm, args.iters, args.cpu_seconds, threads, gpu)
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

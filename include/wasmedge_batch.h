@@ -97,7 +97,7 @@ WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName
 /* Staged form of BatchExecute, for callers that keep inputs resident on the device
  * and time the interpreter alone (bench.py):
  *   SetArgs  -> resolve FuncName, check types (FuncSigMismatch), upload params
- *   Reset    -> fresh instances: memory image + globals (instantiate/*.cpp)
+ *   Reset    -> fresh instances: memory image + globals (lib/executor/instantiate/)
  *   Run      -> launch the interpreter; *KernelSeconds = HIP-event time on the
  *               library's stream (may be NULL)
  *   Results  -> copy returns / statuses / counts back. */

@@ -1,0 +1,57 @@
+"""Multi-GPU path, rehearsed on CPU: bench.py shards instances by id across ranks with no
+data-path collective; only the timing bracket (barrier + max over ranks) and the job-wide
+instruction total (sum) cross ranks.  world_size 2 over gloo, 127.0.0.1 rendezvous."""
+import os
+import socket
+import sys
+
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    d = bench.Dist()
+    d.init()
+    d.barrier()
+    ids = bench.shard_ids(d.rank, 1000)
+    q.put((rank, d.max(float(rank + 1)), d.sum(float(len(ids))), int(ids[0]), int(ids[-1])))
+    d.barrier()
+    d.td.destroy_process_group()
+
+
+def test_dist_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert [o[1] for o in out] == [2.0, 2.0]        # max over ranks
+    assert [o[2] for o in out] == [2000.0, 2000.0]  # job-wide total
+    assert out[0][3:] == (0, 999) and out[1][3:] == (1000, 1999)   # disjoint id shards
+
+
+def test_single_rank_needs_no_process_group():
+    import bench
+    d = bench.Dist()
+    d.init()
+    assert d.td is None and d.max(3.0) == 3.0 and d.sum(2.0) == 2.0
+    assert list(bench.shard_ids(0, 4)) == [0, 1, 2, 3]

@@ -83,3 +83,4 @@ def test_gpu_fib_64k_divergent(built):
     for i in range(n):
         k = 20 + (i % 11)
         assert rets[i] == ref[k][1] and int(cnt[i]) == ref[k][2], i
+

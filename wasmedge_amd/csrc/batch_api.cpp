@@ -272,7 +272,7 @@ WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSecond
   k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
   double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
   k.max_ticks = uint64_t(tl * 1e8);
-  // launch geometry: 4 waves per block when the frames fit, 1 otherwise
+  // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
   size_t wave_lds = size_t(k.total_cells) * 64 * 4;
   if (wave_lds > 160 * 1024)
     return R(C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
@@ -386,6 +386,7 @@ WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *C, uint32_t Inst,
 }
 
 uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *C) { return C ? C->n : 0; }
+
 
 uint32_t WasmEdge_BatchGetCodeSize(const WasmEdge_BatchContext *C) {
   return C ? uint32_t(C->prog.code.size()) : 0;

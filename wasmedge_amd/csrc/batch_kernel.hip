@@ -40,38 +40,42 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 
 
 // ======================================================================= interpreter
-extern "C" __global__ void __launch_bounds__(256)
-wb_exec_kernel(const KParams p) {
-  extern __shared__ uint32_t lds[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wib = threadIdx.x >> 6;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t inst = wave * 64u + lane;
-  uint32_t *const fr = lds + ((wib * p.total_cells) << 6) + lane;
-  uint32_t *const gs = p.gstack + (size_t)wave * p.gs_depth * 64u + lane;
-  uint32_t *const mem = p.mem + (size_t)wave * p.mem_words * 64u + lane;
+// Frame storage: cell-major / lane-minor LDS, so every cell access (a wave-uniform cell
+// index decoded from the scalar-loaded instruction) is one conflict-free ds_read_b32.
+// (Register-resident frames via s_set_gpr_idx were measured 10-45% slower on every
+// workload -- see DESIGN.md "Frames" -- and removed.)
+struct LdsFrame {
+  uint32_t *fr;
+  __device__ __forceinline__ uint32_t get(uint32_t i) const { return fr[i << 6]; }
+  __device__ __forceinline__ void set(uint32_t i, uint32_t v) { fr[i << 6] = v; }
+};
+
+template <class Frame>
+__device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
+                                       uint32_t *const gs, uint32_t *const mem) {
   // the bytecode is read through the constant address space so every fetch is one
   // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
   typedef uint32_t w4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(4))) const w4 *cptr;
   const cptr code = (cptr)p.code;
 
-#define CELL(x) fr[(uint32_t)(x) << 6]
-#define R32(x) CELL(x)
-#define W32(x, v) (CELL(x) = (uint32_t)(v))
-#define R64(x) ((uint64_t)CELL(x) | ((uint64_t)CELL((x) + 1) << 32))
-#define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
+#define R32(x) F.get((uint32_t)(x))
+#define R64(x) ((uint64_t)F.get((uint32_t)(x)) | ((uint64_t)F.get((uint32_t)(x) + 1) << 32))
+#define W32(c, v) F.set((uint32_t)(c), (uint32_t)(v))
+#define W64(c, v) do { const uint64_t _v = (v); F.set((uint32_t)(c), (uint32_t)_v); F.set((uint32_t)(c) + 1, (uint32_t)(_v >> 32)); } while (0)
+#define W128(c, v) do { for (int _k = 0; _k < 4; _k++) F.set((uint32_t)(c) + _k, (v)[_k]); } while (0)
+#define WLOOP(c, v) F.set((uint32_t)(c), (uint32_t)(v))
 #define GS(slot) gs[(size_t)(slot) << 6]
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
 
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   uint32_t pc = p.entry_pc, gsp = 0, pages = p.init_pages, dropped = p.init_dropped;
   uint64_t count = 0;
+  for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, p.global_init[c]);
   if (status == WB_STATUS_RUNNING) {
-    for (uint32_t c = 0; c < p.global_cells; c++) W32(c, p.global_init[c]);
     const uint32_t *prm = p.params + (size_t)inst * p.param_cells;
-    for (uint32_t c = 0; c < p.param_cells; c++) W32(p.global_cells + c, prm[c]);
-    GS(0) = DBC_EXIT_PC;   // return record of the entry frame: L = 0, pc = EXIT
+    for (uint32_t c = 0; c < p.param_cells; c++) F.set(p.global_cells + c, prm[c]);
+    GS(0) = DBC_EXIT_PC;   // return record of the entry frame: pc = EXIT
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -81,7 +85,6 @@ wb_exec_kernel(const KParams p) {
   uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
   uint32_t pcs = p.entry_pc;
   bool conv = true;
-  w4 I = code[pcs];
 
   while (runmask) {
     if (!conv) {
@@ -95,7 +98,6 @@ wb_exec_kernel(const KParams p) {
         m = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
       }
       conv = m == runmask;
-      I = code[pcs];
     }
     // safety: fuel / wall-clock limit (ErrCode::Interrupted, mirrors StopToken)
     if ((++steps & 1023u) == 0) {
@@ -105,8 +107,8 @@ wb_exec_kernel(const KParams p) {
         break;
       }
     }
+    const w4 I = code[pcs];
     const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
-    const w4 In = code[pcs + 1];          // prefetch the fall-through successor
     const bool ex = status == WB_STATUS_RUNNING && (conv || pc == pcs);
     uint32_t npc = pcs + 1;
     if (ex) {
@@ -122,7 +124,6 @@ wb_exec_kernel(const KParams p) {
     if (!(w0 & DBC_CTL)) {               // falls through, cannot trap
       if (!conv && ex) pc = npc;
       pcs += 1;
-      I = In;
       continue;
     }
     runmask = __ballot(status == WB_STATUS_RUNNING);
@@ -131,8 +132,7 @@ wb_exec_kernel(const KParams p) {
       const uint32_t first = (uint32_t)__builtin_ctzll(runmask);
       const uint32_t n0 = __builtin_amdgcn_readlane(npc, first);
       if (__ballot(status == WB_STATUS_RUNNING && npc == n0) == runmask) {
-        I = n0 == pcs + 1 ? In : code[n0];  // uniform branch: stay converged
-        pcs = n0;
+        pcs = n0;                        // uniform branch: stay converged
         continue;
       }
       pc = npc;
@@ -141,12 +141,30 @@ wb_exec_kernel(const KParams p) {
       pc = npc;
     }
   }
-#undef CELL
+#undef R32
+#undef R64
+#undef W32
+#undef W64
+#undef W128
+#undef WLOOP
+#undef GS
+#undef TRAP
   if (inst < p.n) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
     p.pages_out[inst] = pages;
   }
+}
+
+// General kernel: frames of any size in LDS (4 waves per block when they fit).
+extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t inst = wave * 64u + lane;
+  LdsFrame F{lds + ((wib * p.total_cells) << 6) + lane};
+  interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+         p.mem + (size_t)wave * p.mem_words * 64u + lane);
 }
 
 // ======================================================================= helpers
@@ -189,8 +207,8 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
                                      size_t lds_bytes, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);

@@ -76,6 +76,8 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
 #define GS(slot) gs[(size_t)(slot)]
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+#define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
+#define WLOOP(c, v) W32(c, v)
     uint32_t status = WB_STATUS_RUNNING, pc = F.entry_pc, gsp = 0, pages = P.mem_min;
     uint32_t dropped = init_dropped;
     uint64_t count = 0, steps = 0;

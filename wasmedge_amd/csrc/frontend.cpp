@@ -686,9 +686,11 @@ void Lowerer::do_call(uint32_t callee) {
   if (P.funcs[callee].imported) {
     emit(OP_UNREACHABLE, 0, 0, 0, 0, WB_ERR_HOST_CALL);
   } else {
+    uint32_t rc = 0;
+    for (uint8_t r : t.results) rc += cells_of(r);
     emit(OP_CALL, L, argcells, P.funcs[callee].local_cells, 0, 0);
     callfix->push_back(CallFix{uint32_t(last_emit), callee});
-    emit(OP_POST_CALL, L);
+    emit(OP_POST_CALL, L, rc);
   }
   for (uint8_t r : t.results) push_cell(r);
   uint32_t hi = L + argcells;
@@ -958,8 +960,10 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           uint32_t ic = src(idx);
           if (ic + 1 > max_cell) max_cell = ic + 1;
           st.resize(st.size() - args.size());
+          uint32_t rc = 0;
+          for (uint8_t r : t.results) rc += cells_of(r);
           emit(OP_CALL_INDIRECT, L, argcells, ic, tab, P.type_canon[ti]);
-          emit(OP_POST_CALL, L);
+          emit(OP_POST_CALL, L, rc);
         }
         for (uint8_t rt : t.results) push_cell(rt);
         break;
