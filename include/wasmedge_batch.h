@@ -65,9 +65,11 @@ typedef struct WasmEdge_BatchConfigure {
   uint32_t MaxMemoryPage;
   /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
   uint32_t CallStackCells;
-  /* Dispatch budget per wavefront (0 = unlimited) and wall-clock limit per launch in
-   * seconds (0 = 600); exceeding either marks running instances Interrupted (0x07),
-   * mirroring the reference's StopToken / --time-limit (helper.cpp:24-27). */
+  /* Instruction budget per instance (0 = unlimited; counted in the reference's
+   * Statistics units, enforced at 1024-dispatch granularity) and wall-clock limit per
+   * launch in seconds (0 = 600); exceeding either marks the instance Interrupted (0x07),
+   * mirroring the reference's cost limit / StopToken (statistics.h:69-91,
+   * helper.cpp:24-27). */
   uint64_t MaxSteps;
   double TimeLimitSeconds;
   /* HIP device ordinal (-1 = the current device). */

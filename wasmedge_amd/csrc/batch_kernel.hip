@@ -66,7 +66,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) F.set((uint32_t)(c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) F.set((uint32_t)(c), (uint32_t)(v))
 #define GS(slot) gs[(size_t)(slot) << 6]
-#define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+  // counting: the run's uniform count lives in an SGPR (sc += cnt per dispatch); per-lane
+  // deviations -- taken-branch tcnt, the `post` correction of a trapping lane -- go to cadj
+#define CADJ(x) (cadj += (x))
+#define TRAP(code) do { status = (code); cadj -= (int32_t)post8; } while (0)
 
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   uint32_t pc = p.entry_pc, gsp = 0, pages = p.init_pages, dropped = p.init_dropped;
@@ -79,66 +82,74 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t steps = 0;
-  // Wave-uniform dispatch state (SGPRs): pcs = the pc being dispatched; conv = every
-  // running lane is at pcs (per-lane `pc` is then stale and not maintained).
-  uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
-  uint32_t pcs = p.entry_pc;
-  bool conv = true;
+  const uint32_t lane = __lane_id();
 
-  while (runmask) {
-    if (!conv) {
-      // reconverge: the minimum pc over running lanes (structured control flow puts
-      // join points above both arms, so min-pc scheduling re-joins divergent lanes)
-      const uint32_t first = (uint32_t)__builtin_ctzll(runmask);
-      pcs = __builtin_amdgcn_readlane(pc, first);
-      uint64_t m = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
-      if (m != runmask) {
-        pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
-        m = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
-      }
-      conv = m == runmask;
+  for (;;) {
+    // ---- schedule: the lanes at the minimum pc run next (structured control flow puts
+    // join points above both arms, so min-pc scheduling reconverges divergent lanes);
+    // `other` = the lowest pc of the lanes left waiting.
+    const uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
+    if (!runmask) break;
+    uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(runmask));
+    uint64_t act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
+    uint32_t other = 0xFFFFFFFFu;
+    if (act != runmask) {
+      pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
+      act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
+      if (act != runmask)
+        other = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
     }
-    // safety: fuel / wall-clock limit (ErrCode::Interrupted, mirrors StopToken)
-    if ((++steps & 1023u) == 0) {
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (steps >= p.max_steps || now - t0 > p.max_ticks) {
-        if (status == WB_STATUS_RUNNING) status = WB_ERR_INTERRUPTED;
-        break;
-      }
-    }
-    const w4 I = code[pcs];
-    const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
-    const bool ex = status == WB_STATUS_RUNNING && (conv || pc == pcs);
-    uint32_t npc = pcs + 1;
-    if (ex) {
-      const uint32_t op = w0 & 0xFFFFu;
-      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
-      int32_t add = (int32_t)cnt8;
-      const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
-      switch (op) {
+    // (select by the ballot bit, not by `pc == pcs`: under that condition the compiler
+    // would substitute the per-lane pc for pcs and make the whole run divergent)
+    if ((act >> lane) & 1u) {
+      // ---- run the active lanes (EXEC = act for the whole run) until a control op
+      // splits them, stops one of them, or lands at/after a waiting lane's pc.
+      uint32_t sc = 0, tick = 1024;
+      int32_t cadj = 0;
+      uint32_t npc = pcs + 1;
+      w4 I = code[pcs];
+      for (;;) {
+        const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
+        // Prefetch the fall-through successor only after I is resident: SMEM returns out
+        // of order, so a use of I issued after the prefetch would wait for both.
+        asm volatile("" ::"s"(w0), "s"(w1), "s"(w2), "s"(w3));
+        const w4 In = code[pcs + 1];
+        const uint32_t op = w0 & 0xFFFFu;
+        const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
+        const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+        npc = pcs + 1;
+        switch (op) {
 #include "dbc_step.inc"
+        }
+        sc += cnt8;
+        if (--tick == 0) {
+          // every 1024 dispatches: flush the counters, apply the instruction budget and
+          // the wall-clock limit (ErrCode::Interrupted, mirrors the StopToken)
+          count += (uint64_t)sc + (int64_t)cadj;
+          sc = 0;
+          cadj = 0;
+          tick = 1024;
+          if (count >= p.max_steps ||
+              __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks)
+            if (status == WB_STATUS_RUNNING) status = WB_ERR_INTERRUPTED;
+          if (__ballot(status == WB_STATUS_RUNNING) != act) break;
+        }
+        if (!(w0 & DBC_CTL)) {           // falls through, cannot trap
+          pcs += 1;
+          I = In;
+          continue;
+        }
+        if (__ballot(status == WB_STATUS_RUNNING) != act) break;   // trap / exit
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(npc);
+        if (__ballot(npc == n0) != act || n0 >= other) break;       // split / merge
+        I = n0 == pcs + 1 ? In : code[n0];
+        pcs = n0;
       }
-      count += (int64_t)add;
-    }
-    if (!(w0 & DBC_CTL)) {               // falls through, cannot trap
-      if (!conv && ex) pc = npc;
-      pcs += 1;
-      continue;
-    }
-    runmask = __ballot(status == WB_STATUS_RUNNING);
-    if (conv) {
-      if (!runmask) break;
-      const uint32_t first = (uint32_t)__builtin_ctzll(runmask);
-      const uint32_t n0 = __builtin_amdgcn_readlane(npc, first);
-      if (__ballot(status == WB_STATUS_RUNNING && npc == n0) == runmask) {
-        pcs = n0;                        // uniform branch: stay converged
-        continue;
-      }
+      count += (uint64_t)sc + (int64_t)cadj;
       pc = npc;
-      conv = false;
-    } else if (ex) {
-      pc = npc;
+      if (status == WB_STATUS_RUNNING &&
+          (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks))
+        status = WB_ERR_INTERRUPTED;
     }
   }
 #undef R32
@@ -148,6 +159,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef W128
 #undef WLOOP
 #undef GS
+#undef CADJ
 #undef TRAP
   if (inst < p.n) {
     p.status[inst] = (uint8_t)status;

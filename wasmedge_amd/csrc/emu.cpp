@@ -78,15 +78,16 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
+#define CADJ(x) (add += (x))
     uint32_t status = WB_STATUS_RUNNING, pc = F.entry_pc, gsp = 0, pages = P.mem_min;
     uint32_t dropped = init_dropped;
-    uint64_t count = 0, steps = 0;
+    uint64_t count = 0;
     for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
     for (uint32_t c = 0; c < pcells; c++) W32(P.global_cells + c, params[size_t(inst) * pcells + c]);
     GS(0) = DBC_EXIT_PC;
     gsp = 1;
     while (status == WB_STATUS_RUNNING) {
-      if (max_steps && ++steps > max_steps) { status = 0x07; break; }
+      if (max_steps && count >= max_steps) { status = 0x07; break; }
       const uint32_t pcs = pc;
       const DInstr I = P.code[pcs];
       const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;

@@ -34,6 +34,6 @@ struct KParams {
   uint32_t init_pages, mem_max_pages;
   uint32_t gs_depth;            // call-stack cells per lane
   uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
-  uint64_t max_steps;           // dispatch budget per wave (fuel)
+  uint64_t max_steps;           // instruction budget per instance
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
 };
