@@ -44,8 +44,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // index decoded from the scalar-loaded instruction) is one conflict-free ds_read_b32.
 // (Register-resident frames via s_set_gpr_idx were measured 10-45% slower on every
 // workload -- see DESIGN.md "Frames" -- and removed.)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 struct LdsFrame {
-  uint32_t *fr;
+  lds_u32 *fr;   // LDS-typed so the compiler knows frame cells never alias HBM
   __device__ __forceinline__ uint32_t get(uint32_t i) const { return fr[i << 6]; }
   __device__ __forceinline__ void set(uint32_t i, uint32_t v) { fr[i << 6] = v; }
 };
@@ -66,10 +67,6 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) F.set((uint32_t)(c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) F.set((uint32_t)(c), (uint32_t)(v))
 #define GS(slot) gs[(size_t)(slot) << 6]
-  // counting: the run's uniform count lives in an SGPR (sc += cnt per dispatch); per-lane
-  // deviations -- taken-branch tcnt, the `post` correction of a trapping lane -- go to cadj
-#define CADJ(x) (cadj += (x))
-#define TRAP(code) do { status = (code); cadj -= (int32_t)post8; } while (0)
 
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   uint32_t pc = p.entry_pc, gsp = 0, pages = p.init_pages, dropped = p.init_dropped;
@@ -99,14 +96,40 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       if (act != runmask)
         other = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
     }
+    bool slow = false;   // the run stopped at an instruction that needs the slow step
     // (select by the ballot bit, not by `pc == pcs`: under that condition the compiler
     // would substitute the per-lane pc for pcs and make the whole run divergent)
     if ((act >> lane) & 1u) {
-      // ---- run the active lanes (EXEC = act for the whole run) until a control op
-      // splits them, stops one of them, or lands at/after a waiting lane's pc.
-      uint32_t sc = 0, tick = 1024;
-      int32_t cadj = 0;
-      uint32_t npc = pcs + 1;
+      // ================================================================ fast run
+      // EXEC = act for the whole run. Every branch inside is wave-uniform (the compiler
+      // leaves the dispatch tree as plain scalar branches); a dispatch continues with
+      //   fall out of the switch      -> k_next: pcs + 1
+      //   JUMP(t, tc)                 -> uniform jump (tc = taken-branch count correction)
+      //   BRANCH(c, t, tc)            -> all lanes agree: stay; split: leave the run
+      //   JUMP_LANE(t, tc)            -> per-lane target: stay when uniform, else leave
+      //   TRAP(code) + TRAP_CHECK()   -> leave when any lane trapped
+      //   SLOW_IF(c) / SLOW_OP()      -> leave before any side effect; the slow step
+      //                                  below executes this instruction per lane
+      // Per-lane state (pc, status, count corrections) changes only on exit paths.
+#define WB_FAST 1
+#define JUMP(t, tc) do { sc += cnt8 + (uint32_t)(tc); pcs = (t); goto k_jump; } while (0)
+#define BRANCH(c, t, tc) do { const bool _c = (c); const uint64_t _m = __ballot(_c); \
+    if (_m == act) JUMP(t, tc); \
+    if (_m) { xpc = _c ? (uint32_t)(t) : pcs + 1; xadj = _c ? (int32_t)(tc) : 0; goto k_exit; } \
+    goto k_next; } while (0)
+#define JUMP_LANE(t, tc) do { const uint32_t _t = (t); const int32_t _tc = (tc); \
+    const uint32_t _n0 = __builtin_amdgcn_readfirstlane(_t); \
+    const int32_t _c0 = __builtin_amdgcn_readfirstlane(_tc); \
+    if (__ballot(_t == _n0 && _tc == _c0) == act) JUMP(_n0, _c0); \
+    xpc = _t; xadj = _tc; goto k_exit; } while (0)
+#define TRAP(code) (tcode = (code))
+#define FINISH() (tcode = WB_TCODE_DONE)
+#define EXIT_IF_TRAPPED(t) do { if (__ballot(tcode != 0)) { xpc = (t); xadj = 0; goto k_exit; } } while (0)
+#define TRAP_CHECK() EXIT_IF_TRAPPED(pcs + 1)
+#define SLOW_OP() goto k_slow
+#define SLOW_IF(c) do { if (__ballot(c)) goto k_slow; } while (0)
+      uint32_t sc = 0, tick = 1024, xpc = 0, xpost = 0, tcode = 0;
+      int32_t xadj = 0;
       w4 I = code[pcs];
       for (;;) {
         const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
@@ -117,40 +140,98 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         const uint32_t op = w0 & 0xFFFFu;
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
-        npc = pcs + 1;
         switch (op) {
 #include "dbc_step.inc"
         }
+      k_next:
         sc += cnt8;
-        if (--tick == 0) {
-          // every 1024 dispatches: flush the counters, apply the instruction budget and
-          // the wall-clock limit (ErrCode::Interrupted, mirrors the StopToken)
-          count += (uint64_t)sc + (int64_t)cadj;
-          sc = 0;
-          cadj = 0;
-          tick = 1024;
-          if (count >= p.max_steps ||
-              __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks)
-            if (status == WB_STATUS_RUNNING) status = WB_ERR_INTERRUPTED;
-          if (__ballot(status == WB_STATUS_RUNNING) != act) break;
-        }
-        if (!(w0 & DBC_CTL)) {           // falls through, cannot trap
-          pcs += 1;
-          I = In;
-          continue;
-        }
-        if (__ballot(status == WB_STATUS_RUNNING) != act) break;   // trap / exit
-        const uint32_t n0 = __builtin_amdgcn_readfirstlane(npc);
-        if (__ballot(npc == n0) != act || n0 >= other) break;       // split / merge
-        I = n0 == pcs + 1 ? In : code[n0];
-        pcs = n0;
+        pcs += 1;
+        if (pcs >= other) { xpc = pcs; goto k_leave; }   // reached a waiting lane
+        I = In;
+        continue;
+      k_jump:
+        // every 1024 taken jumps (and before the SGPR count could overflow) the run
+        // returns to the scheduler, which flushes counts and checks the limits
+        if (--tick == 0 || (int32_t)sc < 0 || pcs >= other) goto k_leave;
+        I = code[pcs];
+        continue;
+      k_exit:
+        sc += cnt8;
+        xpost = post8;
+        break;
+      k_slow:
+        slow = true;
+      k_leave:
+        xpc = pcs;
+        tcode = 0;
+        xadj = 0;
+        break;
       }
-      count += (uint64_t)sc + (int64_t)cadj;
-      pc = npc;
-      if (status == WB_STATUS_RUNNING &&
-          (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks))
-        status = WB_ERR_INTERRUPTED;
+#undef WB_FAST
+#undef JUMP
+#undef BRANCH
+#undef JUMP_LANE
+#undef TRAP
+#undef FINISH
+#undef EXIT_IF_TRAPPED
+#undef TRAP_CHECK
+#undef SLOW_OP
+#undef SLOW_IF
+      count += (uint64_t)sc;
+      if (tcode == 0) {
+        pc = xpc;
+        count += (int64_t)xadj;
+      } else if (tcode == WB_TCODE_DONE) {
+        status = WB_STATUS_OK;
+      } else {
+        status = tcode;
+        count -= xpost;
+      }
     }
+    const uint64_t slowmask = __ballot(slow);
+    if (slowmask && ((slowmask >> lane) & 1u)) {
+      // ================================================================ slow step
+      // One dispatch with fully per-lane semantics (the same step code, WB_FAST 0):
+      // misaligned / out-of-bounds memory, traps, bulk memory ops, memory.grow,
+      // call_indirect, leaving the entry function.
+#define WB_FAST 0
+#define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+#define FINISH() (status = WB_STATUS_OK)
+#define JUMP(t, tc) do { npc = (t); add += (tc); goto s_next; } while (0)
+#define JUMP_LANE(t, tc) JUMP(t, tc)
+#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); } goto s_next; } while (0)
+#define EXIT_IF_TRAPPED(t) ((void)0)
+#define TRAP_CHECK() ((void)0)
+#define SLOW_OP() ((void)0)
+#define SLOW_IF(c) ((void)0)
+      const uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(slowmask));
+      const w4 I = code[pcs];
+      const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
+      const uint32_t op = w0 & 0xFFFFu;
+      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
+      const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+      uint32_t npc = pcs + 1;
+      int32_t add = (int32_t)cnt8;
+      switch (op) {
+#include "dbc_step.inc"
+      }
+    s_next:
+      count += (int64_t)add;
+      pc = npc;
+#undef WB_FAST
+#undef JUMP
+#undef BRANCH
+#undef JUMP_LANE
+#undef TRAP
+#undef FINISH
+#undef EXIT_IF_TRAPPED
+#undef TRAP_CHECK
+#undef SLOW_OP
+#undef SLOW_IF
+    }
+    if (status == WB_STATUS_RUNNING &&
+        (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks))
+      status = WB_ERR_INTERRUPTED;
   }
 #undef R32
 #undef R64
@@ -159,8 +240,6 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef W128
 #undef WLOOP
 #undef GS
-#undef CADJ
-#undef TRAP
   if (inst < p.n) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
@@ -174,7 +253,7 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t inst = wave * 64u + lane;
-  LdsFrame F{lds + ((wib * p.total_cells) << 6) + lane};
+  LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
   interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
          p.mem + (size_t)wave * p.mem_words * 64u + lane);
 }

@@ -21,6 +21,7 @@
 #pragma once
 #include <stdint.h>
 
+#define WB_TCODE_DONE 0x100u    // internal: the lane returned from its entry function
 #define DBC_CTL 0x80000000u      // w0 flag: control transfer / trap possible
 #define DBC_EXIT_PC 0xFFFFFu      // 20-bit return-pc field value that ends the lane
 #define DBC_MAX_PC 0xFFFF0u

@@ -76,9 +76,17 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
 #define GS(slot) gs[(size_t)(slot)]
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
+#define FINISH() (status = WB_STATUS_OK)
+#define JUMP(t, tc) do { npc = (t); add += (tc); goto e_next; } while (0)
+#define JUMP_LANE(t, tc) JUMP(t, tc)
+#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); } goto e_next; } while (0)
+#define EXIT_IF_TRAPPED(t) ((void)0)
+#define TRAP_CHECK() ((void)0)
+#define SLOW_OP() ((void)0)
+#define SLOW_IF(c) ((void)0)
+#define WB_FAST 0
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
-#define CADJ(x) (add += (x))
     uint32_t status = WB_STATUS_RUNNING, pc = F.entry_pc, gsp = 0, pages = P.mem_min;
     uint32_t dropped = init_dropped;
     uint64_t count = 0;
@@ -99,6 +107,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
       switch (op) {
 #include "dbc_step.inc"
       }
+    e_next:
       count += (int64_t)add;
       pc = npc;
     }
