@@ -10,6 +10,7 @@ fall-through and are reported. A tuning aid for the dispatch overhead; not a tes
 """
 import re
 import sys
+TRACE = False
 
 
 def parse(path):
@@ -69,6 +70,7 @@ def run(path, op, ctl=False):
     while steps < 4000:
         steps += 1
         s = ins[pc]
+        if TRACE: print("   ", s)
         mnem = s.split()[0]
         cls = ("branch" if mnem.startswith("s_cbranch") or mnem == "s_branch" else
                "salu" if mnem.startswith("s_") else "valu" if mnem.startswith("v_") else
