@@ -3,6 +3,7 @@
 // per-instance result buffers.  See the header for the reference interfaces mirrored.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -10,6 +11,7 @@
 
 #include "../../include/wasmedge_batch.h"
 #include "frontend.h"
+#include "tc.h"
 #include "kparams.h"
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
@@ -61,6 +63,8 @@ struct WasmEdge_BatchContext {
   std::string last_error;
   // module buffers
   DevBuf<DInstr> code;
+  DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
+  bool threaded = true;
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
   DevBuf<DFunc> funcs;
   DevBuf<uint8_t> data_pool;
@@ -140,7 +144,13 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     fv.push_back(DFunc{f.imported ? 0xFFFFFFFFu : f.entry_pc, P.type_canon[f.type]});
   std::vector<DInstr> codepad = P.code;   // +1: the kernel prefetches pc+1
   codepad.push_back(DInstr{0, 0, 0, 0});
-  bool ok = C->code.upload(codepad, s) && C->brtab.upload(P.brtab, s) &&
+  // threaded code for the hand-written dispatch core; WB_THREADED=0 runs every op
+  // through the compiled step instead (A/B measurement aid)
+  const char *thr = getenv("WB_THREADED");
+  C->threaded = !(thr && thr[0] == '0');
+  std::vector<TInstr> tcv;
+  if (C->threaded) tcv = wb::build_threaded(P, codepad);
+  bool ok = C->code.upload(codepad, s) && (!C->threaded || C->tcode.upload(tcv, s)) && C->brtab.upload(P.brtab, s) &&
             C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
             C->global_init.upload(P.global_init, s) && C->image.upload(img, s) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
@@ -254,6 +264,7 @@ WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSecond
   k.code = C->code.ptr; k.brtab = C->brtab.ptr; k.vconst = C->vconst.ptr;
   k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
   k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
+  k.tcode = C->threaded ? C->tcode.ptr : nullptr;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.params = C->params.ptr;
   k.results = C->results.ptr; k.status = C->status.ptr; k.counts = C->counts.ptr;
   k.pages_out = C->pages.ptr;
@@ -274,14 +285,15 @@ WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSecond
   k.max_ticks = uint64_t(tl * 1e8);
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
   size_t wave_lds = size_t(k.total_cells) * 64 * 4;
-  if (wave_lds > 160 * 1024)
+  if (wave_lds + 256 > 160 * 1024)
     return R(C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
                                         " cells exceeds LDS (global-frame mode: next)"));
   uint32_t wpb = 4;
-  while (wpb > 1 && wave_lds * wpb > 160 * 1024) wpb >>= 1;
+  while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
   uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
   (void)hipEventRecord(C->ev0, C->stream);
-  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb, C->stream), "launch"))
+  // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
+  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->stream), "launch"))
     return R(kRuntimeError);
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return R(kRuntimeError);

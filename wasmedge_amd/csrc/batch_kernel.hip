@@ -28,6 +28,22 @@
 
 
 #include "dbc_ops.h"
+#include "tc.h"
+
+// The threaded dispatch core (gen_tc.py): hand-written gfx950 handlers. hipcc drops
+// file-scope asm in device code, so the blob is the body of a kernel that is never
+// launched (it would end at its first instruction); wb_exec_kernel enters and leaves
+// the handlers through tc_run() below.
+extern "C" __global__ void wb_tc_holder_kernel() {
+  asm volatile("s_endpgm\n"
+#include "tc_blob.inc"
+               ::: "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
+               "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
+               "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
+               "s92", "s93", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
+               "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
+               "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
+}
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -49,7 +65,56 @@ struct LdsFrame {
   lds_u32 *fr;   // LDS-typed so the compiler knows frame cells never alias HBM
   __device__ __forceinline__ uint32_t get(uint32_t i) const { return fr[i << 6]; }
   __device__ __forceinline__ void set(uint32_t i, uint32_t v) { fr[i << 6] = v; }
+  __device__ __forceinline__ uint32_t lds_addr() const { return (uint32_t)(uintptr_t)fr; }
 };
+
+// Run the threaded core from uniform pc `pc` for the lanes in EXEC until it meets an
+// instruction it cannot finish for all of them (reason 0: the C++ step executes that
+// instruction next), or reaches `other` / the count limit (reason 1: back to the
+// scheduler). Returns the new uniform pc; *ncnt = wasm instructions retired.
+// Register contract: gen_tc.py (s60-s93, v104-v127 belong to the core).
+__device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other,
+                                           uint32_t fr, uint32_t pages, const uint32_t *mem,
+                                           uint32_t *ncnt, uint32_t *reason) {
+  uint32_t npc, cnt, why;
+  const uint32_t oth = other >= (1u << 26) ? 0xFFFFFFFFu : other << 5;
+  const uint64_t m = (uint64_t)(uintptr_t)mem;
+  const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
+  asm volatile(
+      "s_mov_b64 s[60:61], %[code]\n\t"
+      "s_lshl_b32 s62, %[pc], 5\n\t"
+      "s_mov_b32 s63, %[oth]\n\t"
+      "s_mov_b32 s64, %[lim]\n\t"
+      "s_mov_b32 s65, 0\n\t"
+      "v_mov_b32 v104, %[fr]\n\t"
+      "v_mov_b32 v105, %[pages]\n\t"
+      "v_mov_b32 v106, %[mlo]\n\t"
+      "v_mov_b32 v107, %[mhi]\n\t"
+      "s_getpc_b64 s[66:67]\n"
+      "Ltc_ret_%=:\n\t"
+      "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t"
+      "s_addc_u32 s67, s67, 0\n\t"
+      "s_getpc_b64 s[68:69]\n\t"
+      "s_add_u32 s68, s68, wb_tc_entry@rel32@lo+4\n\t"
+      "s_addc_u32 s69, s69, wb_tc_entry@rel32@hi+12\n\t"
+      "s_setpc_b64 s[68:69]\n"
+      "Ltc_back_%=:\n\t"
+      "s_lshr_b32 %[npc], s62, 5\n\t"
+      "s_mov_b32 %[cnt], s65\n\t"
+      "s_mov_b32 %[why], s92"
+      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why)
+      : [code] "s"(tcode), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr),
+        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi)
+      : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
+        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83",
+        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
+        "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113",
+        "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123",
+        "v124", "v125", "v126", "v127", "vcc", "scc", "memory");
+  *ncnt = cnt;
+  *reason = why;
+  return npc;
+}
 
 template <class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
@@ -80,6 +145,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t lane = __lane_id();
+  const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
 
   for (;;) {
     // ---- schedule: the lanes at the minimum pc run next (structured control flow puts
@@ -130,14 +196,24 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define SLOW_IF(c) do { if (__ballot(c)) goto k_slow; } while (0)
       uint32_t sc = 0, tick = 1024, xpc = 0, xpost = 0, tcode = 0;
       int32_t xadj = 0;
+      uint64_t asc = 0;     // instructions retired inside the threaded core
       w4 I = code[pcs];
       for (;;) {
+        if (p.tcode && (I.x & DBC_HOT)) {
+          // hand the run to the threaded core; it returns at an instruction this
+          // C++ step must execute (reason 0), or for the scheduler (reason 1)
+          uint32_t ncnt, why;
+          pcs = tc_run(p.tcode, pcs, other, fr_lds, pages, mem, &ncnt, &why);
+          asc += ncnt;
+          if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
+          I = code[pcs];
+        }
         const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
         // Prefetch the fall-through successor only after I is resident: SMEM returns out
         // of order, so a use of I issued after the prefetch would wait for both.
         asm volatile("" ::"s"(w0), "s"(w1), "s"(w2), "s"(w3));
         const w4 In = code[pcs + 1];
-        const uint32_t op = w0 & 0xFFFFu;
+        const uint32_t op = w0 & 0x7FFFu;
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
         switch (op) {
@@ -177,7 +253,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef TRAP_CHECK
 #undef SLOW_OP
 #undef SLOW_IF
-      count += (uint64_t)sc;
+      count += (uint64_t)sc + asc;
       if (tcode == 0) {
         pc = xpc;
         count += (int64_t)xadj;
@@ -207,7 +283,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       const uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(slowmask));
       const w4 I = code[pcs];
       const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
-      const uint32_t op = w0 & 0xFFFFu;
+      const uint32_t op = w0 & 0x7FFFu;
       const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
       const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
       uint32_t npc = pcs + 1;

@@ -14,10 +14,15 @@
 #include "kparams.h"
 
 static std::string g_err;
+static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuning aid)
 
 extern "C" {
 
 __attribute__((visibility("default"))) const char *wb_emu_last_error() { return g_err.c_str(); }
+
+// Count dispatches per DBC op into h[DBC_NUM_OPS] during later wb_emu_execute calls (NULL: off).
+__attribute__((visibility("default"))) void wb_emu_set_histogram(uint64_t *h) { g_hist = h; }
+__attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 
 // Returns ErrCode of the call; per-instance outputs like WasmEdge_BatchExecute.
 // params: [n][param cells] u32; results: [n][result cells] u32.
@@ -100,6 +105,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
       const DInstr I = P.code[pcs];
       const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
       const uint32_t op = w0 & 0xFFFFu;
+      if (g_hist) g_hist[op]++;
       const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
       int32_t add = (int32_t)cnt8;
       uint32_t npc = pcs + 1;

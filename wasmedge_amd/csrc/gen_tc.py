@@ -1,0 +1,464 @@
+#!/usr/bin/env python3
+"""Generator of the direct-threaded gfx950 dispatch core (tc = "threaded code").
+
+Why: on CDNA4 a wave issues one instruction per ~4 cycles and every scalar branch costs
+15-30 cycles (tools/ubench/lat.hip). The compiled C++ dispatch loop walks a binary
+compare tree over ~330 opcodes (≈9 compare+branch pairs) and waits for each
+instruction's LDS operands serially: ≈526 cycles per dispatch on C2 (profiles/r01b_*).
+This core replaces that, for the hot opcodes, with hand-written handlers:
+
+  * direct threading: every 32-byte threaded instruction (TInstr, see tc.h) carries its
+    handler's byte offset; dispatch is `s_add/s_addc/s_setpc_b64` (no compare tree);
+  * fixed 256-byte handler slots, laid out in four banks: {converged, diverged} x
+    {A, B}. The instruction being executed sits in SGPR bank A or B; its handler
+    prefetches the fall-through successor into the other bank, so no SGPR copies;
+  * software-pipelined operands: a handler issues the LDS reads of the NEXT
+    instruction's operands (a, b, d; each a ds_read2_b32 of cells k and k+1) before it
+    dispatches, so their latency overlaps the dispatch itself;
+  * the "diverged" banks additionally stop when the uniform pc reaches the lowest pc of
+    the waiting lanes (min-pc reconvergence, see batch_kernel.hip).
+
+Anything a handler cannot finish for every active lane (an opcode without a handler, a
+branch whose lanes disagree, a misaligned or out-of-bounds access) leaves the core
+BEFORE the instruction has any effect; the compiled C++ step (dbc_step.inc) then
+executes it with full per-lane semantics. So the core never traps, and every result it
+produces is one the C++ step would produce.
+
+Outputs (both written next to this file; run by the Makefile):
+  tc_blob.inc   the handler blob as a C string for a file-scope asm() (device pass only)
+  tc_slots.h    opcode -> slot map for the host translator (tc.cpp)
+"""
+import os
+import sys
+
+SLOT = 256                         # bytes per handler slot
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# ---------------------------------------------------------------- register conventions
+# SGPRs (all clobbered by the kernel's asm statement)
+CODE = "s[60:61]"     # TInstr array base
+PCOFF = "s62"         # current pc * 32
+OTHER = "s63"         # lowest waiting pc * 32 (diverged banks stop there)
+LIM = "s64"           # count limit: leave at a taken branch once CNT >= LIM
+CNT = "s65"           # wasm instructions retired in this call
+RET = "s[66:67]"      # return address into the kernel
+T = ("s68", "s69")    # temp pair (dispatch target)
+TP = "s[68:69]"
+BA = ("s70", "s71")   # bank-A handler base of the current mode
+BB = ("s72", "s73")   # bank-B handler base
+T2 = "s[74:75]"       # temp pair (lane masks)
+T2L, T2H = "s74", "s75"
+IA = 76               # s[76:83] instruction in bank A (w0..w7)
+IB = 84               # s[84:91] instruction in bank B
+REASON = "s92"        # 0: execute pc in the C++ step; 1: back to the scheduler
+# VGPRs (v104..v127, clobbered)
+FR = "v104"           # LDS byte address of this lane's cell 0
+PAGES = "v105"        # this lane's memory size in pages
+MEM = "v[106:107]"    # this lane's linear-memory word 0 (lane-interleaved)
+A = ("v108", "v109"); AP = "v[108:109]"   # operand a: cells a, a+1
+B = ("v110", "v111"); BP = "v[110:111]"   # operand b
+D = ("v112", "v113"); DP = "v[112:113]"   # operand d
+R = ("v114", "v115"); RP = "v[114:115]"   # result
+W = ("v116", "v117"); WP = "v[116:117]"   # word index, 0 (v117 is always 0)
+X = ("v118", "v119"); XP = "v[118:119]"   # temps / 64-bit address
+Y = ("v120", "v121"); YP = "v[120:121]"
+AADDR, BADDR, DADDR, CADDR = "v122", "v123", "v124", "v125"
+Z = ("v126", "v127"); ZP = "v[126:127]"
+
+
+def sreg(bank, k):
+    return "s%d" % ((IA if bank == "A" else IB) + k)
+
+
+def sbank(bank):
+    b = IA if bank == "A" else IB
+    return "s[%d:%d]" % (b, b + 7)
+
+
+# ---------------------------------------------------------------- handler specs
+# Each spec: name -> (DBC op names it serves, body function(g) -> list of lines).
+# A body runs after `s_waitcnt lgkmcnt(0)` (operands of this instruction are in A/B/D,
+# the prefetched successor is in the other bank). It ends with one of the tails:
+#   g.next()        fall through (count cnt, pc += 1)
+#   g.exit_here()   leave before this instruction had any effect
+#   explicit branch code using g.taken(...)
+
+
+class Gen:
+    def __init__(self, mode, bank):
+        self.mode, self.bank = mode, bank          # mode "C" converged / "D" diverged
+        self.other = "B" if bank == "A" else "A"
+        self.n = 0
+
+    def x(self, k):                                # field k of the current instruction
+        return sreg(self.bank, k)
+
+    def y(self, k):                                # field k of the successor bank
+        return sreg(self.other, k)
+
+    _uid = [0]
+
+    def lab(self, tag):
+        Gen._uid[0] += 1
+        return "Ltc_%s_%d" % (tag, Gen._uid[0])
+
+    def exit_here(self):
+        return ["s_branch %s" % self.xh()]
+
+    def xh(self):     # exit stubs live in slot 0 of every bank (s_branch reaches +-128 KB)
+        return "Ltc_xh_%s%s" % (self.mode, self.bank)
+
+    def xs(self):
+        return "Ltc_xs_%s%s" % (self.mode, self.bank)
+
+    def issue_reads(self, bank):
+        """LDS reads of the operands of the instruction in `bank` (fields 1, 2, 5)."""
+        f = lambda k: sreg(bank, k)
+        return ["v_add_u32 %s, %s, %s" % (AADDR, f(1), FR),
+                "v_add_u32 %s, %s, %s" % (BADDR, f(2), FR),
+                "v_add_u32 %s, %s, %s" % (DADDR, f(5), FR),
+                "ds_read2_b32 %s, %s offset1:64" % (AP, AADDR),
+                "ds_read2_b32 %s, %s offset1:64" % (BP, BADDR),
+                "ds_read2_b32 %s, %s offset1:64" % (DP, DADDR)]
+
+    def dispatch(self, bank):
+        base = BA if bank == "A" else BB
+        return ["s_add_u32 %s, %s, %s" % (T[0], base[0], sreg(bank, 0)),
+                "s_addc_u32 %s, %s, 0" % (T[1], base[1]),
+                "s_setpc_b64 %s" % TP]
+
+    def next(self, cnt=True):
+        """Fall through to the prefetched successor (other bank)."""
+        out = []
+        if cnt:
+            out.append("s_add_u32 %s, %s, %s" % (CNT, CNT, self.x(6)))
+        out.append("s_add_u32 %s, %s, 32" % (PCOFF, PCOFF))
+        if self.mode == "D":
+            out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
+        out += self.issue_reads(self.other)
+        # prefetch the successor's successor into this bank (its fields are dead now)
+        out.append("s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank(self.bank), CODE, PCOFF))
+        out += self.dispatch(self.other)
+        return out
+
+    def taken(self, target, cnt):
+        """Uniform jump to byte offset `target` (SGPR), adding count `cnt` (SGPR)."""
+        out = ["s_mov_b32 %s, %s" % (PCOFF, target),
+               "s_add_u32 %s, %s, %s" % (CNT, CNT, cnt),
+               "s_cmp_ge_u32 %s, %s" % (CNT, LIM), "s_cbranch_scc1 %s" % self.xs()]
+        if self.mode == "D":
+            out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
+        # the successor prefetch into the other bank has landed (every branch handler
+        # waited lgkmcnt(0) first), so both banks may be reloaded
+        out += ["s_load_dwordx8 %s, %s, %s" % (sbank(self.other), CODE, PCOFF),
+                "s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank(self.bank), CODE, PCOFF),
+                "s_waitcnt lgkmcnt(0)"]
+        out += self.issue_reads(self.other)
+        out += self.dispatch(self.other)
+        return out
+
+    # -- result writes
+    def w32(self, v=None):
+        return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
+                "ds_write_b32 %s, %s" % (CADDR, v or R[0])]
+
+    def w64(self, lo=None, hi=None):
+        return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
+                "ds_write2_b32 %s, %s, %s offset1:64" % (CADDR, lo or R[0], hi or R[1])]
+
+    def bool_result(self):
+        return ["v_cndmask_b32_e64 %s, 0, 1, vcc" % R[0]] + self.w32()
+
+    def cond_branch(self, cmp_lines):
+        """cmp_lines set vcc per lane (true = taken). Uniform outcome -> branch or fall
+        through; lanes that disagree -> leave (the C++ step splits the wave)."""
+        nt = self.lab("nt")
+        return cmp_lines + [
+            "s_and_b64 %s, vcc, exec" % T2,            # SCC = any lane takes it
+            "s_cbranch_scc0 %s" % nt,
+            "s_cmp_eq_u64 %s, exec" % T2,
+            "s_cbranch_scc0 %s" % self.xh(),             # split decision
+        ] + self.taken(self.x(4), self.x(7)) + ["%s:" % nt] + self.next()
+
+
+I32_BIN = {  # name -> (instruction template over (d, a, b)), b may be an SGPR
+    "ADD": "v_add_u32_e64 {d}, {a}, {b}",
+    "SUB": "v_sub_u32_e64 {d}, {a}, {b}",
+    "MUL": "v_mul_lo_u32 {d}, {a}, {b}",
+    "AND": "v_and_b32_e64 {d}, {a}, {b}",
+    "OR": "v_or_b32_e64 {d}, {a}, {b}",
+    "XOR": "v_xor_b32_e64 {d}, {a}, {b}",
+    "SHL": "v_lshlrev_b32_e64 {d}, {b}, {a}",
+    "SHR_S": "v_ashrrev_i32_e64 {d}, {b}, {a}",
+    "SHR_U": "v_lshrrev_b32_e64 {d}, {b}, {a}",
+    "ROTR": "v_alignbit_b32 {d}, {a}, {a}, {b}",
+}
+CMP = {"EQ": "eq_u", "NE": "ne_u", "LT_S": "lt_i", "LT_U": "lt_u", "GT_S": "gt_i",
+       "GT_U": "gt_u", "LE_S": "le_i", "LE_U": "le_u", "GE_S": "ge_i", "GE_U": "ge_u"}
+
+
+def specs():
+    S = []   # (slot name, [dbc ops], body)
+
+    def add(name, ops, body):
+        S.append((name, ops, body))
+
+    # ---- control
+    add("NOP_CNT", ["NOP_CNT"], lambda g: g.next())
+    add("JMP", ["JMP"], lambda g: g.taken(g.x(4), g.x(7)))
+    add("BR_IF", ["BR_IF"], lambda g: g.cond_branch(["v_cmp_ne_u32_e64 vcc, 0, %s" % A[0]]))
+    add("BR_UNLESS", ["BR_UNLESS"],
+        lambda g: g.cond_branch(["v_cmp_eq_u32_e64 vcc, 0, %s" % A[0]]))
+    for c, k in CMP.items():
+        add("BR_" + c, ["BR_" + c],
+            lambda g, k=k: g.cond_branch(["v_cmp_%s32_e64 vcc, %s, %s" % (k, A[0], B[0])]))
+        add("BR_%s_I" % c, ["BR_%s_I" % c],
+            lambda g, k=k: g.cond_branch(["v_cmp_%s32_e64 vcc, %s, %s" % (k, A[0], g.x(3))]))
+    # ---- moves / constants / select
+    add("MOV32", ["MOV32"], lambda g: g.w32(A[0]) + g.next())
+    add("MOV64", ["MOV64"], lambda g: g.w64(A[0], A[1]) + g.next())
+    add("CONST32", ["CONST32"], lambda g: ["v_mov_b32 %s, %s" % (R[0], g.x(4))] + g.w32() + g.next())
+    add("CONST64", ["CONST64"], lambda g: ["v_mov_b32 %s, %s" % (R[0], g.x(4)),
+                                           "v_mov_b32 %s, %s" % (R[1], g.x(7))] + g.w64() + g.next())
+    add("SELECT32", ["SELECT32"], lambda g: [
+        "v_cmp_ne_u32_e64 vcc, 0, %s" % D[0],
+        "v_cndmask_b32_e64 %s, %s, %s, vcc" % (R[0], B[0], A[0])] + g.w32() + g.next())
+    add("SELECT64", ["SELECT64"], lambda g: [
+        "v_cmp_ne_u32_e64 vcc, 0, %s" % D[0],
+        "v_cndmask_b32_e64 %s, %s, %s, vcc" % (R[0], B[0], A[0]),
+        "v_cndmask_b32_e64 %s, %s, %s, vcc" % (R[1], B[1], A[1])] + g.w64() + g.next())
+    # ---- i32
+    for nm, t in I32_BIN.items():
+        add("I32_" + nm, ["I32_" + nm],
+            lambda g, t=t: [t.format(d=R[0], a=A[0], b=B[0])] + g.w32() + g.next())
+        add("I32_%s_I" % nm, ["I32_%s_I" % nm],
+            lambda g, t=t: [t.format(d=R[0], a=A[0], b=g.x(4))] + g.w32() + g.next())
+    add("I32_ROTL", ["I32_ROTL"], lambda g: [
+        "v_sub_u32_e64 %s, 0, %s" % (X[0], B[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[0], A[0], A[0], X[0])] + g.w32() + g.next())
+    for c, k in CMP.items():
+        add("I32_" + c, ["I32_" + c], lambda g, k=k: [
+            "v_cmp_%s32_e64 vcc, %s, %s" % (k, A[0], B[0])] + g.bool_result() + g.next())
+        add("I32_%s_I" % c, ["I32_%s_I" % c], lambda g, k=k: [
+            "v_cmp_%s32_e64 vcc, %s, %s" % (k, A[0], g.x(4))] + g.bool_result() + g.next())
+    add("I32_EQZ", ["I32_EQZ"], lambda g: ["v_cmp_eq_u32_e64 vcc, 0, %s" % A[0]] +
+        g.bool_result() + g.next())
+    add("I32_ADD3", ["I32_ADD3"], lambda g: [
+        "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + g.next())
+    add("I32_XOR_ROTR_I", ["I32_XOR_ROTR_I"], lambda g: [
+        "v_xor_b32_e32 %s, %s, %s" % (X[0], A[0], B[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[0], X[0], X[0], g.x(4))] + g.w32() + g.next())
+    add("I32_CLZ", ["I32_CLZ"], lambda g: [
+        "v_ffbh_u32_e32 %s, %s" % (X[0], A[0]),
+        "v_min_u32_e32 %s, 32, %s" % (R[0], X[0])] + g.w32() + g.next())
+    add("I32_CTZ", ["I32_CTZ"], lambda g: [
+        "v_ffbl_b32_e32 %s, %s" % (X[0], A[0]),
+        "v_min_u32_e32 %s, 32, %s" % (R[0], X[0])] + g.w32() + g.next())
+    add("I32_POPCNT", ["I32_POPCNT"], lambda g: [
+        "v_bcnt_u32_b32 %s, %s, 0" % (R[0], A[0])] + g.w32() + g.next())
+    add("I32_EXT8S", ["I32_EXT8S"], lambda g: ["v_bfe_i32 %s, %s, 0, 8" % (R[0], A[0])] +
+        g.w32() + g.next())
+    add("I32_EXT16S", ["I32_EXT16S"], lambda g: ["v_bfe_i32 %s, %s, 0, 16" % (R[0], A[0])] +
+        g.w32() + g.next())
+    # ---- i64 (operands A = a.lo/a.hi; *_I: imm sign-extended from w4)
+    def imm64(g):   # VGPRs, so VOP3 ops keep to gfx9's one-SGPR constant-bus limit
+        return ["v_mov_b32 %s, %s" % (Z[0], g.x(4)), "v_ashrrev_i32_e32 %s, 31, %s" % (Z[1], Z[0])]
+
+    def i64_bin(name, body):   # body(g, b_lo, b_hi, b_pair) -> lines
+        add("I64_" + name, ["I64_" + name],
+            lambda g: body(g, B[0], B[1], BP) + g.w64() + g.next())
+        add("I64_%s_I" % name, ["I64_%s_I" % name],
+            lambda g: imm64(g) + body(g, Z[0], Z[1], ZP) + g.w64() + g.next())
+
+    i64_bin("ADD", lambda g, lo, hi, p: ["v_lshl_add_u64 %s, %s, 0, %s" % (RP, AP, p)])
+    i64_bin("SUB", lambda g, lo, hi, p: ["v_sub_co_u32_e64 %s, vcc, %s, %s" % (R[0], A[0], lo),
+                                         "v_subb_co_u32_e64 %s, vcc, %s, %s, vcc" % (R[1], A[1], hi)])
+    for nm, ins in (("AND", "v_and_b32_e64"), ("OR", "v_or_b32_e64"), ("XOR", "v_xor_b32_e64")):
+        i64_bin(nm, lambda g, lo, hi, p, ins=ins: ["%s %s, %s, %s" % (ins, R[0], A[0], lo),
+                                                   "%s %s, %s, %s" % (ins, R[1], A[1], hi)])
+    i64_bin("MUL", lambda g, lo, hi, p: [
+        "v_mul_hi_u32 %s, %s, %s" % (X[0], A[0], lo),
+        "v_mul_lo_u32 %s, %s, %s" % (X[1], A[0], hi),
+        "v_mul_lo_u32 %s, %s, %s" % (Y[0], A[1], lo),
+        "v_mul_lo_u32 %s, %s, %s" % (R[0], A[0], lo),
+        "v_add3_u32 %s, %s, %s, %s" % (R[1], X[0], X[1], Y[0])])
+    i64_bin("SHL", lambda g, lo, hi, p: ["v_lshlrev_b64 %s, %s, %s" % (RP, lo, AP)])
+    i64_bin("SHR_S", lambda g, lo, hi, p: ["v_ashrrev_i64 %s, %s, %s" % (RP, lo, AP)])
+    i64_bin("SHR_U", lambda g, lo, hi, p: ["v_lshrrev_b64 %s, %s, %s" % (RP, lo, AP)])
+    i64_bin("ROTL", lambda g, lo, hi, p: [
+        "v_sub_u32_e64 %s, 0, %s" % (Y[0], lo),
+        "v_lshlrev_b64 %s, %s, %s" % (XP, lo, AP),
+        "v_lshrrev_b64 %s, %s, %s" % (RP, Y[0], AP),
+        "v_or_b32_e32 %s, %s, %s" % (R[0], R[0], X[0]),
+        "v_or_b32_e32 %s, %s, %s" % (R[1], R[1], X[1])])
+    i64_bin("ROTR", lambda g, lo, hi, p: [
+        "v_sub_u32_e64 %s, 0, %s" % (Y[0], lo),
+        "v_lshrrev_b64 %s, %s, %s" % (XP, lo, AP),
+        "v_lshlrev_b64 %s, %s, %s" % (RP, Y[0], AP),
+        "v_or_b32_e32 %s, %s, %s" % (R[0], R[0], X[0]),
+        "v_or_b32_e32 %s, %s, %s" % (R[1], R[1], X[1])])
+    for c, k in CMP.items():
+        k64 = k + "64"
+        add("I64_" + c, ["I64_" + c], lambda g, k64=k64: [
+            "v_cmp_%s_e64 vcc, %s, %s" % (k64, AP, BP)] + g.bool_result() + g.next())
+        add("I64_%s_I" % c, ["I64_%s_I" % c], lambda g, k64=k64: imm64(g) + [
+            "v_cmp_%s_e64 vcc, %s, %s" % (k64, AP, ZP)] + g.bool_result() + g.next())
+    add("I64_EQZ", ["I64_EQZ"], lambda g: ["v_cmp_eq_u64_e64 vcc, 0, %s" % AP] +
+        g.bool_result() + g.next())
+    add("I64_EXTEND_I32_S", ["I64_EXTEND_I32_S", "I64_EXT32S"], lambda g: [
+        "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], A[0])] + g.w64(A[0], R[1]) + g.next())
+    add("I64_EXTEND_I32_U", ["I64_EXTEND_I32_U"], lambda g: [
+        "v_mov_b32 %s, 0" % R[1]] + g.w64(A[0], R[1]) + g.next())
+    add("I64_EXT8S", ["I64_EXT8S"], lambda g: [
+        "v_bfe_i32 %s, %s, 0, 8" % (R[0], A[0]),
+        "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], R[0])] + g.w64() + g.next())
+    add("I64_EXT16S", ["I64_EXT16S"], lambda g: [
+        "v_bfe_i32 %s, %s, 0, 16" % (R[0], A[0]),
+        "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], R[0])] + g.w64() + g.next())
+
+    # ---- linear memory. w4 = offset, w7 = offset + n - 1 (< 2^32, else the op is cold).
+    # In bounds  <=> no carry in a + (offset+n-1)  and  (last byte >> 16) < pages;
+    # natural alignment of ea (4 for n >= 4) <=> (last byte & m) == m.
+    def mem_check(g, n):
+        out = ["v_add_co_u32_e64 %s, %s, %s, %s" % (X[0], T2, A[0], g.x(7)),   # last byte
+               "v_lshrrev_b32_e32 %s, 16, %s" % (X[1], X[0]),
+               "v_cmp_ge_u32_e64 vcc, %s, %s" % (X[1], PAGES),
+               "s_or_b64 %s, %s, vcc" % (T2, T2)]
+        m = 3 if n >= 4 else n - 1
+        if m:
+            out += ["v_and_b32_e32 %s, %d, %s" % (Y[0], m, X[0]),
+                    "v_cmp_ne_u32_e64 vcc, %d, %s" % (m, Y[0]),
+                    "s_or_b64 %s, %s, vcc" % (T2, T2)]
+        out += ["s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh(),
+                # address = mem + (ea >> 2) * 256 (+ ea & 3 for sub-word)
+                "v_add_u32_e64 %s, %s, %s" % (Y[0], A[0], g.x(4)),
+                "v_lshrrev_b32_e32 %s, 2, %s" % (W[0], Y[0]),
+                "v_lshlrev_b64 %s, 8, %s" % (XP, WP),          # W[1] is always 0
+                "v_lshl_add_u64 %s, %s, 0, %s" % (XP, XP, MEM)]
+        if n < 4:   # byte within the lane's word
+            out += ["v_and_b32_e32 %s, 3, %s" % (W[0], Y[0]),
+                    "v_lshl_add_u64 %s, %s, 0, %s" % (XP, WP, XP)]
+        return out
+
+    LOADS = {   # name -> (bytes, load instr, result width, sign-extend high word)
+        "LD32": (4, "global_load_dword", 32, None),
+        "LD8U32": (1, "global_load_ubyte", 32, None),
+        "LD8S32": (1, "global_load_sbyte", 32, None),
+        "LD16U32": (2, "global_load_ushort", 32, None),
+        "LD16S32": (2, "global_load_sshort", 32, None),
+        "LD32U64": (4, "global_load_dword", 64, "zero"),
+        "LD32S64": (4, "global_load_dword", 64, "sign"),
+        "LD8U64": (1, "global_load_ubyte", 64, "zero"),
+        "LD8S64": (1, "global_load_sbyte", 64, "sign"),
+        "LD16U64": (2, "global_load_ushort", 64, "zero"),
+        "LD16S64": (2, "global_load_sshort", 64, "sign"),
+    }
+    for nm, (n, ins, width, ext) in LOADS.items():
+        def body(g, n=n, ins=ins, width=width, ext=ext):
+            out = mem_check(g, n) + ["%s %s, %s, off" % (ins, R[0], XP), "s_waitcnt vmcnt(0)"]
+            if width == 32:
+                return out + g.w32() + g.next()
+            hi = "v_mov_b32 %s, 0" % R[1] if ext == "zero" else \
+                "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], R[0])
+            return out + [hi] + g.w64() + g.next()
+        add(nm, [nm], body)
+    add("LD64", ["LD64"], lambda g: mem_check(g, 8) + [
+        "global_load_dword %s, %s, off" % (R[0], XP),
+        "global_load_dword %s, %s, off offset:256" % (R[1], XP),
+        "s_waitcnt vmcnt(0)"] + g.w64() + g.next())
+    STORES = {"ST8": (1, "global_store_byte"), "ST16": (2, "global_store_short"),
+              "ST32": (4, "global_store_dword")}
+    for nm, (n, ins) in STORES.items():
+        add(nm, [nm], lambda g, n=n, ins=ins: mem_check(g, n) + [
+            "%s %s, %s, off" % (ins, XP, B[0])] + g.next())
+    add("ST64", ["ST64"], lambda g: mem_check(g, 8) + [
+        "global_store_dword %s, %s, off" % (XP, B[0]),
+        "global_store_dword %s, %s, off offset:256" % (XP, B[1])] + g.next())
+    return S
+
+
+SPECIAL_REMAP = {   # DBC op -> (slot op, immediate transform) applied by the translator
+    "I32_ROTL_I": ("I32_ROTR_I", "neg32"),
+    "I32_XOR_ROTL_I": ("I32_XOR_ROTR_I", "neg32"),
+}
+
+
+def main():
+    S = specs()
+    names = ["COLD"] + [s[0] for s in S]
+    nslots = len(names)
+    bank_bytes = nslots * SLOT
+    L = []
+    e = L.append
+    e(".text")
+    e(".p2align 8")
+    # ------------------------------------------------------------- entry
+    # in: CODE, PCOFF (pc*32 of the first instruction), OTHER, LIM, CNT=0, RET,
+    #     FR, PAGES, MEM.  EXEC = the active lanes.
+    e("wb_tc_entry:")
+    e("s_getpc_b64 s[70:71]")
+    e("Ltc_pc0:")
+    e("s_add_u32 s70, s70, Ltc_banks - Ltc_pc0")
+    e("s_addc_u32 s71, s71, 0")
+    e("s_cmp_eq_u32 %s, -1" % OTHER)                  # converged: banks 0/1
+    e("s_cselect_b32 %s, 0, %d" % (T[0], 2 * bank_bytes))
+    e("s_add_u32 s70, s70, %s" % T[0])
+    e("s_addc_u32 s71, s71, 0")
+    e("s_add_u32 s72, s70, %d" % bank_bytes)
+    e("s_addc_u32 s73, s71, 0")
+    e("v_mov_b32 %s, 0" % W[1])
+    e("s_load_dwordx8 %s, %s, %s" % (sbank("A"), CODE, PCOFF))
+    e("s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank("B"), CODE, PCOFF))
+    e("s_waitcnt lgkmcnt(0)")
+    g0 = Gen("C", "B")
+    for ln in g0.issue_reads("A") + g0.dispatch("A"):
+        e(ln)
+    # ------------------------------------------------------------- banks
+    e(".p2align 8")
+    e("Ltc_banks:")
+    for mode in ("C", "D"):
+        for bank in ("A", "B"):
+            for si, nm in enumerate(names):
+                g = Gen(mode, bank)
+                lab = "Ltc_%s%s_%d" % (mode, bank, si)
+                e(".p2align 8")
+                e("%s:" % lab)
+                if nm == "COLD":
+                    # leave before this instruction (reason 0) / at PCOFF for the
+                    # scheduler (reason 1); outstanding memory ops drained first
+                    body = ["%s:" % g.xh(), "s_mov_b32 %s, 0" % REASON,
+                            "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET,
+                            "%s:" % g.xs(), "s_mov_b32 %s, 1" % REASON,
+                            "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET]
+                else:
+                    spec = S[si - 1][2]
+                    body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
+                for ln in body:
+                    e(ln)
+                e(".if (. - %s) > %d" % (lab, SLOT))
+                e('.error "threaded-code handler %s exceeds its slot"' % nm)
+                e(".endif")
+    e(".p2align 8")
+    e("Ltc_banks_end:")
+    with open(os.path.join(HERE, "tc_blob.inc"), "w") as f:
+        f.write("// GENERATED by gen_tc.py -- do not edit. Handler blob of the threaded core.\n")
+        for ln in L:
+            f.write('"%s\\n"\n' % ln.replace('"', '\\"'))
+    # ------------------------------------------------------------- slot map
+    with open(os.path.join(HERE, "tc_slots.h"), "w") as f:
+        f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
+        f.write("#pragma once\n#include \"dbc.h\"\n\n")
+        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n\n" % (SLOT, nslots))
+        f.write("// returns the handler slot (0 = no handler: the C++ step runs the op)\n")
+        f.write("static inline int tc_slot(uint16_t op) {\n  switch (op) {\n")
+        for si, (nm, ops, _) in enumerate(S, start=1):
+            for op in ops:
+                f.write("    case OP_%s: return %d;   // %s\n" % (op, si, nm))
+        for op, (to, _) in SPECIAL_REMAP.items():
+            f.write("    case OP_%s: return %d;   // via %s\n" % (op, names.index(to), to))
+        f.write("    default: return 0;\n  }\n}\n")
+    print("tc: %d slots, %d bytes per bank" % (nslots, bank_bytes), file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,7 @@ struct KParams {
   const uint8_t *data_pool;     // passive/active data bytes (memory.init)
   const uint32_t *data_off;
   const uint32_t *data_len;
+  const void *tcode;            // threaded code for the dispatch core (tc.h), or NULL
   // per-lane state (lane-interleaved per wave)
   uint32_t *mem;                // linear memory, [wave][word][64]
   uint32_t *gstack;             // spilled frames, [wave][slot][64]

@@ -1,0 +1,69 @@
+// tc.cpp -- host translation of the DBC program into threaded code for the gfx950
+// dispatch core (gen_tc.py / tc_blob.inc). Field layout: tc.h.
+#include "tc.h"
+
+#include "frontend.h"
+#include "tc_slots.h"
+
+namespace wb {
+
+static uint32_t mem_bytes(uint16_t op) {
+  switch (op) {
+    case OP_LD8S32: case OP_LD8U32: case OP_LD8S64: case OP_LD8U64: case OP_ST8: return 1;
+    case OP_LD16S32: case OP_LD16U32: case OP_LD16S64: case OP_LD16U64: case OP_ST16: return 2;
+    case OP_LD32: case OP_LD32S64: case OP_LD32U64: case OP_ST32: return 4;
+    case OP_LD64: case OP_ST64: return 8;
+    default: return 0;
+  }
+}
+
+static bool is_branch(uint16_t op) {
+  return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS ||
+         (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
+}
+
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) {
+  const uint32_t T = P.total_cells();
+  auto off = [T](uint32_t cell) { return cell < T ? cell * 256u : 0u; };
+  std::vector<TInstr> tc(P.code.size() + 2, TInstr{{0, 0, 0, 0, 0, 0, 0, 0}});
+  for (size_t pc = 0; pc < P.code.size(); pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
+    const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
+    const uint32_t imm = I.w3, cnt = (I.w0 >> 16) & 0xFFu;
+    int slot = tc_slot(op);
+    if (!slot) continue;
+    TInstr &t = tc[pc];
+    uint32_t *w = t.w;
+    w[1] = off(a); w[2] = off(b); w[3] = off(c); w[4] = imm; w[5] = 0; w[6] = cnt; w[7] = 0;
+    if (op == OP_I32_ADD3 || op == OP_SELECT32 || op == OP_SELECT64) w[5] = off(d);
+    if (is_branch(op)) {
+      const int32_t taken = int32_t(cnt) + int32_t(int16_t(d));
+      if (taken < 0 || imm >= (1u << 26)) continue;
+      w[4] = imm * 32u;
+      w[7] = uint32_t(taken);
+      if (op >= OP_BR_EQ_I && op <= OP_BR_GE_U_I) {
+        w[3] = uint32_t(int32_t(int16_t(b)));
+        w[2] = 0;
+      } else {
+        w[3] = 0;
+      }
+    } else if (const uint32_t n = mem_bytes(op)) {
+      const uint64_t last = uint64_t(imm) + n - 1;
+      if (last > 0xFFFFFFFFull) continue;
+      w[7] = uint32_t(last);
+    } else if (op == OP_CONST64) {
+      w[7] = I.w1;   // high word
+      w[1] = w[2] = 0;
+    } else if (op == OP_CONST32) {
+      w[1] = w[2] = 0;
+    } else if (op == OP_I32_ROTL_I || op == OP_I32_XOR_ROTL_I) {
+      w[4] = (32u - (imm & 31u)) & 31u;     // rotl k == rotr -k
+    }
+    w[0] = uint32_t(slot) * TC_SLOT_BYTES;
+    code[pc].w0 |= DBC_HOT;
+  }
+  return tc;
+}
+
+}  // namespace wb

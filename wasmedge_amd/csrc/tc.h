@@ -1,0 +1,29 @@
+// tc.h -- threaded code (TInstr) for the hand-written dispatch core (gen_tc.py).
+//
+// One TInstr per DBC instruction (same pc), 32 bytes = one s_load_dwordx8:
+//   w0 handler byte offset within a bank (slot * TC_SLOT_BYTES; 0 = no handler)
+//   w1 a, w2 b, w5 d: LDS byte offsets (cell * 256) of the operands the core reads
+//      ahead for every instruction (always valid cells)
+//   w3 c: destination cell offset; compare-and-branch *_I: the sign-extended imm16
+//   w4 immediate / memarg offset; branches: target pc * 32
+//   w6 wasm instructions retired when the instruction falls through
+//   w7 branches: instructions retired when taken (cnt + tcnt); loads/stores:
+//      offset + bytes - 1; const64: the high word
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "dbc.h"
+
+#define DBC_HOT 0x8000u   // w0 bit 15 of a DBC instruction: the core has a handler
+
+struct TInstr {
+  uint32_t w[8];
+};
+
+namespace wb {
+struct Program;
+// Build the TInstr array for P (size = code + 2 padding entries for the core's
+// successor prefetch) and mark DBC_HOT on the device copy `code` of P.code.
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code);
+}  // namespace wb
