@@ -129,6 +129,10 @@ struct DInstr {
   X(V_LD8X8S) X(V_LD8X8U) X(V_LD16X4S) X(V_LD16X4U) X(V_LD32X2S) X(V_LD32X2U)          \
   X(V_LD8SPLAT) X(V_LD16SPLAT) X(V_LD32SPLAT) X(V_LD64SPLAT) X(V_LD32ZERO)             \
   X(V_LD64ZERO)                                                                        \
+  /* generic lane-wise ops, imm = the 0xFD sub-opcode: c = op(a, b) / c = op(a)        */ \
+  X(V_BINX) X(V_UNX)                                                                   \
+  /* a = address cell, b = vector cell, c = dst, d = lane | log2(bytes) << 8, imm = off */ \
+  X(V_LDLANE) X(V_STLANE)                                                              \
   X(DBC_NUM_OPS)
 
 enum DOp : uint16_t {

@@ -142,6 +142,213 @@ WB_HD uint64_t trunc_sat(double z, bool in32, bool sgn, bool out64) {
   return sel64(z != z, 0, sel64(e == 0, r, sel64(z < 0, lo, hi)));
 }
 
+// ------------------------------------------------------------- SIMD128 lane-wise ops
+// The v128 value is four 32-bit cells, little-endian: lane k of width W bytes is bits
+// [8*W*k, 8*W*(k+1)) of the 128-bit value. All loops below have constant trip counts and
+// are unrolled, so lane indices fold to constants (no scratch).
+WB_HD uint32_t vlane(const uint32_t *v, uint32_t W, uint32_t k) {
+  const uint32_t bit = 8 * W * k;
+  return W == 4 ? v[k] : (v[bit >> 5] >> (bit & 31)) & ((1u << (8 * W)) - 1u);
+}
+WB_HD void vlane_set(uint32_t *v, uint32_t W, uint32_t k, uint32_t x) {
+  const uint32_t bit = 8 * W * k;
+  if (W == 4) { v[k] = x; return; }
+  const uint32_t m = ((1u << (8 * W)) - 1u) << (bit & 31);
+  v[bit >> 5] = (v[bit >> 5] & ~m) | ((x << (bit & 31)) & m);
+}
+WB_HD int32_t vsx(uint32_t x, uint32_t W) {   // sign-extend a W-byte lane
+  return W == 4 ? (int32_t)x : (int32_t)(x << (32 - 8 * W)) >> (32 - 8 * W);
+}
+WB_HD int32_t vclamp(int32_t x, int32_t lo, int32_t hi) { return x < lo ? lo : x > hi ? hi : x; }
+
+// OP_V_BINX: c = op(a, b) for the binary 0xFD ops without a dedicated DOp
+// (binary_numeric.ipp:203-567: compares 264-313 (V1 < V2 etc. on signed/unsigned lanes),
+// narrow 285-314, add/sub_sat 349-398, min/max 412-440, avgr 477-491, extmul 493-552,
+// q15mulr 554-566; i32x4.dot engine.cpp:1579-1593).
+WB_HD void vbinx(uint32_t sub, const uint32_t *x, const uint32_t *y, uint32_t *r) {
+  uint32_t o[4] = {0, 0, 0, 0};
+#define WB_LW(W, EXPR) { _Pragma("unroll") for (uint32_t k = 0; k < 16 / (W); k++) { \
+    const uint32_t a = vlane(x, W, k), b = vlane(y, W, k); \
+    const int32_t as = vsx(a, W), bs = vsx(b, W); (void)a; (void)b; (void)as; (void)bs; \
+    vlane_set(o, W, k, (uint32_t)(EXPR)); } } break
+  switch (sub) {
+    // i8x16 / i16x8 ordered compares: lt_s lt_u gt_s gt_u le_s le_u ge_s ge_u
+    case 0x25: WB_LW(1, as < bs ? ~0u : 0u);  case 0x26: WB_LW(1, a < b ? ~0u : 0u);
+    case 0x27: WB_LW(1, as > bs ? ~0u : 0u);  case 0x28: WB_LW(1, a > b ? ~0u : 0u);
+    case 0x29: WB_LW(1, as <= bs ? ~0u : 0u); case 0x2A: WB_LW(1, a <= b ? ~0u : 0u);
+    case 0x2B: WB_LW(1, as >= bs ? ~0u : 0u); case 0x2C: WB_LW(1, a >= b ? ~0u : 0u);
+    case 0x2F: WB_LW(2, as < bs ? ~0u : 0u);  case 0x30: WB_LW(2, a < b ? ~0u : 0u);
+    case 0x31: WB_LW(2, as > bs ? ~0u : 0u);  case 0x32: WB_LW(2, a > b ? ~0u : 0u);
+    case 0x33: WB_LW(2, as <= bs ? ~0u : 0u); case 0x34: WB_LW(2, a <= b ? ~0u : 0u);
+    case 0x35: WB_LW(2, as >= bs ? ~0u : 0u); case 0x36: WB_LW(2, a >= b ? ~0u : 0u);
+    // saturating add/sub, min/max, rounding average
+    case 0x6F: WB_LW(1, vclamp(as + bs, -128, 127));
+    case 0x70: WB_LW(1, a + b > 255u ? 255u : a + b);
+    case 0x72: WB_LW(1, vclamp(as - bs, -128, 127));
+    case 0x73: WB_LW(1, a > b ? a - b : 0u);
+    case 0x76: WB_LW(1, as > bs ? b : a);  case 0x77: WB_LW(1, a > b ? b : a);
+    case 0x78: WB_LW(1, bs > as ? b : a);  case 0x79: WB_LW(1, b > a ? b : a);
+    case 0x7B: WB_LW(1, (a + b + 1) >> 1);
+    case 0x82: WB_LW(2, vclamp((as * bs + 0x4000) >> 15, -32768, 32767));
+    case 0x8F: WB_LW(2, vclamp(as + bs, -32768, 32767));
+    case 0x90: WB_LW(2, a + b > 65535u ? 65535u : a + b);
+    case 0x92: WB_LW(2, vclamp(as - bs, -32768, 32767));
+    case 0x93: WB_LW(2, a > b ? a - b : 0u);
+    case 0x96: WB_LW(2, as > bs ? b : a);  case 0x97: WB_LW(2, a > b ? b : a);
+    case 0x98: WB_LW(2, bs > as ? b : a);  case 0x99: WB_LW(2, b > a ? b : a);
+    case 0x9B: WB_LW(2, (a + b + 1) >> 1);
+    case 0xB6: WB_LW(4, as > bs ? b : a);  case 0xB7: WB_LW(4, a > b ? b : a);
+    case 0xB8: WB_LW(4, bs > as ? b : a);  case 0xB9: WB_LW(4, b > a ? b : a);
+    // narrow: x's lanes then y's, saturated to the half width
+    case 0x65: case 0x66: case 0x85: case 0x86: {
+      const uint32_t W = (sub == 0x65 || sub == 0x66) ? 1 : 2, n = 8 / W;
+      const bool sg = sub == 0x65 || sub == 0x85;
+      const int32_t lo = sg ? -(1 << (8 * W - 1)) : 0;
+      const int32_t hi = sg ? (1 << (8 * W - 1)) - 1 : (1 << (8 * W)) - 1;
+      _Pragma("unroll") for (uint32_t k = 0; k < 8; k++) {
+        if (k < n) {
+          vlane_set(o, W, k, (uint32_t)vclamp(vsx(vlane(x, 2 * W, k), 2 * W), lo, hi));
+          vlane_set(o, W, k + n, (uint32_t)vclamp(vsx(vlane(y, 2 * W, k), 2 * W), lo, hi));
+        }
+      }
+      break;
+    }
+    // extmul low/high (s, u) into 16- and 32-bit lanes
+    case 0x9C: case 0x9D: case 0x9E: case 0x9F: case 0xBC: case 0xBD: case 0xBE: case 0xBF: {
+      const uint32_t W = sub < 0xBC ? 1 : 2, n = 8 / W, off = (sub & 1) ? n : 0;
+      const bool sg = (sub & 2) == 0;
+      _Pragma("unroll") for (uint32_t k = 0; k < 8; k++) {
+        if (k < n) {
+          const uint32_t a = vlane(x, W, k + off), b = vlane(y, W, k + off);
+          const uint32_t p = sg ? (uint32_t)(vsx(a, W) * vsx(b, W)) : a * b;
+          vlane_set(o, 2 * W, k, p);
+        }
+      }
+      break;
+    }
+    case 0xDC: case 0xDD: case 0xDE: case 0xDF: {   // i64x2.extmul_{low,high}_i32x4_{s,u}
+      const uint32_t off = (sub & 1) ? 2 : 0;
+      _Pragma("unroll") for (uint32_t k = 0; k < 2; k++) {
+        const uint64_t p = (sub & 2) ? (uint64_t)x[k + off] * y[k + off]
+                                     : (uint64_t)((int64_t)(int32_t)x[k + off] * (int32_t)y[k + off]);
+        o[2 * k] = (uint32_t)p; o[2 * k + 1] = (uint32_t)(p >> 32);
+      }
+      break;
+    }
+    case 0xBA: {   // i32x4.dot_i16x8_s: pairwise products summed (wrapping)
+      _Pragma("unroll") for (uint32_t k = 0; k < 4; k++)
+        o[k] = (uint32_t)(vsx(vlane(x, 2, 2 * k), 2) * vsx(vlane(y, 2, 2 * k), 2)) +
+               (uint32_t)(vsx(vlane(x, 2, 2 * k + 1), 2) * vsx(vlane(y, 2, 2 * k + 1), 2));
+      break;
+    }
+    default: break;
+  }
+#undef WB_LW
+  r[0] = o[0]; r[1] = o[1]; r[2] = o[2]; r[3] = o[3];
+}
+
+WB_HD uint32_t demote_bits(uint64_t a) {   // cast_numeric.ipp f32.demote_f64 (x86 NaN)
+  uint32_t r = b32((float)f64(a));
+  if (isnan64(a)) r = (uint32_t)(a >> 32 & 0x80000000u) | 0x7FC00000u | (uint32_t)((a >> 29) & 0x003FFFFFu);
+  return r;
+}
+WB_HD uint64_t promote_bits(uint32_t a) {
+  uint64_t r = b64((double)f32(a));
+  if (isnan32(a)) r = ((uint64_t)(a & 0x80000000u) << 32) | 0x7FF8000000000000ull | ((uint64_t)(a & 0x003FFFFFu) << 29);
+  return r;
+}
+
+// OP_V_UNX: c = op(a) for the unary 0xFD ops without a dedicated DOp
+// (unary_numeric.ipp:98-415: extend 121-165, extadd_pairwise 167-178, abs/neg 180-207,
+// popcnt 209-216, trunc_sat 230-267, convert 269-282, demote/promote 284-297,
+// ceil/floor/trunc/nearest 372-412).
+WB_HD void vunx(uint32_t sub, const uint32_t *x, uint32_t *r) {
+  uint32_t o[4] = {0, 0, 0, 0};
+#define WB_LU(W, EXPR) { _Pragma("unroll") for (uint32_t k = 0; k < 16 / (W); k++) { \
+    const uint32_t a = vlane(x, W, k); const int32_t as = vsx(a, W); (void)a; (void)as; \
+    vlane_set(o, W, k, (uint32_t)(EXPR)); } } break
+  switch (sub) {
+    case 0x60: WB_LU(1, as < 0 ? 0u - a : a);
+    case 0x61: WB_LU(1, 0u - a);
+    case 0x62: WB_LU(1, __builtin_popcount(a));
+    case 0x80: WB_LU(2, as < 0 ? 0u - a : a);
+    case 0x81: WB_LU(2, 0u - a);
+    case 0x67: WB_LU(4, nan_fix32(b32(ceilf(f32(a))), a, a));
+    case 0x68: WB_LU(4, nan_fix32(b32(floorf(f32(a))), a, a));
+    case 0x69: WB_LU(4, nan_fix32(b32(truncf(f32(a))), a, a));
+    case 0x6A: WB_LU(4, nan_fix32(b32(rintf(f32(a))), a, a));
+    case 0xF8: WB_LU(4, (uint32_t)trunc_sat((double)f32(a), true, true, false));
+    case 0xF9: WB_LU(4, (uint32_t)trunc_sat((double)f32(a), true, false, false));
+    case 0xFA: WB_LU(4, b32((float)(int32_t)a));
+    case 0xFB: WB_LU(4, b32((float)a));
+    case 0x74: case 0x75: case 0x7A: case 0x94: {
+      _Pragma("unroll") for (uint32_t k = 0; k < 2; k++) {
+        const uint64_t a = x[2 * k] | ((uint64_t)x[2 * k + 1] << 32);
+        const double d = f64(a);
+        const double t = sub == 0x74 ? ceil(d) : sub == 0x75 ? floor(d) : sub == 0x7A ? trunc(d) : rint(d);
+        const uint64_t v = nan_fix64(b64(t), a, a);
+        o[2 * k] = (uint32_t)v; o[2 * k + 1] = (uint32_t)(v >> 32);
+      }
+      break;
+    }
+    case 0x7C: case 0x7D: case 0x7E: case 0x7F: {   // extadd_pairwise
+      const uint32_t W = sub <= 0x7D ? 1 : 2;
+      const bool sg = (sub & 1) == 0;
+      _Pragma("unroll") for (uint32_t k = 0; k < 8; k++) {
+        if (k < 8 / W) {
+          const uint32_t a = vlane(x, W, 2 * k), b = vlane(x, W, 2 * k + 1);
+          vlane_set(o, 2 * W, k, sg ? (uint32_t)(vsx(a, W) + vsx(b, W)) : a + b);
+        }
+      }
+      break;
+    }
+    case 0x87: case 0x88: case 0x89: case 0x8A: case 0xA7: case 0xA8: case 0xA9: case 0xAA: {
+      const uint32_t W = sub <= 0x8A ? 1 : 2, n = 8 / W, off = (sub & 1) ? 0 : n;
+      const bool sg = sub == 0x87 || sub == 0x88 || sub == 0xA7 || sub == 0xA8;
+      _Pragma("unroll") for (uint32_t k = 0; k < 8; k++) {
+        if (k < n) {
+          const uint32_t a = vlane(x, W, k + off);
+          vlane_set(o, 2 * W, k, sg ? (uint32_t)vsx(a, W) : a);
+        }
+      }
+      break;
+    }
+    case 0xC7: case 0xC8: case 0xC9: case 0xCA: {   // i64x2.extend_{low,high}_i32x4_{s,u}
+      const uint32_t off = (sub & 1) ? 0 : 2;
+      const bool sg = sub <= 0xC8;
+      _Pragma("unroll") for (uint32_t k = 0; k < 2; k++) {
+        o[2 * k] = x[k + off];
+        o[2 * k + 1] = sg && (int32_t)x[k + off] < 0 ? ~0u : 0u;
+      }
+      break;
+    }
+    case 0xFC: case 0xFD: {   // i32x4.trunc_sat_f64x2_{s,u}_zero
+      _Pragma("unroll") for (uint32_t k = 0; k < 2; k++)
+        o[k] = (uint32_t)trunc_sat(f64(x[2 * k] | ((uint64_t)x[2 * k + 1] << 32)), false, sub == 0xFC, false);
+      break;
+    }
+    case 0xFE: case 0xFF: {   // f64x2.convert_low_i32x4_{s,u}
+      _Pragma("unroll") for (uint32_t k = 0; k < 2; k++) {
+        const uint64_t v = b64(sub == 0xFE ? (double)(int32_t)x[k] : (double)x[k]);
+        o[2 * k] = (uint32_t)v; o[2 * k + 1] = (uint32_t)(v >> 32);
+      }
+      break;
+    }
+    case 0x5E:   // f32x4.demote_f64x2_zero
+      o[0] = demote_bits(x[0] | ((uint64_t)x[1] << 32));
+      o[1] = demote_bits(x[2] | ((uint64_t)x[3] << 32));
+      break;
+    case 0x5F: {   // f64x2.promote_low_f32x4
+      const uint64_t p0 = promote_bits(x[0]), p1 = promote_bits(x[1]);
+      o[0] = (uint32_t)p0; o[1] = (uint32_t)(p0 >> 32); o[2] = (uint32_t)p1; o[3] = (uint32_t)(p1 >> 32);
+      break;
+    }
+    default: break;
+  }
+#undef WB_LU
+  r[0] = o[0]; r[1] = o[1]; r[2] = o[2]; r[3] = o[3];
+}
+
 // ------------------------------------------------------------- linear memory access
 // m points at word 0 of this lane (stride 64 words between consecutive words).
 WB_HD uint32_t mword(const uint32_t *m, uint32_t w) {

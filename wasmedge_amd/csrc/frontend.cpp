@@ -67,6 +67,7 @@ struct SimpleOp {
   int16_t dop_imm;     // register-immediate variant, -1 if none
   const char *sig;     // "pops:pushes", i=i32 l=i64 f=f32 d=f64 v=v128
   bool commutative;
+  uint32_t imm = 0;    // OP_V_BINX / OP_V_UNX: the 0xFD sub-opcode
 };
 
 std::unordered_map<uint16_t, SimpleOp> build_simple() {
@@ -132,7 +133,7 @@ std::unordered_map<uint16_t, SimpleOp> build_simple() {
                           OP_I64_TRUNC_SAT_F64_S, OP_I64_TRUNC_SAT_F64_U};
   const char *satsig[] = {"f:i", "f:i", "d:i", "d:i", "f:l", "f:l", "d:l", "d:l"};
   for (int k = 0; k < 8; k++) add(0xFC00 + k, sat[k], -1, satsig[k]);
-  // SIMD subset lowered in this round (the rest are rejected at load time)
+  // SIMD128 (engine.cpp:748-1609): ops with a dedicated DOp
   add(0xFD4D, OP_V_NOT, -1, "v:v"); add(0xFD4E, OP_V_AND, -1, "vv:v", true);
   add(0xFD4F, OP_V_ANDNOT, -1, "vv:v"); add(0xFD50, OP_V_OR, -1, "vv:v", true);
   add(0xFD51, OP_V_XOR, -1, "vv:v", true); add(0xFD52, OP_V_BITSELECT, -1, "vvv:v");
@@ -185,6 +186,23 @@ std::unordered_map<uint16_t, SimpleOp> build_simple() {
   add(0xFDE3, OP_V_F32X4_SQRT, -1, "v:v");
   add(0xFDEC, OP_V_F64X2_ABS, -1, "v:v"); add(0xFDED, OP_V_F64X2_NEG, -1, "v:v");
   add(0xFDEF, OP_V_F64X2_SQRT, -1, "v:v");
+  // the remaining lane-wise SIMD ops share two generic DOps keyed by the sub-opcode
+  // (binary_numeric.ipp:203-567, unary_numeric.ipp:98-415, engine.cpp:748-1609)
+  auto addx = [&](uint16_t w, uint16_t d, const char *s) { t[w] = SimpleOp{d, -1, s, false, uint32_t(w & 0xFF)}; };
+  const uint8_t binx[] = {0x25, 0x26, 0x27, 0x28, 0x29, 0x2A, 0x2B, 0x2C,   // i8x16 lt..ge
+                          0x2F, 0x30, 0x31, 0x32, 0x33, 0x34, 0x35, 0x36,   // i16x8 lt..ge
+                          0x65, 0x66, 0x85, 0x86,                           // narrow
+                          0x6F, 0x70, 0x72, 0x73, 0x76, 0x77, 0x78, 0x79, 0x7B,
+                          0x82, 0x8F, 0x90, 0x92, 0x93, 0x96, 0x97, 0x98, 0x99, 0x9B,
+                          0x9C, 0x9D, 0x9E, 0x9F,                           // i16x8 extmul
+                          0xB6, 0xB7, 0xB8, 0xB9, 0xBA, 0xBC, 0xBD, 0xBE, 0xBF,
+                          0xDC, 0xDD, 0xDE, 0xDF};                          // i64x2 extmul
+  for (uint8_t w : binx) addx(0xFD00 | w, OP_V_BINX, "vv:v");
+  const uint8_t unx[] = {0x5E, 0x5F, 0x60, 0x61, 0x62, 0x67, 0x68, 0x69, 0x6A, 0x74, 0x75,
+                         0x7A, 0x94, 0x7C, 0x7D, 0x7E, 0x7F, 0x80, 0x81, 0x87, 0x88, 0x89,
+                         0x8A, 0xA7, 0xA8, 0xA9, 0xAA, 0xC7, 0xC8, 0xC9, 0xCA, 0xF8, 0xF9,
+                         0xFA, 0xFB, 0xFC, 0xFD, 0xFE, 0xFF};
+  for (uint8_t w : unx) addx(0xFD00 | w, OP_V_UNX, "v:v");
   return t;
 }
 
@@ -293,7 +311,7 @@ class Lowerer {
       case OP_TABLE_GET: case OP_V_LD8X8S: case OP_V_LD8X8U: case OP_V_LD16X4S:
       case OP_V_LD16X4U: case OP_V_LD32X2S: case OP_V_LD32X2U: case OP_V_LD8SPLAT:
       case OP_V_LD16SPLAT: case OP_V_LD32SPLAT: case OP_V_LD64SPLAT: case OP_V_LD32ZERO:
-      case OP_V_LD64ZERO:
+      case OP_V_LD64ZERO: case OP_V_LDLANE: case OP_V_STLANE:
         return true;
       default:
         return op >= OP_BR_EQ && op <= OP_BR_GE_U_I;
@@ -573,7 +591,7 @@ void Lowerer::do_simple(const SimpleOp &s) {
   uint32_t a = npop >= 1 ? src(ops[0]) : 0;
   uint32_t b = npop >= 2 ? src(ops[1]) : 0;
   uint32_t d = npop >= 3 ? src(ops[2]) : 0;
-  emit(s.dop, a, b, c, d);
+  emit(s.dop, a, b, c, d, s.imm);
   if (rt) push_cell(rt, last_emit);
 }
 
@@ -1161,6 +1179,22 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
       case 0xFD5C: do_load(OP_V_LD32ZERO, V128, r); break;
       case 0xFD5D: do_load(OP_V_LD64ZERO, V128, r); break;
       case 0xFD0B: do_store(OP_ST128, V128, r); break;
+      case 0xFD54: case 0xFD55: case 0xFD56: case 0xFD57:     // v128.loadN_lane
+      case 0xFD58: case 0xFD59: case 0xFD5A: case 0xFD5B: {   // v128.storeN_lane
+        const bool ld = op <= 0xFD57;
+        const uint32_t lg = (op - 0xFD54) & 3;                 // log2 of the lane bytes
+        r.u32();
+        uint32_t off = r.u32();
+        uint8_t lane = r.u8();
+        if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        if (lane >= (16u >> lg)) fail(E_TYPECHECK, "invalid lane index");
+        Entry v = pop_t(V128), a = pop_t(I32);
+        if (!live()) { if (ld) push_cell(V128); break; }
+        uint32_t ac = src(a), vc = src(v);
+        emit(ld ? OP_V_LDLANE : OP_V_STLANE, ac, vc, ld ? a.cell : 0, lane | (lg << 8), off);
+        if (ld) push_cell(V128, last_emit);
+        break;
+      }
       case 0xFD0C: {
         uint32_t k[4];
         for (int q = 0; q < 4; q++) {
