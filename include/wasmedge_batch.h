@@ -78,14 +78,17 @@ typedef struct WasmEdge_BatchConfigure {
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
 
-/* Load + validate + lower `WasmBuf` and allocate device state for NumInstances
- * instances. Replaces VM::loadWasm/validate/instantiate (lib/vm/vm.cpp) for the batch.
- * Returns NULL on failure with the ErrCode in *Res (may be NULL). */
+/* Load + validate + lower `WasmBuf`, allocate device state for NumInstances instances
+ * and instantiate them (BatchReset). Replaces VM::loadWasm/validate/instantiate
+ * (lib/vm/vm.cpp) for the batch. Returns NULL on failure with the ErrCode in *Res (may
+ * be NULL). */
 WASMEDGE_BATCH_API WasmEdge_BatchContext *
 WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf, const uint8_t *WasmBuf,
                      uint32_t WasmLen, uint32_t NumInstances, WasmEdge_Result *Res);
 
-/* Run `FuncName` on every instance from a fresh instantiation (one instance per lane).
+/* Run `FuncName` on every instance (one instance per lane). Instance state -- linear
+ * memory and its size, globals, dropped data segments -- persists from one Execute/Run
+ * to the next until BatchReset, as an instantiated module does in the reference VM.
  * Params: [NumInstances][ParamLen] row-major; Returns: [NumInstances][ReturnLen].
  * PerInstance[i]: 0 ok, else trap/status code. InstrCounts[i]: the reference's
  * instruction count (include/common/statistics.h:44). Either may be NULL.
@@ -99,7 +102,9 @@ WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName
 /* Staged form of BatchExecute, for callers that keep inputs resident on the device
  * and time the interpreter alone (bench.py):
  *   SetArgs  -> resolve FuncName, check types (FuncSigMismatch), upload params
- *   Reset    -> fresh instances: memory image + globals (lib/executor/instantiate/)
+ *   Reset    -> fresh instances: memory image, globals, then the start function
+ *               (lib/executor/instantiate/module.cpp:16-172); a lane whose start
+ *               function traps reports that trap from every later Run
  *   Run      -> launch the interpreter; *KernelSeconds = HIP-event time on the
  *               library's stream (may be NULL)
  *   Results  -> copy returns / statuses / counts back. */
@@ -123,7 +128,7 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContex
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *Cxt,
                                                            uint32_t Inst, uint32_t Off,
                                                            uint8_t *Dst, uint32_t Len);
-/* Current page count of instance Inst's memory (after the last Run). */
+/* Current page count of instance Inst's memory. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *Cxt,
                                                          uint32_t Inst);
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *Cxt);

@@ -144,6 +144,39 @@ class Module:
                 "hashes": hashes, "seconds": secs}
 
 
+class Instance:
+    """One instantiated module (om_instantiate, start function included) that keeps its
+    state -- memory, globals, tables -- across invoke() calls, like a module
+    instantiated once in the reference VM and executed repeatedly."""
+
+    def __init__(self, module):
+        L = lib()
+        self.module = module
+        err = ctypes.c_int(0)
+        self._h = L.om_instantiate(module._h, ctypes.byref(err))
+        self.error = err.value if not self._h else 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().om_inst_free(self._h)
+            self._h = None
+
+    def invoke(self, name, args):
+        """(code, results, count, memhash) of one invocation on this instance."""
+        if not self._h:
+            return self.error, [], 0, 0
+        L = lib()
+        idx, pt, rt = self.module.func(name)
+        params = (ctypes.c_uint64 * (2 * max(1, len(pt))))()
+        for k, a in enumerate(args):
+            params[2 * k], params[2 * k + 1] = _split(a)
+        res = (ctypes.c_uint64 * (2 * max(1, len(rt))))()
+        cnt = ctypes.c_uint64(0)
+        code = L.om_invoke(self._h, idx, params, res, ctypes.byref(cnt))
+        vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
+        return code, vals, cnt.value, L.om_mem_hash(self._h)
+
+
 def hash_bytes(data, pages):
     buf = ctypes.create_string_buffer(bytes(data), len(data))
     return lib().om_hash_bytes(buf, len(data), pages)

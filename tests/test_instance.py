@@ -1,0 +1,96 @@
+"""Instance semantics: instantiation with a start function, state
+that persists across invocations on the same instances (memory, memory size, globals,
+dropped data segments) and BatchReset back to a fresh instantiation. Expected values:
+the oracle's om_instantiate + repeated om_invoke on one instance (oracle_py.Instance),
+which follows lib/executor/instantiate/module.cpp:16-172 and executor.cpp:82-116."""
+import pytest
+
+import oracle_py as O
+from helpers import compare, emu_run
+from wasmedge_amd.wat import assemble
+
+I32 = 0x7F
+
+STATEFUL = assemble(r"""
+(module
+  (memory 1 4)
+  (global $g (mut i32) (i32.const 5))
+  (global $h (mut i64) (i64.const 0))
+  (data (i32.const 0) "\03\00\00\00")
+  (data $p "\aa\bb\cc\dd")
+  (func $start
+    (global.set $g (i32.add (global.get $g) (i32.load (i32.const 0))))
+    (i32.store (i32.const 8) (i32.const 77)))
+  (start $start)
+  (func (export "step") (param $x i32) (result i32)
+    (global.set $g (i32.add (global.get $g) (local.get $x)))
+    (i32.store (i32.const 8) (i32.add (i32.load (i32.const 8)) (local.get $x)))
+    (if (i32.eq (i32.rem_u (local.get $x) (i32.const 7)) (i32.const 3))
+      (then (drop (memory.grow (i32.const 1)))))
+    (if (i32.eq (i32.rem_u (local.get $x) (i32.const 5)) (i32.const 1))
+      (then (memory.init $p (i32.const 16) (i32.const 0) (i32.const 4)) (data.drop $p)))
+    (if (i32.eq (local.get $x) (i32.const 41)) (then unreachable))
+    (global.set $h (i64.add (global.get $h) (i64.extend_i32_u (global.get $g))))
+    (i32.add (i32.add (global.get $g) (i32.load (i32.const 8)))
+             (i32.add (memory.size) (i32.wrap_i64 (global.get $h))))))
+""")
+
+START_TRAPS = assemble(r"""
+(module
+  (memory 1)
+  (func $start (i32.store (i32.const 65534) (i32.const 1)))
+  (start $start)
+  (func (export "f") (result i32) (i32.const 1)))
+""")
+
+ROUNDS = [[[i % 50] for i in range(130)], [[(3 * i + 1) % 50] for i in range(130)],
+          [[(7 * i + 2) % 50] for i in range(130)]]
+
+
+def _oracle_sequence(wasm, rounds, func="step"):
+    m = O.Module(wasm)
+    insts = [O.Instance(m) for _ in rounds[0]]
+    return [[inst.invoke(func, row) for inst, row in zip(insts, rows)] for rows in rounds]
+
+
+def test_start_function_emulator(built):
+    """First invocation after instantiation: the start function has run (globals and
+    memory it wrote are visible), its instructions are not counted."""
+    ref = _oracle_sequence(STATEFUL, ROUNDS[:1])[0]
+    rets, st, cnt, h = emu_run(STATEFUL, "step", ROUNDS[0], [I32], [I32])
+    assert compare(ref, rets, st, cnt, h, [I32]) == []
+
+
+def test_start_trap_oracle():
+    m = O.Module(START_TRAPS)
+    assert O.Instance(m).error == 0x88
+
+
+@pytest.mark.gpu
+def test_gpu_state_persists_across_runs(built):
+    from wasmedge_amd import batch
+    ref = _oracle_sequence(STATEFUL, ROUNDS)
+    ctx = batch.BatchContext(STATEFUL, len(ROUNDS[0]), device=0)
+    try:
+        for r, rows in enumerate(ROUNDS):
+            rets, st, cnt = ctx.execute("step", batch.make_values(rows, [I32]), 1)
+            h = ctx.memory_hash()
+            ints = batch.ret_ints(rets)
+            got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref[r], got, st, cnt, h, [I32]) == [], "round %d" % r
+        # BatchReset = fresh instantiation: round 0 again gives round 0's answers
+        ctx.reset()
+        rets, st, cnt = ctx.execute("step", batch.make_values(ROUNDS[0], [I32]), 1)
+        ints = batch.ret_ints(rets)
+        got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(ROUNDS[0]))]
+        assert compare(ref[0], got, st, cnt, ctx.memory_hash(), [I32]) == []
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_start_trap_fails_create(built):
+    from wasmedge_amd import batch
+    with pytest.raises(batch.WasmEdgeError) as e:
+        batch.BatchContext(START_TRAPS, 64, device=0)
+    assert e.value.code == 0x88

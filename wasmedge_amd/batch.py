@@ -178,9 +178,10 @@ class BatchContext:
         return rets[:, :nret], status, counts
 
     def execute(self, func, values, nret):
-        """Fresh instantiation + run. Returns (returns[n, nret] VALUE_DTYPE, status, counts)."""
+        """Invoke `func` on every instance (WasmEdge_BatchExecute: state persists from
+        the previous invocation; reset() re-instantiates). Returns (returns[n, nret]
+        VALUE_DTYPE, status, counts)."""
         self.set_args(func, values)
-        self.reset()
         self.run()
         return self.results(nret)
 

@@ -19,9 +19,13 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves, hipStream_t s);
-extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *pages,
-                                         uint64_t *hashes, uint32_t mem_words, uint32_t n,
-                                         hipStream_t s);
+extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
+                                         uint32_t ls_slots, uint64_t *hashes,
+                                         uint32_t mem_words, uint32_t n, hipStream_t s);
+extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
+                                           uint32_t global_cells, uint32_t ls_slots,
+                                           uint32_t init_pages, uint32_t init_dropped,
+                                           uint32_t nwaves, hipStream_t s);
 
 namespace {
 
@@ -32,6 +36,11 @@ constexpr uint8_t kRuntimeError = 0x02, kWrongVMWorkflow = 0x04, kFuncNotFound =
 std::string g_last_create_error;
 
 WasmEdge_Result R(uint8_t c) { return WasmEdge_Result{c}; }
+
+std::string hexbyte(uint8_t c) {
+  const char *d = "0123456789ABCDEF";
+  return std::string(1, d[c >> 4]) + d[c & 15];
+}
 
 template <typename T>
 struct DevBuf {
@@ -69,16 +78,16 @@ struct WasmEdge_BatchContext {
   DevBuf<DFunc> funcs;
   DevBuf<uint8_t> data_pool;
   // instance state
-  DevBuf<uint32_t> mem, gstack, params, results, pages;
+  DevBuf<uint32_t> mem, gstack, lstate, params, results;
   DevBuf<uint8_t> status;
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0;
-  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0;
+  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0;
   // current invocation
   int func = -1;
   uint32_t param_cells = 0, result_cells = 0;
   std::vector<uint8_t> result_types;
-  bool ran = false;
+  bool ran = false;         // a Run completed since the last Reset (results are valid)
 
   uint8_t fail(uint8_t code, const std::string &m) {
     last_error = m;
@@ -157,9 +166,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
             C->data_off.upload(doff, s) && C->data_len.upload(dlen, s);
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
   size_t nw = C->nwaves;
+  C->ls_slots = LS_GLOBALS + P.global_cells;
   if (!C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64) ||
-      !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) || !C->status.alloc(C->n + 1) ||
-      !C->counts.alloc(C->n + 1) || !C->pages.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1))
+      !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) ||
+      !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
+      !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
@@ -168,6 +179,59 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
 }
 
 uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
+
+// One interpreter launch over every instance: entry_pc with the staged params (or the
+// start function when is_start). Shared by BatchRun and BatchReset.
+uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
+                    double *KernelSeconds) {
+  const wb::Program &P = C->prog;
+  KParams k{};
+  k.code = C->code.ptr; k.brtab = C->brtab.ptr; k.vconst = C->vconst.ptr;
+  k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
+  k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
+  k.tcode = C->threaded ? C->tcode.ptr : nullptr;
+  k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
+  k.params = is_start ? nullptr : C->params.ptr;
+  k.results = is_start ? nullptr : C->results.ptr;
+  k.status = C->status.ptr; k.counts = C->counts.ptr;
+  k.n = C->n;
+  k.entry_pc = entry_pc;
+  k.param_cells = is_start ? 0 : C->param_cells;
+  k.result_cells = is_start ? 0 : C->result_cells;
+  k.global_cells = P.global_cells;
+  k.total_cells = P.total_cells() ? P.total_cells() : 1;
+  k.table_size = uint32_t(P.table0.size());
+  k.mem_words = C->mem_words;
+  k.init_pages = P.mem_min;
+  k.mem_max_pages = C->mem_max_pages;
+  k.gs_depth = C->gs_depth;
+  k.init_dropped = C->init_dropped;
+  k.ls_slots = C->ls_slots;
+  k.is_start = is_start ? 1u : 0u;
+  k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
+  double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
+  k.max_ticks = uint64_t(tl * 1e8);
+  // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
+  size_t wave_lds = size_t(k.total_cells) * 64 * 4;
+  if (wave_lds + 256 > 160 * 1024)
+    return C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
+                                      " cells exceeds LDS (global-frame mode: next)");
+  uint32_t wpb = 4;
+  while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
+  uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
+  (void)hipEventRecord(C->ev0, C->stream);
+  // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
+  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->stream), "launch"))
+    return kRuntimeError;
+  (void)hipEventRecord(C->ev1, C->stream);
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;
+  if (KernelSeconds) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
+    *KernelSeconds = ms * 1e-3;
+  }
+  return 0;
+}
 
 }  // namespace
 
@@ -186,6 +250,7 @@ WasmEdge_BatchContext *WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf,
   else C->conf.DeviceOrdinal = -1;
   C->n = NumInstances;
   uint8_t e = setup(C, WasmBuf, WasmLen);
+  if (!e) e = WasmEdge_BatchReset(C, nullptr).Code;   // instantiate every instance
   if (e) {
     g_last_create_error = C->last_error;
     if (Res) *Res = R(e);
@@ -244,64 +309,42 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->stream), "mem init"))
     return R(kRuntimeError);
+  if (!C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->global_init.ptr, P.global_cells,
+                                      C->ls_slots, P.mem_min, C->init_dropped, C->nwaves,
+                                      C->stream), "state init"))
+    return R(kRuntimeError);
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
-  if (KernelSeconds) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
-    *KernelSeconds = ms * 1e-3;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
+  double secs = ms * 1e-3;
+  // module.cpp:160-170: the start function runs as the last step of instantiation; a
+  // lane whose start function traps keeps that ErrCode as its instance status
+  if (P.start_func >= 0) {
+    double ks = 0;
+    uint8_t e = launch_exec(C, P.funcs[P.start_func].entry_pc, true, &ks);
+    if (e) return R(e);
+    secs += ks;
+    // the start function takes no input, so every lane ends alike: a trap there fails
+    // the instantiation itself, reported like the reference's VM::instantiate
+    std::vector<uint8_t> st(C->n);
+    if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, C->n, hipMemcpyDeviceToHost), "status"))
+      return R(kRuntimeError);
+    for (uint8_t c : st)
+      if (c) return R(C->fail(c, "start function trapped (ErrCode 0x" + hexbyte(c) + ")"));
   }
+  if (KernelSeconds) *KernelSeconds = secs;
+  C->ran = false;
   return R(0);
 }
 
 WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSeconds) {
   if (!C) return R(kWrongVMWorkflow);
   if (C->func < 0) return R(C->fail(kWrongVMWorkflow, "BatchSetArgs not called"));
-  const wb::Program &P = C->prog;
-  const wb::FuncInfo &F = P.funcs[C->func];
+  const wb::FuncInfo &F = C->prog.funcs[C->func];
   if (F.imported) return R(C->fail(kRuntimeError, "exported function is a host import"));
-  KParams k{};
-  k.code = C->code.ptr; k.brtab = C->brtab.ptr; k.vconst = C->vconst.ptr;
-  k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
-  k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
-  k.tcode = C->threaded ? C->tcode.ptr : nullptr;
-  k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.params = C->params.ptr;
-  k.results = C->results.ptr; k.status = C->status.ptr; k.counts = C->counts.ptr;
-  k.pages_out = C->pages.ptr;
-  k.n = C->n;
-  k.entry_pc = F.entry_pc;
-  k.param_cells = C->param_cells;
-  k.result_cells = C->result_cells;
-  k.global_cells = P.global_cells;
-  k.total_cells = P.total_cells() ? P.total_cells() : 1;
-  k.table_size = uint32_t(P.table0.size());
-  k.mem_words = C->mem_words;
-  k.init_pages = P.mem_min;
-  k.mem_max_pages = C->mem_max_pages;
-  k.gs_depth = C->gs_depth;
-  k.init_dropped = C->init_dropped;
-  k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
-  double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
-  k.max_ticks = uint64_t(tl * 1e8);
-  // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
-  size_t wave_lds = size_t(k.total_cells) * 64 * 4;
-  if (wave_lds + 256 > 160 * 1024)
-    return R(C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
-                                        " cells exceeds LDS (global-frame mode: next)"));
-  uint32_t wpb = 4;
-  while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
-  uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
-  (void)hipEventRecord(C->ev0, C->stream);
-  // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
-  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->stream), "launch"))
-    return R(kRuntimeError);
-  (void)hipEventRecord(C->ev1, C->stream);
-  if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return R(kRuntimeError);
-  if (KernelSeconds) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
-    *KernelSeconds = ms * 1e-3;
-  }
+  uint8_t e = launch_exec(C, F.entry_pc, false, KernelSeconds);
+  if (e) return R(e);
   C->ran = true;
   return R(0);
 }
@@ -349,8 +392,6 @@ WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_S
   if (!C) return R(kWrongVMWorkflow);
   WasmEdge_Result r = WasmEdge_BatchSetArgs(C, FuncName, Params, ParamLen);
   if (r.Code) return r;
-  r = WasmEdge_BatchReset(C, nullptr);
-  if (r.Code) return r;
   r = WasmEdge_BatchRun(C, nullptr);
   if (r.Code) return r;
   return WasmEdge_BatchResults(C, Returns, ReturnLen, PerInstance, InstrCounts);
@@ -358,9 +399,8 @@ WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_S
 
 WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Hashes) {
   if (!C) return R(kWrongVMWorkflow);
-  if (!C->ran) return R(C->fail(kWrongVMWorkflow, "BatchRun not called"));
-  if (!C->hip_ok(wb_launch_mem_hash(C->mem.ptr, C->pages.ptr, C->hashes.ptr, C->mem_words,
-                                    C->n, C->stream), "hash"))
+  if (!C->hip_ok(wb_launch_mem_hash(C->mem.ptr, C->lstate.ptr, C->ls_slots, C->hashes.ptr,
+                                    C->mem_words, C->n, C->stream), "hash"))
     return R(kRuntimeError);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "hash")) return R(kRuntimeError);
   if (!C->hip_ok(hipMemcpy(Hashes, C->hashes.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "hash"))
@@ -369,9 +409,10 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
 }
 
 uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
-  if (!C || Inst >= C->n || !C->ran) return 0;
+  if (!C || Inst >= C->n || !C->prog.has_mem) return 0;
   uint32_t p = 0;
-  (void)hipMemcpy(&p, C->pages.ptr + Inst, 4, hipMemcpyDeviceToHost);
+  const size_t at = (size_t(Inst / 64) * C->ls_slots + LS_PAGES) * 64 + Inst % 64;
+  (void)hipMemcpy(&p, C->lstate.ptr + at, 4, hipMemcpyDeviceToHost);
   return p;
 }
 
@@ -379,7 +420,7 @@ WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *C, uint32_t Inst,
                                         uint8_t *Dst, uint32_t Len) {
   if (!C) return R(kWrongVMWorkflow);
   if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
-  uint32_t pages = C->ran ? WasmEdge_BatchGetMemoryPages(C, Inst) : C->prog.mem_min;
+  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
   if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return R(kMemoryOutOfBounds);
   if (Len == 0) return R(0);
   // gather the lane's interleaved words: word w at ((wave*W + w)*64 + lane)

@@ -118,7 +118,8 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
 
 template <class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
-                                       uint32_t *const gs, uint32_t *const mem) {
+                                       uint32_t *const gs, uint32_t *const mem,
+                                       uint32_t *const ls) {
   // the bytecode is read through the constant address space so every fetch is one
   // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
   typedef uint32_t w4 __attribute__((ext_vector_type(4)));
@@ -133,10 +134,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define WLOOP(c, v) F.set((uint32_t)(c), (uint32_t)(v))
 #define GS(slot) gs[(size_t)(slot) << 6]
 
+#define LS(slot) ls[(size_t)(slot) << 6]
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
-  uint32_t pc = p.entry_pc, gsp = 0, pages = p.init_pages, dropped = p.init_dropped;
+  uint32_t pc = p.entry_pc, gsp = 0, pages = LS(LS_PAGES), dropped = LS(LS_DROPPED);
   uint64_t count = 0;
-  for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, p.global_init[c]);
+  const uint32_t istatus = LS(LS_ISTATUS);
+  if (status == WB_STATUS_RUNNING && istatus) status = istatus;   // instance never came up
+  for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, LS(LS_GLOBALS + c));
   if (status == WB_STATUS_RUNNING) {
     const uint32_t *prm = p.params + (size_t)inst * p.param_cells;
     for (uint32_t c = 0; c < p.param_cells; c++) F.set(p.global_cells + c, prm[c]);
@@ -319,8 +323,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   if (inst < p.n) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
-    p.pages_out[inst] = pages;
+    LS(LS_PAGES) = pages;
+    LS(LS_DROPPED) = dropped;
+    for (uint32_t c = 0; c < p.global_cells; c++) LS(LS_GLOBALS + c) = F.get(c);
+    if (p.is_start && status != WB_STATUS_OK) LS(LS_ISTATUS) = status;
   }
+#undef LS
 }
 
 // General kernel: frames of any size in LDS (4 waves per block when they fit).
@@ -331,7 +339,8 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p
   const uint32_t inst = wave * 64u + lane;
   LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
   interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
-         p.mem + (size_t)wave * p.mem_words * 64u + lane);
+         p.mem + (size_t)wave * p.mem_words * 64u + lane,
+         p.lstate + (size_t)wave * p.ls_slots * 64u + lane);
 }
 
 // ======================================================================= helpers
@@ -350,15 +359,33 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
   }
 }
 
+// Instance state at instantiation (instantiate/module.cpp: memory of `min` pages, active
+// data segments dropped, globals from their initialisers, no failure yet).
+extern "C" __global__ void __launch_bounds__(256)
+wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_cells,
+                     uint32_t ls_slots, uint32_t init_pages, uint32_t init_dropped,
+                     uint32_t nwaves) {
+  const size_t total = (size_t)nwaves * ls_slots * 64u;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t slot = (uint32_t)((i >> 6) % ls_slots);
+    uint32_t v = 0;
+    if (slot == LS_PAGES) v = init_pages;
+    else if (slot == LS_DROPPED) v = init_dropped;
+    else if (slot >= LS_GLOBALS) v = global_init[slot - LS_GLOBALS];
+    ls[i] = v;
+  }
+}
+
 // Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
 extern "C" __global__ void __launch_bounds__(256)
-wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *pages_of, uint64_t *hashes,
-                   uint32_t mem_words, uint32_t n) {
+wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
+                   uint64_t *hashes, uint32_t mem_words, uint32_t n) {
   const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
   if (inst >= n) return;
   const uint32_t wave = inst >> 6, lane = inst & 63u;
   const uint32_t *m = mem + (size_t)wave * mem_words * 64u + lane;
-  const uint32_t pages = pages_of ? pages_of[inst] : 0;
+  const uint32_t pages = ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + lane];
   const uint64_t nw = (uint64_t)pages << 13;
   uint64_t h = 0;
   for (uint64_t i = 0; i < nw; i++) {
@@ -392,11 +419,22 @@ extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                      image_words, init_words, mem_words, nwaves);
   return hipGetLastError();
 }
-extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *pages,
-                                         uint64_t *hashes, uint32_t mem_words, uint32_t n,
-                                         hipStream_t s) {
+extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
+                                         uint32_t ls_slots, uint64_t *hashes,
+                                         uint32_t mem_words, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mem, pages,
-                     hashes, mem_words, n);
+  hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mem, ls,
+                     ls_slots, hashes, mem_words, n);
+  return hipGetLastError();
+}
+extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
+                                           uint32_t global_cells, uint32_t ls_slots,
+                                           uint32_t init_pages, uint32_t init_dropped,
+                                           uint32_t nwaves, hipStream_t s) {
+  const size_t total = (size_t)nwaves * ls_slots * 64u;
+  size_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(wb_state_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ls,
+                     global_init, global_cells, ls_slots, init_pages, init_dropped, nwaves);
   return hipGetLastError();
 }

@@ -92,31 +92,45 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define WB_FAST 0
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
-    uint32_t status = WB_STATUS_RUNNING, pc = F.entry_pc, gsp = 0, pages = P.mem_min;
-    uint32_t dropped = init_dropped;
-    uint64_t count = 0;
+    uint32_t pages = P.mem_min, dropped = init_dropped;
     for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
-    for (uint32_t c = 0; c < pcells; c++) W32(P.global_cells + c, params[size_t(inst) * pcells + c]);
-    GS(0) = DBC_EXIT_PC;
-    gsp = 1;
-    while (status == WB_STATUS_RUNNING) {
-      if (max_steps && count >= max_steps) { status = 0x07; break; }
-      const uint32_t pcs = pc;
-      const DInstr I = P.code[pcs];
-      const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
-      const uint32_t op = w0 & 0xFFFFu;
-      if (g_hist) g_hist[op]++;
-      const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
-      int32_t add = (int32_t)cnt8;
-      uint32_t npc = pcs + 1;
-      const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
-      switch (op) {
+    // one invocation of the function at `entry` on this instance's state
+    auto invoke = [&](uint32_t entry, const uint32_t *prm, uint32_t ncells, uint64_t &count) {
+      uint32_t status = WB_STATUS_RUNNING, pc = entry, gsp = 0;
+      for (uint32_t c = 0; c < ncells; c++) W32(P.global_cells + c, prm[c]);
+      GS(0) = DBC_EXIT_PC;
+      gsp = 1;
+      while (status == WB_STATUS_RUNNING) {
+        if (max_steps && count >= max_steps) { status = 0x07; break; }
+        const uint32_t pcs = pc;
+        const DInstr I = P.code[pcs];
+        const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
+        const uint32_t op = w0 & 0xFFFFu;
+        if (g_hist) g_hist[op]++;
+        const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
+        int32_t add = (int32_t)cnt8;
+        uint32_t npc = pcs + 1;
+        const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+        switch (op) {
 #include "dbc_step.inc"
+        }
+      e_next:
+        count += (int64_t)add;
+        pc = npc;
       }
-    e_next:
-      count += (int64_t)add;
-      pc = npc;
+      return status;
+    };
+    // instantiation ends with the start function (module.cpp:160-170); its count is
+    // not part of the invocation's
+    uint64_t count = 0, start_count = 0;
+    uint32_t status = WB_STATUS_OK;
+    if (P.start_func >= 0) {
+      p.result_cells = 0;
+      status = invoke(P.funcs[P.start_func].entry_pc, nullptr, 0, start_count);
+      p.result_cells = rcells;
     }
+    if (status == WB_STATUS_OK)
+      status = invoke(F.entry_pc, params + size_t(inst) * pcells, pcells, count);
     statuses[inst] = uint8_t(status);
     counts[inst] = count;
     if (hashes) {

@@ -1507,7 +1507,11 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   for (auto &d : P.datas)
     if (d.active && uint64_t(d.offset) + d.bytes.size() > uint64_t(P.mem_min) * 65536)
       throw Err{0x63, "data segment does not fit"};
-  if (P.start_func >= 0) throw Err{E_UNSUPPORTED, "start function not supported by the batched path"};
+  if (P.start_func >= 0) {   // validator.cpp: the start function has type [] -> []
+    if (uint64_t(P.start_func) >= P.funcs.size()) throw Err{E_TYPECHECK, "unknown function"};
+    const FuncType &st = P.types[P.funcs[P.start_func].type];
+    if (!st.params.empty() || !st.results.empty()) throw Err{E_TYPECHECK, "invalid start function"};
+  }
   // lower
   Lowerer L(P, wasm);
   std::vector<CallFix> callfix;

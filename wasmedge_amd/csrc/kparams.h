@@ -19,12 +19,12 @@ struct KParams {
   // per-lane state (lane-interleaved per wave)
   uint32_t *mem;                // linear memory, [wave][word][64]
   uint32_t *gstack;             // spilled frames, [wave][slot][64]
+  uint32_t *lstate;             // instance state, [wave][ls_slots][64]: LS_* slots below
   // per-instance inputs / outputs
   const uint32_t *params;       // [n][param_cells]
   uint32_t *results;            // [n][result_cells]
   uint8_t *status;              // [n]
   uint64_t *counts;             // [n]
-  uint32_t *pages_out;          // [n]
   // sizes
   uint32_t n;                   // instances in this launch
   uint32_t entry_pc;
@@ -35,6 +35,17 @@ struct KParams {
   uint32_t init_pages, mem_max_pages;
   uint32_t gs_depth;            // call-stack cells per lane
   uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
+  uint32_t ls_slots;            // LS_GLOBALS + global_cells
+  uint32_t is_start;            // this launch runs the start function (instantiation)
   uint64_t max_steps;           // instruction budget per instance
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
 };
+
+// Per-lane instance state that persists across invocations until the next Reset (the
+// reference keeps it in ModuleInstance / MemoryInstance / GlobalInstance): memory size,
+// dropped data segments, instantiation status (a trapped start function fails the
+// instance, module.cpp:160-170), then the global cells.
+#define LS_PAGES 0u
+#define LS_DROPPED 1u
+#define LS_ISTATUS 2u
+#define LS_GLOBALS 3u
