@@ -119,6 +119,39 @@ WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchResults(WasmEdge_BatchContext *Cxt, WasmEdge_Value *Returns,
                       const uint32_t ReturnLen, uint8_t *PerInstance, uint64_t *InstrCounts);
 
+/* ---- host functions (the yield path) --------------------------------
+ * A lane that calls an imported function parks on the device; BatchRun / BatchReset then
+ * call the host function registered for that import on the CPU, once per parked lane,
+ * write its results back and resume the lanes, until none is parked -- the batched form
+ * of the reference's host-function call (lib/executor/helper.cpp:35-97,
+ * include/runtime/hostfunc.h:25-40). The signature mirrors WasmEdge_HostFunc_t
+ * (include/api/wasmedge/wasmedge.h:2269-2271); MemCxt is the calling instance's memory.
+ * A non-zero Result ends that instance with the code in PerInstance (Terminated 0x01,
+ * as from proc_exit, ends it "successfully" with zeroed returns; engine.cpp:62-64). An
+ * import without a registered function ends the instance with 0xB1. */
+typedef struct WasmEdge_BatchMemoryContext WasmEdge_BatchMemoryContext;
+typedef WasmEdge_Result (*WasmEdge_BatchHostFunc_t)(void *Data,
+                                                    WasmEdge_BatchMemoryContext *MemCxt,
+                                                    const WasmEdge_Value *Params,
+                                                    WasmEdge_Value *Returns);
+/* Bind `Func` to every import named ModuleName.FuncName (WasmEdge_ImportObjectAddFunction,
+ * wasmedge.h:2814). Register before the first Run (and before Reset when the start
+ * function calls imports). */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *Cxt, const WasmEdge_String ModuleName,
+                              const WasmEdge_String FuncName, WasmEdge_BatchHostFunc_t Func,
+                              void *Data);
+/* Inside a host function: the calling instance and its memory
+ * (WasmEdge_MemoryInstanceGetData / SetData, wasmedge.h:2552-2569). */
+WASMEDGE_BATCH_API uint32_t
+WasmEdge_BatchMemoryGetInstance(const WasmEdge_BatchMemoryContext *MemCxt);
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchMemoryGetData(const WasmEdge_BatchMemoryContext *MemCxt, uint8_t *Data,
+                            const uint32_t Offset, const uint32_t Length);
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *MemCxt, const uint8_t *Data,
+                            const uint32_t Offset, const uint32_t Length);
+
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *Cxt,
@@ -128,6 +161,10 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContex
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *Cxt,
                                                            uint32_t Inst, uint32_t Off,
                                                            uint8_t *Dst, uint32_t Len);
+/* Write Len bytes into instance Inst's linear memory at Off (0x88 if outside it). */
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext *Cxt,
+                                                           uint32_t Inst, uint32_t Off,
+                                                           const uint8_t *Src, uint32_t Len);
 /* Current page count of instance Inst's memory. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *Cxt,
                                                          uint32_t Inst);

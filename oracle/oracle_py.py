@@ -35,6 +35,8 @@ def lib():
         L.om_invoke.restype = ctypes.c_int
         L.om_invoke.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.om_terminated.restype = ctypes.c_int
+        L.om_terminated.argtypes = [ctypes.c_void_p]
         L.om_mem_pages.restype = ctypes.c_uint32
         L.om_mem_pages.argtypes = [ctypes.c_void_p]
         L.om_mem_data.restype = ctypes.c_void_p
@@ -49,6 +51,12 @@ def lib():
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
+
+
+# The reference ends a proc_exit'ed run "successfully" with unspecified return values
+# (engine.cpp:62-64); the wrappers report it as this code with no values, like the
+# batched path's PerInstance.
+TERMINATED = 0x01
 
 
 class OracleError(Exception):
@@ -102,6 +110,8 @@ class Module:
             res = (ctypes.c_uint64 * (2 * max(1, len(rt))))()
             cnt = ctypes.c_uint64(0)
             code = L.om_invoke(inst, idx, params, res, ctypes.byref(cnt))
+            if code == 0 and L.om_terminated(inst):
+                code = TERMINATED
             vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
             return code, vals, cnt.value, L.om_mem_hash(inst)
         finally:
@@ -173,6 +183,8 @@ class Instance:
         res = (ctypes.c_uint64 * (2 * max(1, len(rt))))()
         cnt = ctypes.c_uint64(0)
         code = L.om_invoke(self._h, idx, params, res, ctypes.byref(cnt))
+        if code == 0 and L.om_terminated(self._h):
+            code = TERMINATED
         vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
         return code, vals, cnt.value, L.om_mem_hash(self._h)
 

@@ -65,6 +65,7 @@ typedef struct {
   uint8_t *ltypes;                  /* params + locals */
   uint32_t start, len;              /* range into code[] */
   int imported;
+  char imod[32], iname[32];         /* import names (imports only) */
 } Func;
 
 typedef struct { uint8_t reftype; uint32_t min, max; int has_max; } TableT;
@@ -105,6 +106,7 @@ struct OInst {
   struct Frame { int has_module; uint32_t from; uint32_t locals, arity; uint64_t vpos; } *fs;
   uint64_t fsp, fcap;
   uint64_t count;
+  int terminated;                   /* the last invoke ended in Terminated (proc_exit) */
 };
 
 /* ------------------------------------------------------------------ reader */
@@ -662,14 +664,21 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
     case 2: {
       uint32_t n = rd_u32(&s);
       for (uint32_t k = 0; k < n; k++) {
-        uint32_t l1 = rd_u32(&s); s.p += l1;
-        uint32_t l2 = rd_u32(&s); s.p += l2;
+        char nm[2][32] = {{0}};
+        for (int q = 0; q < 2; q++) {
+          uint32_t l = rd_u32(&s);
+          if (s.p + l > s.end) { *err = E_MALFORMED; break; }
+          memcpy(nm[q], s.p, l < 31 ? l : 31);
+          s.p += l;
+        }
         uint8_t kind = rd_u8(&s);
         if (kind != 0) { *err = E_UNKNOWN_IMPORT; break; }
         uint32_t ti = rd_u32(&s);
         m->funcs = realloc(m->funcs, sizeof(Func) * (m->nfuncs + 1));
         memset(&m->funcs[m->nfuncs], 0, sizeof(Func));
         m->funcs[m->nfuncs].type = ti;
+        memcpy(m->funcs[m->nfuncs].imod, nm[0], 32);
+        memcpy(m->funcs[m->nfuncs].iname, nm[1], 32);
         m->funcs[m->nfuncs].imported = 1;
         m->nfuncs++; m->nimported++;
       }

@@ -44,6 +44,10 @@ void om_inst_free(OInst *i);
 int om_invoke(OInst *i, uint32_t fidx, const uint64_t *params, uint64_t *results,
               uint64_t *count);
 
+/* 1 if the last om_invoke on this instance ended in Terminated (a host proc_exit; the
+ * reference treats it as success, engine.cpp:62-64, with unspecified return values). */
+int om_terminated(const OInst *i);
+
 /* Linear memory 0 view and hash (hash defined in DESIGN.md, shared with the GPU). */
 uint32_t om_mem_pages(const OInst *i);
 const uint8_t *om_mem_data(const OInst *i);

@@ -20,6 +20,7 @@ def emu_lib():
         E.wb_emu_execute.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32] + [ctypes.c_void_p] * 5 + \
             [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        E.wb_emu_set_host.argtypes = [ctypes.c_void_p]
         E.wb_emu_disasm.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]
         _emu = E
@@ -46,8 +47,11 @@ def from_cells(cells, types):
     return vals
 
 
-def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0):
+def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0,
+            host=None):
+    """host: a wb_emu_host_t ctypes callback serving imports inline (hostfuncs.emu_host)."""
     E = emu_lib()
+    E.wb_emu_set_host(host)
     n = len(arg_rows)
     pc = sum(CELLS[t] for t in ptypes)
     rc = sum(CELLS[t] for t in rtypes)

@@ -1,0 +1,117 @@
+"""The test host module "env" on the batched path: the same functions the oracle defines
+(oracle/wasm_oracle_exec.inc host_call), registered through WasmEdge_BatchAddHostFunction.
+Used by the host-import yield-path parity tests."""
+import struct
+
+from wasmedge_amd.batch import WasmEdgeError
+
+MEM_OOB, HOST_FAILED, TERMINATED = 0x88, 0x8D, 0x01
+M64 = (1 << 64) - 1
+
+
+def _f64(bits):
+    return struct.unpack("<d", struct.pack("<Q", bits & M64))[0]
+
+
+def _bits(d):
+    return struct.unpack("<Q", struct.pack("<d", d))[0]
+
+
+def _i32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >> 31 else v
+
+
+def add_i64(mem, a):
+    return 0, [(a[0] + a[1]) & M64]
+
+
+def mem_sum(mem, a):
+    p, n = a[0] & 0xFFFFFFFF, a[1] & 0xFFFFFFFF
+    try:
+        return 0, [sum(mem.read(p, n)) & 0xFFFFFFFF]
+    except WasmEdgeError:
+        return MEM_OOB, []
+
+
+def mem_fill(mem, a):
+    p, n, b = a[0] & 0xFFFFFFFF, a[1] & 0xFFFFFFFF, a[2] & 0xFF
+    try:
+        mem.write(p, bytes([b]) * n)
+    except WasmEdgeError:
+        return MEM_OOB, []
+    return 0, []
+
+
+def fail(mem, a):
+    return (HOST_FAILED, []) if a[0] & 0xFFFFFFFF else (0, [7])
+
+
+def exit_(mem, a):
+    return TERMINATED, []
+
+
+def mix(mem, a):
+    return 0, [_bits(float(_i32(a[0])) * _f64(a[1]) + 0.5)]
+
+
+ENV = {"add_i64": (add_i64, 2, 1), "mem_sum": (mem_sum, 2, 1), "mem_fill": (mem_fill, 3, 0),
+       "fail": (fail, 1, 1), "exit": (exit_, 1, 0), "mix": (mix, 2, 1)}
+
+
+def register(ctx):
+    for name, (fn, np_, nr) in ENV.items():
+        ctx.add_host_function("env", name, fn, np_, nr)
+
+
+# ---- the same functions on the host emulator's inline host hook (wb_emu_set_host)
+SIGS = {"add_i64": ("ll", "l"), "mem_sum": ("ii", "i"), "mem_fill": ("iii", ""),
+        "fail": ("i", "i"), "exit": ("i", ""), "mix": ("id", "d")}
+_CELLS = {"i": 1, "f": 1, "l": 2, "d": 2}
+
+
+class _EmuMem:
+    def __init__(self, ptr, size):
+        self.ptr, self.size = ptr, size
+
+    def read(self, off, n):
+        import ctypes
+        if off + n > self.size:
+            raise WasmEdgeError(MEM_OOB, "read")
+        return ctypes.string_at(self.ptr + off, n)
+
+    def write(self, off, data):
+        import ctypes
+        if off + len(data) > self.size:
+            raise WasmEdgeError(MEM_OOB, "write")
+        ctypes.memmove(self.ptr + off, bytes(data), len(data))
+
+
+def emu_host(import_names):
+    """A wb_emu_host_t callback serving the module's imports (listed in import order)."""
+    import ctypes
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                             ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                             ctypes.c_void_p, ctypes.c_uint64)
+
+    def cb(inst, func, args, rets, mem, size):
+        name = import_names[func]
+        fn = ENV[name][0]
+        ps, rs = SIGS[name]
+        vals, at = [], 0
+        for t in ps:
+            v = 0
+            for q in range(_CELLS[t]):
+                v |= args[at] << (32 * q)
+                at += 1
+            vals.append(v)
+        code, res = fn(_EmuMem(mem, size), vals)
+        if code:
+            return code
+        at = 0
+        for t, v in zip(rs, res):
+            for q in range(_CELLS[t]):
+                rets[at] = (v >> (32 * q)) & 0xFFFFFFFF
+                at += 1
+        return 0
+    return proto(cb)

@@ -50,6 +50,32 @@ class _Result(ctypes.Structure):
 
 _lib = None
 
+# WasmEdge_BatchHostFunc_t: WasmEdge_Result(void *Data, MemCxt *, const Value *, Value *).
+# WasmEdge_Result is a one-byte struct, returned in a register exactly like a uint8_t.
+HOST_FUNC = ctypes.CFUNCTYPE(ctypes.c_uint8, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p)
+
+
+class HostMemory:
+    """The calling instance's linear memory inside a host function
+    (WasmEdge_BatchMemoryGetData / SetData)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self.instance = lib().WasmEdge_BatchMemoryGetInstance(handle)
+
+    def read(self, off, length):
+        buf = ctypes.create_string_buffer(max(length, 1))
+        r = lib().WasmEdge_BatchMemoryGetData(self._h, buf, off, length)
+        if r.Code:
+            raise WasmEdgeError(r.Code, "memory read")
+        return buf.raw[:length]
+
+    def write(self, off, data):
+        r = lib().WasmEdge_BatchMemorySetData(self._h, bytes(data), off, len(data))
+        if r.Code:
+            raise WasmEdgeError(r.Code, "memory write")
+
 
 def lib():
     """Load the HIP library (raises if it was not built -- no silent fallback)."""
@@ -84,6 +110,17 @@ def lib():
         L.WasmEdge_BatchGetLastError.argtypes = [vp]
         L.WasmEdge_BatchDelete.restype = None
         L.WasmEdge_BatchDelete.argtypes = [vp]
+        for name, args in [
+            ("WasmEdge_BatchSetMemory", [vp, u32, u32, ctypes.c_char_p, u32]),
+            ("WasmEdge_BatchAddHostFunction", [vp, _String, _String, HOST_FUNC, vp]),
+            ("WasmEdge_BatchMemoryGetData", [vp, vp, u32, u32]),
+            ("WasmEdge_BatchMemorySetData", [vp, ctypes.c_char_p, u32, u32]),
+        ]:
+            f = getattr(L, name)
+            f.restype = _Result
+            f.argtypes = args
+        L.WasmEdge_BatchMemoryGetInstance.restype = u32
+        L.WasmEdge_BatchMemoryGetInstance.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -200,6 +237,37 @@ class BatchContext:
 
     def code_size(self):
         return lib().WasmEdge_BatchGetCodeSize(self._h)
+
+    def set_memory(self, inst, off, data):
+        self._check(lib().WasmEdge_BatchSetMemory(self._h, inst, off, bytes(data), len(data)))
+
+    def add_host_function(self, module, name, fn, nparams, nresults):
+        """Bind `fn(mem: HostMemory, args: list[int]) -> (code, results: list[int])` to
+        the import module.name (WasmEdge_BatchAddHostFunction). Values are raw bits
+        (uint128 as python ints); code 0 = success, else the ErrCode ending the instance
+        (0x01 Terminated)."""
+        def tramp(_data, memcxt, params, returns):
+            pv = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * max(nparams, 1))).from_address(params)) \
+                if nparams else None
+            args = []
+            if nparams:
+                vals = pv.view(VALUE_DTYPE)
+                args = [int(vals["lo"][k]) | (int(vals["hi"][k]) << 64) for k in range(nparams)]
+            try:
+                code, res = fn(HostMemory(memcxt), args)
+            except WasmEdgeError as e:
+                return e.code
+            if code == 0 and nresults:
+                rv = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * nresults)).from_address(returns)).view(VALUE_DTYPE)
+                for k in range(nresults):
+                    v = int(res[k]) & ((1 << 128) - 1)
+                    rv["lo"][k] = v & 0xFFFFFFFFFFFFFFFF
+                    rv["hi"][k] = v >> 64
+            return code
+        cb = HOST_FUNC(tramp)
+        self._hosts = getattr(self, "_hosts", []) + [cb]   # keep the trampoline alive
+        self._check(lib().WasmEdge_BatchAddHostFunction(self._h, self._name(module),
+                                                        self._name(name), cb, None))
 
 
 def ret_ints(rets):

@@ -3,6 +3,7 @@
 // per-instance result buffers.  See the header for the reference interfaces mirrored.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -62,6 +63,11 @@ struct DevBuf {
 
 }  // namespace
 
+struct WasmEdge_BatchMemoryContext {   // one instance's linear memory, for host functions
+  WasmEdge_BatchContext *ctx;
+  uint32_t inst;
+};
+
 struct WasmEdge_BatchContext {
   wb::Program prog;
   WasmEdge_BatchConfigure conf{};
@@ -79,6 +85,11 @@ struct WasmEdge_BatchContext {
   DevBuf<uint8_t> data_pool;
   // instance state
   DevBuf<uint32_t> mem, gstack, lstate, params, results;
+  // host-import yield path (only allocated when the module imports functions)
+  DevBuf<uint32_t> fsave, hcall, hbuf;
+  uint32_t hb_cells = 0;
+  struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; };
+  std::vector<HostFn> hosts;      // per function index (imports only)
   DevBuf<uint8_t> status;
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0;
@@ -167,10 +178,20 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
   size_t nw = C->nwaves;
   C->ls_slots = LS_GLOBALS + P.global_cells;
+  C->hosts.assign(P.funcs.size(), {});
+  C->hb_cells = 1;
+  for (uint32_t f = 0; f < P.n_imported; f++) {
+    uint32_t a = 0, r = 0;
+    for (uint8_t t : P.types[P.funcs[f].type].params) a += wb::cells_of(t);
+    for (uint8_t t : P.types[P.funcs[f].type].results) r += wb::cells_of(t);
+    C->hb_cells = std::max(C->hb_cells, std::max(a, r));
+  }
   if (!C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64) ||
       !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) ||
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
-      !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1))
+      !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
+      (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells()) * 64) ||
+                        !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
@@ -182,7 +203,30 @@ uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
 
 // One interpreter launch over every instance: entry_pc with the staged params (or the
 // start function when is_start). Shared by BatchRun and BatchReset.
-uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
+// Read (dst) or write (src) bytes of one instance's linear memory: gather the lane's
+// interleaved words (word w of lane l in wave v at ((v*W + w)*64 + l)), patch, scatter.
+uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
+               uint8_t *Dst, const uint8_t *Src) {
+  if (Inst >= C->n) return C->fail(kRuntimeError, "instance index out of range");
+  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
+  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
+  if (Len == 0) return 0;
+  const uint32_t wave = Inst / 64, lane = Inst % 64;
+  const uint32_t w0 = Off / 4, w1 = uint32_t((uint64_t(Off) + Len + 3) / 4);
+  const size_t pitch = 64 * sizeof(uint32_t);
+  uint32_t *base = C->mem.ptr + (size_t(wave) * C->mem_words + w0) * 64 + lane;
+  std::vector<uint32_t> words(w1 - w0);
+  if (!C->hip_ok(hipMemcpy2D(words.data(), 4, base, pitch, 4, words.size(), hipMemcpyDeviceToHost), "memory"))
+    return kRuntimeError;
+  uint8_t *bytes = reinterpret_cast<uint8_t *>(words.data()) + (Off & 3);
+  if (Dst) { memcpy(Dst, bytes, Len); return 0; }
+  memcpy(bytes, Src, Len);
+  if (!C->hip_ok(hipMemcpy2D(base, pitch, words.data(), 4, 4, words.size(), hipMemcpyHostToDevice), "memory"))
+    return kRuntimeError;
+  return 0;
+}
+
+uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, bool resume,
                     double *KernelSeconds) {
   const wb::Program &P = C->prog;
   KParams k{};
@@ -191,6 +235,7 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
   k.tcode = C->threaded ? C->tcode.ptr : nullptr;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
+  k.fsave = C->fsave.ptr; k.hcall = C->hcall.ptr; k.hbuf = C->hbuf.ptr;
   k.params = is_start ? nullptr : C->params.ptr;
   k.results = is_start ? nullptr : C->results.ptr;
   k.status = C->status.ptr; k.counts = C->counts.ptr;
@@ -208,6 +253,8 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   k.init_dropped = C->init_dropped;
   k.ls_slots = C->ls_slots;
   k.is_start = is_start ? 1u : 0u;
+  k.resume = resume ? 1u : 0u;
+  k.hb_cells = C->hb_cells;
   k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
   double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
   k.max_ticks = uint64_t(tl * 1e8);
@@ -228,9 +275,83 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   if (KernelSeconds) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
-    *KernelSeconds = ms * 1e-3;
+    *KernelSeconds += ms * 1e-3;
   }
   return 0;
+}
+
+// Service every lane parked at a host import (helper.cpp:35-97 on the CPU executor):
+// call its host function with the args the kernel staged in hbuf, stage the results
+// (or end the lane with the host's ErrCode; Terminated 0x01 ends it too, engine.cpp:
+// 62-64). Returns the number of lanes to resume, or -1 on a device error.
+int64_t service_host_calls(WasmEdge_BatchContext *C) {
+  const wb::Program &P = C->prog;
+  const uint32_t n = C->n, hb = C->hb_cells;
+  std::vector<uint8_t> st(n);
+  if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, n, hipMemcpyDeviceToHost), "status"))
+    return -1;
+  std::vector<uint32_t> parked;
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] == WB_ERR_HOST_CALL) parked.push_back(i);
+  if (parked.empty()) return 0;
+  std::vector<uint32_t> hcall(n), hbuf(size_t(n) * hb);
+  if (!C->hip_ok(hipMemcpy(hcall.data(), C->hcall.ptr, size_t(n) * 4, hipMemcpyDeviceToHost), "hcall") ||
+      !C->hip_ok(hipMemcpy(hbuf.data(), C->hbuf.ptr, hbuf.size() * 4, hipMemcpyDeviceToHost), "hbuf"))
+    return -1;
+  int64_t resumed = 0;
+  std::vector<WasmEdge_Value> args, rets;
+  for (uint32_t i : parked) {
+    const uint32_t f = hcall[i];
+    const WasmEdge_BatchContext::HostFn h = f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
+    if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
+    const wb::FuncType &t = P.types[P.funcs[f].type];
+    uint32_t *cells = &hbuf[size_t(i) * hb];
+    args.assign(t.params.size(), WasmEdge_Value{});
+    rets.assign(t.results.size(), WasmEdge_Value{});
+    uint32_t at = 0;
+    for (size_t k = 0; k < t.params.size(); k++) {
+      uint128_t v = 0;
+      for (uint32_t q = 0; q < wb::cells_of(t.params[k]); q++) v |= uint128_t(cells[at++]) << (32 * q);
+      args[k].Value = v;
+      args[k].Type = static_cast<enum WasmEdge_ValType>(t.params[k]);
+    }
+    for (size_t k = 0; k < t.results.size(); k++) rets[k].Type = static_cast<enum WasmEdge_ValType>(t.results[k]);
+    WasmEdge_BatchMemoryContext mc{C, i};
+    const WasmEdge_Result r = h.fn(h.data, &mc, args.data(), rets.data());
+    if (r.Code) {            // host error or Terminated: the lane ends with that code
+      st[i] = r.Code;
+      hcall[i] = 0xFFFFFFFFu;
+      continue;
+    }
+    at = 0;
+    for (size_t k = 0; k < t.results.size(); k++)
+      for (uint32_t q = 0; q < wb::cells_of(t.results[k]); q++) cells[at++] = uint32_t(rets[k].Value >> (32 * q));
+    hcall[i] = at;
+    resumed++;
+  }
+  if (!C->hip_ok(hipMemcpy(C->status.ptr, st.data(), n, hipMemcpyHostToDevice), "status") ||
+      !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
+      !C->hip_ok(hipMemcpy(C->hbuf.ptr, hbuf.data(), hbuf.size() * 4, hipMemcpyHostToDevice), "hbuf"))
+    return -1;
+  return resumed;
+}
+
+// One interpreter invocation over every instance: entry_pc with the staged params (or the
+// start function when is_start), then host-import rounds until no lane is parked.
+// Shared by BatchRun and BatchReset.
+uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
+                    double *KernelSeconds) {
+  if (KernelSeconds) *KernelSeconds = 0;
+  uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
+  if (e || !C->prog.n_imported) return e;
+  for (;;) {
+    // every round resumes the lanes the host serviced; lanes it ended keep its code
+    const int64_t k = service_host_calls(C);
+    if (k < 0) return kRuntimeError;
+    if (k == 0) return 0;
+    e = launch_once(C, entry_pc, is_start, true, KernelSeconds);
+    if (e) return e;
+  }
 }
 
 }  // namespace
@@ -419,23 +540,43 @@ uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
 WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off,
                                         uint8_t *Dst, uint32_t Len) {
   if (!C) return R(kWrongVMWorkflow);
-  if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
-  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
-  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return R(kMemoryOutOfBounds);
-  if (Len == 0) return R(0);
-  // gather the lane's interleaved words: word w at ((wave*W + w)*64 + lane)
-  uint32_t wave = Inst / 64, lane = Inst % 64;
-  uint32_t w0 = Off / 4, w1 = (Off + Len + 3) / 4;
-  std::vector<uint32_t> rows(size_t(w1 - w0) * 64);
-  const uint32_t *src = C->mem.ptr + (size_t(wave) * C->mem_words + w0) * 64;
-  if (!C->hip_ok(hipMemcpy(rows.data(), src, rows.size() * 4, hipMemcpyDeviceToHost), "memory"))
-    return R(kRuntimeError);
-  for (uint32_t b = 0; b < Len; b++) {
-    uint32_t a = Off + b;
-    uint32_t w = rows[size_t(a / 4 - w0) * 64 + lane];
-    Dst[b] = uint8_t(w >> (8 * (a & 3)));
-  }
+  return R(mem_rw(C, Inst, Off, Len, Dst, nullptr));
+}
+
+WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off,
+                                        const uint8_t *Src, uint32_t Len) {
+  if (!C) return R(kWrongVMWorkflow);
+  return R(mem_rw(C, Inst, Off, Len, nullptr, Src));
+}
+
+WasmEdge_Result WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *C,
+                                              const WasmEdge_String ModuleName,
+                                              const WasmEdge_String FuncName,
+                                              WasmEdge_BatchHostFunc_t Func, void *Data) {
+  if (!C || !Func) return R(kWrongVMWorkflow);
+  const std::string mod(ModuleName.Buf ? ModuleName.Buf : "", ModuleName.Length);
+  const std::string name(FuncName.Buf ? FuncName.Buf : "", FuncName.Length);
+  // every import of that (module, name) binds to it, as an import object would
+  for (uint32_t f = 0; f < C->prog.n_imported; f++)
+    if (C->prog.funcs[f].import_module == mod && C->prog.funcs[f].import_name == name)
+      C->hosts[f] = WasmEdge_BatchContext::HostFn{Func, Data};
   return R(0);
+}
+
+uint32_t WasmEdge_BatchMemoryGetInstance(const WasmEdge_BatchMemoryContext *M) {
+  return M ? M->inst : 0;
+}
+
+WasmEdge_Result WasmEdge_BatchMemoryGetData(const WasmEdge_BatchMemoryContext *M, uint8_t *Data,
+                                            const uint32_t Offset, const uint32_t Length) {
+  if (!M) return R(kWrongVMWorkflow);
+  return R(mem_rw(M->ctx, M->inst, Offset, Length, Data, nullptr));
+}
+
+WasmEdge_Result WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *M, const uint8_t *Data,
+                                            const uint32_t Offset, const uint32_t Length) {
+  if (!M) return R(kWrongVMWorkflow);
+  return R(mem_rw(M->ctx, M->inst, Offset, Length, nullptr, Data));
 }
 
 uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *C) { return C ? C->n : 0; }

@@ -119,7 +119,7 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
 template <class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
                                        uint32_t *const gs, uint32_t *const mem,
-                                       uint32_t *const ls) {
+                                       uint32_t *const ls, uint32_t *const fs) {
   // the bytecode is read through the constant address space so every fetch is one
   // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
   typedef uint32_t w4 __attribute__((ext_vector_type(4)));
@@ -141,7 +141,28 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   const uint32_t istatus = LS(LS_ISTATUS);
   if (status == WB_STATUS_RUNNING && istatus) status = istatus;   // instance never came up
   for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, LS(LS_GLOBALS + c));
-  if (status == WB_STATUS_RUNNING) {
+  uint32_t ycall = 0, ybase = 0;   // host import being called when the lane yields
+  bool active = inst < p.n;        // this launch owns the lane's outputs
+  if (p.resume) {
+    // continue a lane parked at a host import: frame from fsave, the host function's
+    // results (hcall = their cell count, ~0 = the host ended the lane) into its cells
+    const uint32_t rpc = LS(LS_RPC);
+    const bool parked = status == WB_STATUS_RUNNING && rpc != 0xFFFFFFFFu;
+    const uint32_t nres = parked ? p.hcall[inst] : 0xFFFFFFFFu;
+    active = parked && nres != 0xFFFFFFFFu;
+    if (parked) LS(LS_RPC) = 0xFFFFFFFFu;
+    if (active) {
+      pc = rpc;
+      gsp = LS(LS_GSP);
+      count = p.counts[inst];
+      for (uint32_t c = p.global_cells; c < p.total_cells; c++) F.set(c, fs[(size_t)c << 6]);
+      const uint32_t base = LS(LS_HBASE);
+      for (uint32_t k = 0; k < nres; k++) F.set(base + k, p.hbuf[(size_t)inst * p.hb_cells + k]);
+    } else {
+      status = WB_STATUS_OK;
+    }
+  } else if (status == WB_STATUS_RUNNING) {
+    if (fs) LS(LS_RPC) = 0xFFFFFFFFu;   // a fresh invocation: nothing parked
     const uint32_t *prm = p.params + (size_t)inst * p.param_cells;
     for (uint32_t c = 0; c < p.param_cells; c++) F.set(p.global_cells + c, prm[c]);
     GS(0) = DBC_EXIT_PC;   // return record of the entry frame: pc = EXIT
@@ -198,6 +219,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define TRAP_CHECK() EXIT_IF_TRAPPED(pcs + 1)
 #define SLOW_OP() goto k_slow
 #define SLOW_IF(c) do { if (__ballot(c)) goto k_slow; } while (0)
+#define HOST_YIELD(f, base) SLOW_OP()
       uint32_t sc = 0, tick = 1024, xpc = 0, xpost = 0, tcode = 0;
       int32_t xadj = 0;
       uint64_t asc = 0;     // instructions retired inside the threaded core
@@ -257,6 +279,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef TRAP_CHECK
 #undef SLOW_OP
 #undef SLOW_IF
+#undef HOST_YIELD
       count += (uint64_t)sc + asc;
       if (tcode == 0) {
         pc = xpc;
@@ -284,6 +307,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define TRAP_CHECK() ((void)0)
 #define SLOW_OP() ((void)0)
 #define SLOW_IF(c) ((void)0)
+#define HOST_YIELD(f, base) do { status = WB_ERR_HOST_CALL; ycall = (f); ybase = (base); } while (0)
       const uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(slowmask));
       const w4 I = code[pcs];
       const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
@@ -308,6 +332,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef TRAP_CHECK
 #undef SLOW_OP
 #undef SLOW_IF
+#undef HOST_YIELD
     }
     if (status == WB_STATUS_RUNNING &&
         (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks))
@@ -320,9 +345,18 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef W128
 #undef WLOOP
 #undef GS
-  if (inst < p.n) {
+  if (active) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
+    if (status == WB_ERR_HOST_CALL && fs) {   // park: the host loop takes over
+      LS(LS_RPC) = pc;
+      LS(LS_GSP) = gsp;
+      LS(LS_HBASE) = ybase;
+      p.hcall[inst] = ycall;
+      for (uint32_t c = p.global_cells; c < p.total_cells; c++) fs[(size_t)c << 6] = F.get(c);
+      for (uint32_t k = 0; k < p.hb_cells && ybase + k < p.total_cells; k++)
+        p.hbuf[(size_t)inst * p.hb_cells + k] = F.get(ybase + k);
+    }
     LS(LS_PAGES) = pages;
     LS(LS_DROPPED) = dropped;
     for (uint32_t c = 0; c < p.global_cells; c++) LS(LS_GLOBALS + c) = F.get(c);
@@ -340,7 +374,8 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p
   LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
   interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
          p.mem + (size_t)wave * p.mem_words * 64u + lane,
-         p.lstate + (size_t)wave * p.ls_slots * 64u + lane);
+         p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
+         p.fsave ? p.fsave + (size_t)wave * p.total_cells * 64u + lane : nullptr);
 }
 
 // ======================================================================= helpers
@@ -372,6 +407,7 @@ wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_
     uint32_t v = 0;
     if (slot == LS_PAGES) v = init_pages;
     else if (slot == LS_DROPPED) v = init_dropped;
+    else if (slot == LS_RPC) v = 0xFFFFFFFFu;
     else if (slot >= LS_GLOBALS) v = global_init[slot - LS_GLOBALS];
     ls[i] = v;
   }

@@ -47,6 +47,8 @@ struct DInstr {
   X(POST_CALL)    /* a = L                                                           */ \
   X(ZERO_LOCALS)  /* a = first cell, b = count                                       */ \
   X(UNREACHABLE)                                                                       \
+  X(HOST_CALL)    /* a = first arg cell (results land there), b = arg cells,         */ \
+                  /* c = result cells, imm = function index of the import            */ \
   /* data movement: a -> c ; d = cond cell for select                                 */ \
   X(MOV32) X(MOV64) X(MOV128) X(CONST32) X(CONST64) X(CONST128)                       \
   X(SELECT32) X(SELECT64) X(SELECT128)                                                 \
@@ -152,4 +154,7 @@ struct DFunc {
 #define WB_STATUS_OK 0x00u
 #define WB_ERR_INTERRUPTED 0x07u        // ErrCode::Interrupted (fuel / time limit)
 #define WB_ERR_STACK_EXHAUSTED 0xB0u    // device call stack full (no reference code)
-#define WB_ERR_HOST_CALL 0xB1u          // lane reached a host import (yield path: next)
+#define WB_ERR_HOST_CALL 0xB1u          // lane yielded at a host import; BatchRun's host loop
+                                        // services it and resumes the lane. It stays the
+                                        // final status only when no host function is
+                                        // registered for that import.

@@ -15,6 +15,11 @@
 
 static std::string g_err;
 static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuning aid)
+// Host-import callback of the emulator (the batched library's yield path, run inline):
+// returns 0 and writes the result cells, or an ErrCode that ends the instance.
+typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
+                             uint32_t *rets, uint8_t *mem, uint64_t mem_bytes);
+static wb_emu_host_t g_host = nullptr;
 
 extern "C" {
 
@@ -23,6 +28,7 @@ __attribute__((visibility("default"))) const char *wb_emu_last_error() { return 
 // Count dispatches per DBC op into h[DBC_NUM_OPS] during later wb_emu_execute calls (NULL: off).
 __attribute__((visibility("default"))) void wb_emu_set_histogram(uint64_t *h) { g_hist = h; }
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
+__attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 
 // Returns ErrCode of the call; per-instance outputs like WasmEdge_BatchExecute.
 // params: [n][param cells] u32; results: [n][result cells] u32.
@@ -89,6 +95,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define TRAP_CHECK() ((void)0)
 #define SLOW_OP() ((void)0)
 #define SLOW_IF(c) ((void)0)
+#define HOST_YIELD(f, base) do { status = WB_ERR_HOST_CALL; ycall = (f); ybase = (base); } while (0)
 #define WB_FAST 0
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
@@ -96,7 +103,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
     // one invocation of the function at `entry` on this instance's state
     auto invoke = [&](uint32_t entry, const uint32_t *prm, uint32_t ncells, uint64_t &count) {
-      uint32_t status = WB_STATUS_RUNNING, pc = entry, gsp = 0;
+      uint32_t status = WB_STATUS_RUNNING, pc = entry, gsp = 0, ycall = 0, ybase = 0;
       for (uint32_t c = 0; c < ncells; c++) W32(P.global_cells + c, prm[c]);
       GS(0) = DBC_EXIT_PC;
       gsp = 1;
@@ -117,6 +124,15 @@ __attribute__((visibility("default"))) int wb_emu_execute(
       e_next:
         count += (int64_t)add;
         pc = npc;
+        if (status == WB_ERR_HOST_CALL && g_host) {   // run the host function inline
+          const wb::FuncType &ht = P.types[P.funcs[ycall].type];
+          uint32_t rets[64] = {0}, nr = 0;
+          for (uint8_t t : ht.results) nr += wb::cells_of(t);
+          const int e = g_host(inst, ycall, &fr[ybase], rets, mb, uint64_t(pages) << 16);
+          if (e) { status = uint32_t(e); break; }
+          for (uint32_t k = 0; k < nr; k++) W32(ybase + k, rets[k]);
+          status = WB_STATUS_RUNNING;
+        }
       }
       return status;
     };

@@ -297,6 +297,7 @@ class Lowerer {
     switch (op) {
       case OP_JMP: case OP_BR_IF: case OP_BR_UNLESS: case OP_BR_IF_MOV1: case OP_BR_IF_MOV2:
       case OP_BR_TABLE: case OP_CALL: case OP_CALL_INDIRECT: case OP_RET: case OP_UNREACHABLE:
+      case OP_HOST_CALL:
       case OP_I32_DIV_S: case OP_I32_DIV_U: case OP_I32_REM_S: case OP_I32_REM_U:
       case OP_I32_DIV_S_I: case OP_I32_DIV_U_I: case OP_I32_REM_S_I: case OP_I32_REM_U_I:
       case OP_I64_DIV_S: case OP_I64_DIV_U: case OP_I64_REM_S: case OP_I64_REM_U:
@@ -701,8 +702,10 @@ void Lowerer::do_call(uint32_t callee) {
   for (auto &e : args) argcells += cells_of(e.type);
   uint32_t L = top_cell() - argcells;
   st.resize(st.size() - np);
-  if (P.funcs[callee].imported) {
-    emit(OP_UNREACHABLE, 0, 0, 0, 0, WB_ERR_HOST_CALL);
+  if (P.funcs[callee].imported) {   // helper.cpp:35-97: runs on the CPU executor
+    uint32_t rc = 0;
+    for (uint8_t r : t.results) rc += cells_of(r);
+    emit(OP_HOST_CALL, L, argcells, rc, 0, callee);
   } else {
     uint32_t rc = 0;
     for (uint8_t r : t.results) rc += cells_of(r);

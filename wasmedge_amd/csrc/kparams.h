@@ -20,6 +20,9 @@ struct KParams {
   uint32_t *mem;                // linear memory, [wave][word][64]
   uint32_t *gstack;             // spilled frames, [wave][slot][64]
   uint32_t *lstate;             // instance state, [wave][ls_slots][64]: LS_* slots below
+  uint32_t *fsave;              // frames of lanes parked at a host import, [wave][cell][64]
+  uint32_t *hcall;              // [n] import being called (out) / result cells (in, ~0: done)
+  uint32_t *hbuf;               // [n][hb_cells] import args (out) / results (in)
   // per-instance inputs / outputs
   const uint32_t *params;       // [n][param_cells]
   uint32_t *results;            // [n][result_cells]
@@ -37,6 +40,8 @@ struct KParams {
   uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
   uint32_t ls_slots;            // LS_GLOBALS + global_cells
   uint32_t is_start;            // this launch runs the start function (instantiation)
+  uint32_t resume;              // continue the lanes parked at a host import
+  uint32_t hb_cells;
   uint64_t max_steps;           // instruction budget per instance
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
 };
@@ -44,8 +49,12 @@ struct KParams {
 // Per-lane instance state that persists across invocations until the next Reset (the
 // reference keeps it in ModuleInstance / MemoryInstance / GlobalInstance): memory size,
 // dropped data segments, instantiation status (a trapped start function fails the
-// instance, module.cpp:160-170), then the global cells.
+// instance, module.cpp:160-170), the resume point of a lane parked at a host import
+// (pc, call-stack depth, arg/result cell; pc ~0 = not parked), then the global cells.
 #define LS_PAGES 0u
 #define LS_DROPPED 1u
 #define LS_ISTATUS 2u
-#define LS_GLOBALS 3u
+#define LS_RPC 3u
+#define LS_GSP 4u
+#define LS_HBASE 5u
+#define LS_GLOBALS 6u
