@@ -74,6 +74,12 @@ typedef struct WasmEdge_BatchConfigure {
   double TimeLimitSeconds;
   /* HIP device ordinal (-1 = the current device). */
   int32_t DeviceOrdinal;
+  /* Gas limit per instance with the reference's default unit cost table
+   * (StatisticsConfigure::setCostLimit, statistics.h:32,69-91; 0 = none). Exact: an
+   * instance executes CostLimit wasm instructions and the next one fails with
+   * CostLimitExceeded (0x03), its count = CostLimit + 1 as in engine.cpp:1616-1630.
+   * Metered runs use the compiled step only (no threaded dispatch core). */
+  uint64_t CostLimit;
 } WasmEdge_BatchConfigure;
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
@@ -98,6 +104,12 @@ WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName
                       const WasmEdge_Value *Params, const uint32_t ParamLen,
                       WasmEdge_Value *Returns, const uint32_t ReturnLen,
                       uint8_t *PerInstance, uint64_t *InstrCounts);
+
+/* Ask a running BatchExecute/BatchRun on this context to stop (any thread): every
+ * instance still running ends with Interrupted (0x07) within ~1024 dispatches, like the
+ * reference's StopToken / async cancel (helper.cpp:24-27, include/common/async.h:73-77).
+ * The request is cleared when the next Run starts. */
+WASMEDGE_BATCH_API void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *Cxt);
 
 /* Staged form of BatchExecute, for callers that keep inputs resident on the device
  * and time the interpreter alone (bench.py):

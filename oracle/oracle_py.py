@@ -35,6 +35,8 @@ def lib():
         L.om_invoke.restype = ctypes.c_int
         L.om_invoke.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.om_set_cost_limit.restype = None
+        L.om_set_cost_limit.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.om_terminated.restype = ctypes.c_int
         L.om_terminated.argtypes = [ctypes.c_void_p]
         L.om_mem_pages.restype = ctypes.c_uint32
@@ -159,12 +161,14 @@ class Instance:
     state -- memory, globals, tables -- across invoke() calls, like a module
     instantiated once in the reference VM and executed repeatedly."""
 
-    def __init__(self, module):
+    def __init__(self, module, cost_limit=0):
         L = lib()
         self.module = module
         err = ctypes.c_int(0)
         self._h = L.om_instantiate(module._h, ctypes.byref(err))
         self.error = err.value if not self._h else 0
+        if self._h and cost_limit:
+            L.om_set_cost_limit(self._h, cost_limit)
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -30,7 +30,7 @@ enum { T_I32 = 0x7F, T_I64 = 0x7E, T_F32 = 0x7D, T_F64 = 0x7C, T_V128 = 0x7B,
        T_FUNCREF = 0x70, T_EXTERNREF = 0x6F, T_UNKNOWN = 0 };
 
 /* ErrCode values (include/common/enum.inc:573-749) */
-enum { E_OK = 0, E_TERMINATED = 0x01, E_FUNC_NOT_FOUND = 0x05, E_MALFORMED = 0x21,
+enum { E_OK = 0, E_TERMINATED = 0x01, E_COST_LIMIT = 0x03, E_FUNC_NOT_FOUND = 0x05, E_MALFORMED = 0x21,
        E_ILLEGAL_OPCODE = 0x37, E_TYPECHECK = 0x41, E_FUNCSIG = 0x83, E_DIV0 = 0x84,
        E_INTOVF = 0x85, E_CONV = 0x86, E_TABLE_OOB = 0x87, E_MEM_OOB = 0x88,
        E_UNREACHABLE = 0x89, E_UNINIT_ELEM = 0x8A, E_UNDEF_ELEM = 0x8B,
@@ -107,6 +107,7 @@ struct OInst {
   uint64_t fsp, fcap;
   uint64_t count;
   int terminated;                   /* the last invoke ended in Terminated (proc_exit) */
+  uint64_t cost_limit;              /* unit-cost gas limit per invocation (statistics.h) */
 };
 
 /* ------------------------------------------------------------------ reader */

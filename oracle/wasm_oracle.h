@@ -48,6 +48,9 @@ int om_invoke(OInst *i, uint32_t fidx, const uint64_t *params, uint64_t *results
  * reference treats it as success, engine.cpp:62-64, with unspecified return values). */
 int om_terminated(const OInst *i);
 
+/* Gas limit per invocation with unit costs (0 = none): statistics.h:69-91. */
+void om_set_cost_limit(OInst *i, uint64_t limit);
+
 /* Linear memory 0 view and hash (hash defined in DESIGN.md, shared with the GPU). */
 uint32_t om_mem_pages(const OInst *i);
 const uint8_t *om_mem_data(const OInst *i);

@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EMU_PATH = os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch_emu.so")
+EMU_PATH = os.environ.get("WB_EMU_LIB") or os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch_emu.so")
 _emu = None
 
 CELLS = {0x7F: 1, 0x7E: 2, 0x7D: 1, 0x7C: 2, 0x7B: 4, 0x70: 1, 0x6F: 1}
@@ -21,6 +21,7 @@ def emu_lib():
                                      ctypes.c_uint32] + [ctypes.c_void_p] * 5 + \
             [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         E.wb_emu_set_host.argtypes = [ctypes.c_void_p]
+        E.wb_emu_set_cost_limit.argtypes = [ctypes.c_uint64]
         E.wb_emu_disasm.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]
         _emu = E
@@ -48,10 +49,12 @@ def from_cells(cells, types):
 
 
 def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0,
-            host=None):
-    """host: a wb_emu_host_t ctypes callback serving imports inline (hostfuncs.emu_host)."""
+            host=None, cost_limit=0):
+    """host: a wb_emu_host_t ctypes callback serving imports inline (hostfuncs.emu_host);
+    cost_limit: exact unit-cost gas limit (0 = none)."""
     E = emu_lib()
     E.wb_emu_set_host(host)
+    E.wb_emu_set_cost_limit(cost_limit)
     n = len(arg_rows)
     pc = sum(CELLS[t] for t in ptypes)
     rc = sum(CELLS[t] for t in rtypes)

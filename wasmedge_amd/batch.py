@@ -37,7 +37,7 @@ class WasmEdgeError(RuntimeError):
 class _Conf(ctypes.Structure):
     _fields_ = [("MaxMemoryPage", ctypes.c_uint32), ("CallStackCells", ctypes.c_uint32),
                 ("MaxSteps", ctypes.c_uint64), ("TimeLimitSeconds", ctypes.c_double),
-                ("DeviceOrdinal", ctypes.c_int32)]
+                ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64)]
 
 
 class _String(ctypes.Structure):
@@ -119,6 +119,8 @@ def lib():
             f = getattr(L, name)
             f.restype = _Result
             f.argtypes = args
+        L.WasmEdge_BatchInterrupt.restype = None
+        L.WasmEdge_BatchInterrupt.argtypes = [vp]
         L.WasmEdge_BatchMemoryGetInstance.restype = u32
         L.WasmEdge_BatchMemoryGetInstance.argtypes = [vp]
         _lib = L
@@ -159,9 +161,9 @@ class BatchContext:
     """N instances of one module on one GPU (WasmEdge_BatchContext)."""
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
-                 time_limit=0.0, device=-1):
+                 time_limit=0.0, device=-1, cost_limit=0):
         L = lib()
-        conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device)
+        conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit)
         res = _Result(0)
         self._h = L.WasmEdge_BatchCreate(ctypes.byref(conf), bytes(wasm), len(wasm), n,
                                          ctypes.byref(res))
@@ -237,6 +239,9 @@ class BatchContext:
 
     def code_size(self):
         return lib().WasmEdge_BatchGetCodeSize(self._h)
+
+    def interrupt(self):
+        lib().WasmEdge_BatchInterrupt(self._h)
 
     def set_memory(self, inst, off, data):
         self._check(lib().WasmEdge_BatchSetMemory(self._h, inst, off, bytes(data), len(data)))

@@ -74,6 +74,8 @@ struct WasmEdge_BatchContext {
   uint32_t n = 0, nwaves = 0;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t ctl_stream = nullptr;  // interrupt requests, while `stream` runs a kernel
+  uint32_t *stop = nullptr;          // uncached device word polled by the kernel
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string last_error;
   // module buffers
@@ -115,7 +117,7 @@ namespace {
 
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
-  std::string err = wb::load_program(wasm, len, C->prog, &ec);
+  std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
   if (C->conf.DeviceOrdinal >= 0) {
@@ -124,6 +126,12 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   (void)hipGetDevice(&C->device);
   if (!C->hip_ok(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking), "stream"))
     return kRuntimeError;
+  if (!C->hip_ok(hipStreamCreateWithFlags(&C->ctl_stream, hipStreamNonBlocking), "stream"))
+    return kRuntimeError;
+  if (hipExtMallocWithFlags(reinterpret_cast<void **>(&C->stop), 4, hipDeviceMallocUncached) != hipSuccess &&
+      !C->hip_ok(hipMalloc(&C->stop, 4), "interrupt flag"))
+    return kRuntimeError;
+  (void)hipMemset(C->stop, 0, 4);
   (void)hipEventCreate(&C->ev0);
   (void)hipEventCreate(&C->ev1);
   hipStream_t s = C->stream;
@@ -233,7 +241,11 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.code = C->code.ptr; k.brtab = C->brtab.ptr; k.vconst = C->vconst.ptr;
   k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
   k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
-  k.tcode = C->threaded ? C->tcode.ptr : nullptr;
+  // metered runs take the exact compiled step (the threaded core counts per run only)
+  k.tcode = C->threaded && !C->conf.CostLimit ? C->tcode.ptr : nullptr;
+  // the gas limit applies per invocation; instantiation (start function) is not metered
+  k.cost_limit = C->conf.CostLimit && !is_start ? C->conf.CostLimit : ~0ull;
+  k.stop = C->stop;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
   k.fsave = C->fsave.ptr; k.hcall = C->hcall.ptr; k.hbuf = C->hbuf.ptr;
   k.params = is_start ? nullptr : C->params.ptr;
@@ -342,6 +354,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
 uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
                     double *KernelSeconds) {
   if (KernelSeconds) *KernelSeconds = 0;
+  if (!C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
   if (e || !C->prog.n_imported) return e;
   for (;;) {
@@ -590,9 +603,18 @@ const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
   return C ? C->last_error.c_str() : g_last_create_error.c_str();
 }
 
+void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *C) {
+  if (!C || !C->stop) return;
+  static const uint32_t one = 1;
+  (void)hipMemcpyAsync(C->stop, &one, 4, hipMemcpyHostToDevice, C->ctl_stream);
+  (void)hipStreamSynchronize(C->ctl_stream);
+}
+
 void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   if (!C) return;
   if (C->stream) (void)hipStreamSynchronize(C->stream);
+  if (C->ctl_stream) (void)hipStreamDestroy(C->ctl_stream);
+  if (C->stop) (void)hipFree(C->stop);
   if (C->ev0) (void)hipEventDestroy(C->ev0);
   if (C->ev1) (void)hipEventDestroy(C->ev1);
   hipStream_t s = C->stream;

@@ -169,6 +169,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t rounds = 0;
   const uint32_t lane = __lane_id();
   const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
 
@@ -242,6 +243,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         const uint32_t op = w0 & 0x7FFFu;
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+        // metered: a dispatch that may cross the gas limit runs in the exact slow step
+        // (the threaded core is off when metering, see launch_once)
+        if (p.cost_limit != ~0ull)
+          SLOW_IF(count + sc + cnt8 + (uint32_t)(tcnt > 0 ? tcnt : 0) > p.cost_limit);
         switch (op) {
 #include "dbc_step.inc"
         }
@@ -316,10 +321,23 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
       uint32_t npc = pcs + 1;
       int32_t add = (int32_t)cnt8;
+      // engine.cpp:1616-1630 with unit costs: an instruction is counted, then its cost
+      // is added; past the limit it fails with CostLimitExceeded before it executes
+      const bool metered = p.cost_limit != ~0ull;
+      if (metered && count + cnt8 - post8 > p.cost_limit) {
+        status = 0x03u;
+        add = (int32_t)(p.cost_limit + 1 - count);
+        goto s_next;
+      }
       switch (op) {
 #include "dbc_step.inc"
       }
     s_next:
+      if (metered && count + (int64_t)add > p.cost_limit &&
+          (status == WB_STATUS_RUNNING || status == WB_STATUS_OK)) {
+        status = 0x03u;   // the limit fell on a trailing folded / landing instruction
+        add = (int32_t)(p.cost_limit + 1 - count);
+      }
       count += (int64_t)add;
       pc = npc;
 #undef WB_FAST
@@ -334,8 +352,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_IF
 #undef HOST_YIELD
     }
+    // budget, wall clock, and (every 64th round) the host's interrupt request, read
+    // from uncached device memory at system scope
+    const bool stop = (++rounds & 63u) == 0 &&
+                      __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (status == WB_STATUS_RUNNING &&
-        (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks))
+        (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks || stop))
       status = WB_ERR_INTERRUPTED;
   }
 #undef R32

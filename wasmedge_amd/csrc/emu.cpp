@@ -20,6 +20,7 @@ static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuni
 typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
                              uint32_t *rets, uint8_t *mem, uint64_t mem_bytes);
 static wb_emu_host_t g_host = nullptr;
+static uint64_t g_cost_limit = ~0ull;   // exact unit-cost gas limit (0 = none)
 
 extern "C" {
 
@@ -29,6 +30,7 @@ __attribute__((visibility("default"))) const char *wb_emu_last_error() { return 
 __attribute__((visibility("default"))) void wb_emu_set_histogram(uint64_t *h) { g_hist = h; }
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
+__attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
 
 // Returns ErrCode of the call; per-instance outputs like WasmEdge_BatchExecute.
 // params: [n][param cells] u32; results: [n][result cells] u32.
@@ -38,7 +40,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     uint32_t max_pages, uint32_t gs_depth, uint64_t max_steps) {
   wb::Program P;
   uint8_t ec = 0;
-  g_err = wb::load_program(wasm, len, P, &ec);
+  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull);
   if (!g_err.empty()) return ec ? ec : 2;
   int f = wb::find_export(P, func);
   if (f < 0) { g_err = "function not found"; return 0x05; }
@@ -78,7 +80,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     memv.assign(size_t(budget) << 14, 0u);
     uint8_t *mb = reinterpret_cast<uint8_t *>(memv.data());
     for (const auto &d : P.datas)
-      if (d.active) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
+      if (d.active && !d.bytes.empty()) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
     uint32_t *fr = frame.data(), *gs = gstack.data(), *mem = memv.data();
 #define CELL(x) fr[(uint32_t)(x)]
 #define R32(x) CELL(x)
@@ -118,10 +120,21 @@ __attribute__((visibility("default"))) int wb_emu_execute(
         int32_t add = (int32_t)cnt8;
         uint32_t npc = pcs + 1;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+        const bool metered = g_cost_limit != ~0ull;   // as the kernel's slow step
+        if (metered && count + cnt8 - post8 > g_cost_limit) {
+          status = 0x03u;
+          add = (int32_t)(g_cost_limit + 1 - count);
+          goto e_next;
+        }
         switch (op) {
 #include "dbc_step.inc"
         }
       e_next:
+        if (metered && count + (int64_t)add > g_cost_limit &&
+            (status == WB_STATUS_RUNNING || status == WB_STATUS_OK)) {
+          status = 0x03u;
+          add = (int32_t)(g_cost_limit + 1 - count);
+        }
         count += (int64_t)add;
         pc = npc;
         if (status == WB_ERR_HOST_CALL && g_host) {   // run the host function inline
@@ -140,10 +153,13 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     // not part of the invocation's
     uint64_t count = 0, start_count = 0;
     uint32_t status = WB_STATUS_OK;
-    if (P.start_func >= 0) {
+    if (P.start_func >= 0) {   // instantiation is not metered (limit per invocation)
+      const uint64_t lim = g_cost_limit;
+      g_cost_limit = ~0ull;
       p.result_cells = 0;
       status = invoke(P.funcs[P.start_func].entry_pc, nullptr, 0, start_count);
       p.result_cells = rcells;
+      g_cost_limit = lim;
     }
     if (status == WB_STATUS_OK)
       status = invoke(F.entry_pc, params + size_t(inst) * pcells, pcells, count);

@@ -39,17 +39,17 @@ struct Reader {
     return v;
   }
   int64_t sleb(int bits) {
-    int64_t v = 0;
+    uint64_t v = 0;   // unsigned accumulation: shifting into bit 63 is defined
     int sh = 0;
     uint8_t b;
     do {
       b = u8();
-      v |= int64_t(b & 0x7F) << sh;
+      if (sh < 64) v |= uint64_t(b & 0x7F) << sh;
       sh += 7;
       if (sh >= bits + 7) throw Err{E_MALFORMED, "integer representation too long"};
     } while (b & 0x80);
-    if (sh < 64 && (b & 0x40)) v |= -(int64_t(1) << sh);
-    return v;
+    if (sh < 64 && (b & 0x40)) v |= ~uint64_t(0) << sh;
+    return int64_t(v);
   }
   uint32_t u32() { return uint32_t(uleb(32)); }
   std::string name() {
@@ -1045,7 +1045,8 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           if (!P.global_mut[gi]) fail(E_TYPECHECK, "global is immutable");
           Entry v = pop_t(t);
           if (!live()) break;
-          if (!try_retarget(v, P.global_cell[gi])) materialize_into(v, P.global_cell[gi]);
+          if (P.exact_globals || !try_retarget(v, P.global_cell[gi]))
+            materialize_into(v, P.global_cell[gi]);
         }
         break;
       }
@@ -1525,9 +1526,11 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
 
 }  // namespace
 
-std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode) {
+std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
+                         bool exact_globals) {
   try {
     out = Program();
+    out.exact_globals = exact_globals;
     parse_and_lower(wasm, len, out);
     *errcode = 0;
     return "";

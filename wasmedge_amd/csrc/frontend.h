@@ -72,11 +72,15 @@ struct Program {
   uint32_t frame_cells = 0;            // max over functions (excluding globals)
   uint32_t total_cells() const { return global_cells + frame_cells; }
   uint32_t max_wasm_instrs_per_dispatch = 0;
+  // metered lowering: global.set never retargets its producer, so a cost-limit trap
+  // between a value and its global.set leaves the global unwritten as in the reference
+  bool exact_globals = false;
 };
 
 // Load + validate + lower. Returns empty string on success, else an error message;
 // *errcode receives the reference ErrCode byte (include/common/enum.inc).
-std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode);
+std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
+                         bool exact_globals = false);
 
 int find_export(const Program &p, const std::string &name);
 

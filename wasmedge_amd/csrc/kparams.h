@@ -42,7 +42,9 @@ struct KParams {
   uint32_t is_start;            // this launch runs the start function (instantiation)
   uint32_t resume;              // continue the lanes parked at a host import
   uint32_t hb_cells;
-  uint64_t max_steps;           // instruction budget per instance
+  uint64_t max_steps;           // instruction budget per instance (Interrupted, coarse)
+  uint64_t cost_limit;          // exact unit-cost gas limit (CostLimitExceeded), ~0 = none
+  uint32_t *stop;               // host-set interrupt request (WasmEdge_BatchInterrupt)
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
 };
 
