@@ -38,6 +38,37 @@ def c2_mem_bytes(iters):
     return 96 + 128 * iters + 4
 
 
+def workload(name, args):
+    """(wasm, export, rows builder(ids) -> int64[n, k], param types, description) of a
+    BASELINE.json config. The default bench line is C2 (configs[1]); the others are
+    selectable with --workload for the per-config numbers in DESIGN.md."""
+    from wasmedge_amd import batch, workloads
+    I32 = batch.I32
+    if name == "c2":
+        it = args.iters
+        return (workloads.blake3_wasm(), "run", lambda ids: np.stack([ids, np.full_like(ids, it)], 1),
+                [I32, I32], "C2 BLAKE3 compression loop (configs[1])", {"iters": it})
+    if name == "c1":
+        fib = open(os.path.join(ROOT, "tests", "golden", "fibonacci.wasm"), "rb").read()
+        return (fib, "fib", lambda ids: (20 + ids % 11)[:, None], [I32],
+                "C1 recursive fib(n), n = 20 + id mod 11 (configs[0] on the GPU)", {})
+    if name == "c3":
+        el = args.elements
+        return (workloads.qsort_wasm(), "sort", lambda ids: np.stack([ids, np.full_like(ids, el)], 1),
+                [I32, I32], "C3 quicksort of %d i32 per instance (configs[2])" % el,
+                {"elements": el})
+    if name == "c4":
+        return (workloads.collatz_wasm(), "collatz",
+                lambda ids: np.stack([ids, np.full_like(ids, 10000)], 1), [I32, I32],
+                "C4 Collatz br_table state machine + per-lane traps (configs[3])", {})
+    if name == "c5":
+        return (workloads.mandel_wasm(), "tile",
+                lambda ids: np.stack([ids, np.full_like(ids, 4096), np.full_like(ids, 50)], 1),
+                [I32, I32, I32], "C5 f64x2 Mandelbrot 8x8 tiles of 4096^2, 50 iters (configs[4])",
+                {})
+    raise SystemExit("unknown workload " + name)
+
+
 class Dist:
     """Barrier + max over ranks. torch.distributed (gloo, CPU-side) only when
     WORLD_SIZE > 1, imported after the HIP library so the two HIP runtimes never mix
@@ -137,25 +168,28 @@ def main():
     ap.add_argument("--instances", type=int, default=INSTANCES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     args = ap.parse_args()
 
     dist = Dist()
-    from wasmedge_amd import batch, workloads
-    wasm = workloads.blake3_wasm()
+    from wasmedge_amd import batch
+    wasm, func, build_rows, ptypes, desc, extra = workload(args.workload, args)
     n = args.instances
-    ctx = batch.BatchContext(wasm, n, device=dist.local_rank)
-    rows = np.zeros((n, 2), np.int64)
-    rows[:, 0] = shard_ids(dist.rank, n)
-    rows[:, 1] = args.iters
-    ctx.set_args("run", batch.make_values(rows, [batch.I32, batch.I32]))
+    kw = {"max_memory_page": 17} if args.workload == "c3" else {}
+    ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
+    rows = build_rows(shard_ids(dist.rank, n))
+    ctx.set_args(func, batch.make_values(rows, ptypes))
+    nret = 1
     dist.init()
 
     for _ in range(args.warmup):
         ctx.reset()
         ctx.run()
-    _, st, cnt = ctx.results(1)
-    if int((st != 0).sum()):
-        raise SystemExit("C2 instances trapped: %s" % np.unique(st))
+    _, st, cnt = ctx.results(nret)
+    traps = int((st != 0).sum())
+    if traps and args.workload != "c4":
+        raise SystemExit("%s instances trapped: %s" % (args.workload, np.unique(st)))
     instrs_per_step = float(cnt.sum())
 
     dist.barrier()
@@ -168,18 +202,14 @@ def main():
     dist.barrier()
     elapsed = dist.max(elapsed)
     total_instrs = dist.sum(instrs_per_step) * args.steps
-    rets, st, cnt = ctx.results(1)
-    assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == 0
+    rets, st, cnt = ctx.results(nret)
+    assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == traps
     # checksum of checksums over every instance's final linear memory (hash kernel, after
     # the timed region)
     hashes = ctx.memory_hash()
     checksum = int(hashes.sum(dtype=np.uint64))
     gpu = {"counts": cnt, "hashes": hashes, "ret": rets["lo"][:, 0] & 0xFFFFFFFF}
-
     kernel_avg = ksum / args.steps
-    bytes_launch = float(c2_mem_bytes(args.iters)) * n
-    achieved = bytes_launch / kernel_avg / 1e9
-    traffic = load_profile_traffic()
     out = {
         "metric": METRIC,
         "value": total_instrs / elapsed,
@@ -191,25 +221,31 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "i32",
-        "data": "synthetic: per-instance BLAKE3 input from splitmix64(instance id), "
-                "generated inside the wasm module",
-        "config": {"workload": "C2 BLAKE3 compression loop (configs[1])",
-                   "instances_per_gpu": n, "iters": args.iters,
-                   "instrs_per_instance": instrs_per_step / n,
-                   "parallelism": "instance-sharded, 1 process per GPU"},
+        "dtype": "i32" if args.workload != "c5" else "f64",
+        "data": "synthetic: per-instance inputs derived from the instance id inside the "
+                "wasm module",
+        "config": dict({"workload": desc, "instances_per_gpu": n,
+                        "instrs_per_instance": instrs_per_step / n,
+                        "parallelism": "instance-sharded, 1 process per GPU"}, **extra),
         "memory_checksum": "%016x" % checksum,
         "kernel_instr_per_s": total_instrs / (dist.max(kernel_avg) * args.steps),
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "note": "algorithmic = linear-memory bytes the wasm program moves; the "
-                             "path is dispatch-issue bound, see issue_roofline"},
-        "issue_roofline": {"achieved": total_instrs / elapsed / dist.world,
-                           "unit": "wasm instr/s per GPU",
-                           "dispatch_bound": "see DESIGN.md 'Roofline'"},
     }
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+    if args.workload == "c4":
+        out["config"]["trapped_instances"] = traps
+    if args.workload == "c2":
+        bytes_launch = float(c2_mem_bytes(args.iters)) * n
+        achieved = bytes_launch / kernel_avg / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                           "traffic": load_profile_traffic(),
+                           "note": "algorithmic = linear-memory bytes the wasm program moves; "
+                                   "the path is dispatch-issue bound, see issue_roofline"}
+        out["issue_roofline"] = {"achieved": total_instrs / elapsed / dist.world,
+                                 "unit": "wasm instr/s per GPU",
+                                 "dispatch_bound": "see DESIGN.md 'Roofline'"}
+    else:
+        out["data"] = "synthetic: per-instance inputs derived from the instance id"
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         threads = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(wasm, args.iters, args.cpu_seconds, threads, gpu)
     if dist.rank == 0:
