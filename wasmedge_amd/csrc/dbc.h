@@ -71,6 +71,10 @@ struct DInstr {
   X(I32_EQZ) X(I32_CLZ) X(I32_CTZ) X(I32_POPCNT) X(I32_EXT8S) X(I32_EXT16S)            \
   /* superinstructions: c = a + b + d ; c = rot(a ^ b, imm)                           */ \
   X(I32_ADD3) X(I32_XOR_ROTR_I) X(I32_XOR_ROTL_I)                                      \
+  /* ARX pairs (peephole, see frontend.cpp fuse_arx): c = a + b (+ d);                 */ \
+  /*   ADD_XROTR_I:  d = rotr(d ^ c, imm)                                             */ \
+  /*   ADD3_XROTR_I: y = rotr(y ^ c, imm >> 16), y = imm & 0xFFFF                      */ \
+  X(I32_ADD_XROTR_I) X(I32_ADD3_XROTR_I)                                               \
   /* i64 binary (compares write an i32 cell)                                          */ \
   X(I64_ADD) X(I64_SUB) X(I64_MUL) X(I64_DIV_S) X(I64_DIV_U) X(I64_REM_S) X(I64_REM_U) \
   X(I64_AND) X(I64_OR) X(I64_XOR) X(I64_SHL) X(I64_SHR_S) X(I64_SHR_U) X(I64_ROTL)     \

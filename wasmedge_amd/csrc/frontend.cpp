@@ -1309,6 +1309,74 @@ ConstVal eval_const(Reader &r, const Program &P, const std::vector<ConstVal> &gl
   return v;
 }
 
+// Peephole over the finished program: an i32 add (or ADD3) followed by an in-place
+// xor-rotate of another cell with the sum (the add-xor-rotate step of BLAKE3's G, ChaCha's
+// quarter round, ...) becomes one dispatch. The second instruction is removed and every
+// pc reference is remapped; pairs whose second half is a branch/call target are kept.
+static bool is_pc_branch(uint16_t op) {
+  return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS || op == OP_BR_IF_MOV1 ||
+         op == OP_BR_IF_MOV2 || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
+}
+
+void fuse_arx(Program &P) {
+  const size_t n = P.code.size();
+  std::vector<uint8_t> target(n + 1, 0);
+  for (size_t pc = 0; pc < n; pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = I.w0 & 0x7FFF;
+    if ((is_pc_branch(op) || op == OP_CALL) && I.w3 < n) target[I.w3] = 1;
+    if (op == OP_CALL || op == OP_CALL_INDIRECT) target[pc + 1] = 1;   // return pc
+  }
+  for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
+    if (P.brtab[k] < n) target[P.brtab[k]] = 1;
+  for (const auto &f : P.funcs)
+    if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
+  std::vector<uint8_t> drop(n, 0);
+  size_t fused = 0;
+  for (size_t pc = 0; pc + 1 < n; pc++) {
+    DInstr &I = P.code[pc], &J = P.code[pc + 1];
+    const uint16_t op1 = I.w0 & 0x7FFF, op2 = J.w0 & 0x7FFF;
+    if ((op1 != OP_I32_ADD && op1 != OP_I32_ADD3) || target[pc + 1] || drop[pc]) continue;
+    if (op2 != OP_I32_XOR_ROTR_I && op2 != OP_I32_XOR_ROTL_I) continue;
+    const uint32_t sum = I.w2 & 0xFFFF, ja = J.w1 & 0xFFFF, jb = J.w1 >> 16, jc = J.w2 & 0xFFFF;
+    const uint32_t y = ja == sum ? jb : ja;
+    if ((ja != sum && jb != sum) || jc != y || y == sum) continue;   // y = rot(y ^ sum)
+    const uint32_t cnt = ((I.w0 >> 16) & 0xFF) + ((J.w0 >> 16) & 0xFF);
+    if (cnt > 255 || y > 0xFFFF) continue;
+    const uint32_t k = op2 == OP_I32_XOR_ROTR_I ? (J.w3 & 31u) : ((32u - (J.w3 & 31u)) & 31u);
+    const uint32_t post = (J.w0 >> 24) & 0x7F;
+    if (op1 == OP_I32_ADD) {
+      I.w0 = OP_I32_ADD_XROTR_I | (cnt << 16) | (post << 24);
+      I.w2 = sum | (y << 16);
+      I.w3 = k;
+    } else {
+      I.w0 = OP_I32_ADD3_XROTR_I | (cnt << 16) | (post << 24);
+      I.w3 = y | (k << 16);
+    }
+    if (cnt > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = cnt;
+    drop[pc + 1] = 1;
+    fused++;
+  }
+  if (!fused) return;
+  std::vector<uint32_t> remap(n + 1);
+  std::vector<DInstr> out;
+  out.reserve(n - fused);
+  for (size_t pc = 0; pc < n; pc++) {
+    remap[pc] = uint32_t(out.size());
+    if (!drop[pc]) out.push_back(P.code[pc]);
+  }
+  remap[n] = uint32_t(out.size());
+  for (DInstr &I : out) {
+    const uint16_t op = I.w0 & 0x7FFF;
+    if ((is_pc_branch(op) || op == OP_CALL) && I.w3 <= n) I.w3 = remap[I.w3];
+  }
+  for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
+    if (P.brtab[k] <= n) P.brtab[k] = remap[P.brtab[k]];
+  for (auto &f : P.funcs)
+    if (!f.imported) { f.entry_pc = remap[f.entry_pc]; f.body_pc = remap[f.body_pc]; }
+  P.code.swap(out);
+}
+
 void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   if (len < 8 || memcmp(wasm, "\0asm\1\0\0\0", 8)) throw Err{0x23, "magic header not detected"};
   Reader r{wasm + 8, wasm + len};
@@ -1521,6 +1589,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   std::vector<CallFix> callfix;
   for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
   for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
+  fuse_arx(P);
   if (P.code.size() >= DBC_MAX_PC) throw Err{E_UNSUPPORTED, "module too large for 20-bit pcs"};
 }
 

@@ -248,6 +248,21 @@ def specs():
     add("I32_XOR_ROTR_I", ["I32_XOR_ROTR_I"], lambda g: [
         "v_xor_b32_e32 %s, %s, %s" % (X[0], A[0], B[0]),
         "v_alignbit_b32 %s, %s, %s, %s" % (R[0], X[0], X[0], g.x(4))] + g.w32() + g.next())
+    # ARX pairs: sum -> c, then d (or the 4th cell y, read here) = rotr(. ^ sum, k)
+    add("I32_ADD_XROTR_I", ["I32_ADD_XROTR_I"], lambda g: [
+        "v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0])] + g.w32() + [
+        "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
+        "v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
+        "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next())
+    add("I32_ADD3_XROTR_I", ["I32_ADD3_XROTR_I"], lambda g: [
+        "v_add_u32 %s, %s, %s" % (X[1], g.x(7), FR),
+        "ds_read_b32 %s, %s" % (Y[0], X[1]),
+        "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + [
+        "s_waitcnt lgkmcnt(0)",
+        "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
+        "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
     add("I32_CLZ", ["I32_CLZ"], lambda g: [
         "v_ffbh_u32_e32 %s, %s" % (X[0], A[0]),
         "v_min_u32_e32 %s, 32, %s" % (R[0], X[0])] + g.w32() + g.next())

@@ -36,7 +36,13 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     TInstr &t = tc[pc];
     uint32_t *w = t.w;
     w[1] = off(a); w[2] = off(b); w[3] = off(c); w[4] = imm; w[5] = 0; w[6] = cnt; w[7] = 0;
-    if (op == OP_I32_ADD3 || op == OP_SELECT32 || op == OP_SELECT64) w[5] = off(d);
+    if (op == OP_I32_ADD3 || op == OP_SELECT32 || op == OP_SELECT64 ||
+        op == OP_I32_ADD_XROTR_I || op == OP_I32_ADD3_XROTR_I)
+      w[5] = off(d);
+    if (op == OP_I32_ADD3_XROTR_I) {   // the 4th operand (y) is read by the handler itself
+      w[7] = off(imm & 0xFFFFu);
+      w[4] = imm >> 16;
+    }
     if (is_branch(op)) {
       const int32_t taken = int32_t(cnt) + int32_t(int16_t(d));
       if (taken < 0 || imm >= (1u << 26)) continue;
