@@ -127,8 +127,10 @@ class Gen:
                 "s_addc_u32 %s, %s, 0" % (T[1], base[1]),
                 "s_setpc_b64 %s" % TP]
 
-    def next(self, cnt=True):
-        """Fall through to the prefetched successor (other bank)."""
+    def next(self, cnt=True, pf4=False):
+        """Fall through to the prefetched successor (other bank). pf4: also read the
+        successor's 4th operand (field 7) into Y0, its address kept in X1 (only for
+        successors the translator gave an *_E handler, see tc.cpp)."""
         out = []
         if cnt:
             out.append("s_add_u32 %s, %s, %s" % (CNT, CNT, self.x(6)))
@@ -136,6 +138,9 @@ class Gen:
         if self.mode == "D":
             out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
         out += self.issue_reads(self.other)
+        if pf4:
+            out += ["v_add_u32 %s, %s, %s" % (X[1], sreg(self.other, 7), FR),
+                    "ds_read_b32 %s, %s" % (Y[0], X[1])]
         # prefetch the successor's successor into this bank (its fields are dead now)
         out.append("s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank(self.bank), CODE, PCOFF))
         out += self.dispatch(self.other)
@@ -260,6 +265,19 @@ def specs():
         "ds_read_b32 %s, %s" % (Y[0], X[1]),
         "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + [
         "s_waitcnt lgkmcnt(0)",
+        "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
+        "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
+    # pipelined pair (tc.cpp picks these when ADD_XROTR falls into ADD3_XROTR and the
+    # latter is no jump target): the first prefetches the second's 4th operand y
+    add("I32_ADD_XROTR_I_PF4", [], lambda g: [
+        "v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0])] + g.w32() + [
+        "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
+        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
+        "v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
+        "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next(pf4=True))
+    add("I32_ADD3_XROTR_I_E", [], lambda g: [
+        "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + [
         "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
         "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
         "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
@@ -464,7 +482,9 @@ def main():
         f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
         f.write("#pragma once\n#include \"dbc.h\"\n\n")
         f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n\n" % (SLOT, nslots))
-        f.write("// returns the handler slot (0 = no handler: the C++ step runs the op)\n")
+        for si, (nm, ops, _) in enumerate(S, start=1):
+            f.write("#define TC_SLOT_%s %d\n" % (nm, si))
+        f.write("\n// returns the handler slot (0 = no handler: the C++ step runs the op)\n")
         f.write("static inline int tc_slot(uint16_t op) {\n  switch (op) {\n")
         for si, (nm, ops, _) in enumerate(S, start=1):
             for op in ops:

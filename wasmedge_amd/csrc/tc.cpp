@@ -69,6 +69,32 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     w[0] = uint32_t(slot) * TC_SLOT_BYTES;
     code[pc].w0 |= DBC_HOT;
   }
+  // Pipelined ARX pairs: ADD_XROTR falling into ADD3_XROTR prefetches the latter's 4th
+  // operand. The *_E handler relies on that, so it must only ever be entered by that
+  // fall-through: not a jump/call/return target, and not an entry point of the core
+  // (DBC_HOT cleared: a run that stops in front of it resumes in the C++ step).
+  const size_t n = P.code.size();
+  std::vector<uint8_t> target(n + 1, 0);
+  for (size_t pc = 0; pc < n; pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
+    if ((is_branch(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2 || op == OP_CALL) && I.w3 < n)
+      target[I.w3] = 1;
+    if (op == OP_CALL || op == OP_CALL_INDIRECT) target[pc + 1] = 1;
+  }
+  for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
+    if (P.brtab[k] < n) target[P.brtab[k]] = 1;
+  for (const auto &f : P.funcs)
+    if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
+  for (size_t pc = 1; pc < n; pc++) {
+    const uint16_t op = uint16_t(P.code[pc].w0 & 0x7FFFu), prev = uint16_t(P.code[pc - 1].w0 & 0x7FFFu);
+    if (op == OP_I32_ADD3_XROTR_I && prev == OP_I32_ADD_XROTR_I && !target[pc] &&
+        tc[pc].w[0] && tc[pc - 1].w[0]) {
+      tc[pc - 1].w[0] = TC_SLOT_I32_ADD_XROTR_I_PF4 * TC_SLOT_BYTES;
+      tc[pc].w[0] = TC_SLOT_I32_ADD3_XROTR_I_E * TC_SLOT_BYTES;
+      code[pc].w0 &= ~DBC_HOT;
+    }
+  }
   return tc;
 }
 
