@@ -1,0 +1,52 @@
+"""Per-wave scheduler statistics of the interpreter on each config workload (profiling
+build libwasmedge_batch_stats.so, -DWB_STATS). Prints, per workload: wasm instrs,
+scheduler rounds, fast runs and mean active lanes, threaded-core entries, compiled-step
+dispatches, slow steps, and the split of shader cycles (sched / fast run / slow step),
+averaged over waves. Usage: python tools/sched_stats.py"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["WB_BATCH_LIB"] = os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch_stats.so")
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+from wasmedge_amd import batch, workloads as W  # noqa: E402
+
+NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow"]
+
+
+def run(name, wasm, func, rows, types):
+    n = len(rows)
+    L = batch.lib()
+    L.wb_stats_read.restype = ctypes.c_uint32
+    L.wb_stats_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    ctx = batch.BatchContext(wasm, n, device=0)
+    ctx.set_args(func, batch.make_values(np.asarray(rows, dtype=np.int64), types))
+    ctx.reset()
+    t = ctx.run()
+    _, st, cnt = ctx.results(1)
+    nw = (n + 63) // 64
+    buf = np.zeros((nw, 9), np.uint64)
+    L.wb_stats_read(ctx._h, buf.ctypes.data)
+    m = buf.astype(np.float64).mean(0)
+    d = dict(zip(NAMES, m))
+    cyc = (d["cyc_sched"] + d["cyc_fast"] + d["cyc_slow"]) * 16
+    print("%-10s instr/s=%.3e wasm/inst=%.3e rounds=%.3e fast-lanes=%.1f tc=%.3e cpp=%.3e "
+          "slow=%.3e | cycles/wave=%.3e sched=%.0f%% fast=%.0f%% slow=%.0f%% | cyc/round=%.0f"
+          % (name, cnt.sum() / t, cnt.mean(), d["rounds"], d["lanes"] / max(d["fast"], 1),
+             d["tc"], d["cpp"], d["slow"], cyc, 100 * 16 * d["cyc_sched"] / cyc,
+             100 * 16 * d["cyc_fast"] / cyc, 100 * 16 * d["cyc_slow"] / cyc,
+             cyc / max(d["rounds"], 1)), flush=True)
+    ctx.close()
+
+
+I32 = batch.I32
+N = 65536
+fib = open(os.path.join(ROOT, "tests/golden/fibonacci.wasm"), "rb").read()
+run("c2", W.blake3_wasm(), "run", [[i, 100] for i in range(N)], [I32, I32])
+run("c1-div", fib, "fib", [[20 + i % 11] for i in range(N)], [I32])
+run("fib-uni", fib, "fib", [[22] for i in range(N)], [I32])
+run("c3-4k", W.qsort_wasm(), "sort", [[i, 4096] for i in range(N)], [I32, I32])
+run("c4", W.collatz_wasm(), "collatz", [[i, 10000] for i in range(N)], [I32, I32])
+run("c5", W.mandel_wasm(), "tile", [[i, 4096, 50] for i in range(N)], [I32, I32, I32])

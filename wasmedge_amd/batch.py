@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwasmedge_batch.so")
+# WB_BATCH_LIB selects a profiling variant (libwasmedge_batch_stats.so, tools/ only)
+LIB_PATH = os.environ.get("WB_BATCH_LIB") or os.path.join(_HERE, "libwasmedge_batch.so")
 
 # valtypes (include/api/wasmedge/enum_types.h)
 I32, I64, F32, F64, V128, FUNCREF, EXTERNREF = 0x7F, 0x7E, 0x7D, 0x7C, 0x7B, 0x70, 0x6F

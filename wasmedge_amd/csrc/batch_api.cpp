@@ -76,6 +76,7 @@ struct WasmEdge_BatchContext {
   hipStream_t stream = nullptr;
   hipStream_t ctl_stream = nullptr;  // interrupt requests, while `stream` runs a kernel
   uint32_t *stop = nullptr;          // uncached device word polled by the kernel
+  uint64_t *stats = nullptr;         // WB_STATS builds: per-wave counters (WB_STATS_OUT)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string last_error;
   // module buffers
@@ -95,7 +96,7 @@ struct WasmEdge_BatchContext {
   DevBuf<uint8_t> status;
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0;
-  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0;
+  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
   // current invocation
   int func = -1;
   uint32_t param_cells = 0, result_cells = 0;
@@ -186,6 +187,16 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
   size_t nw = C->nwaves;
   C->ls_slots = LS_GLOBALS + P.global_cells;
+  // LDS call-stack slots per lane: what the frames leave of the LDS share each wave gets
+  // at the occupancy this batch reaches (nwaves over 256 CUs, at most 16 waves per CU)
+  {
+    const uint32_t tc = P.total_cells() ? P.total_cells() : 1;
+    const uint32_t per_cu = std::min<uint32_t>(16, std::max<uint32_t>(4, (C->nwaves + 255) / 256));
+    const uint32_t wave_cells = (160 * 1024 - 1024) / 256 / per_cu;   // 256 B per cell row
+    uint32_t s = wave_cells > tc + 1 ? wave_cells - tc - 1 : 0;
+    if (s > C->gs_depth) s = C->gs_depth;
+    C->gs_lds = s >= 8 ? s : 0;
+  }
   C->hosts.assign(P.funcs.size(), {});
   C->hb_cells = 1;
   for (uint32_t f = 0; f < P.n_imported; f++) {
@@ -198,11 +209,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) ||
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
-      (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells()) * 64) ||
+      (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
+#ifdef WB_STATS
+  if (!C->hip_ok(hipMalloc(&C->stats, nw * 9 * sizeof(uint64_t)), "stats")) return kRuntimeError;
+#endif
   if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
   return 0;
 }
@@ -262,6 +276,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.init_pages = P.mem_min;
   k.mem_max_pages = C->mem_max_pages;
   k.gs_depth = C->gs_depth;
+  k.gs_lds = C->gs_lds;
   k.init_dropped = C->init_dropped;
   k.ls_slots = C->ls_slots;
   k.is_start = is_start ? 1u : 0u;
@@ -270,8 +285,12 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
   double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
   k.max_ticks = uint64_t(tl * 1e8);
+  k.stats = C->stats;
+#ifdef WB_STATS
+  (void)hipMemsetAsync(C->stats, 0, size_t(C->nwaves) * 9 * sizeof(uint64_t), C->stream);
+#endif
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
-  size_t wave_lds = size_t(k.total_cells) * 64 * 4;
+  size_t wave_lds = size_t(k.total_cells + k.gs_lds) * 64 * 4;
   if (wave_lds + 256 > 160 * 1024)
     return C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
                                       " cells exceeds LDS (global-frame mode: next)");
@@ -603,6 +622,16 @@ const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
   return C ? C->last_error.c_str() : g_last_create_error.c_str();
 }
 
+#ifdef WB_STATS
+// profiling builds only: per-wave counters of the last launch, [waves][9] (batch_kernel.hip)
+__attribute__((visibility("default"))) uint32_t wb_stats_read(WasmEdge_BatchContext *C,
+                                                              uint64_t *out) {
+  if (!C || !C->stats) return 0;
+  (void)hipMemcpy(out, C->stats, size_t(C->nwaves) * 9 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  return C->nwaves;
+}
+#endif
+
 void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *C) {
   if (!C || !C->stop) return;
   static const uint32_t one = 1;
@@ -615,6 +644,7 @@ void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   if (C->stream) (void)hipStreamSynchronize(C->stream);
   if (C->ctl_stream) (void)hipStreamDestroy(C->ctl_stream);
   if (C->stop) (void)hipFree(C->stop);
+  if (C->stats) (void)hipFree(C->stats);
   if (C->ev0) (void)hipEventDestroy(C->ev0);
   if (C->ev1) (void)hipEventDestroy(C->ev1);
   hipStream_t s = C->stream;

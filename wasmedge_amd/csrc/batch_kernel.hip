@@ -45,13 +45,25 @@ extern "C" __global__ void wb_tc_holder_kernel() {
                "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
 }
 
+// Minimum over the wave (all 64 lanes active), in VALU DPP steps instead of LDS permutes:
+// row_shr 1/2/4/8 leave each row's prefix minimum in its lane 15, row_bcast:15 and
+// row_bcast:31 fold rows 0-2 into rows 1-3, so lane 63 holds the wave minimum. Lanes whose
+// DPP source is out of range keep the identity (`old` = ~0).
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
-    v = o < v ? o : v;
-  }
-  return __builtin_amdgcn_readfirstlane(v);
+  const int I = -1;
+#define WB_DPP_MIN(ctrl, rmask)                                                            \
+  do {                                                                                    \
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, ctrl, rmask, 0xF, false); \
+    v = t < v ? t : v;                                                                    \
+  } while (0)
+  WB_DPP_MIN(0x111, 0xF);   // row_shr:1
+  WB_DPP_MIN(0x112, 0xF);   // row_shr:2
+  WB_DPP_MIN(0x114, 0xF);   // row_shr:4
+  WB_DPP_MIN(0x118, 0xF);   // row_shr:8
+  WB_DPP_MIN(0x142, 0xA);   // row_bcast:15 into rows 1 and 3
+  WB_DPP_MIN(0x143, 0xC);   // row_bcast:31 into rows 2 and 3
+#undef WB_DPP_MIN
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
 
@@ -60,6 +72,26 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // index decoded from the scalar-loaded instruction) is one conflict-free ds_read_b32.
 // (Register-resident frames via s_set_gpr_idx were measured 10-45% slower on every
 // workload -- see DESIGN.md "Frames" -- and removed.)
+// Optional per-wave execution statistics (profiling builds: -DWB_STATS, see
+// tools/sched_stats.py): scheduler rounds, fast runs and their active lanes, threaded-core
+// entries, compiled-step dispatches, slow steps, and shader cycles per phase.
+#ifdef WB_STATS
+enum { ST_ROUNDS, ST_FAST, ST_LANES, ST_TC, ST_CPP, ST_SLOW, ST_CYC_SCHED, ST_CYC_FAST,
+       ST_CYC_SLOW, ST_N };
+// one relaxed atomic add per event from the first active lane (also inside divergent
+// regions, where a per-wave count must be taken once); cycles in units of 16 clocks
+#define WB_STAT_ADD(k, v)                                                              \
+  do {                                                                                 \
+    const uint64_t _m = __ballot(1);                                                   \
+    if (stw && __lane_id() == (uint32_t)__builtin_ctzll(_m))                           \
+      __hip_atomic_fetch_add(&stw[k], (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+  } while (0)
+#define WB_NOW() (__builtin_amdgcn_s_memtime() >> 4)
+#else
+#define WB_STAT_ADD(k, v) ((void)0)
+#define WB_NOW() 0ull
+#endif
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 struct LdsFrame {
   lds_u32 *fr;   // LDS-typed so the compiler knows frame cells never alias HBM
@@ -119,7 +151,8 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
 template <class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
                                        uint32_t *const gs, uint32_t *const mem,
-                                       uint32_t *const ls, uint32_t *const fs) {
+                                       uint32_t *const ls, uint32_t *const fs,
+                                       lds_u32 *const stk) {
   // the bytecode is read through the constant address space so every fetch is one
   // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
   typedef uint32_t w4 __attribute__((ext_vector_type(4)));
@@ -132,7 +165,17 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define W64(c, v) do { const uint64_t _v = (v); F.set((uint32_t)(c), (uint32_t)_v); F.set((uint32_t)(c) + 1, (uint32_t)(_v >> 32)); } while (0)
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) F.set((uint32_t)(c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) F.set((uint32_t)(c), (uint32_t)(v))
-#define GS(slot) gs[(size_t)(slot) << 6]
+// Call stack: slots [0, gs_lds) in LDS (`stk`, cell-major like frames), the rest in HBM
+// (`gs`, lane-interleaved). The fast loop only touches the LDS part (GS_FAST checks it
+// per wave); the per-lane step handles either.
+  const uint32_t S_lds = p.gs_lds;
+#define GS_RD(s) ((uint32_t)(s) < S_lds ? stk[(uint32_t)(s) << 6] : gs[(size_t)((uint32_t)(s) - S_lds) << 6])
+#define GS_WR(s, v) do { const uint32_t _s = (s), _v = (v); \
+    if (_s < S_lds) stk[_s << 6] = _v; else gs[(size_t)(_s - S_lds) << 6] = _v; } while (0)
+#define GS_FAST(hi) ((hi) <= S_lds)
+#define GSF_BASE(s) (&stk[(uint32_t)(s) << 6])
+#define GS_PTR lds_u32 *const
+#define GS_CPTR const lds_u32 *const
 
 #define LS(slot) ls[(size_t)(slot) << 6]
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
@@ -156,6 +199,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       gsp = LS(LS_GSP);
       count = p.counts[inst];
       for (uint32_t c = p.global_cells; c < p.total_cells; c++) F.set(c, fs[(size_t)c << 6]);
+      for (uint32_t k = 0; k < gsp && k < S_lds; k++) stk[k << 6] = fs[(size_t)(p.total_cells + k) << 6];
       const uint32_t base = LS(LS_HBASE);
       for (uint32_t k = 0; k < nres; k++) F.set(base + k, p.hbuf[(size_t)inst * p.hb_cells + k]);
     } else {
@@ -165,11 +209,14 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     if (fs) LS(LS_RPC) = 0xFFFFFFFFu;   // a fresh invocation: nothing parked
     const uint32_t *prm = p.params + (size_t)inst * p.param_cells;
     for (uint32_t c = 0; c < p.param_cells; c++) F.set(p.global_cells + c, prm[c]);
-    GS(0) = DBC_EXIT_PC;   // return record of the entry frame: pc = EXIT
+    GS_WR(0u, DBC_EXIT_PC);   // return record of the entry frame: pc = EXIT
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t rounds = 0;
+#ifdef WB_STATS
+  uint64_t *const stw = p.stats ? p.stats + (size_t)(inst >> 6) * ST_N : nullptr;
+#endif
   const uint32_t lane = __lane_id();
   const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
 
@@ -179,6 +226,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     // `other` = the lowest pc of the lanes left waiting.
     const uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
     if (!runmask) break;
+    const uint64_t ts0 = WB_NOW();
+    WB_STAT_ADD(ST_ROUNDS, 1);
     uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(runmask));
     uint64_t act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
     uint32_t other = 0xFFFFFFFFu;
@@ -189,6 +238,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         other = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
     }
     bool slow = false;   // the run stopped at an instruction that needs the slow step
+    const uint64_t ts1 = WB_NOW();
+    WB_STAT_ADD(ST_CYC_SCHED, ts1 - ts0);
+    WB_STAT_ADD(ST_FAST, 1);
+    WB_STAT_ADD(ST_LANES, __builtin_popcountll(act));
     // (select by the ballot bit, not by `pc == pcs`: under that condition the compiler
     // would substitute the per-lane pc for pcs and make the whole run divergent)
     if ((act >> lane) & 1u) {
@@ -230,6 +283,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // hand the run to the threaded core; it returns at an instruction this
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
+          WB_STAT_ADD(ST_TC, 1);
           pcs = tc_run(p.tcode, pcs, other, fr_lds, pages, mem, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
@@ -243,6 +297,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         const uint32_t op = w0 & 0x7FFFu;
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
+        WB_STAT_ADD(ST_CPP, 1);
         // metered: a dispatch that may cross the gas limit runs in the exact slow step
         // (the threaded core is off when metering, see launch_once)
         if (p.cost_limit != ~0ull)
@@ -297,6 +352,9 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       }
     }
     const uint64_t slowmask = __ballot(slow);
+    const uint64_t ts2 = WB_NOW();
+    WB_STAT_ADD(ST_CYC_FAST, ts2 - ts1);
+    if (slowmask) WB_STAT_ADD(ST_SLOW, 1);
     if (slowmask && ((slowmask >> lane) & 1u)) {
       // ================================================================ slow step
       // One dispatch with fully per-lane semantics (the same step code, WB_FAST 0):
@@ -352,6 +410,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_IF
 #undef HOST_YIELD
     }
+    WB_STAT_ADD(ST_CYC_SLOW, WB_NOW() - ts2);
     // budget, wall clock, and (every 64th round) the host's interrupt request, read
     // from uncached device memory at system scope
     const bool stop = (++rounds & 63u) == 0 &&
@@ -366,7 +425,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef W64
 #undef W128
 #undef WLOOP
-#undef GS
+#undef GS_RD
+#undef GS_WR
+#undef GS_FAST
+#undef GSF_BASE
+#undef GS_PTR
+#undef GS_CPTR
   if (active) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
@@ -376,6 +440,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       LS(LS_HBASE) = ybase;
       p.hcall[inst] = ycall;
       for (uint32_t c = p.global_cells; c < p.total_cells; c++) fs[(size_t)c << 6] = F.get(c);
+      for (uint32_t k = 0; k < gsp && k < S_lds; k++) fs[(size_t)(p.total_cells + k) << 6] = stk[k << 6];
       for (uint32_t k = 0; k < p.hb_cells && ybase + k < p.total_cells; k++)
         p.hbuf[(size_t)inst * p.hb_cells + k] = F.get(ybase + k);
     }
@@ -394,10 +459,12 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t inst = wave * 64u + lane;
   LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
+  // LDS call-stack slots of this wave follow the frames of all the block's waves
+  lds_u32 *const stk = (lds_u32 *)(lds + ((((blockDim.x >> 6) * p.total_cells) + wib * p.gs_lds) << 6) + lane);
   interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
          p.mem + (size_t)wave * p.mem_words * 64u + lane,
          p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
-         p.fsave ? p.fsave + (size_t)wave * p.total_cells * 64u + lane : nullptr);
+         p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
 }
 
 // ======================================================================= helpers

@@ -88,6 +88,12 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define R64(x) ((uint64_t)CELL(x) | ((uint64_t)CELL((x) + 1) << 32))
 #define W64(x, v) do { const uint64_t _v = (v); CELL(x) = (uint32_t)_v; CELL((x) + 1) = (uint32_t)(_v >> 32); } while (0)
 #define GS(slot) gs[(size_t)(slot)]
+#define GS_RD(s) GS(s)
+#define GS_WR(s, v) (GS(s) = (v))
+#define GS_FAST(hi) true
+#define GSF_BASE(s) (&GS(s))
+#define GS_PTR uint32_t *const
+#define GS_CPTR const uint32_t *const
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
 #define FINISH() (status = WB_STATUS_OK)
 #define JUMP(t, tc) do { npc = (t); add += (tc); goto e_next; } while (0)

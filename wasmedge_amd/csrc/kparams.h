@@ -37,6 +37,7 @@ struct KParams {
   uint32_t mem_words;           // words per lane reserved (= mem_max_pages * 16384)
   uint32_t init_pages, mem_max_pages;
   uint32_t gs_depth;            // call-stack cells per lane
+  uint32_t gs_lds;              // of which the first gs_lds live in LDS (after the frames)
   uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
   uint32_t ls_slots;            // LS_GLOBALS + global_cells
   uint32_t is_start;            // this launch runs the start function (instantiation)
@@ -46,6 +47,7 @@ struct KParams {
   uint64_t cost_limit;          // exact unit-cost gas limit (CostLimitExceeded), ~0 = none
   uint32_t *stop;               // host-set interrupt request (WasmEdge_BatchInterrupt)
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
+  uint64_t *stats;              // WB_STATS builds: per-wave counters (else unused)
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
