@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 from wasmedge_amd import batch, workloads as W  # noqa: E402
 
-NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow"]
+NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow",
+         "x_call", "x_ret", "x_post", "x_br", "x_other"]
 
 
 def run(name, wasm, func, rows, types):
@@ -27,7 +28,7 @@ def run(name, wasm, func, rows, types):
     t = ctx.run()
     _, st, cnt = ctx.results(1)
     nw = (n + 63) // 64
-    buf = np.zeros((nw, 9), np.uint64)
+    buf = np.zeros((nw, 14), np.uint64)
     L.wb_stats_read(ctx._h, buf.ctypes.data)
     m = buf.astype(np.float64).mean(0)
     d = dict(zip(NAMES, m))
@@ -38,6 +39,8 @@ def run(name, wasm, func, rows, types):
              d["tc"], d["cpp"], d["slow"], cyc, 100 * 16 * d["cyc_sched"] / cyc,
              100 * 16 * d["cyc_fast"] / cyc, 100 * 16 * d["cyc_slow"] / cyc,
              cyc / max(d["rounds"], 1)), flush=True)
+    print("           core exits at: call=%.3e ret=%.3e post_call=%.3e branch=%.3e other=%.3e"
+          % (d["x_call"], d["x_ret"], d["x_post"], d["x_br"], d["x_other"]), flush=True)
     ctx.close()
 
 

@@ -77,7 +77,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // entries, compiled-step dispatches, slow steps, and shader cycles per phase.
 #ifdef WB_STATS
 enum { ST_ROUNDS, ST_FAST, ST_LANES, ST_TC, ST_CPP, ST_SLOW, ST_CYC_SCHED, ST_CYC_FAST,
-       ST_CYC_SLOW, ST_N };
+       ST_CYC_SLOW, ST_X_CALL, ST_X_RET, ST_X_POST, ST_X_BR, ST_X_OTHER, ST_N };
 // one relaxed atomic add per event from the first active lane (also inside divergent
 // regions, where a per-wave count must be taken once); cycles in units of 16 clocks
 #define WB_STAT_ADD(k, v)                                                              \
@@ -107,13 +107,20 @@ struct LdsFrame {
 // Register contract: gen_tc.py (s60-s93, v104-v127 belong to the core).
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem,
+                                           uint32_t &gsp, uint32_t stk, uint32_t slds,
                                            uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
-  const uint32_t oth = other >= (1u << 26) ? 0xFFFFFFFFu : other << 5;
+  const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
   const uint64_t m = (uint64_t)(uintptr_t)mem;
   const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
+  const uint64_t cp = (uint64_t)(uintptr_t)tcode;   // as two words: no aligned pair needed
+  const uint32_t clo = (uint32_t)cp, chi = (uint32_t)(cp >> 32);
+  // all of these are wave-uniform; readfirstlane keeps them in SGPRs even where the
+  // compiler's divergence analysis cannot prove it (profiling builds)
+  pc = __builtin_amdgcn_readfirstlane(pc);
   asm volatile(
-      "s_mov_b64 s[60:61], %[code]\n\t"
+      "s_mov_b32 s60, %[clo]\n\t"
+      "s_mov_b32 s61, %[chi]\n\t"
       "s_lshl_b32 s62, %[pc], 5\n\t"
       "s_mov_b32 s63, %[oth]\n\t"
       "s_mov_b32 s64, %[lim]\n\t"
@@ -122,6 +129,9 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
       "v_mov_b32 v105, %[pages]\n\t"
       "v_mov_b32 v106, %[mlo]\n\t"
       "v_mov_b32 v107, %[mhi]\n\t"
+      "v_mov_b32 v102, %[gsp]\n\t"
+      "v_mov_b32 v103, %[stk]\n\t"
+      "s_mov_b32 s93, %[slds]\n\t"
       "s_getpc_b64 s[66:67]\n"
       "Ltc_ret_%=:\n\t"
       "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t"
@@ -133,14 +143,18 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
       "Ltc_back_%=:\n\t"
       "s_lshr_b32 %[npc], s62, 5\n\t"
       "s_mov_b32 %[cnt], s65\n\t"
-      "s_mov_b32 %[why], s92"
-      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why)
-      : [code] "s"(tcode), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr),
-        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi)
+      "s_mov_b32 %[why], s92\n\t"
+      "v_mov_b32 %[gsp], v102"
+      // gsp is read-write: only the run's lanes (EXEC) take the core's value, the
+      // waiting lanes keep theirs
+      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp)
+      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr),
+        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk),
+        [slds] "s"(slds)
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83",
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
-        "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113",
+        "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113",
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123",
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory");
   *ncnt = cnt;
@@ -219,6 +233,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #endif
   const uint32_t lane = __lane_id();
   const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
+  const uint32_t stk_lds = (uint32_t)(uintptr_t)stk;   // its call-stack slot 0
 
   for (;;) {
     // ---- schedule: the lanes at the minimum pc run next (structured control flow puts
@@ -226,7 +241,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     // `other` = the lowest pc of the lanes left waiting.
     const uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
     if (!runmask) break;
-    const uint64_t ts0 = WB_NOW();
+    [[maybe_unused]] const uint64_t ts0 = WB_NOW();
     WB_STAT_ADD(ST_ROUNDS, 1);
     uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(runmask));
     uint64_t act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
@@ -238,7 +253,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         other = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
     }
     bool slow = false;   // the run stopped at an instruction that needs the slow step
-    const uint64_t ts1 = WB_NOW();
+    [[maybe_unused]] const uint64_t ts1 = WB_NOW();
     WB_STAT_ADD(ST_CYC_SCHED, ts1 - ts0);
     WB_STAT_ADD(ST_FAST, 1);
     WB_STAT_ADD(ST_LANES, __builtin_popcountll(act));
@@ -284,10 +299,18 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
-          pcs = tc_run(p.tcode, pcs, other, fr_lds, pages, mem, &ncnt, &why);
+          pcs = tc_run(p.tcode, pcs, other, fr_lds, pages, mem, gsp, stk_lds, S_lds, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
           I = code[pcs];
+#ifdef WB_STATS
+          {
+            const uint32_t xo = I.x & 0x7FFFu;
+            WB_STAT_ADD(xo == OP_CALL || xo == OP_CALL_INDIRECT ? ST_X_CALL : xo == OP_RET ? ST_X_RET
+                        : xo == OP_POST_CALL ? ST_X_POST : (xo >= OP_JMP && xo <= OP_BR_TABLE) ? ST_X_BR
+                        : ST_X_OTHER, 1);
+          }
+#endif
         }
         const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
         // Prefetch the fall-through successor only after I is resident: SMEM returns out
@@ -352,7 +375,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       }
     }
     const uint64_t slowmask = __ballot(slow);
-    const uint64_t ts2 = WB_NOW();
+    [[maybe_unused]] const uint64_t ts2 = WB_NOW();
     WB_STAT_ADD(ST_CYC_FAST, ts2 - ts1);
     if (slowmask) WB_STAT_ADD(ST_SLOW, 1);
     if (slowmask && ((slowmask >> lane) & 1u)) {

@@ -64,6 +64,9 @@ X = ("v118", "v119"); XP = "v[118:119]"   # temps / 64-bit address
 Y = ("v120", "v121"); YP = "v[120:121]"
 AADDR, BADDR, DADDR, CADDR = "v122", "v123", "v124", "v125"
 Z = ("v126", "v127"); ZP = "v[126:127]"
+GSP = "v102"          # this lane's call-stack depth (slots), in/out
+SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
+SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
 
 
 def sreg(bank, k):
@@ -205,8 +208,10 @@ CMP = {"EQ": "eq_u", "NE": "ne_u", "LT_S": "lt_i", "LT_U": "lt_u", "GT_S": "gt_i
 def specs():
     S = []   # (slot name, [dbc ops], body)
 
-    def add(name, ops, body):
+    def add(name, ops, body, slots=1):
         S.append((name, ops, body))
+        for k in range(1, slots):            # a handler may span several slots
+            S.append((name + "+%d" % k, [], None))
 
     # ---- control
     add("NOP_CNT", ["NOP_CNT"], lambda g: g.next())
@@ -281,6 +286,87 @@ def specs():
         "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
         "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
         "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
+    # ---- calls (dbc_step.inc OP_CALL / OP_RET / OP_POST_CALL, LDS part of the call stack
+    # only; anything else -- HBM slots, divergent return targets, leaving the entry
+    # function -- leaves the core before any effect). Fields (tc.cpp): w1 = L or the
+    # result cell, w2 = frame base fb (cell offsets); CALL: w3 = return record,
+    # w4 = target*32, w7 = nargs | nlocals << 16; RET/POST_CALL: w3 = result cells.
+    def copy(src, dst, cnt, tag, g, step="0x100", sub=False):
+        top, end = g.lab(tag), g.lab(tag + "e")
+        mv = "v_subrev_u32_e32" if sub else "v_add_u32_e32"
+        return ["%s:" % top, "s_cmp_eq_u32 %s, 0" % cnt, "s_cbranch_scc1 %s" % end,
+                "ds_read_b32 %s, %s" % (Y[0], src), "s_waitcnt lgkmcnt(0)",
+                "ds_write_b32 %s, %s" % (dst, Y[0]),
+                "%s %s, %s, %s" % (mv, src, step, src), "%s %s, %s, %s" % (mv, dst, step, dst),
+                "s_sub_u32 %s, %s, 1" % (cnt, cnt), "s_branch %s" % top, "%s:" % end]
+
+    def lds_guard(g, vreg):     # leave unless every active lane's vreg <= SLDS
+        return ["v_cmp_lt_u32_e64 vcc, %s, %s" % (SLDS, vreg),
+                "s_and_b64 %s, vcc, exec" % T2, "s_cbranch_scc1 %s" % g.xh()]
+
+    def call_body(g):
+        n, n1 = "s68", "s69"
+        out = ["s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)), "s_lshr_b32 %s, %s, 8" % (n, n),
+               "s_add_u32 %s, %s, 1" % (n1, n),
+               "v_add_u32_e64 %s, %s, %s" % (X[0], n1, GSP)] + lds_guard(g, X[0])
+        out += ["v_lshl_add_u32 %s, %s, 8, %s" % (X[1], GSP, SB0),     # &stack[gsp]
+                "v_add_u32_e64 %s, %s, %s" % (X[0], g.x(2), FR)]       # &frame[fb]
+        out += copy(X[0], X[1], n, "sp", g)                            # spill [fb, L)
+        out += ["v_mov_b32 %s, %s" % (Y[1], g.x(3)), "ds_write_b32 %s, %s" % (X[1], Y[1]),
+                "v_add_u32_e64 %s, %s, %s" % (GSP, n1, GSP),
+                "s_and_b32 %s, %s, 0xffff" % (n, g.x(7)),
+                "v_add_u32_e64 %s, %s, %s" % (X[0], g.x(1), FR),
+                "v_add_u32_e64 %s, %s, %s" % (X[1], g.x(2), FR)]
+        out += copy(X[0], X[1], n, "ar", g)                            # args -> fb
+        out += ["s_lshr_b32 %s, %s, 16" % (n, g.x(7)), "v_mov_b32 %s, 0" % Y[0]]
+        zt, ze = g.lab("zl"), g.lab("zle")
+        out += ["%s:" % zt, "s_cmp_eq_u32 %s, 0" % n, "s_cbranch_scc1 %s" % ze,
+                "ds_write_b32 %s, %s" % (X[1], Y[0]), "v_add_u32_e32 %s, 0x100, %s" % (X[1], X[1]),
+                "s_sub_u32 %s, %s, 1" % (n, n), "s_branch %s" % zt, "%s:" % ze]
+        return out + g.taken(g.x(4), g.x(6))
+
+    def ret_body(g):
+        t = "s68"
+        out = lds_guard(g, GSP) + [
+            "v_lshl_add_u32 %s, %s, 8, %s" % (X[1], GSP, SB0),
+            "v_subrev_u32_e32 %s, 0x100, %s" % (X[1], X[1]),           # &stack[gsp - 1]
+            "ds_read_b32 %s, %s" % (Y[1], X[1]), "s_waitcnt lgkmcnt(0)",
+            # the raw record (pc | L << 20) must agree across lanes; readfirstlane reads
+            # the loaded VGPR directly (a VALU-written VGPR would need wait states first)
+            "v_readfirstlane_b32 %s, %s" % (t, Y[1]),
+            "s_nop 1",                                   # VALU-written SGPR -> VALU read
+            "v_cmp_ne_u32_e64 %s, %s, %s" % (T2, t, Y[1]),
+            "s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh(),   # split returns
+            "s_and_b32 %s, %s, 0xfffff" % (t, t),
+            "s_cmp_eq_u32 %s, 0xfffff" % t, "s_cbranch_scc1 %s" % g.xh(),   # entry function
+            "v_subrev_u32_e32 %s, 1, %s" % (GSP, GSP),
+            "s_mov_b32 s69, %s" % g.x(3),
+            "v_add_u32_e64 %s, %s, %s" % (X[0], g.x(1), FR),
+            "v_add_u32_e64 %s, %s, %s" % (X[1], g.x(2), FR)]
+        out += copy(X[0], X[1], "s69", "rr", g)                       # results -> fb
+        return out + ["s_lshl_b32 %s, %s, 5" % (t, t)] + g.taken(t, g.x(6))
+
+    def post_call_body(g):
+        n, r = "s68", "s69"
+        out = lds_guard(g, GSP) + [
+            "s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)), "s_lshr_b32 %s, %s, 8" % (n, n),
+            "s_mov_b32 %s, %s" % (r, g.x(3)),
+            # results fb.. -> L.. copied from the last one down (L > fb)
+            "s_lshl_b32 %s, %s, 8" % (T2L, r), "s_sub_u32 %s, %s, 0x100" % (T2L, T2L),
+            "s_add_u32 %s, %s, %s" % (T2H, T2L, g.x(2)),
+            "v_add_u32_e64 %s, %s, %s" % (X[0], T2H, FR),
+            "s_add_u32 %s, %s, %s" % (T2H, T2L, g.x(1)),
+            "v_add_u32_e64 %s, %s, %s" % (X[1], T2H, FR)]
+        out += copy(X[0], X[1], r, "pr", g, sub=True)
+        out += ["v_subrev_u32_e64 %s, %s, %s" % (GSP, n, GSP),
+                "v_lshl_add_u32 %s, %s, 8, %s" % (X[0], GSP, SB0),
+                "v_add_u32_e64 %s, %s, %s" % (X[1], g.x(2), FR)]
+        out += copy(X[0], X[1], n, "rs", g)                            # restore [fb, L)
+        return out + g.next()
+
+    add("CALL", ["CALL"], call_body, slots=2)
+    add("RET", ["RET"], ret_body, slots=2)
+    add("POST_CALL", ["POST_CALL"], post_call_body, slots=2)
     add("I32_CLZ", ["I32_CLZ"], lambda g: [
         "v_ffbh_u32_e32 %s, %s" % (X[0], A[0]),
         "v_min_u32_e32 %s, 32, %s" % (R[0], X[0])] + g.w32() + g.next())
@@ -452,6 +538,11 @@ def main():
     for mode in ("C", "D"):
         for bank in ("A", "B"):
             for si, nm in enumerate(names):
+                if si and S[si - 1][2] is None:
+                    continue                       # covered by the multi-slot handler before
+                span = 1
+                while si + span < nslots and S[si + span - 1][2] is None:
+                    span += 1
                 g = Gen(mode, bank)
                 lab = "Ltc_%s%s_%d" % (mode, bank, si)
                 e(".p2align 8")
@@ -468,9 +559,11 @@ def main():
                     body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
                 for ln in body:
                     e(ln)
-                e(".if (. - %s) > %d" % (lab, SLOT))
+                e(".if (. - %s) > %d" % (lab, SLOT * span))
                 e('.error "threaded-code handler %s exceeds its slot"' % nm)
                 e(".endif")
+                if span > 1:
+                    e(".org %s + %d" % (lab, SLOT * span))
     e(".p2align 8")
     e("Ltc_banks_end:")
     with open(os.path.join(HERE, "tc_blob.inc"), "w") as f:
@@ -482,8 +575,9 @@ def main():
         f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
         f.write("#pragma once\n#include \"dbc.h\"\n\n")
         f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n\n" % (SLOT, nslots))
-        for si, (nm, ops, _) in enumerate(S, start=1):
-            f.write("#define TC_SLOT_%s %d\n" % (nm, si))
+        for si, (nm, ops, body) in enumerate(S, start=1):
+            if body is not None:
+                f.write("#define TC_SLOT_%s %d\n" % (nm, si))
         f.write("\n// returns the handler slot (0 = no handler: the C++ step runs the op)\n")
         f.write("static inline int tc_slot(uint16_t op) {\n  switch (op) {\n")
         for si, (nm, ops, _) in enumerate(S, start=1):

@@ -66,6 +66,20 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     } else if (op == OP_I32_ROTL_I || op == OP_I32_XOR_ROTL_I) {
       w[4] = (32u - (imm & 31u)) & 31u;     // rotl k == rotr -k
     }
+    if (op == OP_CALL || op == OP_RET || op == OP_POST_CALL) {   // gen_tc.py call handlers
+      const uint32_t fb = P.global_cells;
+      if (a >= T || fb >= T) continue;
+      w[1] = a * 256u;
+      w[2] = fb * 256u;
+      w[3] = b;                                   // RET / POST_CALL: result cells
+      w[4] = 0; w[5] = 0; w[7] = 0;
+      if (op == OP_CALL) {
+        if (imm >= (1u << 26) || a < fb) continue;
+        w[3] = ((uint32_t(pc) + 1) & 0xFFFFFu) | (a << 20);   // return record
+        w[4] = imm * 32u;
+        w[7] = b | (c << 16);                     // nargs | nlocals << 16
+      }
+    }
     w[0] = uint32_t(slot) * TC_SLOT_BYTES;
     code[pc].w0 |= DBC_HOT;
   }
