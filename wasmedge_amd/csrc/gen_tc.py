@@ -174,6 +174,12 @@ class Gen:
         return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
                 "ds_write2_b32 %s, %s, %s offset1:64" % (CADDR, lo or R[0], hi or R[1])]
 
+    def w128(self, lo, hi):
+        """lo/hi: VGPR pair names (cells c, c+1 and c+2, c+3)."""
+        return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
+                "ds_write2_b32 %s, %s, %s offset1:64" % (CADDR, lo[0], lo[1]),
+                "ds_write2_b32 %s, %s, %s offset0:128 offset1:192" % (CADDR, hi[0], hi[1])]
+
     def bool_result(self):
         return ["v_cndmask_b32_e64 %s, 0, 1, vcc" % R[0]] + self.w32()
 
@@ -364,6 +370,117 @@ def specs():
         out += copy(X[0], X[1], n, "rs", g)                            # restore [fb, L)
         return out + g.next()
 
+    # ---- floating point. Results equal the reference's (x86 SSE as built by g++) except
+    # for NaN payloads (DESIGN.md "Numerics"): a handler computes into registers, and if
+    # any lane's result is a NaN it leaves before writing, so the compiled step produces
+    # the exact payload; otherwise the IEEE result is the reference's.
+    def nan_exit(g, pairs, w):
+        """pairs: result registers (VGPR names or pairs) to test; w = 32 or 64."""
+        out = []
+        for k, r in enumerate(pairs):
+            dst = T2 if k == 0 else "vcc"
+            out.append("v_cmp_u_f%d_e64 %s, %s, %s" % (w, dst, r, r))
+            if k:
+                out.append("s_or_b64 %s, %s, vcc" % (T2, T2))
+        return out + ["s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh()]
+
+    def hi_reads(g, regs):
+        """cells +2, +3 of the prefetched v128 operands (regs: [(addr, pair), ...])."""
+        return ["ds_read2_b32 %s, %s offset0:128 offset1:192" % (pair, addr) for addr, pair in regs] + \
+            ["s_waitcnt lgkmcnt(0)"]
+
+    FOPS = {"ADD": "v_add_f{w} {d}, {a}, {b}", "SUB": "v_add_f{w} {d}, {a}, -{b}",
+            "MUL": "v_mul_f{w} {d}, {a}, {b}"}
+    for nm, t in FOPS.items():
+        add("F32_" + nm, ["F32_" + nm], lambda g, t=t: [
+            t.format(w=32, d=R[0], a=A[0], b=B[0])] + nan_exit(g, [R[0]], 32) + g.w32() + g.next())
+        add("F64_" + nm, ["F64_" + nm], lambda g, t=t: [
+            t.format(w=64, d=RP, a=AP, b=BP)] + nan_exit(g, [RP], 64) + g.w64() + g.next())
+        add("V_F32X4_" + nm, ["V_F32X4_" + nm], lambda g, t=t: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+            t.format(w=32, d=R[0], a=A[0], b=B[0]), t.format(w=32, d=R[1], a=A[1], b=B[1]),
+            t.format(w=32, d=Z[0], a=X[0], b=Y[0]), t.format(w=32, d=Z[1], a=X[1], b=Y[1])] +
+            nan_exit(g, [R[0], R[1], Z[0], Z[1]], 32) + g.w128(R, Z) + g.next())
+        add("V_F64X2_" + nm, ["V_F64X2_" + nm], lambda g, t=t: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+            t.format(w=64, d=RP, a=AP, b=BP), t.format(w=64, d=ZP, a=XP, b=YP)] +
+            nan_exit(g, [RP, ZP], 64) + g.w128(R, Z) + g.next())
+    FCMP = {"EQ": "eq", "NE": "neq", "LT": "lt", "GT": "gt", "LE": "le", "GE": "ge"}
+    for nm, c in FCMP.items():
+        add("F32_" + nm, ["F32_" + nm], lambda g, c=c: [
+            "v_cmp_%s_f32_e64 vcc, %s, %s" % (c, A[0], B[0])] + g.bool_result() + g.next())
+        add("F64_" + nm, ["F64_" + nm], lambda g, c=c: [
+            "v_cmp_%s_f64_e64 vcc, %s, %s" % (c, AP, BP)] + g.bool_result() + g.next())
+        add("V_F32X4_" + nm, ["V_F32X4_" + nm], lambda g, c=c: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+            "v_cmp_%s_f32_e64 vcc, %s, %s" % (c, A[0], B[0]), "v_cndmask_b32_e64 %s, 0, -1, vcc" % R[0],
+            "v_cmp_%s_f32_e64 vcc, %s, %s" % (c, A[1], B[1]), "v_cndmask_b32_e64 %s, 0, -1, vcc" % R[1],
+            "v_cmp_%s_f32_e64 vcc, %s, %s" % (c, X[0], Y[0]), "v_cndmask_b32_e64 %s, 0, -1, vcc" % Z[0],
+            "v_cmp_%s_f32_e64 vcc, %s, %s" % (c, X[1], Y[1]), "v_cndmask_b32_e64 %s, 0, -1, vcc" % Z[1]] +
+            g.w128(R, Z) + g.next())
+        add("V_F64X2_" + nm, ["V_F64X2_" + nm], lambda g, c=c: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+            "v_cmp_%s_f64_e64 vcc, %s, %s" % (c, AP, BP), "v_cndmask_b32_e64 %s, 0, -1, vcc" % R[0],
+            "v_mov_b32 %s, %s" % (R[1], R[0]),
+            "v_cmp_%s_f64_e64 vcc, %s, %s" % (c, XP, YP), "v_cndmask_b32_e64 %s, 0, -1, vcc" % Z[0],
+            "v_mov_b32 %s, %s" % (Z[1], Z[0])] + g.w128(R, Z) + g.next())
+    add("F32_ABS", ["F32_ABS"], lambda g: ["v_and_b32_e32 %s, 0x7fffffff, %s" % (R[0], A[0])] +
+        g.w32() + g.next())
+    add("F32_NEG", ["F32_NEG"], lambda g: ["v_xor_b32_e32 %s, 0x80000000, %s" % (R[0], A[0])] +
+        g.w32() + g.next())
+    add("F64_ABS", ["F64_ABS"], lambda g: ["v_and_b32_e32 %s, 0x7fffffff, %s" % (R[1], A[1])] +
+        g.w64(A[0], R[1]) + g.next())
+    add("F64_NEG", ["F64_NEG"], lambda g: ["v_xor_b32_e32 %s, 0x80000000, %s" % (R[1], A[1])] +
+        g.w64(A[0], R[1]) + g.next())
+    # (VOP3 takes no literal on gfx9: the mask goes through an SGPR)
+    add("F32_COPYSIGN", ["F32_COPYSIGN"], lambda g: ["s_mov_b32 s68, 0x7fffffff",
+        "v_bfi_b32 %s, s68, %s, %s" % (R[0], A[0], B[0])] + g.w32() + g.next())
+    add("F64_COPYSIGN", ["F64_COPYSIGN"], lambda g: ["s_mov_b32 s68, 0x7fffffff",
+        "v_bfi_b32 %s, s68, %s, %s" % (R[1], A[1], B[1])] + g.w64(A[0], R[1]) + g.next())
+    add("F64_CONVERT_I32_S", ["F64_CONVERT_I32_S"], lambda g: [
+        "v_cvt_f64_i32_e32 %s, %s" % (RP, A[0])] + g.w64() + g.next())
+    add("F64_CONVERT_I32_U", ["F64_CONVERT_I32_U"], lambda g: [
+        "v_cvt_f64_u32_e32 %s, %s" % (RP, A[0])] + g.w64() + g.next())
+    add("F32_CONVERT_I32_S", ["F32_CONVERT_I32_S"], lambda g: [
+        "v_cvt_f32_i32_e32 %s, %s" % (R[0], A[0])] + g.w32() + g.next())
+    add("F32_CONVERT_I32_U", ["F32_CONVERT_I32_U"], lambda g: [
+        "v_cvt_f32_u32_e32 %s, %s" % (R[0], A[0])] + g.w32() + g.next())
+    add("F64_PROMOTE_F32", ["F64_PROMOTE_F32"], lambda g: [
+        "v_cvt_f64_f32_e32 %s, %s" % (RP, A[0])] + nan_exit(g, [RP], 64) + g.w64() + g.next())
+    add("F32_DEMOTE_F64", ["F32_DEMOTE_F64"], lambda g: [
+        "v_cvt_f32_f64_e32 %s, %s" % (R[0], AP)] + nan_exit(g, [R[0]], 32) + g.w32() + g.next())
+    # ---- SIMD128 data movement / integer lanes (4 cells; cells +2, +3 read here)
+    add("MOV128", ["MOV128"], lambda g: hi_reads(g, [(AADDR, XP)]) + g.w128(A, X) + g.next())
+    add("V_SPLAT32", ["V_I32X4_SPLAT", "V_F32X4_SPLAT"], lambda g: g.w128((A[0], A[0]), (A[0], A[0])) + g.next())
+    add("V_SPLAT64", ["V_I64X2_SPLAT", "V_F64X2_SPLAT"], lambda g: g.w128(A, A) + g.next())
+    VBIT = {"V_AND": "v_and_b32_e32 {d}, {a}, {b}", "V_OR": "v_or_b32_e32 {d}, {a}, {b}",
+            "V_XOR": "v_xor_b32_e32 {d}, {a}, {b}", "V_I32X4_ADD": "v_add_u32_e32 {d}, {a}, {b}",
+            "V_I32X4_SUB": "v_sub_u32_e32 {d}, {a}, {b}", "V_I32X4_MUL": "v_mul_lo_u32 {d}, {a}, {b}"}
+    for nm, t in VBIT.items():
+        add(nm, [nm], lambda g, t=t: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+            t.format(d=R[0], a=A[0], b=B[0]), t.format(d=R[1], a=A[1], b=B[1]),
+            t.format(d=Z[0], a=X[0], b=Y[0]), t.format(d=Z[1], a=X[1], b=Y[1])] + g.w128(R, Z) + g.next())
+    add("V_I64X2_ADD", ["V_I64X2_ADD"], lambda g: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+        "v_lshl_add_u64 %s, %s, 0, %s" % (RP, AP, BP), "v_lshl_add_u64 %s, %s, 0, %s" % (ZP, XP, YP)] +
+        g.w128(R, Z) + g.next())
+    add("V_I64X2_SUB", ["V_I64X2_SUB"], lambda g: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+        "v_sub_co_u32_e64 %s, vcc, %s, %s" % (R[0], A[0], B[0]),
+        "v_subb_co_u32_e64 %s, vcc, %s, %s, vcc" % (R[1], A[1], B[1]),
+        "v_sub_co_u32_e64 %s, vcc, %s, %s" % (Z[0], X[0], Y[0]),
+        "v_subb_co_u32_e64 %s, vcc, %s, %s, vcc" % (Z[1], X[1], Y[1])] + g.w128(R, Z) + g.next())
+    add("V_I64X2_EQ", ["V_I64X2_EQ"], lambda g: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
+        "v_cmp_eq_u64_e64 vcc, %s, %s" % (AP, BP), "v_cndmask_b32_e64 %s, 0, -1, vcc" % R[0],
+        "v_mov_b32 %s, %s" % (R[1], R[0]),
+        "v_cmp_eq_u64_e64 vcc, %s, %s" % (XP, YP), "v_cndmask_b32_e64 %s, 0, -1, vcc" % Z[0],
+        "v_mov_b32 %s, %s" % (Z[1], Z[0])] + g.w128(R, Z) + g.next())
+    add("V_ANY_TRUE", ["V_ANY_TRUE"], lambda g: hi_reads(g, [(AADDR, XP)]) + [
+        "v_or3_b32 %s, %s, %s, %s" % (R[0], A[0], A[1], X[0]),
+        "v_or_b32_e32 %s, %s, %s" % (R[0], R[0], X[1]),
+        "v_cmp_ne_u32_e64 vcc, 0, %s" % R[0]] + g.bool_result() + g.next())
+    add("V_I32X4_BITMASK", ["V_I32X4_BITMASK"], lambda g: hi_reads(g, [(AADDR, XP)]) + [
+        "v_lshrrev_b32_e32 %s, 31, %s" % (R[0], A[0]),
+        "v_lshrrev_b32_e32 %s, 31, %s" % (R[1], A[1]),
+        "v_lshl_or_b32 %s, %s, 1, %s" % (R[0], R[1], R[0]),
+        "v_lshrrev_b32_e32 %s, 31, %s" % (R[1], X[0]),
+        "v_lshl_or_b32 %s, %s, 2, %s" % (R[0], R[1], R[0]),
+        "v_lshrrev_b32_e32 %s, 31, %s" % (R[1], X[1]),
+        "v_lshl_or_b32 %s, %s, 3, %s" % (R[0], R[1], R[0])] + g.w32() + g.next())
     add("CALL", ["CALL"], call_body, slots=2)
     add("RET", ["RET"], ret_body, slots=2)
     add("POST_CALL", ["POST_CALL"], post_call_body, slots=2)

@@ -32,10 +32,15 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
     const uint32_t imm = I.w3, cnt = (I.w0 >> 16) & 0xFFu;
     int slot = tc_slot(op);
+    uint32_t a_eff = a;
+    if (op == OP_V_EXTRACT32 || op == OP_V_EXTRACT64) {   // a lane of a v128 = a cell move
+      a_eff = a + (op == OP_V_EXTRACT32 ? d : 2 * d);
+      slot = tc_slot(op == OP_V_EXTRACT32 ? OP_MOV32 : OP_MOV64);
+    }
     if (!slot) continue;
     TInstr &t = tc[pc];
     uint32_t *w = t.w;
-    w[1] = off(a); w[2] = off(b); w[3] = off(c); w[4] = imm; w[5] = 0; w[6] = cnt; w[7] = 0;
+    w[1] = off(a_eff); w[2] = off(b); w[3] = off(c); w[4] = imm; w[5] = 0; w[6] = cnt; w[7] = 0;
     if (op == OP_I32_ADD3 || op == OP_SELECT32 || op == OP_SELECT64 ||
         op == OP_I32_ADD_XROTR_I || op == OP_I32_ADD3_XROTR_I)
       w[5] = off(d);
