@@ -84,10 +84,11 @@ struct WasmEdge_BatchContext {
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
   bool threaded = true;
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
+  DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
   DevBuf<DFunc> funcs;
   DevBuf<uint8_t> data_pool;
   // instance state
-  DevBuf<uint32_t> mem, gstack, lstate, params, results;
+  DevBuf<uint32_t> mem, gstack, lstate, params, results, ltab;
   // host-import yield path (only allocated when the module imports functions)
   DevBuf<uint32_t> fsave, hcall, hbuf;
   uint32_t hb_cells = 0;
@@ -179,14 +180,24 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   C->threaded = !(thr && thr[0] == '0');
   std::vector<TInstr> tcv;
   if (C->threaded) tcv = wb::build_threaded(P, codepad);
+  // LS image from slot LS_GLOBALS on: globals, then (per-lane tables) table sizes and
+  // the dropped-elem mask
+  std::vector<uint32_t> ls_init = P.global_init;
+  if (P.mut_tables) {
+    for (const auto &t : P.tables) ls_init.push_back(t.min);
+    ls_init.push_back(P.init_edropped);
+  }
   bool ok = C->code.upload(codepad, s) && (!C->threaded || C->tcode.upload(tcv, s)) && C->brtab.upload(P.brtab, s) &&
             C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
-            C->global_init.upload(P.global_init, s) && C->image.upload(img, s) &&
+            C->global_init.upload(ls_init, s) && C->image.upload(img, s) &&
+            C->tab_image.upload(P.tab_image, s) && C->tabinfo.upload(P.tabinfo, s) &&
+            C->elem_pool.upload(P.elem_pool, s) && C->elem_off.upload(P.elem_off, s) &&
+            C->elem_len.upload(P.elem_len, s) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
             C->data_off.upload(doff, s) && C->data_len.upload(dlen, s);
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
   size_t nw = C->nwaves;
-  C->ls_slots = LS_GLOBALS + P.global_cells;
+  C->ls_slots = LS_GLOBALS + uint32_t(ls_init.size());
   // LDS call-stack slots per lane: what the frames leave of the LDS share each wave gets
   // at the occupancy this batch reaches (nwaves over 256 CUs, at most 16 waves per CU)
   {
@@ -208,6 +219,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (!C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64) ||
       !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) ||
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
+      !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
       (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
@@ -260,6 +272,12 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   // the gas limit applies per invocation; instantiation (start function) is not metered
   k.cost_limit = C->conf.CostLimit && !is_start ? C->conf.CostLimit : ~0ull;
   k.stop = C->stop;
+  if (P.mut_tables) {
+    k.ltab = C->ltab.ptr; k.tabinfo = C->tabinfo.ptr; k.elem_pool = C->elem_pool.ptr;
+    k.elem_off = C->elem_off.ptr; k.elem_len = C->elem_len.ptr;
+    k.mut_tables = 1; k.ntables = P.ntables; k.tab_words = P.tab_words;
+  }
+  k.ls_tab = LS_GLOBALS + P.global_cells;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
   k.fsave = C->fsave.ptr; k.hcall = C->hcall.ptr; k.hbuf = C->hbuf.ptr;
   k.params = is_start ? nullptr : C->params.ptr;
@@ -461,6 +479,11 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->stream), "mem init"))
+    return R(kRuntimeError);
+  // per-lane tables (instantiate/table.cpp + elem.cpp): every lane starts from the image
+  if (P.mut_tables &&
+      !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
+                                    P.tab_words, C->nwaves, C->stream), "table init"))
     return R(kRuntimeError);
   if (!C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->global_init.ptr, P.global_cells,
                                       C->ls_slots, P.mem_min, C->init_dropped, C->nwaves,

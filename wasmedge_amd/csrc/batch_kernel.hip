@@ -192,6 +192,11 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define GS_CPTR const lds_u32 *const
 
 #define LS(slot) ls[(size_t)(slot) << 6]
+  // per-lane tables: entries lane-interleaved like memory, sizes + dropped elems in LS
+  uint32_t *const lt = p.ltab ? p.ltab + (size_t)(inst >> 6) * p.tab_words * 64u + (inst & 63u) : nullptr;
+#define TSIZE(t) LS(p.ls_tab + (t))
+#define TENT(t, i) lt[(size_t)(p.tabinfo[2u * (t)] + (i)) << 6]
+#define EDROP LS(p.ls_tab + p.ntables)
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   uint32_t pc = p.entry_pc, gsp = 0, pages = LS(LS_PAGES), dropped = LS(LS_DROPPED);
   uint64_t count = 0;

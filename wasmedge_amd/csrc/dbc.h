@@ -58,6 +58,13 @@ struct DInstr {
   X(ST8) X(ST16) X(ST32) X(ST64) X(ST128)                                               \
   X(MEM_SIZE) X(MEM_GROW) X(MEM_FILL) X(MEM_COPY) X(MEM_INIT) X(DATA_DROP)             \
   X(TABLE_GET)    /* a = index cell, c = dst, d = table                              */ \
+  X(TABLE_SET)    /* a = index cell, b = ref cell, d = table (per-lane tables)       */ \
+  X(TABLE_SIZE)   /* c = dst, d = table                                              */ \
+  X(TABLE_GROW)   /* a = init ref cell, b = n cell, c = dst, d = table               */ \
+  X(TABLE_FILL)   /* a = dst idx cell, b = ref cell, c = n cell, imm = table         */ \
+  X(TABLE_COPY)   /* a = dst idx, b = src idx, c = n, imm = dst table | src table<<16 */ \
+  X(TABLE_INIT)   /* a = dst idx, b = src idx, c = n, imm = table | elem seg<<16     */ \
+  X(ELEM_DROP)    /* imm = elem segment                                              */ \
   /* i32 binary: c = a op b ; *_I: c = a op imm                                       */ \
   X(I32_ADD) X(I32_SUB) X(I32_MUL) X(I32_DIV_S) X(I32_DIV_U) X(I32_REM_S) X(I32_REM_U) \
   X(I32_AND) X(I32_OR) X(I32_XOR) X(I32_SHL) X(I32_SHR_S) X(I32_SHR_U) X(I32_ROTL)     \

@@ -73,6 +73,14 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   p.global_cells = P.global_cells; p.total_cells = P.total_cells();
   p.table_size = uint32_t(P.table0.size()); p.mem_max_pages = budget;
   p.gs_depth = gs_depth;
+  p.mut_tables = P.mut_tables ? 1u : 0u; p.ntables = P.ntables; p.tab_words = P.tab_words;
+  p.tabinfo = P.tabinfo.data(); p.elem_pool = P.elem_pool.data();
+  p.elem_off = P.elem_off.data(); p.elem_len = P.elem_len.data();
+  std::vector<uint32_t> ltabv, tsz;   // this instance's tables (per-lane table mode)
+  uint32_t edrop = 0;
+#define TSIZE(t) tsz[(uint32_t)(t)]
+#define TENT(t, i) ltabv[P.tabinfo[2u * (t)] + (i)]
+#define EDROP edrop
   std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
   std::vector<uint32_t> memv;
   for (uint32_t inst = 0; inst < n; inst++) {
@@ -108,6 +116,10 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
     uint32_t pages = P.mem_min, dropped = init_dropped;
+    ltabv = P.tab_image;
+    tsz.clear();
+    for (const auto &t : P.tables) tsz.push_back(t.min);
+    edrop = P.init_edropped;
     for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
     // one invocation of the function at `entry` on this instance's state
     auto invoke = [&](uint32_t entry, const uint32_t *prm, uint32_t ncells, uint64_t &count) {

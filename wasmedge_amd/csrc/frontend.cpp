@@ -19,6 +19,7 @@ struct Err {
   uint8_t code;
   std::string msg;
 };
+struct NeedMutTables {};
 
 struct Reader {
   const uint8_t *p, *end;
@@ -285,6 +286,9 @@ class Lowerer {
   std::vector<CallFix> *callfix = nullptr;
 
   [[noreturn]] void fail(uint8_t code, const std::string &m) { throw Err{code, m}; }
+  // a table-mutating op in a module lowered for a shared immutable table: start over
+  // with per-lane tables (parse_and_lower catches this)
+  void need_mut_tables() { if (!P.mut_tables) throw NeedMutTables{}; }
 
   bool live() const { return !ctrl.back().unreachable; }
 
@@ -309,7 +313,9 @@ class Lowerer {
       case OP_LD8S64: case OP_LD8U64: case OP_LD16S64: case OP_LD16U64: case OP_LD32S64:
       case OP_LD32U64: case OP_LD64: case OP_LD128: case OP_ST8: case OP_ST16: case OP_ST32:
       case OP_ST64: case OP_ST128: case OP_MEM_FILL: case OP_MEM_COPY: case OP_MEM_INIT:
-      case OP_TABLE_GET: case OP_V_LD8X8S: case OP_V_LD8X8U: case OP_V_LD16X4S:
+      case OP_TABLE_GET: case OP_TABLE_SET: case OP_TABLE_SIZE: case OP_TABLE_GROW:
+      case OP_TABLE_FILL: case OP_TABLE_COPY: case OP_TABLE_INIT: case OP_ELEM_DROP:
+      case OP_V_LD8X8S: case OP_V_LD8X8U: case OP_V_LD16X4S:
       case OP_V_LD16X4U: case OP_V_LD32X2S: case OP_V_LD32X2U: case OP_V_LD8SPLAT:
       case OP_V_LD16SPLAT: case OP_V_LD32SPLAT: case OP_V_LD64SPLAT: case OP_V_LD32ZERO:
       case OP_V_LD64ZERO: case OP_V_LDLANE: case OP_V_STLANE:
@@ -968,6 +974,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         uint32_t ti = r.u32();
         uint32_t tab = r.u32();
         if (ti >= P.types.size() || tab >= P.ntables) fail(E_TYPECHECK, "unknown type/table");
+        if (P.tables[tab].type != FUNCREF) fail(E_TYPECHECK, "type mismatch");
         Entry idx = pop_t(I32);
         const FuncType &t = P.types[ti];
         std::vector<Entry> args(t.params.size());
@@ -1050,14 +1057,25 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         }
         break;
       }
-      case 0x25: {  // table.get (immutable funcref table)
+      case 0x25: {  // table.get (tableInstr.cpp; shared table 0 or the lane's own table)
         uint32_t tab = r.u32();
         if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        const uint8_t rt = P.tables[tab].type;
         Entry idx = pop_t(I32);
-        if (!live()) { push_cell(FUNCREF); break; }
+        if (!live()) { push_cell(rt); break; }
         uint32_t ic = src(idx);
         emit(OP_TABLE_GET, ic, 0, idx.cell, tab);
-        push_cell(FUNCREF, last_emit);
+        push_cell(rt, last_emit);
+        break;
+      }
+      case 0x26: {  // table.set
+        uint32_t tab = r.u32();
+        if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        need_mut_tables();
+        Entry v = pop_t(P.tables[tab].type), idx = pop_t(I32);
+        if (!live()) break;
+        uint32_t ic = src(idx), vc = src(v);
+        emit(OP_TABLE_SET, ic, vc, 0, tab);
         break;
       }
       // ---- memory (memory.ipp:12-68)
@@ -1161,11 +1179,68 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         emit(op == 0xFC0A ? OP_MEM_COPY : OP_MEM_FILL, dc, sc, nc);
         break;
       }
-      case 0xFC10: {  // table.size of an immutable table is a constant
+      case 0xFC10: {  // table.size: a constant for the shared immutable table
         uint32_t tab = r.u32();
         if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
-        uint32_t k[4] = {uint32_t(P.table0.size()), 0, 0, 0};
-        push_const(I32, k);
+        if (!P.mut_tables) {
+          uint32_t k[4] = {uint32_t(P.table0.size()), 0, 0, 0};
+          push_const(I32, k);
+        } else if (live()) {
+          emit(OP_TABLE_SIZE, 0, 0, top_cell(), tab);
+          push_cell(I32, last_emit);
+        } else {
+          push_cell(I32);
+        }
+        break;
+      }
+      case 0xFC0C: {  // table.init elem table (tableInstr.cpp)
+        uint32_t ei = r.u32(), tab = r.u32();
+        if (tab >= P.ntables || ei >= P.elems.size()) fail(E_TYPECHECK, "unknown table/elem");
+        if (P.elems[ei].type != P.tables[tab].type) fail(E_TYPECHECK, "type mismatch");
+        need_mut_tables();
+        Entry n = pop_t(I32), sidx = pop_t(I32), d = pop_t(I32);
+        if (!live()) break;
+        uint32_t dc = src(d), sc = src(sidx), nc = src(n);
+        emit(OP_TABLE_INIT, dc, sc, nc, 0, tab | (ei << 16));
+        break;
+      }
+      case 0xFC0D: {  // elem.drop
+        uint32_t ei = r.u32();
+        if (ei >= P.elems.size()) fail(E_TYPECHECK, "unknown elem");
+        need_mut_tables();
+        if (live()) emit(OP_ELEM_DROP, 0, 0, 0, 0, ei);
+        break;
+      }
+      case 0xFC0E: {  // table.copy dst src
+        uint32_t td = r.u32(), ts = r.u32();
+        if (td >= P.ntables || ts >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        if (P.tables[td].type != P.tables[ts].type) fail(E_TYPECHECK, "type mismatch");
+        need_mut_tables();
+        Entry n = pop_t(I32), sidx = pop_t(I32), d = pop_t(I32);
+        if (!live()) break;
+        uint32_t dc = src(d), sc = src(sidx), nc = src(n);
+        emit(OP_TABLE_COPY, dc, sc, nc, 0, td | (ts << 16));
+        break;
+      }
+      case 0xFC0F: {  // table.grow
+        uint32_t tab = r.u32();
+        if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        need_mut_tables();
+        Entry n = pop_t(I32), v = pop_t(P.tables[tab].type);
+        if (!live()) { push_cell(I32); break; }
+        uint32_t vc = src(v), nc = src(n);
+        emit(OP_TABLE_GROW, vc, nc, v.cell, tab);
+        push_cell(I32, last_emit);
+        break;
+      }
+      case 0xFC11: {  // table.fill
+        uint32_t tab = r.u32();
+        if (tab >= P.ntables) fail(E_TYPECHECK, "unknown table");
+        need_mut_tables();
+        Entry n = pop_t(I32), v = pop_t(P.tables[tab].type), d = pop_t(I32);
+        if (!live()) break;
+        uint32_t dc = src(d), vc = src(v), nc = src(n);
+        emit(OP_TABLE_FILL, dc, vc, nc, 0, tab);
         break;
       }
       // ---- SIMD memory
@@ -1382,9 +1457,6 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   Reader r{wasm + 8, wasm + len};
   std::vector<uint32_t> decl_types;
   std::vector<ConstVal> gvals;
-  struct ElemSeg { bool active; uint32_t table, offset; std::vector<uint32_t> funcs; };
-  std::vector<ElemSeg> elems;
-  std::vector<uint32_t> table_min;
   uint32_t ncode = 0;
   while (r.p < r.end) {
     uint8_t sid = r.u8();
@@ -1435,14 +1507,16 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
       case 4: {
         uint32_t n = s.u32();
         for (uint32_t k = 0; k < n; k++) {
-          uint8_t rt = s.u8();
+          TableInfo t;
+          t.type = s.u8();
+          if (t.type != FUNCREF && t.type != EXTERNREF) throw Err{E_MALFORMED, "malformed reference type"};
           uint8_t fl = s.u8();
-          uint32_t mn = s.u32();
-          if (fl & 1) s.u32();
-          if (rt != FUNCREF) throw Err{E_UNSUPPORTED, "externref tables not supported"};
-          table_min.push_back(mn);
+          t.min = s.u32();
+          if (fl & 1) { t.has_max = true; t.max = s.u32(); }
+          if (t.has_max && t.max < t.min) throw Err{0x43, "size minimum must not be greater than maximum"};
+          P.tables.push_back(t);
         }
-        P.ntables = n;
+        P.ntables = uint32_t(P.tables.size());
         break;
       }
       case 5: {
@@ -1485,20 +1559,28 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
       case 9: {
         uint32_t n = s.u32();
         for (uint32_t k = 0; k < n; k++) {
+          // elem.cpp / binary format: bit 0 passive-or-declarative, bit 1 explicit
+          // table (active) or declarative (passive), bit 2 items as const expressions
           uint32_t flags = s.u32();
-          ElemSeg e{!(flags & 1), 0, 0, {}};
-          if (!(flags & 1)) {
+          if (flags > 7) throw Err{E_MALFORMED, "malformed elements segment kind"};
+          ElemSeg e;
+          e.active = !(flags & 1);
+          e.declarative = (flags & 3) == 3;
+          if (e.active) {
             if (flags & 2) e.table = s.u32();
             ConstVal off = eval_const(s, P, gvals);
             e.offset = off.k[0];
           }
-          if (flags & 3) s.u8();
+          if (flags & 3) {
+            uint8_t k = s.u8();   // elemkind 0x00 (= funcref) or a reftype
+            e.type = (flags & 4) ? k : FUNCREF;
+          }
           uint32_t m = s.u32();
           for (uint32_t q = 0; q < m; q++) {
-            if (flags & 4) e.funcs.push_back(eval_const(s, P, gvals).k[0]);
-            else e.funcs.push_back(s.u32());
+            if (flags & 4) e.items.push_back(eval_const(s, P, gvals).k[0]);
+            else e.items.push_back(s.u32());
           }
-          elems.push_back(e);
+          P.elems.push_back(e);
         }
         break;
       }
@@ -1565,17 +1647,24 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
     gc += w;
   }
   P.global_cells = gc;
-  // table 0 image from active element segments (elem.cpp), immutable in this path
-  if (P.ntables > 1) throw Err{E_UNSUPPORTED, "multiple tables"};
-  if (P.ntables) {
-    P.table0.assign(table_min[0], 0xFFFFFFFFu);
-    for (auto &e : elems) {
-      if (!e.active) continue;
-      if (uint64_t(e.offset) + e.funcs.size() > P.table0.size())
-        throw Err{0x64, "elements segment does not fit"};
-      for (size_t q = 0; q < e.funcs.size(); q++) P.table0[e.offset + q] = e.funcs[q];
-    }
+  // tables at instantiation (instantiate/table.cpp + elem.cpp): `min` null refs, then
+  // the active element segments in order
+  for (auto &e : P.elems) {
+    if (e.active && e.table >= P.ntables) throw Err{E_TYPECHECK, "unknown table"};
+    if (e.active && e.type != P.tables[e.table].type) throw Err{E_TYPECHECK, "type mismatch"};
   }
+  std::vector<std::vector<uint32_t>> timg(P.ntables);
+  for (uint32_t t = 0; t < P.ntables; t++) timg[t].assign(P.tables[t].min, 0xFFFFFFFFu);
+  for (auto &e : P.elems) {
+    if (!e.active) continue;
+    auto &T = timg[e.table];
+    if (uint64_t(e.offset) + e.items.size() > T.size())
+      throw Err{0x64, "elements segment does not fit"};
+    for (size_t q = 0; q < e.items.size(); q++) T[e.offset + q] = e.items[q];
+  }
+  if (P.ntables) P.table0 = timg[0];
+  // several tables or an externref table: per-lane tables from the start
+  P.mut_tables = P.ntables > 1 || (P.ntables && P.tables[0].type != FUNCREF);
   for (auto &d : P.datas)
     if (d.active && uint64_t(d.offset) + d.bytes.size() > uint64_t(P.mem_min) * 65536)
       throw Err{0x63, "data segment does not fit"};
@@ -1585,10 +1674,44 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
     if (!st.params.empty() || !st.results.empty()) throw Err{E_TYPECHECK, "invalid start function"};
   }
   // lower
-  Lowerer L(P, wasm);
-  std::vector<CallFix> callfix;
-  for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
-  for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
+  const Program before = P;
+  for (;;) {
+    try {
+      Lowerer L(P, wasm);
+      std::vector<CallFix> callfix;
+      for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
+      for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
+      break;
+    } catch (NeedMutTables &) {
+      P = before;
+      P.mut_tables = true;
+    }
+  }
+  if (P.mut_tables) {
+    // per-lane table words: each table gets min + kTableGrowLimit slots (bounded by its
+    // max); element segment pool for table.init; active and declarative segments
+    // start dropped (elem.cpp)
+    if (P.elems.size() > 32) throw Err{E_UNSUPPORTED, "more than 32 element segments"};
+    for (uint32_t t = 0; t < P.ntables; t++) {
+      const TableInfo &T = P.tables[t];
+      uint64_t cap = uint64_t(T.min) + kTableGrowLimit;
+      if (T.has_max && cap > T.max) cap = T.max;
+      if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;
+      if (uint64_t(P.tab_words) + cap > (1u << 24)) throw Err{E_UNSUPPORTED, "tables too large"};
+      P.tabinfo.push_back(P.tab_words);
+      P.tabinfo.push_back(uint32_t(cap));
+      P.tab_image.insert(P.tab_image.end(), timg[t].begin(), timg[t].end());
+      P.tab_image.resize(P.tab_words + cap, 0xFFFFFFFFu);
+      P.tab_words += uint32_t(cap);
+    }
+    for (size_t k = 0; k < P.elems.size(); k++) {
+      const ElemSeg &e = P.elems[k];
+      P.elem_off.push_back(uint32_t(P.elem_pool.size()));
+      P.elem_len.push_back(uint32_t(e.items.size()));
+      P.elem_pool.insert(P.elem_pool.end(), e.items.begin(), e.items.end());
+      if (e.active || e.declarative) P.init_edropped |= 1u << k;
+    }
+  }
   fuse_arx(P);
   if (P.code.size() >= DBC_MAX_PC) throw Err{E_UNSUPPORTED, "module too large for 20-bit pcs"};
 }

@@ -31,6 +31,23 @@ struct DataSeg {
   std::vector<uint8_t> bytes;
 };
 
+struct TableInfo {
+  uint8_t type = FUNCREF;
+  uint32_t min = 0, max = 0;
+  bool has_max = false;
+};
+
+struct ElemSeg {
+  bool active = false, declarative = false;
+  uint8_t type = FUNCREF;
+  uint32_t table = 0, offset = 0;
+  std::vector<uint32_t> items;        // function index per item, 0xFFFFFFFF = null ref
+};
+
+// Per-lane table capacity beyond `min` when the table has no (or a larger) max: the
+// device analogue of the memory page budget (table.grow past it returns -1).
+constexpr uint32_t kTableGrowLimit = 4096;
+
 struct ExportFunc {
   std::string name;
   uint32_t func;
@@ -64,6 +81,17 @@ struct Program {
   uint32_t global_cells = 0;           // G = frame base
   std::vector<uint32_t> table0;        // funcref table 0 (immutable), 0xFFFFFFFF = null
   uint32_t ntables = 0;
+  std::vector<TableInfo> tables;
+  std::vector<ElemSeg> elems;
+  // Per-lane tables (tableInstr.cpp): set when the code mutates a table (table.set/grow/
+  // fill/copy/init, elem.drop), or has several tables or an externref table. Then every
+  // lane owns tab_words words (tables back to back, tabinfo = {first word, capacity} per
+  // table) initialised from tab_image, sizes and dropped elem segments live in its
+  // instance state, and table0 is unused.
+  bool mut_tables = false;
+  std::vector<uint32_t> tab_image, tabinfo;
+  std::vector<uint32_t> elem_pool, elem_off, elem_len;
+  uint32_t tab_words = 0, init_edropped = 0;
   int64_t start_func = -1;
   // lowered code
   std::vector<DInstr> code;

@@ -45,6 +45,13 @@ struct KParams {
   uint32_t hb_cells;
   uint64_t max_steps;           // instruction budget per instance (Interrupted, coarse)
   uint64_t cost_limit;          // exact unit-cost gas limit (CostLimitExceeded), ~0 = none
+  // per-lane tables (frontend.h Program::mut_tables), else NULL / 0 and `table` serves
+  uint32_t *ltab;               // [wave][tab_words][64] refs, ~0 = null
+  const uint32_t *tabinfo;      // [ntables][2]: first word, capacity
+  const uint32_t *elem_pool;    // element segment items (function index, ~0 = null)
+  const uint32_t *elem_off, *elem_len;
+  uint32_t mut_tables, ntables, tab_words;
+  uint32_t ls_tab;              // LS slot of table 0's size; ls_tab + ntables: dropped elems
   uint32_t *stop;               // host-set interrupt request (WasmEdge_BatchInterrupt)
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
   uint64_t *stats;              // WB_STATS builds: per-wave counters (else unused)
@@ -54,7 +61,8 @@ struct KParams {
 // reference keeps it in ModuleInstance / MemoryInstance / GlobalInstance): memory size,
 // dropped data segments, instantiation status (a trapped start function fails the
 // instance, module.cpp:160-170), the resume point of a lane parked at a host import
-// (pc, call-stack depth, arg/result cell; pc ~0 = not parked), then the global cells.
+// (pc, call-stack depth, arg/result cell; pc ~0 = not parked), then the global cells,
+// then (per-lane tables only) each table's size and the dropped-elem-segment mask.
 #define LS_PAGES 0u
 #define LS_DROPPED 1u
 #define LS_ISTATUS 2u

@@ -326,7 +326,10 @@ class Assembler:
             elif k == "start":
                 self.start = fld[1]
             elif k == "elem":
-                self.elems.append(fld[1:])
+                rest = fld[1:]
+                if rest and isinstance(rest[0], str) and rest[0].startswith("$"):
+                    self.elem_names[rest[0]] = len(self.elems)
+                self.elems.append(rest)
             elif k == "data":
                 rest = fld[1:]
                 if rest and isinstance(rest[0], str) and rest[0].startswith("$"):
@@ -339,6 +342,43 @@ class Assembler:
         if f.name:
             self.func_names[f.name] = len(self.funcs)
         self.funcs.append(f)
+
+    def _elem_seg(self, rest):
+        """One element segment in the binary format's 8 encodings: flags bit 0 passive or
+        declarative, bit 1 explicit table index (active) / declarative (passive), bit 2
+        items as const expressions."""
+        if rest and isinstance(rest[0], str) and rest[0].startswith("$"):
+            rest = rest[1:]
+        declare = bool(rest) and rest[0] == "declare"
+        if declare:
+            rest = rest[1:]
+        table = None
+        if rest and isinstance(rest[0], list) and rest[0][0] == "table":
+            table = self._resolve(rest[0][1], self.table_names)
+            rest = rest[1:]
+        off = None
+        if rest and isinstance(rest[0], list) and (rest[0][0] == "offset" or
+                                                   rest[0][0].endswith(".const") or
+                                                   rest[0][0] == "global.get"):
+            off = rest[0][1:] if rest[0][0] == "offset" else [rest[0]]
+            rest = rest[1:]
+        exprs, rtype = False, 0x70
+        if rest and rest[0] in ("funcref", "externref"):
+            exprs, rtype = True, VALTYPES[rest[0]]
+            rest = rest[1:]
+        elif rest and rest[0] == "func":
+            rest = rest[1:]
+        if exprs:
+            items = _vec([self._const_expr([x if x[0] != "item" else x[1]]) for x in rest])
+        else:
+            items = _vec([uleb(self._resolve(x, self.func_names)) for x in rest])
+        if off is not None:
+            if table is None:
+                return bytes([4 if exprs else 0]) + self._const_expr(off) + items
+            return bytes([6 if exprs else 2]) + uleb(table) + self._const_expr(off) + \
+                (bytes([rtype]) if exprs else b"\x00") + items
+        flags = (3 if declare else 1) | (4 if exprs else 0)
+        return bytes([flags]) + (bytes([rtype]) if exprs else b"\x00") + items
 
     # -- const expressions (globals, offsets)
     def _const_expr(self, items, f=None):
@@ -679,19 +719,7 @@ class Assembler:
         if self.elems:
             segs = []
             for e in self.elems:
-                rest = list(e)
-                if rest and isinstance(rest[0], str) and rest[0].startswith("$"):
-                    rest = rest[1:]
-                off = rest[0]
-                if isinstance(off, list) and off[0] == "offset":
-                    off = off[1:]
-                else:
-                    off = [off]
-                items = rest[1:]
-                if items and items[0] == "func":
-                    items = items[1:]
-                segs.append(b"\x00" + self._const_expr(off) +
-                            _vec([uleb(self._resolve(x, self.func_names)) for x in items]))
+                segs.append(self._elem_seg(list(e)))
             section(9, _vec(segs))
         if self.datas and any(1 for d in self.datas):
             pass
