@@ -177,6 +177,34 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext *Cxt,
                                                            uint32_t Inst, uint32_t Off,
                                                            const uint8_t *Src, uint32_t Len);
+/* Exported tables and globals of one instance, by export name (the batched form of
+ * WasmEdge_StoreFindTable/FindGlobal + WasmEdge_TableInstanceGetData/SetData/GetSize,
+ * lib/api/wasmedge.cpp:2099-2139, and WasmEdge_GlobalInstanceGetValue/SetValue,
+ * :2273-2295). Inst = WASMEDGE_BATCH_ALL_INSTANCES writes every instance. Reference
+ * values are 32-bit on the device: a funcref is the module's function index, an
+ * externref a host-chosen handle (a host function receives it in its argument), null is
+ * 0xFFFFFFFF. TableGetData/SetData: TableOutOfBounds (0x87) past the instance's table
+ * size, RefTypeMismatch (0x8E) for a value of the wrong reference type. GlobalSetValue
+ * ignores a constant global or a value of another type, as the reference does. An
+ * unknown export name gives FuncNotFound (0x05). Writes persist until BatchReset. */
+#define WASMEDGE_BATCH_ALL_INSTANCES 0xFFFFFFFFu
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchTableGetSize(WasmEdge_BatchContext *Cxt,
+                                                              const WasmEdge_String TableName,
+                                                              uint32_t Inst, uint32_t *Size);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchTableGetData(WasmEdge_BatchContext *Cxt,
+                                                              const WasmEdge_String TableName,
+                                                              uint32_t Inst, WasmEdge_Value *Data,
+                                                              uint32_t Offset);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *Cxt,
+                                                              const WasmEdge_String TableName,
+                                                              uint32_t Inst, WasmEdge_Value Data,
+                                                              uint32_t Offset);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGlobalGetValue(WasmEdge_BatchContext *Cxt,
+                                                                const WasmEdge_String GlobalName,
+                                                                uint32_t Inst, WasmEdge_Value *Value);
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchContext *Cxt,
+                                                                const WasmEdge_String GlobalName,
+                                                                uint32_t Inst, WasmEdge_Value Value);
 /* Current page count of instance Inst's memory. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *Cxt,
                                                          uint32_t Inst);

@@ -47,6 +47,13 @@ def lib():
         L.om_mem_hash.argtypes = [ctypes.c_void_p]
         L.om_hash_bytes.restype = ctypes.c_uint64
         L.om_hash_bytes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+        L.om_set_extern_value.restype = None
+        L.om_set_extern_value.argtypes = [ctypes.c_uint32, ctypes.c_int32]
+        L.om_table_set.restype = ctypes.c_int
+        L.om_table_set.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.om_global_get.restype = None
+        L.om_global_get.argtypes = [ctypes.c_void_p, ctypes.c_uint32,
+                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.om_run_batch.restype = ctypes.c_double
         L.om_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -191,6 +198,22 @@ class Instance:
             code = TERMINATED
         vals = [res[2 * k] | (res[2 * k + 1] << 64) for k in range(len(rt))] if code == 0 else []
         return code, vals, cnt.value, L.om_mem_hash(self._h)
+
+
+    def table_set(self, tab, off, ref):
+        """Write one table entry (ref: function index / externref handle, None = null);
+        returns the ErrCode (0x87 out of bounds)."""
+        return lib().om_table_set(self._h, tab, off, (1 << 64) - 1 if ref is None else ref)
+
+    def global_get(self, g):
+        lo, hi = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        lib().om_global_get(self._h, g, ctypes.byref(lo), ctypes.byref(hi))
+        return lo.value | (hi.value << 64)
+
+
+def set_extern_value(handle, value):
+    """The int32 an externref handle points to, for the "extern" test host module."""
+    lib().om_set_extern_value(handle, value)
 
 
 def hash_bytes(data, pages):

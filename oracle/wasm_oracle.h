@@ -51,6 +51,13 @@ int om_terminated(const OInst *i);
 /* Gas limit per invocation with unit costs (0 = none): statistics.h:69-91. */
 void om_set_cost_limit(OInst *i, uint64_t limit);
 
+/* Test host module "extern" (the reference API test's): the int32 an externref handle
+ * points to. Table entry write (ref: function index / handle, UINT64_MAX null) and a
+ * global's value bits, as the reference C API's TableInstanceSetData / GlobalInstanceGetValue. */
+void om_set_extern_value(uint32_t handle, int32_t v);
+int om_table_set(OInst *i, uint32_t tab, uint32_t off, uint64_t ref);
+void om_global_get(const OInst *i, uint32_t g, uint64_t *lo, uint64_t *hi);
+
 /* Linear memory 0 view and hash (hash defined in DESIGN.md, shared with the GPU). */
 uint32_t om_mem_pages(const OInst *i);
 const uint8_t *om_mem_data(const OInst *i);

@@ -59,6 +59,40 @@ ENV = {"add_i64": (add_i64, 2, 1), "mem_sum": (mem_sum, 2, 1), "mem_fill": (mem_
        "fail": (fail, 1, 1), "exit": (exit_, 1, 0), "mix": (mix, 2, 1)}
 
 
+# ---- the reference API test's import module "extern" (test/api/APIUnitTest.cpp:48-95):
+# {externref, i32} -> {i32} over the int32 an externref points to. Here an externref is a
+# 32-bit handle; EXTERN_VALUES maps it to its int32 (oracle: om_set_extern_value).
+EXTERN_VALUES = {}
+
+
+def _extern_op(op):
+    def f(mem, a):
+        h = a[0] & 0xFFFFFFFF
+        if h >= 256 or h not in EXTERN_VALUES:
+            return HOST_FAILED, []
+        x, y = EXTERN_VALUES[h], _i32(a[1])
+        if op == "div":
+            if y == 0 or (x == -(1 << 31) and y == -1):
+                return HOST_FAILED, []
+            q = abs(x) // abs(y)
+            v = -q if (x < 0) != (y < 0) else q
+        else:
+            v = {"add": x + y, "sub": x - y, "mul": x * y}[op]
+        return 0, [v & 0xFFFFFFFF]
+    return f
+
+
+EXTERN = {"func-add": (_extern_op("add"), 2, 1), "func-sub": (_extern_op("sub"), 2, 1),
+          "func-mul": (_extern_op("mul"), 2, 1), "func-div": (_extern_op("div"), 2, 1),
+          "func-term": (lambda mem, a: (TERMINATED, [1234]), 0, 1),
+          "func-fail": (lambda mem, a: (HOST_FAILED, [5678]), 0, 1)}
+
+
+def register_extern(ctx):
+    for name, (fn, np_, nr) in EXTERN.items():
+        ctx.add_host_function("extern", name, fn, np_, nr)
+
+
 def register(ctx):
     for name, (fn, np_, nr) in ENV.items():
         ctx.add_host_function("env", name, fn, np_, nr)

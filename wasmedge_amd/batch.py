@@ -29,6 +29,24 @@ STATUS_NAMES = {0x00: "ok", 0x07: "interrupted", 0x84: "integer divide by zero",
                 0xB1: "host call (yield path not implemented)"}
 
 
+ALL_INSTANCES = 0xFFFFFFFF
+REF_NULL = 0xFFFFFFFF   # null funcref / externref on the device (32-bit references)
+
+
+class _Value(ctypes.Structure):
+    """WasmEdge_Value passed by value: uint128 as two u64 words, then the type."""
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64), ("type", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32 * 3)]
+
+    @classmethod
+    def make(cls, value, vtype):
+        v = int(value) & ((1 << 128) - 1)
+        return cls(v & 0xFFFFFFFFFFFFFFFF, v >> 64, vtype)
+
+    def int(self):
+        return self.lo | (self.hi << 64)
+
+
 class WasmEdgeError(RuntimeError):
     def __init__(self, code, msg=""):
         super().__init__("WasmEdge_Result 0x%02x %s" % (code, msg))
@@ -116,6 +134,16 @@ def lib():
             ("WasmEdge_BatchAddHostFunction", [vp, _String, _String, HOST_FUNC, vp]),
             ("WasmEdge_BatchMemoryGetData", [vp, vp, u32, u32]),
             ("WasmEdge_BatchMemorySetData", [vp, ctypes.c_char_p, u32, u32]),
+        ]:
+            f = getattr(L, name)
+            f.restype = _Result
+            f.argtypes = args
+        for name, args in [
+            ("WasmEdge_BatchTableGetSize", [vp, _String, u32, ctypes.POINTER(u32)]),
+            ("WasmEdge_BatchTableGetData", [vp, _String, u32, ctypes.POINTER(_Value), u32]),
+            ("WasmEdge_BatchTableSetData", [vp, _String, u32, _Value, u32]),
+            ("WasmEdge_BatchGlobalGetValue", [vp, _String, u32, ctypes.POINTER(_Value)]),
+            ("WasmEdge_BatchGlobalSetValue", [vp, _String, u32, _Value]),
         ]:
             f = getattr(L, name)
             f.restype = _Result
@@ -246,6 +274,33 @@ class BatchContext:
 
     def set_memory(self, inst, off, data):
         self._check(lib().WasmEdge_BatchSetMemory(self._h, inst, off, bytes(data), len(data)))
+
+    # exported tables / globals of one instance (WasmEdge_TableInstance*/GlobalInstance*);
+    # inst=None writes every instance
+    def table_size(self, name, inst):
+        n = ctypes.c_uint32(0)
+        self._check(lib().WasmEdge_BatchTableGetSize(self._h, self._name(name), inst, ctypes.byref(n)))
+        return n.value
+
+    def table_get(self, name, inst, off):
+        v = _Value()
+        self._check(lib().WasmEdge_BatchTableGetData(self._h, self._name(name), inst, ctypes.byref(v), off))
+        return v.int(), v.type
+
+    def table_set(self, name, inst, off, value, vtype):
+        inst = ALL_INSTANCES if inst is None else inst
+        self._check(lib().WasmEdge_BatchTableSetData(self._h, self._name(name), inst,
+                                                     _Value.make(value, vtype), off))
+
+    def global_get(self, name, inst):
+        v = _Value()
+        self._check(lib().WasmEdge_BatchGlobalGetValue(self._h, self._name(name), inst, ctypes.byref(v)))
+        return v.int(), v.type
+
+    def global_set(self, name, inst, value, vtype):
+        inst = ALL_INSTANCES if inst is None else inst
+        self._check(lib().WasmEdge_BatchGlobalSetValue(self._h, self._name(name), inst,
+                                                       _Value.make(value, vtype)))
 
     def add_host_function(self, module, name, fn, nparams, nresults):
         """Bind `fn(mem: HostMemory, args: list[int]) -> (code, results: list[int])` to

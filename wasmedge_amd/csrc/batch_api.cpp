@@ -32,7 +32,8 @@ namespace {
 
 // ErrCodes (include/common/enum.inc)
 constexpr uint8_t kRuntimeError = 0x02, kWrongVMWorkflow = 0x04, kFuncNotFound = 0x05,
-                  kFuncSigMismatch = 0x83, kMemoryOutOfBounds = 0x88;
+                  kFuncSigMismatch = 0x83, kTableOutOfBounds = 0x87, kMemoryOutOfBounds = 0x88,
+                  kRefTypeMismatch = 0x8E;
 
 std::string g_last_create_error;
 
@@ -602,6 +603,130 @@ WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext *C, uint32_t Inst,
                                         const uint8_t *Src, uint32_t Len) {
   if (!C) return R(kWrongVMWorkflow);
   return R(mem_rw(C, Inst, Off, Len, nullptr, Src));
+}
+
+// ---- exported tables and globals (WasmEdge_TableInstance{Get,Set}Data / GetSize,
+// WasmEdge_GlobalInstance{Get,Set}Value, lib/api/wasmedge.cpp:2099-2139, 2273-2295),
+// per instance; Inst = WASMEDGE_BATCH_ALL_INSTANCES writes every instance
+}  // extern "C"
+namespace {
+int find_named(const std::vector<wb::ExportFunc> &v, const WasmEdge_String &n) {
+  const std::string name(n.Buf ? n.Buf : "", n.Length);
+  for (const auto &e : v)
+    if (e.name == name) return int(e.func);
+  return -1;
+}
+// word `slot` (in [0, stride)) of instance Inst in a [wave][stride][64] buffer
+size_t lane_at(uint32_t Inst, size_t stride, size_t slot) {
+  return (size_t(Inst / 64) * stride + slot) * 64 + Inst % 64;
+}
+bool get_lane(WasmEdge_BatchContext *C, const uint32_t *buf, size_t stride, size_t slot,
+              uint32_t Inst, uint32_t *v) {
+  return C->hip_ok(hipMemcpy(v, buf + lane_at(Inst, stride, slot), 4, hipMemcpyDeviceToHost), "read");
+}
+bool put_lane(WasmEdge_BatchContext *C, uint32_t *buf, size_t stride, size_t slot,
+              uint32_t Inst, uint32_t v) {
+  if (Inst != WASMEDGE_BATCH_ALL_INSTANCES)
+    return C->hip_ok(hipMemcpy(buf + lane_at(Inst, stride, slot), &v, 4, hipMemcpyHostToDevice), "write");
+  std::vector<uint32_t> row(size_t(C->nwaves) * 64, v);   // one 64-lane row per wave
+  return C->hip_ok(hipMemcpy2D(buf + slot * 64, stride * 256, row.data(), 256, 256, C->nwaves,
+                               hipMemcpyHostToDevice), "write");
+}
+}  // namespace
+extern "C" {
+
+WasmEdge_Result WasmEdge_BatchTableGetSize(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
+                                           uint32_t Inst, uint32_t *Size) {
+  if (!C || !Size) return R(kWrongVMWorkflow);
+  const int t = find_named(C->prog.table_exports, TableName);
+  if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
+  if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
+  return R(get_lane(C, C->lstate.ptr, C->ls_slots, LS_GLOBALS + C->prog.global_cells + t, Inst, Size)
+               ? 0 : kRuntimeError);
+}
+
+WasmEdge_Result WasmEdge_BatchTableGetData(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
+                                           uint32_t Inst, WasmEdge_Value *Data, uint32_t Offset) {
+  if (!C || !Data) return R(kWrongVMWorkflow);
+  uint32_t size = 0;
+  WasmEdge_Result r = WasmEdge_BatchTableGetSize(C, TableName, Inst, &size);
+  if (r.Code) return r;
+  const wb::Program &P = C->prog;
+  const int t = find_named(P.table_exports, TableName);
+  if (Offset >= size) return R(kTableOutOfBounds);   // table.h:131-138 getRefAddr
+  uint32_t v = 0;
+  if (!get_lane(C, C->ltab.ptr, P.tab_words, P.tabinfo[2 * t] + Offset, Inst, &v))
+    return R(kRuntimeError);
+  Data->Value = v;
+  Data->Type = static_cast<enum WasmEdge_ValType>(P.tables[t].type);
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
+                                           uint32_t Inst, WasmEdge_Value Data, uint32_t Offset) {
+  if (!C) return R(kWrongVMWorkflow);
+  const wb::Program &P = C->prog;
+  const int t = find_named(P.table_exports, TableName);
+  if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
+  if (uint32_t(Data.Type) != P.tables[t].type) return R(kRefTypeMismatch);
+  const uint32_t v = uint32_t(Data.Value);
+  if (P.tables[t].type == wb::FUNCREF && v != 0xFFFFFFFFu && v >= P.funcs.size())
+    return R(C->fail(kRuntimeError, "funcref is not a function index of the module"));
+  if (Inst == WASMEDGE_BATCH_ALL_INSTANCES) {
+    // every lane: bounds against each lane's own size (all lanes checked first)
+    std::vector<uint32_t> sizes(size_t(C->nwaves) * 64);
+    const size_t slot = LS_GLOBALS + P.global_cells + t;
+    if (!C->hip_ok(hipMemcpy2D(sizes.data(), 256, C->lstate.ptr + slot * 64, size_t(C->ls_slots) * 256,
+                               256, C->nwaves, hipMemcpyDeviceToHost), "read"))
+      return R(kRuntimeError);
+    for (uint32_t i = 0; i < C->n; i++)
+      if (Offset >= sizes[i]) return R(kTableOutOfBounds);
+  } else {
+    uint32_t size = 0;
+    WasmEdge_Result r = WasmEdge_BatchTableGetSize(C, TableName, Inst, &size);
+    if (r.Code) return r;
+    if (Offset >= size) return R(kTableOutOfBounds);   // table.h:141-149 setRefAddr
+  }
+  return R(put_lane(C, C->ltab.ptr, P.tab_words, P.tabinfo[2 * t] + Offset, Inst, v) ? 0 : kRuntimeError);
+}
+
+WasmEdge_Result WasmEdge_BatchGlobalGetValue(WasmEdge_BatchContext *C, const WasmEdge_String GlobalName,
+                                             uint32_t Inst, WasmEdge_Value *Value) {
+  if (!C || !Value) return R(kWrongVMWorkflow);
+  const wb::Program &P = C->prog;
+  const int g = find_named(P.global_exports, GlobalName);
+  if (g < 0) return R(C->fail(kFuncNotFound, "global export not found"));
+  if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
+  const uint8_t t = P.global_types[g];
+  uint128_t v = 0;
+  for (uint32_t q = 0; q < wb::cells_of(t); q++) {
+    uint32_t w = 0;
+    if (!get_lane(C, C->lstate.ptr, C->ls_slots, LS_GLOBALS + P.global_cell[g] + q, Inst, &w))
+      return R(kRuntimeError);
+    v |= uint128_t(w) << (32 * q);
+  }
+  if ((t == wb::FUNCREF || t == wb::EXTERNREF) && uint32_t(v) == 0xFFFFFFFFu) v = 0xFFFFFFFFu;
+  Value->Value = v;
+  Value->Type = static_cast<enum WasmEdge_ValType>(t);
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchContext *C, const WasmEdge_String GlobalName,
+                                             uint32_t Inst, WasmEdge_Value Value) {
+  if (!C) return R(kWrongVMWorkflow);
+  const wb::Program &P = C->prog;
+  const int g = find_named(P.global_exports, GlobalName);
+  if (g < 0) return R(C->fail(kFuncNotFound, "global export not found"));
+  if (Inst >= C->n && Inst != WASMEDGE_BATCH_ALL_INSTANCES)
+    return R(C->fail(kRuntimeError, "instance index out of range"));
+  // wasmedge.cpp:2286-2295: a constant global or a value of another type is ignored
+  const uint8_t t = P.global_types[g];
+  if (!P.global_mut[g] || uint32_t(Value.Type) != t) return R(0);
+  for (uint32_t q = 0; q < wb::cells_of(t); q++)
+    if (!put_lane(C, C->lstate.ptr, C->ls_slots, LS_GLOBALS + P.global_cell[g] + q, Inst,
+                  uint32_t(Value.Value >> (32 * q))))
+      return R(kRuntimeError);
+  return R(0);
 }
 
 WasmEdge_Result WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *C,

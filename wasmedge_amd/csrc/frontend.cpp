@@ -1552,6 +1552,8 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
           uint8_t kind = s.u8();
           uint32_t idx = s.u32();
           if (kind == 0) P.exports.push_back(ExportFunc{nm, idx});
+          if (kind == 1) P.table_exports.push_back(ExportFunc{nm, idx});
+          if (kind == 3) P.global_exports.push_back(ExportFunc{nm, idx});
         }
         break;
       }
@@ -1663,8 +1665,14 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
     for (size_t q = 0; q < e.items.size(); q++) T[e.offset + q] = e.items[q];
   }
   if (P.ntables) P.table0 = timg[0];
-  // several tables or an externref table: per-lane tables from the start
-  P.mut_tables = P.ntables > 1 || (P.ntables && P.tables[0].type != FUNCREF);
+  // several tables, an externref table or an exported table (the host may write it,
+  // WasmEdge_BatchTableSetData): per-lane tables from the start
+  P.mut_tables = P.ntables > 1 || (P.ntables && P.tables[0].type != FUNCREF) ||
+                 !P.table_exports.empty();
+  for (auto &e : P.table_exports)
+    if (e.func >= P.ntables) throw Err{E_TYPECHECK, "unknown table"};
+  for (auto &e : P.global_exports)
+    if (e.func >= P.global_types.size()) throw Err{E_TYPECHECK, "unknown global"};
   for (auto &d : P.datas)
     if (d.active && uint64_t(d.offset) + d.bytes.size() > uint64_t(P.mem_min) * 65536)
       throw Err{0x63, "data segment does not fit"};

@@ -70,6 +70,7 @@ struct Program {
   std::vector<FuncInfo> funcs;
   uint32_t n_imported = 0;
   std::vector<ExportFunc> exports;
+  std::vector<ExportFunc> table_exports, global_exports;   // name -> table / global index
   bool has_mem = false;
   uint32_t mem_min = 0, mem_max = 65536;
   bool mem_has_max = false;
