@@ -13,10 +13,11 @@
 #include "../../include/wasmedge_batch.h"
 #include "frontend.h"
 #include "tc.h"
+#include "tc_slots.h"
 #include "kparams.h"
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
-                                     size_t lds_bytes, hipStream_t s);
+                                     size_t lds_bytes, int vframe, hipStream_t s);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves, hipStream_t s);
@@ -84,6 +85,7 @@ struct WasmEdge_BatchContext {
   DevBuf<DInstr> code;
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
   bool threaded = true;
+  bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
   DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
   DevBuf<DFunc> funcs;
@@ -180,7 +182,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const char *thr = getenv("WB_THREADED");
   C->threaded = !(thr && thr[0] == '0');
   std::vector<TInstr> tcv;
-  if (C->threaded) tcv = wb::build_threaded(P, codepad);
+  // V frames (frame cells in VGPRs while the core runs) when the frame fits in
+  // v128..v255 and the batch needs at most 2 waves per SIMD (the V kernel's 256 VGPRs
+  // allow no more; beyond that the LDS kernel's occupancy wins: C5 at 256K instances
+  // 7.2e11 vs 6.2e11). WB_VFRAME=0 / 1 forces LDS / V frames (A/B measurement aid).
+  const char *vfe = getenv("WB_VFRAME");
+  const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
+  C->vframe = vf_fit && (vfe ? vfe[0] == '1' : C->nwaves <= 2 * 1024);
+  if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);
   // LS image from slot LS_GLOBALS on: globals, then (per-lane tables) table sizes and
   // the dropped-elem mask
   std::vector<uint32_t> ls_init = P.global_init;
@@ -318,7 +327,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
   (void)hipEventRecord(C->ev0, C->stream);
   // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
-  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->stream), "launch"))
+  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->vframe && k.tcode, C->stream), "launch"))
     return kRuntimeError;
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;

@@ -29,6 +29,7 @@
 
 #include "dbc_ops.h"
 #include "tc.h"
+#include "tc_slots.h"
 
 // The threaded dispatch core (gen_tc.py): hand-written gfx950 handlers. hipcc drops
 // file-scope asm in device code, so the blob is the body of a kernel that is never
@@ -37,6 +38,17 @@
 extern "C" __global__ void wb_tc_holder_kernel() {
   asm volatile("s_endpgm\n"
 #include "tc_blob.inc"
+               ::: "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
+               "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
+               "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
+               "s92", "s93", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
+               "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
+               "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
+}
+// The V-frame variant (frame cells in v128..v255, gen_tc.py VB) for wb_exec_vf_kernel.
+extern "C" __global__ void __launch_bounds__(256) wb_vf_holder_kernel() {
+  asm volatile("s_endpgm\n"
+#include "tc_vblob.inc"
                ::: "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
                "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
                "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
@@ -105,10 +117,66 @@ struct LdsFrame {
 // instruction next), or reaches `other` / the count limit (reason 1: back to the
 // scheduler). Returns the new uniform pc; *ncnt = wasm instructions retired.
 // Register contract: gen_tc.py (s60-s93, v104-v127 belong to the core).
+// (gsp is read-write: only the run's lanes (EXEC) take the core's value, the waiting
+// lanes keep theirs)
+#define TC_RUN_ASM(ENTRY, ...) \
+  asm volatile( \
+      "s_mov_b32 s60, %[clo]\n\t" \
+      "s_mov_b32 s61, %[chi]\n\t" \
+      "s_lshl_b32 s62, %[pc], 5\n\t" \
+      "s_mov_b32 s63, %[oth]\n\t" \
+      "s_mov_b32 s64, %[lim]\n\t" \
+      "s_mov_b32 s65, 0\n\t" \
+      "v_mov_b32 v104, %[fr]\n\t" \
+      "v_mov_b32 v105, %[pages]\n\t" \
+      "v_mov_b32 v106, %[mlo]\n\t" \
+      "v_mov_b32 v107, %[mhi]\n\t" \
+      "v_mov_b32 v102, %[gsp]\n\t" \
+      "v_mov_b32 v103, %[stk]\n\t" \
+      "s_mov_b32 s93, %[slds]\n\t" \
+      "s_mov_b32 s94, %[vsync]\n\t" \
+      "s_getpc_b64 s[66:67]\n" \
+      "Ltc_ret_%=:\n\t" \
+      "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t" \
+      "s_addc_u32 s67, s67, 0\n\t" \
+      "s_getpc_b64 s[68:69]\n\t" \
+      "s_add_u32 s68, s68, " ENTRY "@rel32@lo+4\n\t" \
+      "s_addc_u32 s69, s69, " ENTRY "@rel32@hi+12\n\t" \
+      "s_setpc_b64 s[68:69]\n" \
+      "Ltc_back_%=:\n\t" \
+      "s_lshr_b32 %[npc], s62, 5\n\t" \
+      "s_mov_b32 %[cnt], s65\n\t" \
+      "s_mov_b32 %[why], s92\n\t" \
+      "v_mov_b32 %[gsp], v102" \
+      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp) \
+      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
+        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), \
+        [slds] "s"(slds), [vsync] "s"(vsync) \
+      : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
+        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
+        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", \
+        "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
+        "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
+
+// VF: the V-frame core (wb_vf_entry): it loads the frame into v128.. on entry and stores
+// it back on exit (vsync = (TC_VF_CELLS - frame cells) * 8, gen_tc.py VSYNC).
+#define TC_VREGS "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", \
+  "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", \
+  "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", \
+  "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", \
+  "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", \
+  "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", \
+  "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", \
+  "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", \
+  "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", \
+  "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", \
+  "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255"
+template <bool VF>
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem,
                                            uint32_t &gsp, uint32_t stk, uint32_t slds,
-                                           uint32_t *ncnt, uint32_t *reason) {
+                                           uint32_t vsync, uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
   const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
   const uint64_t m = (uint64_t)(uintptr_t)mem;
@@ -118,51 +186,17 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
   // all of these are wave-uniform; readfirstlane keeps them in SGPRs even where the
   // compiler's divergence analysis cannot prove it (profiling builds)
   pc = __builtin_amdgcn_readfirstlane(pc);
-  asm volatile(
-      "s_mov_b32 s60, %[clo]\n\t"
-      "s_mov_b32 s61, %[chi]\n\t"
-      "s_lshl_b32 s62, %[pc], 5\n\t"
-      "s_mov_b32 s63, %[oth]\n\t"
-      "s_mov_b32 s64, %[lim]\n\t"
-      "s_mov_b32 s65, 0\n\t"
-      "v_mov_b32 v104, %[fr]\n\t"
-      "v_mov_b32 v105, %[pages]\n\t"
-      "v_mov_b32 v106, %[mlo]\n\t"
-      "v_mov_b32 v107, %[mhi]\n\t"
-      "v_mov_b32 v102, %[gsp]\n\t"
-      "v_mov_b32 v103, %[stk]\n\t"
-      "s_mov_b32 s93, %[slds]\n\t"
-      "s_getpc_b64 s[66:67]\n"
-      "Ltc_ret_%=:\n\t"
-      "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t"
-      "s_addc_u32 s67, s67, 0\n\t"
-      "s_getpc_b64 s[68:69]\n\t"
-      "s_add_u32 s68, s68, wb_tc_entry@rel32@lo+4\n\t"
-      "s_addc_u32 s69, s69, wb_tc_entry@rel32@hi+12\n\t"
-      "s_setpc_b64 s[68:69]\n"
-      "Ltc_back_%=:\n\t"
-      "s_lshr_b32 %[npc], s62, 5\n\t"
-      "s_mov_b32 %[cnt], s65\n\t"
-      "s_mov_b32 %[why], s92\n\t"
-      "v_mov_b32 %[gsp], v102"
-      // gsp is read-write: only the run's lanes (EXEC) take the core's value, the
-      // waiting lanes keep theirs
-      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp)
-      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr),
-        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk),
-        [slds] "s"(slds)
-      : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
-        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83",
-        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
-        "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113",
-        "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123",
-        "v124", "v125", "v126", "v127", "vcc", "scc", "memory");
+  if constexpr (VF) {
+    TC_RUN_ASM("wb_vf_entry", TC_VREGS);
+  } else {
+    TC_RUN_ASM("wb_tc_entry");
+  }
   *ncnt = cnt;
   *reason = why;
   return npc;
 }
 
-template <class Frame>
+template <bool VF, class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
                                        uint32_t *const gs, uint32_t *const mem,
                                        uint32_t *const ls, uint32_t *const fs,
@@ -304,7 +338,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
-          pcs = tc_run(p.tcode, pcs, other, fr_lds, pages, mem, gsp, stk_lds, S_lds, &ncnt, &why);
+          pcs = tc_run<VF>(p.tcode, pcs, other, fr_lds, pages, mem, gsp, stk_lds, S_lds,
+                            (TC_VF_CELLS - p.total_cells) * 8u, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
           I = code[pcs];
@@ -480,8 +515,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef LS
 }
 
-// General kernel: frames of any size in LDS (4 waves per block when they fit).
-extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p) {
+// General kernel: frames of any size in LDS (4 waves per block when they fit). VF: the
+// threaded core keeps the frame in VGPRs (frames up to TC_VF_CELLS cells; 256 VGPRs).
+template <bool VF>
+__device__ __forceinline__ void exec_body(const KParams &p) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -489,10 +526,17 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p
   LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
   // LDS call-stack slots of this wave follow the frames of all the block's waves
   lds_u32 *const stk = (lds_u32 *)(lds + ((((blockDim.x >> 6) * p.total_cells) + wib * p.gs_lds) << 6) + lane);
-  interp(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+  interp<VF>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
          p.mem + (size_t)wave * p.mem_words * 64u + lane,
          p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
          p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+}
+
+extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p) {
+  exec_body<false>(p);
+}
+extern "C" __global__ void __launch_bounds__(256) wb_exec_vf_kernel(const KParams p) {
+  exec_body<true>(p);
 }
 
 // ======================================================================= helpers
@@ -551,14 +595,19 @@ wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
 // ======================================================================= launchers
 // (host stubs live in this translation unit; the C-ABI layer calls these)
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
-                                     size_t lds_bytes, hipStream_t s) {
+                                     size_t lds_bytes, int vframe, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_vf_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
+  if (vframe)
+    hipLaunchKernelGGL(wb_exec_vf_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
+  else
+    hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,

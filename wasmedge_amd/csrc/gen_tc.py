@@ -29,6 +29,7 @@ Outputs (both written next to this file; run by the Makefile):
   tc_slots.h    opcode -> slot map for the host translator (tc.cpp)
 """
 import os
+import re
 import sys
 
 SLOT = 256                         # bytes per handler slot
@@ -67,6 +68,7 @@ Z = ("v126", "v127"); ZP = "v[126:127]"
 GSP = "v102"          # this lane's call-stack depth (slots), in/out
 SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
 SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
+VSYNC = "s94"         # V frames: (VMAX - frame cells) * 8, the frame-sync jump offset
 
 
 def sreg(bank, k):
@@ -87,11 +89,17 @@ def sbank(bank):
 #   explicit branch code using g.taken(...)
 
 
+VB = 128               # V-frame blob: frame cell i of the lane lives in VGPR v[VB + i]
+VMAX = 128             # cells a V frame can hold (v128..v255)
+
+
 class Gen:
-    def __init__(self, mode, bank):
+    def __init__(self, mode, bank, vf=False):
         self.mode, self.bank = mode, bank          # mode "C" converged / "D" diverged
         self.other = "B" if bank == "A" else "A"
         self.n = 0
+        self.vf = vf                               # frame in VGPRs (GPR-index mode)
+        self.pre = "Lvf" if vf else "Ltc"
 
     def x(self, k):                                # field k of the current instruction
         return sreg(self.bank, k)
@@ -103,16 +111,51 @@ class Gen:
 
     def lab(self, tag):
         Gen._uid[0] += 1
-        return "Ltc_%s_%d" % (tag, Gen._uid[0])
+        return "%s_%s_%d" % (self.pre, tag, Gen._uid[0])
 
     def exit_here(self):
         return ["s_branch %s" % self.xh()]
 
     def xh(self):     # exit stubs live in slot 0 of every bank (s_branch reaches +-128 KB)
-        return "Ltc_xh_%s%s" % (self.mode, self.bank)
+        return "%s_xh_%s%s" % (self.pre, self.mode, self.bank)
 
     def xs(self):
-        return "Ltc_xs_%s%s" % (self.mode, self.bank)
+        return "%s_xs_%s%s" % (self.pre, self.mode, self.bank)
+
+    # -- V frames: cells are VGPRs v[VB + cell], addressed through GPR-index mode with
+    # the cell index in an SGPR (instruction fields hold cell indices, not LDS offsets).
+    # While index mode is on, EVERY VALU operand it names is offset, so each sequence
+    # holds nothing but the indexed moves and is closed before any other VALU or branch.
+    def vread(self, sidx, regs, base=VB):
+        """regs[k] = v[base + k + idx]; sidx: SGPR holding the cell index."""
+        return ["s_set_gpr_idx_on %s, gpr_idx(SRC0)" % sidx] + \
+            ["v_mov_b32 %s, v%d" % (r, base + k) for k, r in enumerate(regs)] + ["s_set_gpr_idx_off"]
+
+    def vwrites(self, items):
+        """items: [(SGPR cell index, [value regs])]: v[VB + idx + k] = regs[k]."""
+        out = []
+        for i, (sidx, regs) in enumerate(items):
+            out.append("s_set_gpr_idx_on %s, gpr_idx(DST)" % sidx if i == 0 else
+                       "s_set_gpr_idx_idx %s" % sidx)
+            out += ["v_mov_b32 v%d, %s" % (VB + k, r) for k, r in enumerate(regs)]
+        return out + ["s_set_gpr_idx_off"]
+
+    def vprologue(self, body):
+        """Fetch the operands (a: field 1, b: field 2, d: field 5; cells k, k+1) that
+        `body` names -- in the LDS blob the previous handler prefetched all of them."""
+        out, on = [], False
+        text = "\n".join(body)
+        for field, regs, pair in ((1, A, AP), (2, B, BP), (5, D, DP)):
+            # a register by name, or the pair "v[lo:hi]" (64-bit operands) for both
+            both = pair in text
+            need = [both or re.search(r"\b%s\b" % r, text) is not None for r in regs]
+            if not any(need):
+                continue
+            out.append("s_set_gpr_idx_idx %s" % self.x(field) if on else
+                       "s_set_gpr_idx_on %s, gpr_idx(SRC0)" % self.x(field))
+            on = True
+            out += ["v_mov_b32 %s, v%d" % (r, VB + k) for k, r in enumerate(regs) if need[k]]
+        return out + (["s_set_gpr_idx_off"] if on else [])
 
     def issue_reads(self, bank):
         """LDS reads of the operands of the instruction in `bank` (fields 1, 2, 5)."""
@@ -140,8 +183,13 @@ class Gen:
         out.append("s_add_u32 %s, %s, 32" % (PCOFF, PCOFF))
         if self.mode == "D":
             out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
-        out += self.issue_reads(self.other)
-        if pf4:
+        if self.vf:
+            # the successor's fields (loaded two dispatches ago) must be resident; no
+            # operand prefetch: the successor reads its operands from VGPRs itself
+            out.append("s_waitcnt lgkmcnt(0)")
+        else:
+            out += self.issue_reads(self.other)
+        if pf4 and not self.vf:
             out += ["v_add_u32 %s, %s, %s" % (X[1], sreg(self.other, 7), FR),
                     "ds_read_b32 %s, %s" % (Y[0], X[1])]
         # prefetch the successor's successor into this bank (its fields are dead now)
@@ -156,26 +204,36 @@ class Gen:
                "s_cmp_ge_u32 %s, %s" % (CNT, LIM), "s_cbranch_scc1 %s" % self.xs()]
         if self.mode == "D":
             out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
-        # the successor prefetch into the other bank has landed (every branch handler
-        # waited lgkmcnt(0) first), so both banks may be reloaded
+        # the successor prefetch into the other bank must have landed before both banks
+        # are reloaded (SMEM returns out of order: a late stale load would win). The LDS
+        # blob waited at handler entry; the V-frame blob waits here.
+        if self.vf:
+            out.append("s_waitcnt lgkmcnt(0)")
         out += ["s_load_dwordx8 %s, %s, %s" % (sbank(self.other), CODE, PCOFF),
                 "s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank(self.bank), CODE, PCOFF),
                 "s_waitcnt lgkmcnt(0)"]
-        out += self.issue_reads(self.other)
+        if not self.vf:
+            out += self.issue_reads(self.other)
         out += self.dispatch(self.other)
         return out
 
     # -- result writes
     def w32(self, v=None):
+        if self.vf:
+            return self.vwrites([(self.x(3), [v or R[0]])])
         return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
                 "ds_write_b32 %s, %s" % (CADDR, v or R[0])]
 
     def w64(self, lo=None, hi=None):
+        if self.vf:
+            return self.vwrites([(self.x(3), [lo or R[0], hi or R[1]])])
         return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
                 "ds_write2_b32 %s, %s, %s offset1:64" % (CADDR, lo or R[0], hi or R[1])]
 
     def w128(self, lo, hi):
         """lo/hi: VGPR pair names (cells c, c+1 and c+2, c+3)."""
+        if self.vf:
+            return self.vwrites([(self.x(3), [lo[0], lo[1], hi[0], hi[1]])])
         return ["v_add_u32 %s, %s, %s" % (CADDR, self.x(3), FR),
                 "ds_write2_b32 %s, %s, %s offset1:64" % (CADDR, lo[0], lo[1]),
                 "ds_write2_b32 %s, %s, %s offset0:128 offset1:192" % (CADDR, hi[0], hi[1])]
@@ -265,33 +323,39 @@ def specs():
         "v_xor_b32_e32 %s, %s, %s" % (X[0], A[0], B[0]),
         "v_alignbit_b32 %s, %s, %s, %s" % (R[0], X[0], X[0], g.x(4))] + g.w32() + g.next())
     # ARX pairs: sum -> c, then d (or the 4th cell y, read here) = rotr(. ^ sum, k)
-    add("I32_ADD_XROTR_I", ["I32_ADD_XROTR_I"], lambda g: [
-        "v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0])] + g.w32() + [
-        "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
-        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
-        "v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
-        "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next())
-    add("I32_ADD3_XROTR_I", ["I32_ADD3_XROTR_I"], lambda g: [
-        "v_add_u32 %s, %s, %s" % (X[1], g.x(7), FR),
-        "ds_read_b32 %s, %s" % (Y[0], X[1]),
-        "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + [
-        "s_waitcnt lgkmcnt(0)",
-        "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
-        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
-        "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
+    def add_xrotr(g, pf4=False):
+        out = ["v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0]),
+               "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
+               "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4))]
+        if g.vf:
+            return out + g.vwrites([(g.x(3), [R[0]]), (g.x(5), [R[1]])]) + g.next()
+        return out + g.w32() + ["v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
+                                "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next(pf4=pf4)
+
+    def add3_xrotr(g, pre=True):
+        """pre: read the 4th cell y here (else the PF4 predecessor read it into Y0)."""
+        if g.vf:
+            return g.vread(g.x(7), [Y[0]]) + [
+                "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0]),
+                "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
+                "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4))] + \
+                g.vwrites([(g.x(3), [R[0]]), (g.x(7), [R[1]])]) + g.next()
+        out = ["v_add_u32 %s, %s, %s" % (X[1], g.x(7), FR), "ds_read_b32 %s, %s" % (Y[0], X[1])] \
+            if pre else []
+        out += ["v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32()
+        if pre:
+            out.append("s_waitcnt lgkmcnt(0)")
+        return out + ["v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
+                      "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
+                      "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next()
+
+    add("I32_ADD_XROTR_I", ["I32_ADD_XROTR_I"], add_xrotr)
+    add("I32_ADD3_XROTR_I", ["I32_ADD3_XROTR_I"], add3_xrotr)
     # pipelined pair (tc.cpp picks these when ADD_XROTR falls into ADD3_XROTR and the
-    # latter is no jump target): the first prefetches the second's 4th operand y
-    add("I32_ADD_XROTR_I_PF4", [], lambda g: [
-        "v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0])] + g.w32() + [
-        "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
-        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
-        "v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
-        "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next(pf4=True))
-    add("I32_ADD3_XROTR_I_E", [], lambda g: [
-        "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32() + [
-        "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
-        "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4)),
-        "ds_write_b32 %s, %s" % (X[1], R[1])] + g.next())
+    # latter is no jump target): the first prefetches the second's 4th operand y.
+    # (LDS blob only; the V-frame translation never selects them.)
+    add("I32_ADD_XROTR_I_PF4", [], lambda g: add_xrotr(g, pf4=True))
+    add("I32_ADD3_XROTR_I_E", [], lambda g: add3_xrotr(g, pre=False))
     # ---- calls (dbc_step.inc OP_CALL / OP_RET / OP_POST_CALL, LDS part of the call stack
     # only; anything else -- HBM slots, divergent return targets, leaving the entry
     # function -- leaves the core before any effect). Fields (tc.cpp): w1 = L or the
@@ -310,7 +374,81 @@ def specs():
         return ["v_cmp_lt_u32_e64 vcc, %s, %s" % (SLDS, vreg),
                 "s_and_b64 %s, vcc, exec" % T2, "s_cbranch_scc1 %s" % g.xh()]
 
+    # V frames: the same protocol, frame cells moved with GPR-index moves. Fields hold
+    # cell indices: w1 = L (RET: the result cell), w2 = fb.
+    def vloop(g, tag, cnt, body):
+        """while (cnt--) body -- cnt: SGPR, body: lines (no VALU left in index mode)."""
+        top, end = g.lab(tag), g.lab(tag + "e")
+        return ["%s:" % top, "s_cmp_eq_u32 %s, 0" % cnt, "s_cbranch_scc1 %s" % end] + body + \
+            ["s_sub_u32 %s, %s, 1" % (cnt, cnt), "s_branch %s" % top, "%s:" % end]
+
+    def vmove(g, tag, cnt, si, di, step):
+        """v[VB+di] = v[VB+si], cnt times, indices stepping by `step` (1 / -1)."""
+        op = "s_add_u32" if step > 0 else "s_sub_u32"
+        return vloop(g, tag, cnt, g.vread(si, [Y[0]]) + g.vwrites([(di, [Y[0]])]) +
+                     ["%s %s, %s, 1" % (op, si, si), "%s %s, %s, 1" % (op, di, di)])
+
+    def call_body_v(g):
+        n, n1, si, di = "s68", "s69", T2L, T2H
+        out = ["s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)),
+               "s_add_u32 %s, %s, 1" % (n1, n),
+               "v_add_u32_e64 %s, %s, %s" % (X[0], n1, GSP)] + lds_guard(g, X[0])
+        out += ["v_lshl_add_u32 %s, %s, 8, %s" % (X[1], GSP, SB0),     # &stack[gsp]
+                "s_mov_b32 %s, %s" % (si, g.x(2))]
+        out += vloop(g, "sp", n, g.vread(si, [Y[0]]) + [               # spill [fb, L)
+            "ds_write_b32 %s, %s" % (X[1], Y[0]), "v_add_u32_e32 %s, 0x100, %s" % (X[1], X[1]),
+            "s_add_u32 %s, %s, 1" % (si, si)])
+        out += ["v_mov_b32 %s, %s" % (Y[1], g.x(3)), "ds_write_b32 %s, %s" % (X[1], Y[1]),
+                "v_add_u32_e64 %s, %s, %s" % (GSP, n1, GSP),
+                "s_and_b32 %s, %s, 0xffff" % (n, g.x(7)),
+                "s_mov_b32 %s, %s" % (si, g.x(1)), "s_mov_b32 %s, %s" % (di, g.x(2))]
+        out += vmove(g, "ar", n, si, di, 1)                            # args -> fb
+        out += ["s_lshr_b32 %s, %s, 16" % (n, g.x(7)), "v_mov_b32 %s, 0" % Y[0]]
+        out += vloop(g, "zl", n, g.vwrites([(di, [Y[0]])]) + ["s_add_u32 %s, %s, 1" % (di, di)])
+        return out + g.taken(g.x(4), g.x(6))
+
+    def ret_record(g, t):
+        return lds_guard(g, GSP) + [
+            "v_lshl_add_u32 %s, %s, 8, %s" % (X[1], GSP, SB0),
+            "v_subrev_u32_e32 %s, 0x100, %s" % (X[1], X[1]),           # &stack[gsp - 1]
+            "ds_read_b32 %s, %s" % (Y[1], X[1]), "s_waitcnt lgkmcnt(0)",
+            # the raw record (pc | L << 20) must agree across lanes; readfirstlane reads
+            # the loaded VGPR directly (a VALU-written VGPR would need wait states first)
+            "v_readfirstlane_b32 %s, %s" % (t, Y[1]),
+            "s_nop 1",                                   # VALU-written SGPR -> VALU read
+            "v_cmp_ne_u32_e64 %s, %s, %s" % (T2, t, Y[1]),
+            "s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh(),   # split returns
+            "s_and_b32 %s, %s, 0xfffff" % (t, t),
+            "s_cmp_eq_u32 %s, 0xfffff" % t, "s_cbranch_scc1 %s" % g.xh(),   # entry function
+            "v_subrev_u32_e32 %s, 1, %s" % (GSP, GSP)]
+
+    def ret_body_v(g):
+        t, si, di = "s68", T2L, T2H
+        out = ret_record(g, t) + ["s_mov_b32 s69, %s" % g.x(3), "s_mov_b32 %s, %s" % (si, g.x(1)),
+                                  "s_mov_b32 %s, %s" % (di, g.x(2))]
+        out += vmove(g, "rr", "s69", si, di, 1)                        # results -> fb
+        return out + ["s_lshl_b32 %s, %s, 5" % (t, t)] + g.taken(t, g.x(6))
+
+    def post_call_body_v(g):
+        n, r, si, di = "s68", "s69", T2L, T2H
+        out = lds_guard(g, GSP) + [
+            "s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)),
+            "s_mov_b32 %s, %s" % (r, g.x(3)),
+            # results fb.. -> L.. copied from the last one down (L > fb)
+            "s_add_u32 %s, %s, %s" % (si, g.x(2), r), "s_sub_u32 %s, %s, 1" % (si, si),
+            "s_add_u32 %s, %s, %s" % (di, g.x(1), r), "s_sub_u32 %s, %s, 1" % (di, di)]
+        out += vmove(g, "pr", r, si, di, -1)
+        out += ["v_subrev_u32_e64 %s, %s, %s" % (GSP, n, GSP),
+                "v_lshl_add_u32 %s, %s, 8, %s" % (X[0], GSP, SB0),
+                "s_mov_b32 %s, %s" % (di, g.x(2))]
+        out += vloop(g, "rs", n, ["ds_read_b32 %s, %s" % (Y[0], X[0]), "s_waitcnt lgkmcnt(0)"] +
+                     g.vwrites([(di, [Y[0]])]) +
+                     ["v_add_u32_e32 %s, 0x100, %s" % (X[0], X[0]), "s_add_u32 %s, %s, 1" % (di, di)])
+        return out + g.next()
+
     def call_body(g):
+        if g.vf:
+            return call_body_v(g)
         n, n1 = "s68", "s69"
         out = ["s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)), "s_lshr_b32 %s, %s, 8" % (n, n),
                "s_add_u32 %s, %s, 1" % (n1, n),
@@ -332,6 +470,8 @@ def specs():
         return out + g.taken(g.x(4), g.x(6))
 
     def ret_body(g):
+        if g.vf:
+            return ret_body_v(g)
         t = "s68"
         out = lds_guard(g, GSP) + [
             "v_lshl_add_u32 %s, %s, 8, %s" % (X[1], GSP, SB0),
@@ -353,6 +493,8 @@ def specs():
         return out + ["s_lshl_b32 %s, %s, 5" % (t, t)] + g.taken(t, g.x(6))
 
     def post_call_body(g):
+        if g.vf:
+            return post_call_body_v(g)
         n, r = "s68", "s69"
         out = lds_guard(g, GSP) + [
             "s_sub_u32 %s, %s, %s" % (n, g.x(1), g.x(2)), "s_lshr_b32 %s, %s, 8" % (n, n),
@@ -386,6 +528,12 @@ def specs():
 
     def hi_reads(g, regs):
         """cells +2, +3 of the prefetched v128 operands (regs: [(addr, pair), ...])."""
+        if g.vf:
+            out = []
+            for addr, pair in regs:
+                lo, hi = pair[2:-1].split(":")
+                out += g.vread(g.x(1 if addr == AADDR else 2), ["v" + lo, "v" + hi], base=VB + 2)
+            return out
         return ["ds_read2_b32 %s, %s offset0:128 offset1:192" % (pair, addr) for addr, pair in regs] + \
             ["s_waitcnt lgkmcnt(0)"]
 
@@ -619,9 +767,10 @@ SPECIAL_REMAP = {   # DBC op -> (slot op, immediate transform) applied by the tr
 }
 
 
-def main():
-    S = specs()
-    names = ["COLD"] + [s[0] for s in S]
+def blob(S, names, vf):
+    """Assembly lines of one handler blob: LDS frames (vf False, entry wb_tc_entry) or
+    V frames (vf True, entry wb_vf_entry)."""
+    pre = "Lvf" if vf else "Ltc"
     nslots = len(names)
     bank_bytes = nslots * SLOT
     L = []
@@ -630,11 +779,11 @@ def main():
     e(".p2align 8")
     # ------------------------------------------------------------- entry
     # in: CODE, PCOFF (pc*32 of the first instruction), OTHER, LIM, CNT=0, RET,
-    #     FR, PAGES, MEM.  EXEC = the active lanes.
-    e("wb_tc_entry:")
+    #     FR, PAGES, MEM (V frames also VSYNC).  EXEC = the active lanes.
+    e("%s:" % ("wb_vf_entry" if vf else "wb_tc_entry"))
     e("s_getpc_b64 s[70:71]")
-    e("Ltc_pc0:")
-    e("s_add_u32 s70, s70, Ltc_banks - Ltc_pc0")
+    e("%s_pc0:" % pre)
+    e("s_add_u32 s70, s70, %s_banks - %s_pc0" % (pre, pre))
     e("s_addc_u32 s71, s71, 0")
     e("s_cmp_eq_u32 %s, -1" % OTHER)                  # converged: banks 0/1
     e("s_cselect_b32 %s, 0, %d" % (T[0], 2 * bank_bytes))
@@ -645,13 +794,30 @@ def main():
     e("v_mov_b32 %s, 0" % W[1])
     e("s_load_dwordx8 %s, %s, %s" % (sbank("A"), CODE, PCOFF))
     e("s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank("B"), CODE, PCOFF))
-    e("s_waitcnt lgkmcnt(0)")
-    g0 = Gen("C", "B")
-    for ln in g0.issue_reads("A") + g0.dispatch("A"):
-        e(ln)
+    g0 = Gen("C", "B", vf)
+    if vf:
+        # frame LDS -> VGPRs: jump into an unrolled run of ds_reads (cells VMAX-1 .. 0;
+        # VSYNC = (VMAX - cells) * 8 skips the ones past the frame)
+        e("s_getpc_b64 s[68:69]")
+        e("Lvf_si_pc:")
+        e("s_add_u32 s68, s68, Lvf_si_base - Lvf_si_pc")
+        e("s_addc_u32 s69, s69, 0")
+        e("s_add_u32 s68, s68, %s" % VSYNC)
+        e("s_addc_u32 s69, s69, 0")
+        e("s_setpc_b64 s[68:69]")
+        e("Lvf_si_base:")
+        for i in range(VMAX - 1, -1, -1):
+            e("ds_read_b32 v%d, %s offset:%d" % (VB + i, FR, i * 256))
+        e("s_waitcnt lgkmcnt(0)")
+        for ln in g0.dispatch("A"):
+            e(ln)
+    else:
+        e("s_waitcnt lgkmcnt(0)")
+        for ln in g0.issue_reads("A") + g0.dispatch("A"):
+            e(ln)
     # ------------------------------------------------------------- banks
     e(".p2align 8")
-    e("Ltc_banks:")
+    e("%s_banks:" % pre)
     for mode in ("C", "D"):
         for bank in ("A", "B"):
             for si, nm in enumerate(names):
@@ -660,20 +826,35 @@ def main():
                 span = 1
                 while si + span < nslots and S[si + span - 1][2] is None:
                     span += 1
-                g = Gen(mode, bank)
-                lab = "Ltc_%s%s_%d" % (mode, bank, si)
+                g = Gen(mode, bank, vf)
+                lab = "%s_%s%s_%d" % (pre, mode, bank, si)
                 e(".p2align 8")
                 e("%s:" % lab)
                 if nm == "COLD":
                     # leave before this instruction (reason 0) / at PCOFF for the
                     # scheduler (reason 1); outstanding memory ops drained first
-                    body = ["%s:" % g.xh(), "s_mov_b32 %s, 0" % REASON,
-                            "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET,
-                            "%s:" % g.xs(), "s_mov_b32 %s, 1" % REASON,
-                            "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET]
+                    if vf:   # V frames go back to LDS first (Lvf_so_base)
+                        body = []
+                        for stub, why in ((g.xh(), 0), (g.xs(), 1)):
+                            pcl = g.lab("so")
+                            body += ["%s:" % stub, "s_mov_b32 %s, %d" % (REASON, why),
+                                     "s_getpc_b64 s[68:69]", "%s:" % pcl,
+                                     "s_add_u32 s68, s68, Lvf_so_base - %s" % pcl,
+                                     "s_addc_u32 s69, s69, 0",
+                                     "s_add_u32 s68, s68, %s" % VSYNC, "s_addc_u32 s69, s69, 0",
+                                     "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 s[68:69]"]
+                    else:
+                        body = ["%s:" % g.xh(), "s_mov_b32 %s, 0" % REASON,
+                                "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET,
+                                "%s:" % g.xs(), "s_mov_b32 %s, 1" % REASON,
+                                "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 %s" % RET]
                 else:
                     spec = S[si - 1][2]
-                    body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
+                    if vf:
+                        b = spec(g)
+                        body = g.vprologue(b) + b
+                    else:
+                        body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
                 for ln in body:
                     e(ln)
                 e(".if (. - %s) > %d" % (lab, SLOT * span))
@@ -682,16 +863,31 @@ def main():
                 if span > 1:
                     e(".org %s + %d" % (lab, SLOT * span))
     e(".p2align 8")
-    e("Ltc_banks_end:")
-    with open(os.path.join(HERE, "tc_blob.inc"), "w") as f:
-        f.write("// GENERATED by gen_tc.py -- do not edit. Handler blob of the threaded core.\n")
-        for ln in L:
-            f.write('"%s\\n"\n' % ln.replace('"', '\\"'))
+    e("%s_banks_end:" % pre)
+    if vf:
+        # frame VGPRs -> LDS, then back to the kernel
+        e("Lvf_so_base:")
+        for i in range(VMAX - 1, -1, -1):
+            e("ds_write_b32 %s, v%d offset:%d" % (FR, VB + i, i * 256))
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_setpc_b64 %s" % RET)
+    return L
+
+
+def main():
+    S = specs()
+    names = ["COLD"] + [s[0] for s in S]
+    nslots = len(names)
+    for fname, vf, what in (("tc_blob.inc", False, "LDS frames"), ("tc_vblob.inc", True, "V frames")):
+        with open(os.path.join(HERE, fname), "w") as f:
+            f.write("// GENERATED by gen_tc.py -- do not edit. Handler blob of the threaded core (%s).\n" % what)
+            for ln in blob(S, names, vf):
+                f.write('"%s\\n"\n' % ln.replace('"', '\\"'))
     # ------------------------------------------------------------- slot map
     with open(os.path.join(HERE, "tc_slots.h"), "w") as f:
         f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
         f.write("#pragma once\n#include \"dbc.h\"\n\n")
-        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n\n" % (SLOT, nslots))
+        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n#define TC_VF_CELLS %d\n\n" % (SLOT, nslots, VMAX))
         for si, (nm, ops, body) in enumerate(S, start=1):
             if body is not None:
                 f.write("#define TC_SLOT_%s %d\n" % (nm, si))
@@ -703,7 +899,7 @@ def main():
         for op, (to, _) in SPECIAL_REMAP.items():
             f.write("    case OP_%s: return %d;   // via %s\n" % (op, names.index(to), to))
         f.write("    default: return 0;\n  }\n}\n")
-    print("tc: %d slots, %d bytes per bank" % (nslots, bank_bytes), file=sys.stderr)
+    print("tc: %d slots, %d bytes per bank" % (nslots, nslots * SLOT), file=sys.stderr)
 
 
 if __name__ == "__main__":

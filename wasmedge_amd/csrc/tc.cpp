@@ -22,9 +22,12 @@ static bool is_branch(uint16_t op) {
          (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
 
-std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) {
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe) {
   const uint32_t T = P.total_cells();
-  auto off = [T](uint32_t cell) { return cell < T ? cell * 256u : 0u; };
+  // operand fields: LDS byte offsets (cell * 256) for the LDS-frame blob, cell indices
+  // (= VGPR index past v128) for the V-frame blob
+  const uint32_t unit = vframe ? 1u : 256u;
+  auto off = [T, unit](uint32_t cell) { return cell < T ? cell * unit : 0u; };
   std::vector<TInstr> tc(P.code.size() + 2, TInstr{{0, 0, 0, 0, 0, 0, 0, 0}});
   for (size_t pc = 0; pc < P.code.size(); pc++) {
     const DInstr &I = P.code[pc];
@@ -74,8 +77,8 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     if (op == OP_CALL || op == OP_RET || op == OP_POST_CALL) {   // gen_tc.py call handlers
       const uint32_t fb = P.global_cells;
       if (a >= T || fb >= T) continue;
-      w[1] = a * 256u;
-      w[2] = fb * 256u;
+      w[1] = a * unit;
+      w[2] = fb * unit;
       w[3] = b;                                   // RET / POST_CALL: result cells
       w[4] = 0; w[5] = 0; w[7] = 0;
       if (op == OP_CALL) {
@@ -105,7 +108,7 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code) 
     if (P.brtab[k] < n) target[P.brtab[k]] = 1;
   for (const auto &f : P.funcs)
     if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
-  for (size_t pc = 1; pc < n; pc++) {
+  for (size_t pc = 1; pc < n && !vframe; pc++) {
     const uint16_t op = uint16_t(P.code[pc].w0 & 0x7FFFu), prev = uint16_t(P.code[pc - 1].w0 & 0x7FFFu);
     if (op == OP_I32_ADD3_XROTR_I && prev == OP_I32_ADD_XROTR_I && !target[pc] &&
         tc[pc].w[0] && tc[pc - 1].w[0]) {

@@ -3,7 +3,8 @@
 // One TInstr per DBC instruction (same pc), 32 bytes = one s_load_dwordx8:
 //   w0 handler byte offset within a bank (slot * TC_SLOT_BYTES; 0 = no handler)
 //   w1 a, w2 b, w5 d: LDS byte offsets (cell * 256) of the operands the core reads
-//      ahead for every instruction (always valid cells)
+//      ahead for every instruction (always valid cells); the V-frame blob takes cell
+//      indices instead (w3, w7 cells alike)
 //   w3 c: destination cell offset; compare-and-branch *_I: the sign-extended imm16
 //   w4 immediate / memarg offset; branches: target pc * 32
 //   w6 wasm instructions retired when the instruction falls through
@@ -24,6 +25,7 @@ struct TInstr {
 namespace wb {
 struct Program;
 // Build the TInstr array for P (size = code + 2 padding entries for the core's
-// successor prefetch) and mark DBC_HOT on the device copy `code` of P.code.
-std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code);
+// successor prefetch) and mark DBC_HOT on the device copy `code` of P.code. vframe:
+// fields for the V-frame blob (frame cells in VGPRs; needs total cells <= TC_VF_CELLS).
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe);
 }  // namespace wb
