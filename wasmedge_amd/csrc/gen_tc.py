@@ -91,6 +91,7 @@ def sbank(bank):
 
 VB = 128               # V-frame blob: frame cell i of the lane lives in VGPR v[VB + i]
 VMAX = 128             # cells a V frame can hold (v128..v255)
+SELF = "#self-fetch"   # first line of a V body that fetches its own operands
 
 
 class Gen:
@@ -327,19 +328,29 @@ def specs():
         out = ["v_add_u32_e32 %s, %s, %s" % (R[0], A[0], B[0]),
                "v_xor_b32_e32 %s, %s, %s" % (X[0], D[0], R[0]),
                "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4))]
-        if g.vf:
-            return out + g.vwrites([(g.x(3), [R[0]]), (g.x(5), [R[1]])]) + g.next()
+        if g.vf:   # operands b, d read as indexed sources; d's new value written indexed
+            return [SELF, "s_set_gpr_idx_on %s, gpr_idx(SRC0)" % g.x(1), "v_mov_b32 %s, v%d" % (A[0], VB),
+                    "s_set_gpr_idx_idx %s" % g.x(2), "v_add_u32_e32 %s, v%d, %s" % (R[0], VB, A[0]),
+                    "s_set_gpr_idx_idx %s" % g.x(5), "v_xor_b32_e32 %s, v%d, %s" % (X[0], VB, R[0]),
+                    "s_set_gpr_idx_on %s, gpr_idx(DST)" % g.x(3), "v_mov_b32 v%d, %s" % (VB, R[0]),
+                    "s_set_gpr_idx_idx %s" % g.x(5),
+                    "v_alignbit_b32 v%d, %s, %s, %s" % (VB, X[0], X[0], g.x(4)),
+                    "s_set_gpr_idx_off"] + g.next()
         return out + g.w32() + ["v_add_u32 %s, %s, %s" % (DADDR, g.x(5), FR),
                                 "ds_write_b32 %s, %s" % (DADDR, R[1])] + g.next(pf4=pf4)
 
     def add3_xrotr(g, pre=True):
         """pre: read the 4th cell y here (else the PF4 predecessor read it into Y0)."""
         if g.vf:
-            return g.vread(g.x(7), [Y[0]]) + [
-                "v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0]),
-                "v_xor_b32_e32 %s, %s, %s" % (X[0], Y[0], R[0]),
-                "v_alignbit_b32 %s, %s, %s, %s" % (R[1], X[0], X[0], g.x(4))] + \
-                g.vwrites([(g.x(3), [R[0]]), (g.x(7), [R[1]])]) + g.next()
+            return [SELF, "s_set_gpr_idx_on %s, gpr_idx(SRC0)" % g.x(1), "v_mov_b32 %s, v%d" % (A[0], VB),
+                    "s_set_gpr_idx_idx %s" % g.x(2), "v_mov_b32 %s, v%d" % (B[0], VB),
+                    "s_set_gpr_idx_idx %s" % g.x(5),
+                    "v_add3_u32 %s, v%d, %s, %s" % (R[0], VB, A[0], B[0]),
+                    "s_set_gpr_idx_idx %s" % g.x(7), "v_xor_b32_e32 %s, v%d, %s" % (X[0], VB, R[0]),
+                    "s_set_gpr_idx_on %s, gpr_idx(DST)" % g.x(3), "v_mov_b32 v%d, %s" % (VB, R[0]),
+                    "s_set_gpr_idx_idx %s" % g.x(7),
+                    "v_alignbit_b32 v%d, %s, %s, %s" % (VB, X[0], X[0], g.x(4)),
+                    "s_set_gpr_idx_off"] + g.next()
         out = ["v_add_u32 %s, %s, %s" % (X[1], g.x(7), FR), "ds_read_b32 %s, %s" % (Y[0], X[1])] \
             if pre else []
         out += ["v_add3_u32 %s, %s, %s, %s" % (R[0], A[0], B[0], D[0])] + g.w32()
@@ -767,6 +778,52 @@ SPECIAL_REMAP = {   # DBC op -> (slot op, immediate transform) applied by the tr
 }
 
 
+def vfuse_src(body):
+    """V-frame peephole: the last operand fetched by an index-mode move that only feeds
+    the next instruction's first source is read there directly as an indexed source."""
+    out = list(body)
+    i = 0
+    while i + 3 < len(out):
+        m = re.match(r"v_mov_b32 (v\d+), v%d$" % VB, out[i + 1])
+        if (m and out[i].startswith(("s_set_gpr_idx_idx", "s_set_gpr_idx_on")) and
+                (out[i].startswith("s_set_gpr_idx_idx") or out[i].endswith("gpr_idx(SRC0)")) and
+                out[i + 2] == "s_set_gpr_idx_off"):
+            q = m.group(1)
+            mi = re.match(r"(v_\w+) ([\w\[\]:]+), %s(, .*)?$" % q, out[i + 3])
+            rest = (mi.group(3) or "") if mi else ""
+            if (mi and not mi.group(1).startswith(("v_readfirstlane", "v_mov")) and
+                    not re.search(r"\b%s\b" % q, rest) and "v[" not in rest and
+                    "v[" not in mi.group(2) and
+                    not any(re.search(r"\b%s\b" % q, ln) for ln in out[i + 4:])):
+                out[i + 1:i + 4] = ["%s %s, v%d%s" % (mi.group(1), mi.group(2), VB, rest),
+                                    "s_set_gpr_idx_off"]
+        i += 1
+    return out
+
+
+def vfuse(body):
+    """V-frame peephole: a VALU op computing R0 that is then only moved into an indexed
+    frame cell computes straight into that cell (its sources are plain VGPRs, so DST
+    indexing touches only the result), and an index-off right before an index-on goes."""
+    r0 = R[0]
+    out = list(body)
+    i = 0
+    while i + 3 < len(out):
+        ins = out[i]
+        m = re.match(r"(v_\w+) %s, (.*)$" % r0, ins)
+        if (m and not m.group(1).startswith(("v_cmp", "v_readfirstlane", "v_mov_b32")) and
+                not re.search(r"\b%s\b" % r0, m.group(2)) and "v[" not in m.group(2) and
+                out[i + 1].startswith("s_set_gpr_idx_on") and out[i + 1].endswith("gpr_idx(DST)") and
+                out[i + 2] == "v_mov_b32 v%d, %s" % (VB, r0) and out[i + 3] == "s_set_gpr_idx_off" and
+                not any(re.search(r"\b%s\b|v\[114:115\]" % r0, ln) for ln in out[i + 4:])):
+            out[i:i + 4] = [out[i + 1], "%s v%d, %s" % (m.group(1), VB, m.group(2)), "s_set_gpr_idx_off"]
+            if i and out[i - 1] == "s_set_gpr_idx_off":
+                del out[i - 1]
+                i -= 1
+        i += 1
+    return out
+
+
 def blob(S, names, vf):
     """Assembly lines of one handler blob: LDS frames (vf False, entry wb_tc_entry) or
     V frames (vf True, entry wb_vf_entry)."""
@@ -852,7 +909,14 @@ def blob(S, names, vf):
                     spec = S[si - 1][2]
                     if vf:
                         b = spec(g)
-                        body = g.vprologue(b) + b
+                        if b and b[0] == SELF:   # reads its operands itself
+                            body = b[1:]
+                        else:
+                            body = vfuse_src(vfuse(g.vprologue(b) + b))
+                        # an index-off directly followed by an index-on is redundant
+                        body = [ln for k, ln in enumerate(body) if not (
+                            ln == "s_set_gpr_idx_off" and k + 1 < len(body) and
+                            body[k + 1].startswith("s_set_gpr_idx_on"))]
                     else:
                         body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
                 for ln in body:
