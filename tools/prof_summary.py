@@ -39,7 +39,10 @@ def main():
     C = {}
     for p in ["fetch", "write", "sq1", "sq2"]:
         C.update(counters(os.path.join(d, p, "run_counter_collection.csv")))
-    K, H = "wb_exec_kernel", "wb_mem_hash_kernel"
+    stats0 = {r["Name"] for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv")))}
+    # the interpreter kernel: the V-frame variant when the batch used it
+    K = "wb_exec_vf_kernel" if "wb_exec_vf_kernel" in stats0 else "wb_exec_kernel"
+    H = "wb_mem_hash_kernel"
     hash_bytes = 65536.0 * inst              # C2 instances keep 1 page each
     fetch_factor = hash_bytes / (C[(H, "FETCH_SIZE")] * 1024.0)
     fetch = C[(K, "FETCH_SIZE")] * 1024.0 * fetch_factor

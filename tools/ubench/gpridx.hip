@@ -44,6 +44,18 @@ __global__ void __launch_bounds__(64) kbench(uint64_t *out, uint32_t *chk) {
   T("s_set_gpr_idx_on s20, gpr_idx(SRC0)\n v_mov_b32 v41, v128\n s_set_gpr_idx_mode gpr_idx(DST)\n s_set_gpr_idx_idx s20\n v_mov_b32 v128, v41\n s_set_gpr_idx_off", ::: CL)
   // 10: SRC0 index with the add reading an indexed operand directly: v40 = v[128+i] + v42
   T("s_set_gpr_idx_on s20, gpr_idx(SRC0)\n v_add_u32 v40, v128, v40\n s_set_gpr_idx_off", ::: CL)
+  // 11: 4 independent v_add
+  T("v_add_u32 v40, v40, 1\n v_add_u32 v41, v41, 1\n v_add_u32 v42, v42, 1\n v_add_u32 v130, v130, 1", ::: CL)
+  // 12: 4 independent s_add
+  T("s_add_u32 s20, s20, 1\n s_add_u32 s21, s21, 1\n s_add_u32 s22, s22, 1\n s_add_u32 s24, s24, 1", ::: CL, "s24")
+  // 13: 4 dependent s_add
+  T("s_add_u32 s20, s20, 1\n s_add_u32 s20, s20, 1\n s_add_u32 s20, s20, 1\n s_add_u32 s20, s20, 1", ::: CL)
+  // 14: 4x s_set_gpr_idx_idx
+  T("s_set_gpr_idx_idx s20\n s_set_gpr_idx_idx s21\n s_set_gpr_idx_idx s22\n s_set_gpr_idx_idx s20", ::: CL)
+  // 15: mixed: 2 s_add indep + 2 v_add indep interleaved
+  T("s_add_u32 s20, s20, 1\n v_add_u32 v40, v40, 1\n s_add_u32 s21, s21, 1\n v_add_u32 v41, v41, 1", ::: CL)
+  // 16: s_setpc to next with precomputed target (s_add+s_addc+setpc)
+  T("s_getpc_b64 s[24:25]\n s_add_u32 s24, s24, 12\n s_addc_u32 s25, s25, 0\n s_setpc_b64 s[24:25]\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0", ::: CL, "s24", "s25")
   // correctness: v[128+5] after chains (lane values)
   uint32_t r0, r1;
   asm volatile("s_mov_b32 s20, 5\n v_mov_b32 v133, 11\n v_mov_b32 v135, 31\n s_mov_b32 s21, 7\n"
@@ -61,7 +73,9 @@ int main() {
   hipMalloc(&chk, 64); hipMemset(chk, 0, 64);
   const char *names[] = {"empty", "LDS round trip + add", "LDS 2-op body (2 reads, add, write)",
     "gpr-idx 2-op body", "gpr-idx 2-op body + nops", "idx on/off", "v_add dep", "s_load_x8+wait",
-    "getpc+add+addc+setpc", "gpr-idx mov32 body", "gpr-idx add with indexed src0"};
+    "getpc+add+addc+setpc", "gpr-idx mov32 body", "gpr-idx add with indexed src0",
+    "4 v_add indep", "4 s_add indep", "4 s_add dep", "4 s_set_gpr_idx_idx", "2 s_add+2 v_add indep",
+    "getpc+add+addc+setpc+4 nops"};
   for (int it = 0; it < 3; it++) {
     hipLaunchKernelGGL(kbench, dim3(1), dim3(64), 0, 0, out, chk);
     hipDeviceSynchronize();
@@ -69,7 +83,7 @@ int main() {
   uint64_t h[64]; uint32_t c[4];
   hipMemcpy(h, out, sizeof h, hipMemcpyDeviceToHost);
   hipMemcpy(c, chk, sizeof c, hipMemcpyDeviceToHost);
-  for (int i = 0; i < 11; i++)
+  for (int i = 0; i < 17; i++)
     printf("%2d %-40s %8.2f ticks/rep\n", i, names[i], (double)(h[i] - h[0]) / 64.0);
   printf("check: v[128+5]=%u (want 11) v[128+7]=%u (want 31) v134=%u (want 77)\n", c[0], c[1], c[2]);
   int rate = 0; hipDeviceGetAttribute(&rate, hipDeviceAttributeClockRate, 0);
