@@ -15,6 +15,8 @@
 
 static std::string g_err;
 static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuning aid)
+static uint64_t *g_pchist = nullptr; // optional per-pc dispatch histogram (tuning aid)
+static uint32_t g_pchist_n = 0;
 // Host-import callback of the emulator (the batched library's yield path, run inline):
 // returns 0 and writes the result cells, or an ErrCode that ends the instance.
 typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
@@ -28,6 +30,7 @@ __attribute__((visibility("default"))) const char *wb_emu_last_error() { return 
 
 // Count dispatches per DBC op into h[DBC_NUM_OPS] during later wb_emu_execute calls (NULL: off).
 __attribute__((visibility("default"))) void wb_emu_set_histogram(uint64_t *h) { g_hist = h; }
+__attribute__((visibility("default"))) void wb_emu_set_pc_histogram(uint64_t *h, uint32_t n) { g_pchist = h; g_pchist_n = n; }
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
@@ -134,6 +137,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
         const uint32_t w0 = I.w0, w1 = I.w1, w2 = I.w2, w3 = I.w3;
         const uint32_t op = w0 & 0xFFFFu;
         if (g_hist) g_hist[op]++;
+        if (g_pchist && pcs < g_pchist_n) g_pchist[pcs]++;
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         int32_t add = (int32_t)cnt8;
         uint32_t npc = pcs + 1;

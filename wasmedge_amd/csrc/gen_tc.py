@@ -101,6 +101,8 @@ class Gen:
         self.n = 0
         self.vf = vf                               # frame in VGPRs (GPR-index mode)
         self.pre = "Lvf" if vf else "Ltc"
+        self.stubs = bank                          # whose exit stubs (slot 0) it uses
+        self.glue = False                          # first half of a fused pair
 
     def x(self, k):                                # field k of the current instruction
         return sreg(self.bank, k)
@@ -118,10 +120,10 @@ class Gen:
         return ["s_branch %s" % self.xh()]
 
     def xh(self):     # exit stubs live in slot 0 of every bank (s_branch reaches +-128 KB)
-        return "%s_xh_%s%s" % (self.pre, self.mode, self.bank)
+        return "%s_xh_%s%s" % (self.pre, self.mode, self.stubs)
 
     def xs(self):
-        return "%s_xs_%s%s" % (self.pre, self.mode, self.bank)
+        return "%s_xs_%s%s" % (self.pre, self.mode, self.stubs)
 
     # -- V frames: cells are VGPRs v[VB + cell], addressed through GPR-index mode with
     # the cell index in an SGPR (instruction fields hold cell indices, not LDS offsets).
@@ -175,6 +177,13 @@ class Gen:
                 "s_setpc_b64 %s" % TP]
 
     def next(self, cnt=True, pf4=False):
+        if self.glue:
+            # first half of a fused pair (V blob, converged mode): retire it, make the
+            # second the current instruction (other bank, loaded by the predecessor)
+            # and start loading the one after into this bank
+            return ["s_add_u32 %s, %s, %s" % (CNT, CNT, self.x(6)),
+                    "s_add_u32 %s, %s, 32" % (PCOFF, PCOFF), "s_waitcnt lgkmcnt(0)",
+                    "s_load_dwordx8 %s, %s, %s offset:0x20" % (sbank(self.bank), CODE, PCOFF)]
         """Fall through to the prefetched successor (other bank). pf4: also read the
         successor's 4th operand (field 7) into Y0, its address kept in X1 (only for
         successors the translator gave an *_E handler, see tc.cpp)."""
@@ -769,7 +778,48 @@ def specs():
     add("ST64", ["ST64"], lambda g: mem_check(g, 8) + [
         "global_store_dword %s, %s, off" % (XP, B[0]),
         "global_store_dword %s, %s, off offset:256" % (XP, B[1])] + g.next())
+    # ---- fused pairs (V blob, converged mode): the instruction at pc (a fall-through
+    # op) and the one at pc + 1 in one handler, saving a dispatch. tc.cpp picks the slot
+    # from the two instructions' own slots (tc_pair_slot); each half reads its own
+    # TInstr (pc's in this bank, pc + 1's in the other), so either may exit before its
+    # effect exactly as alone. Elsewhere (LDS blob, diverged mode) the slot runs pc alone.
+    # Pairs: the most frequent fall-through pairs of the BASELINE workloads
+    # (tools/pair_hist.py).
+    body_of = {nm: b for nm, _, b in S if b is not None}
+
+    def pair_spec(fx, fy):
+        def body(g):
+            if not g.vf or g.mode == "D":
+                return fx(g)
+            gx = Gen(g.mode, g.bank, True)
+            gx.glue = True
+            gy = Gen(g.mode, g.other, True)
+            gy.stubs = g.bank          # stay within branch range of this bank's stubs
+            return [SELF] + vproc(gx, fx(gx)) + vproc(gy, fy(gy))
+        return body
+
+    for x, y in PAIRS:
+        S.append(("P_%s__%s" % (x, y), [], pair_spec(body_of[x], body_of[y])))
+        S.append(("P_%s__%s+1" % (x, y), [], None))
     return S
+
+
+# fall-through op (slot name) x, any op y
+PAIRS = [
+    ("I32_ADD3_XROTR_I", "I32_ADD_XROTR_I"), ("I32_ADD_XROTR_I", "I32_ADD3_XROTR_I"),
+    ("LD32", "LD32"), ("I32_XOR", "ST32"), ("ST32", "I32_XOR"), ("I64_SHR_U_I", "I64_XOR"),
+    ("I64_XOR", "CONST64"), ("CONST64", "I64_MUL"), ("I64_MUL", "I64_SHR_U_I"),
+    ("CONST32", "CONST32"), ("CONST64", "I64_ADD"), ("I64_ADD", "MOV64"),
+    ("I32_SUB_I", "LD32"), ("LD32", "BR_GT_S"), ("I32_ADD_I", "LD32"), ("LD32", "BR_LT_S"),
+    ("LD32", "ST32"), ("ST32", "ST32"), ("ST32", "JMP"), ("I32_SHL_I", "I32_XOR"),
+    ("I32_ADD_I", "JMP"), ("I64_LE_U_I", "BR_UNLESS"), ("I64_AND_I", "I32_ADD_I"),
+    ("I32_ADD_I", "CONST32"), ("CONST32", "JMP"), ("I64_SHR_U_I", "I32_ADD_I"),
+    ("I64_MUL_I", "I64_ADD_I"), ("I64_ADD_I", "I64_GT_U"), ("I64_GT_U", "BR_UNLESS"),
+    ("MOV64", "I32_ADD_I"), ("CONST64", "V_SPLAT64"), ("V_F64X2_MUL", "V_F64X2_ADD"),
+    ("I32_SHL_I", "I32_ADD"), ("V_F64X2_MUL", "V_F64X2_MUL"), ("V_F64X2_ADD", "CONST64"),
+    ("V_SPLAT64", "V_F64X2_LE"), ("V_F64X2_LE", "V_ANY_TRUE"), ("V_ANY_TRUE", "BR_UNLESS"),
+    ("V_I64X2_SUB", "V_F64X2_MUL"), ("V_F64X2_MUL", "CONST64"), ("V_SPLAT64", "V_F64X2_MUL"),
+]
 
 
 SPECIAL_REMAP = {   # DBC op -> (slot op, immediate transform) applied by the translator
@@ -799,6 +849,17 @@ def vfuse_src(body):
                                     "s_set_gpr_idx_off"]
         i += 1
     return out
+
+
+def vproc(g, b):
+    """V-blob processing of one handler body: operand prologue and peepholes."""
+    if b and b[0] == SELF:   # reads its operands itself
+        body = b[1:]
+    else:
+        body = vfuse_src(vfuse(g.vprologue(b) + b))
+    # an index-off directly followed by an index-on is redundant
+    return [ln for k, ln in enumerate(body) if not (
+        ln == "s_set_gpr_idx_off" and k + 1 < len(body) and body[k + 1].startswith("s_set_gpr_idx_on"))]
 
 
 def vfuse(body):
@@ -908,15 +969,7 @@ def blob(S, names, vf):
                 else:
                     spec = S[si - 1][2]
                     if vf:
-                        b = spec(g)
-                        if b and b[0] == SELF:   # reads its operands itself
-                            body = b[1:]
-                        else:
-                            body = vfuse_src(vfuse(g.vprologue(b) + b))
-                        # an index-off directly followed by an index-on is redundant
-                        body = [ln for k, ln in enumerate(body) if not (
-                            ln == "s_set_gpr_idx_off" and k + 1 < len(body) and
-                            body[k + 1].startswith("s_set_gpr_idx_on"))]
+                        body = vproc(g, spec(g))
                     else:
                         body = ["s_waitcnt lgkmcnt(0)"] + spec(g)
                 for ln in body:
@@ -963,6 +1016,13 @@ def main():
         for op, (to, _) in SPECIAL_REMAP.items():
             f.write("    case OP_%s: return %d;   // via %s\n" % (op, names.index(to), to))
         f.write("    default: return 0;\n  }\n}\n")
+        f.write("\n// fused pair handler for (slot at pc, slot at pc + 1), 0 = none (V blob)\n")
+        f.write("static inline int tc_pair_slot(int x, int y) {\n")
+        for si, (nm, ops, body) in enumerate(S, start=1):
+            if nm.startswith("P_") and body is not None:
+                x, y = nm[2:].split("__")
+                f.write("  if (x == TC_SLOT_%s && y == TC_SLOT_%s) return %d;\n" % (x, y, si))
+        f.write("  return 0;\n}\n")
     print("tc: %d slots, %d bytes per bank" % (nslots, nslots * SLOT), file=sys.stderr)
 
 
