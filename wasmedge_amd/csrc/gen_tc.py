@@ -787,25 +787,32 @@ def specs():
     # (tools/pair_hist.py).
     body_of = {nm: b for nm, _, b in S if b is not None}
 
-    def pair_spec(fx, fy):
+    def tuple_spec(fs):
         def body(g):
             if not g.vf or g.mode == "D":
-                return fx(g)
-            gx = Gen(g.mode, g.bank, True)
-            gx.glue = True
-            gy = Gen(g.mode, g.other, True)
-            gy.stubs = g.bank          # stay within branch range of this bank's stubs
-            return [SELF] + vproc(gx, fx(gx)) + vproc(gy, fy(gy))
+                return fs[0](g)
+            out, bank = [SELF], g.bank
+            for k, f in enumerate(fs):
+                gk = Gen(g.mode, bank, True)
+                gk.glue = k + 1 < len(fs)   # all but the last hand over to the next
+                gk.stubs = g.bank           # stay within branch range of this bank's stubs
+                out += vproc(gk, f(gk))
+                bank = gk.other
+            return out
         return body
 
-    for x, y in PAIRS:
-        S.append(("P_%s__%s" % (x, y), [], pair_spec(body_of[x], body_of[y])))
-        S.append(("P_%s__%s+1" % (x, y), [], None))
+    for tup in TUPLES:
+        nm = "P_" + "__".join(tup)
+        S.append((nm, [], tuple_spec([body_of[x] for x in tup])))
+        for k in range(1, max(2, len(tup))):
+            S.append(("%s+%d" % (nm, k), [], None))
     return S
 
 
-# fall-through op (slot name) x, any op y
-PAIRS = [
+# fused tuples: every op but the last falls through; longest match first (tc.cpp)
+ARX = ("I32_ADD3_XROTR_I", "I32_ADD_XROTR_I")
+TUPLES = [ARX * 4, ARX[::-1] * 4, ARX * 2, ARX[::-1] * 2]
+TUPLES_PAIRS = [
     ("I32_ADD3_XROTR_I", "I32_ADD_XROTR_I"), ("I32_ADD_XROTR_I", "I32_ADD3_XROTR_I"),
     ("LD32", "LD32"), ("I32_XOR", "ST32"), ("ST32", "I32_XOR"), ("I64_SHR_U_I", "I64_XOR"),
     ("I64_XOR", "CONST64"), ("CONST64", "I64_MUL"), ("I64_MUL", "I64_SHR_U_I"),
@@ -820,6 +827,7 @@ PAIRS = [
     ("V_SPLAT64", "V_F64X2_LE"), ("V_F64X2_LE", "V_ANY_TRUE"), ("V_ANY_TRUE", "BR_UNLESS"),
     ("V_I64X2_SUB", "V_F64X2_MUL"), ("V_F64X2_MUL", "CONST64"), ("V_SPLAT64", "V_F64X2_MUL"),
 ]
+TUPLES += TUPLES_PAIRS
 
 
 SPECIAL_REMAP = {   # DBC op -> (slot op, immediate transform) applied by the translator
@@ -1016,12 +1024,14 @@ def main():
         for op, (to, _) in SPECIAL_REMAP.items():
             f.write("    case OP_%s: return %d;   // via %s\n" % (op, names.index(to), to))
         f.write("    default: return 0;\n  }\n}\n")
-        f.write("\n// fused pair handler for (slot at pc, slot at pc + 1), 0 = none (V blob)\n")
-        f.write("static inline int tc_pair_slot(int x, int y) {\n")
-        for si, (nm, ops, body) in enumerate(S, start=1):
-            if nm.startswith("P_") and body is not None:
-                x, y = nm[2:].split("__")
-                f.write("  if (x == TC_SLOT_%s && y == TC_SLOT_%s) return %d;\n" % (x, y, si))
+        f.write("\n// fused tuple handler for the slots s[0..n) at pc.., longest first; *len = how\n"
+                "// many instructions it covers; 0 = none (V blob)\n")
+        f.write("static inline int tc_tuple_slot(const int *s, int n, int *len) {\n")
+        tups = sorted([(nm[2:].split("__"), si) for si, (nm, ops, body) in enumerate(S, start=1)
+                       if nm.startswith("P_") and body is not None], key=lambda t: -len(t[0]))
+        for ops_, si in tups:
+            cond = " && ".join("s[%d] == TC_SLOT_%s" % (k, o) for k, o in enumerate(ops_))
+            f.write("  if (n >= %d && %s) { *len = %d; return %d; }\n" % (len(ops_), cond, len(ops_), si))
         f.write("  return 0;\n}\n")
     print("tc: %d slots, %d bytes per bank" % (nslots, nslots * SLOT), file=sys.stderr)
 

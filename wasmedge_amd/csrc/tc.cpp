@@ -110,9 +110,16 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
     if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
   // V blob: fused pair handlers (gen_tc.py PAIRS) for an instruction and the one after
   // it; the instruction at pc + 1 keeps its own handler for jumps and resumes
-  for (size_t pc = 0; vframe && pc + 1 < n; pc++) {
-    const int ps = tc_pair_slot(int(tc[pc].w[0] / TC_SLOT_BYTES), int(tc[pc + 1].w[0] / TC_SLOT_BYTES));
-    if (tc[pc].w[0] && tc[pc + 1].w[0] && ps) tc[pc].w[0] = uint32_t(ps) * TC_SLOT_BYTES;
+  if (vframe) {
+    std::vector<int> sl(n);
+    for (size_t pc = 0; pc < n; pc++) sl[pc] = int(tc[pc].w[0] / TC_SLOT_BYTES);
+    for (size_t pc = 0; pc < n; pc++) {
+      size_t m = 0;   // handled instructions from pc on (a tuple only covers those)
+      while (pc + m < n && m < 8 && sl[pc + m]) m++;
+      int len = 0;
+      const int ps = m >= 2 ? tc_tuple_slot(&sl[pc], int(m), &len) : 0;
+      if (ps) tc[pc].w[0] = uint32_t(ps) * TC_SLOT_BYTES;
+    }
   }
   for (size_t pc = 1; pc < n && !vframe; pc++) {
     const uint16_t op = uint16_t(P.code[pc].w0 & 0x7FFFu), prev = uint16_t(P.code[pc - 1].w0 & 0x7FFFu);
