@@ -113,38 +113,44 @@ def shard_ids(rank, n):
     return np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
 
 
-def cpu_baseline(wasm, iters, budget_s, threads, gpu):
+def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     """The oracle (C restatement of the reference interpreter, oracle/) timed on the
-    box's host cores over a bounded sample of the same workload: chunks of C2 instances
-    (ids 0, 1, 2, ...) until about `budget_s` seconds of CPU work or n_max instances."""
+    box's host cores over a bounded sample of the same workload: chunks of instances
+    (ids 0, 1, 2, ...) until about `budget_s` seconds of CPU work or every instance.
+    The oracle is the checker here too: the GPU's final state for the same instances
+    must match bit for bit (status, return value, count, memory hash). Returns the
+    baseline record and the sample's linear-memory bytes per wasm instruction."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     m = oracle_py.Module(wasm)
-    chunk = 64 * threads
     n_max = len(gpu["counts"])
-    done, instrs, secs = 0, 0.0, 0.0
+    # chunks of about budget_s / 4 at the oracle's ~2e8 instr/s per thread
+    t_inst = float(gpu["counts"].mean()) / 2e8
+    chunk = int(max(threads, min(64 * threads, threads * budget_s / 4 / max(t_inst, 1e-9))))
+    done, instrs, secs, mbytes = 0, 0.0, 0.0, 0.0
+    rmask = 0xFFFFFFFF if gpu["ret32"] else 0xFFFFFFFFFFFFFFFF
     while secs < budget_s and done < n_max:
         k = min(chunk, n_max - done)
-        params = np.zeros((k, 2, 2), np.uint64)
-        params[:, 0, 0] = np.arange(done, done + k, dtype=np.uint64)
-        params[:, 1, 0] = iters
-        out = m.run_batch("run", params, k, threads=threads)
-        if int((out["codes"] != 0).sum()):
-            raise SystemExit("oracle C2 sample trapped")
-        # the oracle is the checker here too: the GPU's final state for the same
-        # instances must match bit for bit (return value, count, memory hash)
+        ids = np.arange(done, done + k, dtype=np.int64)
+        rows = build_rows(ids)
+        params = np.zeros((k, len(ptypes), 2), np.uint64)
+        params[:, :, 0] = rows.astype(np.uint64)
+        out = m.run_batch(func, params, k, threads=threads)
         lo = slice(done, done + k)
-        if not (np.array_equal(out["counts"], gpu["counts"][lo])
+        if not (np.array_equal(out["codes"], gpu["status"][lo])
+                and np.array_equal(out["counts"], gpu["counts"][lo])
                 and np.array_equal(out["hashes"], gpu["hashes"][lo])
-                and np.array_equal(out["results"][:, 0, 0] & 0xFFFFFFFF, gpu["ret"][lo])):
-            raise SystemExit("GPU/oracle mismatch in C2 instances [%d, %d)" % (done, done + k))
+                and np.array_equal((out["results"][:, 0, 0] & rmask)[out["codes"] == 0],
+                                   (gpu["ret"][lo] & rmask)[out["codes"] == 0])):
+            raise SystemExit("GPU/oracle mismatch in instances [%d, %d)" % (done, done + k))
         instrs += float(out["counts"].sum())
+        mbytes += float(out["mem_bytes"].sum())
         secs += out["seconds"]
         done += k
-    return {"value": instrs / secs, "unit": "instr/s", "cores": threads, "kind": "port",
-            "sample": "%d C2 instances x %d compressions (%.3g instrs) in %.2fs on %d threads;"
-                      " bit-exact vs the GPU run on those instances" % (done, iters, instrs,
-                                                                        secs, threads)}
+    return ({"value": instrs / secs, "unit": "instr/s", "cores": threads, "kind": "port",
+             "sample": "%d %s instances (%.3g instrs) in %.2fs on %d threads; bit-exact vs "
+                       "the GPU run on those instances" % (done, what, instrs, secs, threads)},
+            mbytes / instrs)
 
 
 def load_profile_traffic():
@@ -208,7 +214,8 @@ def main():
     # the timed region)
     hashes = ctx.memory_hash()
     checksum = int(hashes.sum(dtype=np.uint64))
-    gpu = {"counts": cnt, "hashes": hashes, "ret": rets["lo"][:, 0] & 0xFFFFFFFF}
+    gpu = {"counts": cnt, "hashes": hashes, "status": st, "ret": rets["lo"][:, 0],
+           "ret32": args.workload != "c5"}
     kernel_avg = ksum / args.steps
     out = {
         "metric": METRIC,
@@ -245,9 +252,20 @@ def main():
                                  "dispatch_bound": "see DESIGN.md 'Roofline'"}
     else:
         out["data"] = "synthetic: per-instance inputs derived from the instance id"
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline and args.workload == "c2":
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(wasm, args.iters, args.cpu_seconds, threads, gpu)
+        out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
+                                                threads, gpu, args.workload.upper())
+        if args.workload == "c3":
+            # algorithmic bytes: the linear-memory bytes the wasm program moves, counted
+            # per instance by the oracle on the sample, per instruction x this launch's
+            # instructions (qsort's bytes per instruction is stable across instances)
+            bytes_launch = bpi * instrs_per_step
+            achieved = bytes_launch / kernel_avg / 1e9
+            out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                               "note": "algorithmic = linear-memory bytes of the wasm loads and "
+                                       "stores (%.3f B per wasm instr on the oracle sample)" % bpi}
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

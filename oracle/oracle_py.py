@@ -58,6 +58,9 @@ def lib():
         L.om_run_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.om_run_batch_mb.restype = ctypes.c_double
+        L.om_run_batch_mb.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + \
+            [ctypes.c_void_p] * 6 + [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -157,10 +160,12 @@ class Module:
         codes = np.zeros(n, dtype=np.uint8)
         counts = np.zeros(n, dtype=np.uint64)
         hashes = np.zeros(n, dtype=np.uint64)
-        secs = L.om_run_batch(self._h, idx, n, params.ctypes.data, results.ctypes.data,
-                              codes.ctypes.data, counts.ctypes.data, hashes.ctypes.data, threads)
+        mem_bytes = np.zeros(n, dtype=np.uint64)
+        secs = L.om_run_batch_mb(self._h, idx, n, params.ctypes.data, results.ctypes.data,
+                                 codes.ctypes.data, counts.ctypes.data, hashes.ctypes.data,
+                                 mem_bytes.ctypes.data, threads)
         return {"results": results[:, :len(rt), :], "codes": codes, "counts": counts,
-                "hashes": hashes, "seconds": secs}
+                "hashes": hashes, "mem_bytes": mem_bytes, "seconds": secs}
 
 
 class Instance:

@@ -108,6 +108,8 @@ struct OInst {
   uint64_t count;
   int terminated;                   /* the last invoke ended in Terminated (proc_exit) */
   uint64_t cost_limit;              /* unit-cost gas limit per invocation (statistics.h) */
+  uint64_t mem_bytes;               /* linear-memory bytes the last invoke accessed (not
+                                       in the reference: the roofline's algorithmic bytes) */
 };
 
 /* ------------------------------------------------------------------ reader */

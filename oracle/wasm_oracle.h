@@ -70,6 +70,11 @@ uint64_t om_hash_bytes(const uint8_t *data, uint64_t nbytes, uint32_t pages);
 double om_run_batch(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
                     uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
                     int threads);
+/* om_run_batch plus mem_bytes[n]: linear-memory bytes each invocation accessed (loads,
+   stores, bulk-op operands), the C3 roofline's algorithmic bytes */
+double om_run_batch_mb(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
+                       uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
+                       uint64_t *mem_bytes, int threads);
 
 #ifdef __cplusplus
 }

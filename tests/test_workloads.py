@@ -101,3 +101,20 @@ def test_gpu_blake3_64k(built):
     idx = list(range(0, 4096, 97))
     assert compare(ref, [rets[i] for i in idx], [st[i] for i in idx], [cnt[i] for i in idx],
                    [h[i] for i in idx], [I32]) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["0", "1", "4"])
+def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
+    """The wave scheduler only decides which lanes run together: min-pc (0) and the
+    loop-aware largest-group policy (1, 4) must give identical per-lane results on the
+    divergent workloads (quicksort with per-lane data, Collatz with traps)."""
+    monkeypatch.setenv("WB_SCHED", sched)
+    cases = _cases()
+    wasm, func, pt, rt, _ = cases["qsort"]
+    cases["qsort"] = (wasm, func, pt, rt, [[i, (i * 37) % 700] for i in range(192)])
+    for name in ("qsort", "collatz"):
+        wasm, func, pt, rt, rows = cases[name]
+        ref = oracle_run(O.Module(wasm), func, rows)
+        rets, st, cnt, h = gpu_run(wasm, func, rows, pt, rt)
+        assert compare(ref, rets, st, cnt, h, rt) == [], name

@@ -86,6 +86,8 @@ struct WasmEdge_BatchContext {
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
   bool threaded = true;
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
+  uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
+  DevBuf<uint32_t> loops;         // Program::loops (scheduler)
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
   DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
   DevBuf<DFunc> funcs;
@@ -187,6 +189,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // allow no more; beyond that the LDS kernel's occupancy wins: C5 at 256K instances
   // 7.2e11 vs 6.2e11). WB_VFRAME=0 / 1 forces LDS / V frames (A/B measurement aid).
   const char *vfe = getenv("WB_VFRAME");
+  const char *sce = getenv("WB_SCHED");
+  C->sched = sce ? (uint32_t)atoi(sce) : 1u;
   const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
   C->vframe = vf_fit && (vfe ? vfe[0] == '1' : C->nwaves <= 2 * 1024);
   if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);
@@ -197,7 +201,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     for (const auto &t : P.tables) ls_init.push_back(t.min);
     ls_init.push_back(P.init_edropped);
   }
-  bool ok = C->code.upload(codepad, s) && (!C->threaded || C->tcode.upload(tcv, s)) && C->brtab.upload(P.brtab, s) &&
+  bool ok = C->code.upload(codepad, s) && C->loops.upload(P.loops, s) && (!C->threaded || C->tcode.upload(tcv, s)) && C->brtab.upload(P.brtab, s) &&
             C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
             C->global_init.upload(ls_init, s) && C->image.upload(img, s) &&
             C->tab_image.upload(P.tab_image, s) && C->tabinfo.upload(P.tabinfo, s) &&
@@ -313,6 +317,8 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.max_steps = C->conf.MaxSteps ? C->conf.MaxSteps : (1ull << 62);
   double tl = C->conf.TimeLimitSeconds > 0 ? C->conf.TimeLimitSeconds : 600.0;
   k.max_ticks = uint64_t(tl * 1e8);
+  k.sched = C->sched;
+  k.loops = C->loops.ptr;
   k.stats = C->stats;
 #ifdef WB_STATS
   (void)hipMemsetAsync(C->stats, 0, size_t(C->nwaves) * 14 * sizeof(uint64_t), C->stream);

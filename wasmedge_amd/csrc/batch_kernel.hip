@@ -9,8 +9,9 @@
 //  * wave-coherent dispatch: the wave fetches ONE 16-byte DBC instruction per step with
 //    a scalar load (uniform pc), and executes it for the lanes whose pc matches.  When
 //    all running lanes share a pc (the common, converged case) that costs one readlane +
-//    one ballot; after divergence the wave picks the minimum pc over running lanes, which
-//    reconverges structured control flow (join points sit at higher pcs than both arms).
+//    one ballot; after divergence the wave runs the largest group of lanes sharing a pc,
+//    which stops where it meets waiting lanes so they merge (KParams::sched = 0: the
+//    minimum pc, which reconverges structured control flow at join points).
 //  * frames: the CURRENT frame of every lane (globals + params + locals + operand cells)
 //    lives in LDS, cell-major / lane-minor, so a cell access is one conflict-free
 //    ds_read_b32/ds_write_b32 for the whole wave.  call spills the caller's live cells
@@ -41,7 +42,7 @@ extern "C" __global__ void wb_tc_holder_kernel() {
                ::: "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
                "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
                "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
-               "s92", "s93", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
+               "s92", "s93", "s94", "s95", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
                "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
                "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
 }
@@ -52,7 +53,7 @@ extern "C" __global__ void __launch_bounds__(256) wb_vf_holder_kernel() {
                ::: "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
                "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
                "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
-               "s92", "s93", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
+               "s92", "s93", "s94", "s95", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",
                "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
                "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
 }
@@ -135,6 +136,7 @@ struct LdsFrame {
       "v_mov_b32 v103, %[stk]\n\t" \
       "s_mov_b32 s93, %[slds]\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
+      "s_mov_b32 s95, %[low]\n\t" \
       "s_getpc_b64 s[66:67]\n" \
       "Ltc_ret_%=:\n\t" \
       "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t" \
@@ -151,10 +153,10 @@ struct LdsFrame {
       : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp) \
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), \
-        [slds] "s"(slds), [vsync] "s"(vsync) \
+        [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
-        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", \
+        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
         "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
@@ -173,12 +175,13 @@ struct LdsFrame {
   "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", \
   "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255"
 template <bool VF>
-__device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other,
+__device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other, uint32_t low,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem,
                                            uint32_t &gsp, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
   const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
+  const uint32_t lw = __builtin_amdgcn_readfirstlane(low >= (1u << 26) ? 0xFFFFFFFFu : low << 5);
   const uint64_t m = (uint64_t)(uintptr_t)mem;
   const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
   const uint64_t cp = (uint64_t)(uintptr_t)tcode;   // as two words: no aligned pair needed
@@ -275,21 +278,47 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   const uint32_t stk_lds = (uint32_t)(uintptr_t)stk;   // its call-stack slot 0
 
   for (;;) {
-    // ---- schedule: the lanes at the minimum pc run next (structured control flow puts
-    // join points above both arms, so min-pc scheduling reconverges divergent lanes);
-    // `other` = the lowest pc of the lanes left waiting.
+    // ---- schedule: which group of lanes (same pc) runs next; `other` = the lowest pc
+    // of the waiting lanes above it, `low` = the lowest pc of all waiting lanes.
     const uint64_t runmask = __ballot(status == WB_STATUS_RUNNING);
     if (!runmask) break;
     [[maybe_unused]] const uint64_t ts0 = WB_NOW();
     WB_STAT_ADD(ST_ROUNDS, 1);
     uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(runmask));
     uint64_t act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
-    uint32_t other = 0xFFFFFFFFu;
+    uint32_t other = 0xFFFFFFFFu, low = 0xFFFFFFFFu;
     if (act != runmask) {
+      // the lowest pc first: structured control flow puts join points above both arms,
+      // so min-pc scheduling reconverges divergent lanes. But a loop at a low pc then
+      // holds every lane waiting past its exit until the loop's slowest lane leaves:
+      // the nested scan loops of a Hoare partition ran 3.5 lanes per dispatch. So when
+      // the min-pc lanes are in a loop, the largest group waiting outside that loop runs
+      // instead if it has >= sched x their lanes; those lanes come back round (outer
+      // loop, recursion) and merge (tools/sched_study.py: C3 3.5 -> 14.3 lanes per
+      // dispatch; groups inside the loop, e.g. the arms of a state machine, keep
+      // min-pc order). A group stops at the next waiting pc above it (`other`), and
+      // after a jump to or below the lowest waiting pc (`low`) at that one.
       pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
       act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
-      if (act != runmask)
-        other = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
+      bool moved = false;
+      if (p.sched) {
+        typedef __attribute__((address_space(4))) const uint32_t *cu32;
+        const uint32_t lh = ((cu32)p.loops)[2 * pcs], le = ((cu32)p.loops)[2 * pcs + 1];
+        const uint32_t nmin = (uint32_t)__builtin_popcountll(act);
+        uint32_t need = nmin * p.sched > nmin ? nmin * p.sched : nmin + 1;
+        uint64_t rem = lh == 0xFFFFFFFFu ? 0 : __ballot(status == WB_STATUS_RUNNING && pc > le);
+        while (rem && (uint32_t)__builtin_popcountll(rem) >= need) {
+          const uint32_t q = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(rem));
+          const uint64_t m = __ballot(status == WB_STATUS_RUNNING && pc == q);
+          const uint32_t k = (uint32_t)__builtin_popcountll(m);
+          if (k >= need) { need = k + 1; pcs = q; act = m; moved = true; }
+          rem &= ~m;
+        }
+      }
+      if (act != runmask) {
+        low = wave_min_u32(status == WB_STATUS_RUNNING && pc != pcs ? pc : 0xFFFFFFFFu);
+        other = moved ? wave_min_u32(status == WB_STATUS_RUNNING && pc > pcs ? pc : 0xFFFFFFFFu) : low;
+      }
     }
     bool slow = false;   // the run stopped at an instruction that needs the slow step
     [[maybe_unused]] const uint64_t ts1 = WB_NOW();
@@ -338,7 +367,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
-          pcs = tc_run<VF>(p.tcode, pcs, other, fr_lds, pages, mem, gsp, stk_lds, S_lds,
+          pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem, gsp, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
@@ -377,6 +406,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       k_jump:
         // every 1024 taken jumps (and before the SGPR count could overflow) the run
         // returns to the scheduler, which flushes counts and checks the limits
+        if (pcs <= low) other = low;   // jumped back below every waiting lane
         if (--tick == 0 || (int32_t)sc < 0 || pcs >= other) goto k_leave;
         I = code[pcs];
         continue;

@@ -17,6 +17,8 @@ static std::string g_err;
 static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuning aid)
 static uint64_t *g_pchist = nullptr; // optional per-pc dispatch histogram (tuning aid)
 static uint32_t g_pchist_n = 0;
+static uint32_t *g_trace = nullptr;  // optional per-lane dispatch pc trace (scheduler studies)
+static uint64_t g_trace_cap = 0, g_trace_len = 0, *g_trace_lens = nullptr;
 // Host-import callback of the emulator (the batched library's yield path, run inline):
 // returns 0 and writes the result cells, or an ErrCode that ends the instance.
 typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
@@ -31,6 +33,12 @@ __attribute__((visibility("default"))) const char *wb_emu_last_error() { return 
 // Count dispatches per DBC op into h[DBC_NUM_OPS] during later wb_emu_execute calls (NULL: off).
 __attribute__((visibility("default"))) void wb_emu_set_histogram(uint64_t *h) { g_hist = h; }
 __attribute__((visibility("default"))) void wb_emu_set_pc_histogram(uint64_t *h, uint32_t n) { g_pchist = h; g_pchist_n = n; }
+// Record every dispatched pc into buf[cap], lane after lane; lens[inst] = its entry count
+// (NULL: off). Lanes run independently, so a lane's pc sequence does not depend on how a
+// wave schedules its lanes: tools/sched_sim.c replays these traces under scheduler policies.
+__attribute__((visibility("default"))) void wb_emu_set_pc_trace(uint32_t *buf, uint64_t cap, uint64_t *lens) {
+  g_trace = buf; g_trace_cap = cap; g_trace_len = 0; g_trace_lens = lens;
+}
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
@@ -138,6 +146,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
         const uint32_t op = w0 & 0xFFFFu;
         if (g_hist) g_hist[op]++;
         if (g_pchist && pcs < g_pchist_n) g_pchist[pcs]++;
+        if (g_trace && g_trace_len < g_trace_cap) { g_trace[g_trace_len++] = pcs; g_trace_lens[inst]++; }
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         int32_t add = (int32_t)cnt8;
         uint32_t npc = pcs + 1;

@@ -1393,6 +1393,33 @@ static bool is_pc_branch(uint16_t op) {
          op == OP_BR_IF_MOV2 || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
 
+// The innermost loop around every pc, for the kernel's scheduler (KParams::loops): every
+// backward branch (pc -> t <= pc, br_table entries included) closes a loop [t, pc]; the
+// innermost one around x is the shortest such span that contains x.
+void find_loops(Program &P) {
+  const uint32_t n = uint32_t(P.code.size());
+  std::vector<std::pair<uint32_t, uint32_t>> spans;
+  for (uint32_t pc = 0; pc < n; pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = I.w0 & 0x7FFF;
+    if (is_pc_branch(op) && I.w3 <= pc) spans.push_back({I.w3, pc});
+    if (op == OP_BR_TABLE) {
+      const uint32_t labels = (I.w1 >> 16) & 0xFFFFu;   // B_: entries [imm, imm + B_]
+      for (uint32_t k = 0; k <= labels && 2 * (I.w3 + k) < P.brtab.size(); k++)
+        if (P.brtab[2 * (I.w3 + k)] <= pc) spans.push_back({P.brtab[2 * (I.w3 + k)], pc});
+    }
+  }
+  P.loops.assign(2 * size_t(n) + 2, 0xFFFFFFFFu);
+  std::vector<uint32_t> len(n + 1, 0xFFFFFFFFu);
+  for (const auto &sp : spans)
+    for (uint32_t x = sp.first; x <= sp.second; x++)
+      if (sp.second - sp.first < len[x]) {
+        len[x] = sp.second - sp.first;
+        P.loops[2 * x] = sp.first;
+        P.loops[2 * x + 1] = sp.second;
+      }
+}
+
 void fuse_arx(Program &P) {
   const size_t n = P.code.size();
   std::vector<uint8_t> target(n + 1, 0);
@@ -1721,6 +1748,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
     }
   }
   fuse_arx(P);
+  find_loops(P);
   if (P.code.size() >= DBC_MAX_PC) throw Err{E_UNSUPPORTED, "module too large for 20-bit pcs"};
 }
 

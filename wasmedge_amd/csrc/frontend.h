@@ -97,6 +97,8 @@ struct Program {
   // lowered code
   std::vector<DInstr> code;
   std::vector<uint32_t> brtab;         // pairs (target pc, tcnt as int32)
+  std::vector<uint32_t> loops;         // per pc: (head, end) of the innermost loop around
+                                       // it (a backward branch end -> head), ~0 if none
   std::vector<uint32_t> vconst;        // v128 pool, 4 words per entry
   uint32_t frame_cells = 0;            // max over functions (excluding globals)
   uint32_t total_cells() const { return global_cells + frame_cells; }

@@ -69,6 +69,7 @@ GSP = "v102"          # this lane's call-stack depth (slots), in/out
 SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
 SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
 VSYNC = "s94"         # V frames: (VMAX - frame cells) * 8, the frame-sync jump offset
+LOW = "s95"           # lowest waiting pc * 32 (<= OTHER; a jump to or below it re-aims OTHER)
 
 
 def sreg(bank, k):
@@ -213,7 +214,10 @@ class Gen:
                "s_add_u32 %s, %s, %s" % (CNT, CNT, cnt),
                "s_cmp_ge_u32 %s, %s" % (CNT, LIM), "s_cbranch_scc1 %s" % self.xs()]
         if self.mode == "D":
-            out += ["s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
+            # a jump back to or below every waiting lane next meets the lowest of them
+            out += ["s_cmp_le_u32 %s, %s" % (PCOFF, LOW),
+                    "s_cselect_b32 %s, %s, %s" % (OTHER, LOW, OTHER),
+                    "s_cmp_ge_u32 %s, %s" % (PCOFF, OTHER), "s_cbranch_scc1 %s" % self.xs()]
         # the successor prefetch into the other bank must have landed before both banks
         # are reloaded (SMEM returns out of order: a late stale load would win). The LDS
         # blob waited at handler entry; the V-frame blob waits here.
@@ -904,14 +908,14 @@ def blob(S, names, vf):
     e(".text")
     e(".p2align 8")
     # ------------------------------------------------------------- entry
-    # in: CODE, PCOFF (pc*32 of the first instruction), OTHER, LIM, CNT=0, RET,
+    # in: CODE, PCOFF (pc*32 of the first instruction), OTHER, LOW, LIM, CNT=0, RET,
     #     FR, PAGES, MEM (V frames also VSYNC).  EXEC = the active lanes.
     e("%s:" % ("wb_vf_entry" if vf else "wb_tc_entry"))
     e("s_getpc_b64 s[70:71]")
     e("%s_pc0:" % pre)
     e("s_add_u32 s70, s70, %s_banks - %s_pc0" % (pre, pre))
     e("s_addc_u32 s71, s71, 0")
-    e("s_cmp_eq_u32 %s, -1" % OTHER)                  # converged: banks 0/1
+    e("s_cmp_eq_u32 %s, -1" % LOW)                    # no lane waiting: banks 0/1
     e("s_cselect_b32 %s, 0, %d" % (T[0], 2 * bank_bytes))
     e("s_add_u32 s70, s70, %s" % T[0])
     e("s_addc_u32 s71, s71, 0")

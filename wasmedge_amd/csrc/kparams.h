@@ -55,6 +55,10 @@ struct KParams {
   uint32_t *stop;               // host-set interrupt request (WasmEdge_BatchInterrupt)
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
   uint64_t *stats;              // WB_STATS builds: per-wave counters (else unused)
+  uint32_t sched;               // diverged waves run the lowest pc's lanes, or the largest
+                                // group outside their innermost loop if it has >= sched x
+                                // as many (0: min pc only)
+  const uint32_t *loops;        // per pc: innermost loop (head, end), ~0 = none
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
