@@ -165,6 +165,12 @@ def load_profile_traffic():
     return None
 
 
+def elapsed_hint(args):
+    """Long steps (full-size C3) report progress on stderr so a run is never silent for
+    minutes; short ones stay quiet inside the timed region."""
+    return args.workload == "c3" and args.elements >= 65536
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,9 +195,15 @@ def main():
     nret = 1
     dist.init()
 
-    for _ in range(args.warmup):
+    def progress(msg):
+        if dist.rank == 0:
+            print("[bench] %s %.1fs" % (msg, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+
+    t_start = time.perf_counter()
+    for w in range(args.warmup):
         ctx.reset()
         ctx.run()
+        progress("warmup %d/%d done" % (w + 1, args.warmup))
     _, st, cnt = ctx.results(nret)
     traps = int((st != 0).sum())
     if traps and args.workload != "c4":
@@ -201,9 +213,11 @@ def main():
     dist.barrier()
     t0 = time.perf_counter()
     ksum = 0.0
-    for _ in range(args.steps):
+    for k in range(args.steps):
         ctx.reset()
         ksum += ctx.run()        # HIP-event time of the interpreter kernel (its stream)
+        if elapsed_hint(args):
+            progress("step %d/%d done" % (k + 1, args.steps))
     elapsed = time.perf_counter() - t0   # BatchRun synchronises its stream
     dist.barrier()
     elapsed = dist.max(elapsed)

@@ -191,6 +191,9 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const char *vfe = getenv("WB_VFRAME");
   const char *sce = getenv("WB_SCHED");
   C->sched = sce ? (uint32_t)atoi(sce) : 1u;
+  // modules without a scan loop keep plain min-pc scheduling (no loop-table lookups)
+  if (std::all_of(P.loops.begin(), P.loops.end(), [](uint32_t v) { return v == 0xFFFFFFFFu; }))
+    C->sched = 0;
   const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
   C->vframe = vf_fit && (vfe ? vfe[0] == '1' : C->nwaves <= 2 * 1024);
   if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);

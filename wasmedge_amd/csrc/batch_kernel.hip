@@ -289,15 +289,17 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     uint32_t other = 0xFFFFFFFFu, low = 0xFFFFFFFFu;
     if (act != runmask) {
       // the lowest pc first: structured control flow puts join points above both arms,
-      // so min-pc scheduling reconverges divergent lanes. But a loop at a low pc then
-      // holds every lane waiting past its exit until the loop's slowest lane leaves:
-      // the nested scan loops of a Hoare partition ran 3.5 lanes per dispatch. So when
-      // the min-pc lanes are in a loop, the largest group waiting outside that loop runs
-      // instead if it has >= sched x their lanes; those lanes come back round (outer
-      // loop, recursion) and merge (tools/sched_study.py: C3 3.5 -> 14.3 lanes per
-      // dispatch; groups inside the loop, e.g. the arms of a state machine, keep
-      // min-pc order). A group stops at the next waiting pc above it (`other`), and
-      // after a jump to or below the lowest waiting pc (`low`) at that one.
+      // so min-pc scheduling reconverges divergent lanes. But a short scan loop at a low
+      // pc (`while (a[i] < p) i++`: data-dependent trip counts) then holds every lane
+      // waiting past its exit until its slowest lane leaves: the scan loops of a Hoare
+      // partition ran 3.5 lanes per dispatch. So when the min-pc lanes are in a scan
+      // loop (the lowering's loop table: innermost loops < 8 instructions), the largest
+      // group waiting past that loop runs instead if it has >= sched x their lanes;
+      // those lanes come back round (outer loop, recursion) and merge
+      // (tools/sched_study.py: C3 3.5 -> 14.3 lanes per dispatch, C4/C5 unchanged;
+      // measured C3 3.9e10 -> 9.1e10 instr/s). A group stops at the next waiting pc
+      // above it (`other`), and after a jump to or below the lowest waiting pc (`low`)
+      // at that one.
       pcs = wave_min_u32(status == WB_STATUS_RUNNING ? pc : 0xFFFFFFFFu);
       act = __ballot(status == WB_STATUS_RUNNING && pc == pcs);
       bool moved = false;

@@ -1393,9 +1393,12 @@ static bool is_pc_branch(uint16_t op) {
          op == OP_BR_IF_MOV2 || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
 
-// The innermost loop around every pc, for the kernel's scheduler (KParams::loops): every
+// Short loops around every pc, for the kernel's scheduler (KParams::loops): every
 // backward branch (pc -> t <= pc, br_table entries included) closes a loop [t, pc]; the
-// innermost one around x is the shortest such span that contains x.
+// innermost one around x is the shortest such span that contains x. Only innermost loops
+// of fewer than kScanLoop instructions are kept: scan loops (`while (a[i] < p) i++`)
+// whose data-dependent trip counts keep the other lanes waiting (see batch_kernel.hip).
+constexpr uint32_t kScanLoop = 8;
 void find_loops(Program &P) {
   const uint32_t n = uint32_t(P.code.size());
   std::vector<std::pair<uint32_t, uint32_t>> spans;
@@ -1418,6 +1421,8 @@ void find_loops(Program &P) {
         P.loops[2 * x] = sp.first;
         P.loops[2 * x + 1] = sp.second;
       }
+  for (uint32_t x = 0; x < n; x++)
+    if (len[x] != 0xFFFFFFFFu && len[x] + 1 >= kScanLoop) P.loops[2 * x] = P.loops[2 * x + 1] = 0xFFFFFFFFu;
 }
 
 void fuse_arx(Program &P) {
