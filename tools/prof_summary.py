@@ -1,6 +1,8 @@
 """Summarise a tools/prof_bench.sh output directory into profiles/.
 
-usage: python tools/prof_summary.py <prof dir> <tag> [iters] [instances]
+usage: python tools/prof_summary.py <prof dir> <tag> [iters] [instances] [pages] [label]
+(pages: linear-memory pages per instance, what wb_mem_hash_kernel reads; label: the
+bench workload, default C2)
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim),
 profiles/<tag>_counters.md (per-kernel PMC means) and profiles/traffic_c2.json
 (HBM bytes per interpreter launch, read by bench.py for roofline.traffic).
@@ -32,6 +34,8 @@ def main():
     d, tag = sys.argv[1], sys.argv[2]
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
     inst = int(sys.argv[4]) if len(sys.argv) > 4 else 65536
+    pages = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    label = sys.argv[6] if len(sys.argv) > 6 else None
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"),
@@ -43,7 +47,7 @@ def main():
     # the interpreter kernel: the V-frame variant when the batch used it
     K = "wb_exec_vf_kernel" if "wb_exec_vf_kernel" in stats0 else "wb_exec_kernel"
     H = "wb_mem_hash_kernel"
-    hash_bytes = 65536.0 * inst              # C2 instances keep 1 page each
+    hash_bytes = 65536.0 * pages * inst      # every instance's pages (C2: 1 page each)
     fetch_factor = hash_bytes / (C[(H, "FETCH_SIZE")] * 1024.0)
     fetch = C[(K, "FETCH_SIZE")] * 1024.0 * fetch_factor
     write = C[(K, "WRITE_SIZE")] * 1024.0
@@ -52,8 +56,8 @@ def main():
     avg_ns = float(stats[K]["AverageNs"])
     waves = C[(K, "SQ_WAVES")]
     smem = C[(K, "SQ_INSTS_SMEM")]
-    lines = ["# %s: rocprofv3 counters, `bench.py --steps 3 --warmup 1` (C2, %d instances x %d"
-             " compressions)" % (tag, inst, iters), "",
+    head = label or ("C2, %d instances x %d compressions" % (inst, iters))
+    lines = ["# %s: rocprofv3 counters, `bench.py` (%s)" % (tag, head), "",
              "Per-kernel means over launches (counter passes run separately, see "
              "tools/prof_bench.sh).", "",
              "| kernel | counter | mean per launch |", "|---|---|---|"]
@@ -82,7 +86,8 @@ def main():
     json.dump({"iters": iters, "instances": inst, "hbm_bytes_per_launch": fetch + write,
                "fetch_bytes": fetch, "write_bytes": write, "fetch_factor": fetch_factor,
                "kernel_avg_ns": avg_ns, "source": tag},
-              open(os.path.join(prof, "traffic_c2.json"), "w"), indent=1)
+              open(os.path.join(prof, "traffic_c2.json" if label is None else
+                                "traffic_%s.json" % tag), "w"), indent=1)
     print("\n".join(lines))
 
 

@@ -59,6 +59,8 @@ void sched_sim(const uint32_t *trace, const uint64_t *off /*[n+1]*/, uint32_t n,
       if (policy == 7 && lhead[minpc] != ~0u && lhead[pcs[best]] != ~0u &&
           cnt[best] >= (uint32_t)arg * cnt[mi] &&
           (pcs[best] > lend[minpc] || pcs[best] < lhead[minpc])) g = best;
+      if (policy == 8 && lhead[minpc] != ~0u && lend[minpc] - lhead[minpc] < (uint32_t)(arg2 >> 8) &&
+          cnt[best] >= (uint32_t)arg * cnt[mi] && pcs[best] > lend[minpc]) g = best;
       if (policy == 5 && lhead[minpc] != ~0u && cnt[best] >= (uint32_t)arg * cnt[mi] &&
           (pcs[best] > lend[minpc] || pcs[best] < lhead[minpc])) g = best;
       /* 4: like 2 (k = arg) but only when the min-pc group has <= arg2 >> 8 lanes */

@@ -31,9 +31,8 @@ def cases(n):
     }
 
 
-POLICIES = [("minpc", 0, 0, 0), ("most+lowmerge", 1, 0, 2), ("k2+lowmerge", 2, 2, 2),
-            ("loop,k1", 5, 1, 2), ("loop,k2", 5, 2, 2), ("loop,k4", 5, 4, 2),
-            ("inloop,k1", 7, 1, 2), ("inloop,k2", 7, 2, 2)]
+POLICIES = [("minpc", 0, 0, 0), ("loop,k1", 5, 1, 2), ("loop,k1,len<8", 8, 1, 2 + (8 << 8)),
+            ("loop,k1,len<16", 8, 1, 2 + (16 << 8)), ("loop,k2,len<8", 8, 2, 2 + (8 << 8))]
 
 
 def loops(wasm):
