@@ -550,6 +550,43 @@ def specs():
                 out.append("s_or_b64 %s, %s, vcc" % (T2, T2))
         return out + ["s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh()]
 
+    nan_labels = [0]
+
+    def nan_fix(g, elems, w):
+        """Exact NaN results in registers instead of leaving the core (the reference's
+        x86 rule, dbc_ops.h nan_fix32/64): per element (r, a, b), a lane whose result is
+        a NaN takes a quieted if a is a NaN, else b quieted if b is, else the default NaN
+        with the sign set. Skipped with one compare + branch when no lane has a NaN.
+        Clobbers the operand registers' high words and D (unused by binary ops)."""
+        out = []
+        hi = (lambda v: v) if w == 32 else (lambda v: "v" + v[2:-1].split(":")[1])
+        lo = (lambda v: v) if w == 32 else (lambda v: "v" + v[2:-1].split(":")[0])
+        q, dflt = ("0x400000", "0xffc00000") if w == 32 else ("0x80000", "0xfff80000")
+        for r, a, b in elems:
+            nan_labels[0] += 1
+            lab = "Lnan_%d" % nan_labels[0]
+            out += ["v_cmp_u_f%d_e64 %s, %s, %s" % (w, T2, r, r),
+                    "s_and_b64 %s, %s, exec" % (T2, T2),
+                    "s_cbranch_scc0 %s" % lab]
+            if w == 64:
+                out += ["v_mov_b32 %s, 0" % D[0]]
+            out += ["v_mov_b32 %s, %s" % (D[1] if w == 64 else D[0], dflt)]
+            for x in (b, a):   # a checked last: it wins
+                out += ["v_cmp_u_f%d_e64 vcc, %s, %s" % (w, x, x),
+                        "v_or_b32_e32 %s, %s, %s" % (hi(x), q, hi(x))]
+                if w == 64:
+                    out += ["v_cndmask_b32_e32 %s, %s, %s, vcc" % (D[0], D[0], lo(x)),
+                            "v_cndmask_b32_e32 %s, %s, %s, vcc" % (D[1], D[1], hi(x))]
+                else:
+                    out += ["v_cndmask_b32_e32 %s, %s, %s, vcc" % (D[0], D[0], x)]
+            if w == 64:
+                out += ["v_cndmask_b32_e64 %s, %s, %s, %s" % (lo(r), lo(r), D[0], T2),
+                        "v_cndmask_b32_e64 %s, %s, %s, %s" % (hi(r), hi(r), D[1], T2)]
+            else:
+                out += ["v_cndmask_b32_e64 %s, %s, %s, %s" % (r, r, D[0], T2)]
+            out.append("%s:" % lab)
+        return out
+
     def hi_reads(g, regs):
         """cells +2, +3 of the prefetched v128 operands (regs: [(addr, pair), ...])."""
         if g.vf:
@@ -563,18 +600,22 @@ def specs():
 
     FOPS = {"ADD": "v_add_f{w} {d}, {a}, {b}", "SUB": "v_add_f{w} {d}, {a}, -{b}",
             "MUL": "v_mul_f{w} {d}, {a}, {b}"}
+    # add/sub/mul fix NaN results in place (nan_fix); the other FP ops still leave
     for nm, t in FOPS.items():
         add("F32_" + nm, ["F32_" + nm], lambda g, t=t: [
-            t.format(w=32, d=R[0], a=A[0], b=B[0])] + nan_exit(g, [R[0]], 32) + g.w32() + g.next())
+            t.format(w=32, d=R[0], a=A[0], b=B[0])] + nan_fix(g, [(R[0], A[0], B[0])], 32) +
+            g.w32() + g.next(), slots=2)
         add("F64_" + nm, ["F64_" + nm], lambda g, t=t: [
-            t.format(w=64, d=RP, a=AP, b=BP)] + nan_exit(g, [RP], 64) + g.w64() + g.next())
+            t.format(w=64, d=RP, a=AP, b=BP)] + nan_fix(g, [(RP, AP, BP)], 64) + g.w64() + g.next(),
+            slots=2)
         add("V_F32X4_" + nm, ["V_F32X4_" + nm], lambda g, t=t: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
             t.format(w=32, d=R[0], a=A[0], b=B[0]), t.format(w=32, d=R[1], a=A[1], b=B[1]),
             t.format(w=32, d=Z[0], a=X[0], b=Y[0]), t.format(w=32, d=Z[1], a=X[1], b=Y[1])] +
-            nan_exit(g, [R[0], R[1], Z[0], Z[1]], 32) + g.w128(R, Z) + g.next())
+            nan_fix(g, [(R[0], A[0], B[0]), (R[1], A[1], B[1]), (Z[0], X[0], Y[0]),
+                        (Z[1], X[1], Y[1])], 32) + g.w128(R, Z) + g.next(), slots=3)
         add("V_F64X2_" + nm, ["V_F64X2_" + nm], lambda g, t=t: hi_reads(g, [(AADDR, XP), (BADDR, YP)]) + [
             t.format(w=64, d=RP, a=AP, b=BP), t.format(w=64, d=ZP, a=XP, b=YP)] +
-            nan_exit(g, [RP, ZP], 64) + g.w128(R, Z) + g.next())
+            nan_fix(g, [(RP, AP, BP), (ZP, XP, YP)], 64) + g.w128(R, Z) + g.next(), slots=2)
     FCMP = {"EQ": "eq", "NE": "neq", "LT": "lt", "GT": "gt", "LE": "le", "GE": "ge"}
     for nm, c in FCMP.items():
         add("F32_" + nm, ["F32_" + nm], lambda g, c=c: [
@@ -808,7 +849,10 @@ def specs():
     for tup in TUPLES:
         nm = "P_" + "__".join(tup)
         S.append((nm, [], tuple_spec([body_of[x] for x in tup])))
-        for k in range(1, max(2, len(tup))):
+        # FP add/sub/mul carry their in-place NaN fix: one more slot each
+        nfix = sum(1 for x in tup if x.split("_")[0] in ("F32", "F64", "V")
+                   and x.split("_")[-1] in ("ADD", "SUB", "MUL") and "F" in x.split("_")[-2])
+        for k in range(1, max(2, len(tup)) + nfix):
             S.append(("%s+%d" % (nm, k), [], None))
     return S
 
