@@ -13,6 +13,10 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 from wasmedge_amd import batch, workloads as W  # noqa: E402
 
+_src = open(os.path.join(ROOT, "wasmedge_amd", "csrc", "dbc.h")).read()
+_i = _src.index("#define DBC_OPS(X)")
+import re  # noqa: E402
+OPS = re.findall(r"X\((\w+)\)", _src[_i:_src.index("enum DOp", _i)])
 NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow",
          "x_call", "x_ret", "x_post", "x_br", "x_other"]
 
@@ -28,8 +32,10 @@ def run(name, wasm, func, rows, types):
     t = ctx.run()
     _, st, cnt = ctx.results(1)
     nw = (n + 63) // 64
-    buf = np.zeros((nw, 14), np.uint64)
-    L.wb_stats_read(ctx._h, buf.ctypes.data)
+    raw = np.zeros(nw * 14 + 1024, np.uint64)
+    L.wb_stats_read(ctx._h, raw.ctypes.data)
+    buf = raw[:nw * 14].reshape(nw, 14)
+    hist = raw[nw * 14:]
     m = buf.astype(np.float64).mean(0)
     d = dict(zip(NAMES, m))
     cyc = (d["cyc_sched"] + d["cyc_fast"] + d["cyc_slow"]) * 16
@@ -41,6 +47,9 @@ def run(name, wasm, func, rows, types):
              cyc / max(d["rounds"], 1)), flush=True)
     print("           core exits at: call=%.3e ret=%.3e post_call=%.3e branch=%.3e other=%.3e"
           % (d["x_call"], d["x_ret"], d["x_post"], d["x_br"], d["x_other"]), flush=True)
+    top = np.argsort(hist)[::-1][:8]
+    print("           exit ops (per wave): " + " ".join(
+        "%s=%.3g" % (OPS[k] if k < len(OPS) else k, hist[k] / nw) for k in top if hist[k]), flush=True)
     ctx.close()
 
 

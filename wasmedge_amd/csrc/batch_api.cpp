@@ -244,7 +244,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
 #ifdef WB_STATS
-  if (!C->hip_ok(hipMalloc(&C->stats, nw * 14 * sizeof(uint64_t)), "stats")) return kRuntimeError;
+  if (!C->hip_ok(hipMalloc(&C->stats, (nw * 14 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
 #endif
   if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
   return 0;
@@ -324,7 +324,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.loops = C->loops.ptr;
   k.stats = C->stats;
 #ifdef WB_STATS
-  (void)hipMemsetAsync(C->stats, 0, size_t(C->nwaves) * 14 * sizeof(uint64_t), C->stream);
+  (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 14 + 1024) * sizeof(uint64_t), C->stream);
 #endif
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
   size_t wave_lds = size_t(k.total_cells + k.gs_lds) * 64 * 4;
@@ -793,7 +793,7 @@ const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
 __attribute__((visibility("default"))) uint32_t wb_stats_read(WasmEdge_BatchContext *C,
                                                               uint64_t *out) {
   if (!C || !C->stats) return 0;
-  (void)hipMemcpy(out, C->stats, size_t(C->nwaves) * 14 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out, C->stats, (size_t(C->nwaves) * 14 + 1024) * sizeof(uint64_t), hipMemcpyDeviceToHost);
   return C->nwaves;
 }
 #endif

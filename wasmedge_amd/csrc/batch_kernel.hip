@@ -380,6 +380,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
             WB_STAT_ADD(xo == OP_CALL || xo == OP_CALL_INDIRECT ? ST_X_CALL : xo == OP_RET ? ST_X_RET
                         : xo == OP_POST_CALL ? ST_X_POST : (xo >= OP_JMP && xo <= OP_BR_TABLE) ? ST_X_BR
                         : ST_X_OTHER, 1);
+            // which op made the core exit: a histogram after the per-wave counters
+            if (stw && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))
+              __hip_atomic_fetch_add(&p.stats[(size_t)((p.n + 63) >> 6) * ST_N + (xo & 1023u)], 1ull,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
 #endif
         }

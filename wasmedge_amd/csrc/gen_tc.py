@@ -662,6 +662,14 @@ def specs():
     add("MOV128", ["MOV128"], lambda g: hi_reads(g, [(AADDR, XP)]) + g.w128(A, X) + g.next())
     add("V_SPLAT32", ["V_I32X4_SPLAT", "V_F32X4_SPLAT"], lambda g: g.w128((A[0], A[0]), (A[0], A[0])) + g.next())
     add("V_SPLAT64", ["V_I64X2_SPLAT", "V_F64X2_SPLAT"], lambda g: g.w128(A, A) + g.next())
+    # i64x2/f64x2.replace_lane: w7 = the lane (tc.cpp); lane 0 -> (b, a.hi), 1 -> (a.lo, b)
+    add("V_REPLACE64", ["V_REPLACE64"], lambda g: hi_reads(g, [(AADDR, XP)]) + [
+        "s_cmp_eq_u32 %s, 0" % g.x(7),
+        "s_cselect_b64 %s, exec, 0" % T2,
+        "v_cndmask_b32_e64 %s, %s, %s, %s" % (R[0], A[0], B[0], T2),
+        "v_cndmask_b32_e64 %s, %s, %s, %s" % (R[1], A[1], B[1], T2),
+        "v_cndmask_b32_e64 %s, %s, %s, %s" % (Z[0], B[0], X[0], T2),
+        "v_cndmask_b32_e64 %s, %s, %s, %s" % (Z[1], B[1], X[1], T2)] + g.w128(R, Z) + g.next())
     VBIT = {"V_AND": "v_and_b32_e32 {d}, {a}, {b}", "V_OR": "v_or_b32_e32 {d}, {a}, {b}",
             "V_XOR": "v_xor_b32_e32 {d}, {a}, {b}", "V_I32X4_ADD": "v_add_u32_e32 {d}, {a}, {b}",
             "V_I32X4_SUB": "v_sub_u32_e32 {d}, {a}, {b}", "V_I32X4_MUL": "v_mul_lo_u32 {d}, {a}, {b}"}

@@ -71,6 +71,9 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
       w[1] = w[2] = 0;
     } else if (op == OP_CONST32) {
       w[1] = w[2] = 0;
+    } else if (op == OP_V_REPLACE64) {
+      w[7] = d;      // the lane
+      if (d > 1) continue;
     } else if (op == OP_I32_ROTL_I || op == OP_I32_XOR_ROTL_I) {
       w[4] = (32u - (imm & 31u)) & 31u;     // rotl k == rotr -k
     }
