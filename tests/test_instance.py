@@ -94,3 +94,54 @@ def test_gpu_start_trap_fails_create(built):
     with pytest.raises(batch.WasmEdgeError) as e:
         batch.BatchContext(START_TRAPS, 64, device=0)
     assert e.value.code == 0x88
+
+
+WRITER = assemble(r"""
+(module
+  (memory 2 3)
+  (data (i32.const 16) "\11\22\33\44")
+  ;; poke: old word at a, then a store of each kind at a (selected by k)
+  (func (export "poke") (param $a i32) (param $k i32) (result i32)
+    (local $old i32)
+    (local.set $old (i32.load (local.get $a)))
+    (if (i32.eq (local.get $k) (i32.const 0)) (then (i32.store (local.get $a) (i32.const 7))))
+    (if (i32.eq (local.get $k) (i32.const 1)) (then (i64.store (local.get $a) (i64.const 0x0707070707070707))))
+    (if (i32.eq (local.get $k) (i32.const 2)) (then (i32.store8 (local.get $a) (i32.const 7))))
+    (if (i32.eq (local.get $k) (i32.const 3)) (then (v128.store (local.get $a) (v128.const i32x4 7 7 7 7))))
+    (if (i32.eq (local.get $k) (i32.const 4)) (then (memory.fill (local.get $a) (i32.const 7) (i32.const 12))))
+    (if (i32.eq (local.get $k) (i32.const 5)) (then (memory.copy (local.get $a) (i32.const 16) (i32.const 4))))
+    (if (i32.eq (local.get $k) (i32.const 6))
+      (then (drop (memory.grow (i32.const 1))) (i32.store (i32.const 131072) (i32.const 9))))
+    (local.get $old)))
+""")
+
+
+@pytest.mark.gpu
+def test_gpu_reset_restores_fresh_memory(built):
+    """BatchReset re-instantiates memory: Reset rewrites only rows below each wave's write
+    mark (LS_HWM), so every store kind (scalar, i64, byte, v128, fill, copy, host
+    SetMemory, stores into grown pages) must raise the mark. After a Reset each lane reads
+    the fresh image again and the memory hash equals a freshly created context's."""
+    from wasmedge_amd import batch
+    n = 256
+    rows = [[(i * 4093) % (2 * 65536 - 16) & ~15, i % 7] for i in range(n)]
+    vals = batch.make_values(rows, [I32, I32])
+    ctx = batch.BatchContext(WRITER, n, device=0)
+    fresh = batch.BatchContext(WRITER, n, device=0)
+    try:
+        h0 = fresh.memory_hash()
+        r0, st, _ = ctx.execute("poke", vals, 1)
+        assert (st == 0).all()
+        ctx.set_memory(5, 100000, b"\x01\x02\x03\x04")        # host write, high offset
+        r1, st, _ = ctx.execute("poke", vals, 1)              # state persists: sees its writes
+        assert (st == 0).all()
+        assert any(int(a) != int(b) for a, b in zip(batch.ret_ints(r0)[:, 0], batch.ret_ints(r1)[:, 0]))
+        ctx.reset()
+        assert list(ctx.memory_hash()) == list(h0)
+        assert ctx.memory(5, 100000, 4) == b"\x00" * 4
+        r2, st, _ = ctx.execute("poke", vals, 1)              # fresh again: same as the first run
+        assert (st == 0).all()
+        assert list(batch.ret_ints(r2)[:, 0]) == list(batch.ret_ints(r0)[:, 0])
+    finally:
+        ctx.close()
+        fresh.close()

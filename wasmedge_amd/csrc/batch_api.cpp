@@ -20,7 +20,9 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
                                      size_t lds_bytes, int vframe, hipStream_t s);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
-                                         uint32_t mem_words, uint32_t nwaves, hipStream_t s);
+                                         uint32_t mem_words, uint32_t nwaves,
+                                         const uint32_t *ls, uint32_t ls_slots, uint32_t full,
+                                         hipStream_t s);
 extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
                                          uint32_t mem_words, uint32_t n, hipStream_t s);
@@ -108,6 +110,7 @@ struct WasmEdge_BatchContext {
   uint32_t param_cells = 0, result_cells = 0;
   std::vector<uint8_t> result_types;
   bool ran = false;         // a Run completed since the last Reset (results are valid)
+  bool mem_fresh = true;    // memory never initialised: the next Reset writes every page
 
   uint8_t fail(uint8_t code, const std::string &m) {
     last_error = m;
@@ -274,6 +277,16 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
   memcpy(bytes, Src, Len);
   if (!C->hip_ok(hipMemcpy2D(base, pitch, words.data(), 4, 4, words.size(), hipMemcpyHostToDevice), "memory"))
     return kRuntimeError;
+  // raise the lane's write mark (LS_HWM) so the next Reset re-initialises these bytes
+  uint32_t *mark = C->lstate.ptr + (size_t(wave) * C->ls_slots + LS_HWM) * 64 + lane;
+  uint32_t hw = 0;
+  if (!C->hip_ok(hipMemcpy(&hw, mark, 4, hipMemcpyDeviceToHost), "memory"))
+    return kRuntimeError;
+  const uint64_t end = uint64_t(Off) + Len;
+  if (end > hw) {
+    hw = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(end);
+    if (!C->hip_ok(hipMemcpy(mark, &hw, 4, hipMemcpyHostToDevice), "memory")) return kRuntimeError;
+  }
   return 0;
 }
 
@@ -497,12 +510,14 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   (void)hipEventRecord(C->ev0, C->stream);
   if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
-                                    C->mem_words, C->nwaves, C->stream), "mem init"))
+                                    C->mem_words, C->nwaves, C->lstate.ptr, C->ls_slots,
+                                    C->mem_fresh ? 1u : 0u, C->stream), "mem init"))
     return R(kRuntimeError);
+  C->mem_fresh = false;   // from now on every lane's write mark (LS_HWM) is valid
   // per-lane tables (instantiate/table.cpp + elem.cpp): every lane starts from the image
   if (P.mut_tables &&
       !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
-                                    P.tab_words, C->nwaves, C->stream), "table init"))
+                                    P.tab_words, C->nwaves, nullptr, 0, 1u, C->stream), "table init"))
     return R(kRuntimeError);
   if (!C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->global_init.ptr, P.global_cells,
                                       C->ls_slots, P.mem_min, C->init_dropped, C->nwaves,

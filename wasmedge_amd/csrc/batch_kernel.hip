@@ -133,6 +133,7 @@ struct LdsFrame {
       "v_mov_b32 v106, %[mlo]\n\t" \
       "v_mov_b32 v107, %[mhi]\n\t" \
       "v_mov_b32 v102, %[gsp]\n\t" \
+      "v_mov_b32 v101, %[hwm]\n\t" \
       "v_mov_b32 v103, %[stk]\n\t" \
       "s_mov_b32 s93, %[slds]\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
@@ -149,15 +150,16 @@ struct LdsFrame {
       "s_lshr_b32 %[npc], s62, 5\n\t" \
       "s_mov_b32 %[cnt], s65\n\t" \
       "s_mov_b32 %[why], s92\n\t" \
-      "v_mov_b32 %[gsp], v102" \
-      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp) \
+      "v_mov_b32 %[gsp], v102\n\t" \
+      "v_mov_b32 %[hwm], v101" \
+      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm) \
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
-        "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 
@@ -177,7 +179,7 @@ struct LdsFrame {
 template <bool VF>
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other, uint32_t low,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem,
-                                           uint32_t &gsp, uint32_t stk, uint32_t slds,
+                                           uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
   const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
@@ -236,6 +238,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define EDROP LS(p.ls_tab + p.ntables)
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   uint32_t pc = p.entry_pc, gsp = 0, pages = LS(LS_PAGES), dropped = LS(LS_DROPPED);
+  // one past the highest memory byte written since instantiation: Reset re-initialises
+  // only [0, hwm) of each lane (plus the image), the rest is still the zero it was given
+  uint32_t hwm = LS(LS_HWM);
+#define WB_MARK(ea, n) (hwm = max(hwm, (uint32_t)min((uint64_t)(ea) + (uint64_t)(n), 0xFFFFFFFFull)))
   uint64_t count = 0;
   const uint32_t istatus = LS(LS_ISTATUS);
   if (status == WB_STATUS_RUNNING && istatus) status = istatus;   // instance never came up
@@ -369,7 +375,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
-          pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem, gsp, stk_lds, S_lds,
+          pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
@@ -545,10 +551,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     }
     LS(LS_PAGES) = pages;
     LS(LS_DROPPED) = dropped;
+    LS(LS_HWM) = hwm;
     for (uint32_t c = 0; c < p.global_cells; c++) LS(LS_GLOBALS + c) = F.get(c);
     if (p.is_start && status != WB_STATUS_OK) LS(LS_ISTATUS) = status;
   }
 #undef LS
+#undef WB_MARK
 }
 
 // General kernel: frames of any size in LDS (4 waves per block when they fit). VF: the
@@ -577,17 +585,40 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_vf_kernel(const KParam
 
 // ======================================================================= helpers
 // Instantiation image broadcast (instantiate/memory.cpp + data.cpp): every lane's
-// pages [0, init_pages) = the module image (data segments), rest of those pages zero.
+// pages [0, init_pages) = the module image (data segments), the rest of those pages zero.
+// Block b covers rows [c*1024, (c+1)*1024) of wave b / chunks (a row = one word of the 64
+// lanes). Unless `full`, only rows below the wave's highest write mark (LS_HWM, bytes)
+// or the image are rewritten: memory above it was zeroed by the previous instantiation
+// and never written since (the kernel's every store path raises the mark), the way the
+// reference's fresh MAP_ANONYMOUS pages are zero without being written. `ls` = nullptr:
+// always full (per-lane table images).
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
-                   uint32_t init_words, uint32_t mem_words, uint32_t nwaves) {
-  const size_t total = (size_t)nwaves * init_words * 64u;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const size_t wave = i / ((size_t)init_words * 64u);
-    const uint32_t rem = (uint32_t)(i - wave * (size_t)init_words * 64u);
-    const uint32_t word = rem >> 6, lane = rem & 63u;
-    mem[(wave * mem_words + word) * 64u + lane] = word < image_words ? image[word] : 0u;
+                   uint32_t init_words, uint32_t mem_words, uint32_t nwaves,
+                   const uint32_t *ls, uint32_t ls_slots, uint32_t full) {
+  const uint32_t chunks = (init_words + 1023u) / 1024u;
+  __shared__ uint32_t smax;
+  for (size_t b = blockIdx.x; b < (size_t)nwaves * chunks; b += gridDim.x) {
+    const size_t wave = b / chunks;
+    const uint32_t r0 = (uint32_t)(b - wave * chunks) * 1024u;
+    uint32_t rows = init_words;
+    if (!full && ls) {
+      if (threadIdx.x == 0) smax = 0;
+      __syncthreads();
+      if (threadIdx.x < 64) atomicMax(&smax, ls[((size_t)wave * ls_slots + LS_HWM) * 64u + threadIdx.x]);
+      __syncthreads();
+      const uint64_t hw = ((uint64_t)smax + 3u) / 4u;
+      rows = (uint32_t)(hw < init_words ? hw : init_words);
+      if (rows < image_words && image_words <= init_words) rows = image_words;
+      __syncthreads();   // smax is reused by the next iteration
+    }
+    const uint32_t r1 = r0 + 1024u < rows ? r0 + 1024u : rows;
+    if (r1 <= r0) continue;
+    uint32_t *wm = mem + wave * mem_words * 64u;
+    for (uint32_t i = r0 * 64u + threadIdx.x; i < r1 * 64u; i += blockDim.x) {
+      const uint32_t word = i >> 6;
+      wm[i] = word < image_words ? image[word] : 0u;
+    }
   }
 }
 
@@ -648,13 +679,14 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
 }
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
-                                         uint32_t mem_words, uint32_t nwaves, hipStream_t s) {
-  const size_t total = (size_t)nwaves * init_words * 64u;
+                                         uint32_t mem_words, uint32_t nwaves,
+                                         const uint32_t *ls, uint32_t ls_slots, uint32_t full,
+                                         hipStream_t s) {
+  const size_t total = (size_t)nwaves * ((init_words + 1023u) / 1024u);
   if (total == 0) return hipSuccess;
-  size_t blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
+  const size_t blocks = total < 262144 ? total : 262144;
   hipLaunchKernelGGL(wb_mem_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, mem, image,
-                     image_words, init_words, mem_words, nwaves);
+                     image_words, init_words, mem_words, nwaves, ls, ls_slots, full);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,

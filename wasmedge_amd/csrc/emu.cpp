@@ -4,6 +4,7 @@
 // It is built into a separate library (libwasmedge_batch_emu.so) that the product never
 // loads; the product path (libwasmedge_batch.so) has no CPU execution path.
 #define WB_MSHIFT 0
+#define WB_MARK(ea, n) ((void)0)   // the emulator re-creates memory per instance
 #include <cstdio>
 #include <cstring>
 #include <string>

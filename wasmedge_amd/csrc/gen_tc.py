@@ -66,6 +66,7 @@ Y = ("v120", "v121"); YP = "v[120:121]"
 AADDR, BADDR, DADDR, CADDR = "v122", "v123", "v124", "v125"
 Z = ("v126", "v127"); ZP = "v[126:127]"
 GSP = "v102"          # this lane's call-stack depth (slots), in/out
+HWM = "v101"          # one past the highest memory byte written (LS_HWM), in/out
 SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
 SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
 VSYNC = "s94"         # V frames: (VMAX - frame cells) * 8, the frame-sync jump offset
@@ -825,12 +826,15 @@ def specs():
         "s_waitcnt vmcnt(0)"] + g.w64() + g.next())
     STORES = {"ST8": (1, "global_store_byte"), "ST16": (2, "global_store_short"),
               "ST32": (4, "global_store_dword")}
+    def mark(n):   # HWM = max(HWM, ea + n), saturating (Y0 = ea from mem_check)
+        return ["v_add_u32_e64 %s, %s, %d clamp" % (Y[1], Y[0], n),
+                "v_max_u32_e32 %s, %s, %s" % (HWM, HWM, Y[1])]
     for nm, (n, ins) in STORES.items():
         add(nm, [nm], lambda g, n=n, ins=ins: mem_check(g, n) + [
-            "%s %s, %s, off" % (ins, XP, B[0])] + g.next())
+            "%s %s, %s, off" % (ins, XP, B[0])] + mark(n) + g.next())
     add("ST64", ["ST64"], lambda g: mem_check(g, 8) + [
         "global_store_dword %s, %s, off" % (XP, B[0]),
-        "global_store_dword %s, %s, off offset:256" % (XP, B[1])] + g.next())
+        "global_store_dword %s, %s, off offset:256" % (XP, B[1])] + mark(8) + g.next())
     # ---- fused pairs (V blob, converged mode): the instruction at pc (a fall-through
     # op) and the one at pc + 1 in one handler, saving a dispatch. tc.cpp picks the slot
     # from the two instructions' own slots (tc_pair_slot); each half reads its own

@@ -73,4 +73,5 @@ struct KParams {
 #define LS_RPC 3u
 #define LS_GSP 4u
 #define LS_HBASE 5u
-#define LS_GLOBALS 6u
+#define LS_HWM 6u      // one past the highest linear-memory byte written since instantiation
+#define LS_GLOBALS 7u
