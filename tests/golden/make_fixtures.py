@@ -8,6 +8,8 @@ answers):
   fibonacci.wasm    tools/wasmedge/examples/fibonacci.wasm (README: fib 8 -> 34)
   factorial.wasm    tools/wasmedge/examples/factorial.wasm (README: fac 12 -> 479001600)
   apitest.wasm      test/api/apiTestData/test.wasm
+  externref_funcs.wasm  test/externref/externrefTestData/funcs.wasm
+                    (answers in test/externref/ExternrefTest.cpp:308-356)
 """
 import json
 import os
@@ -36,6 +38,8 @@ def main():
                     os.path.join(OUT, name + ".wasm"))
     shutil.copy(os.path.join(REF, "test/api/apiTestData/test.wasm"),
                 os.path.join(OUT, "apitest.wasm"))
+    shutil.copy(os.path.join(REF, "test/externref/externrefTestData/funcs.wasm"),
+                os.path.join(OUT, "externref_funcs.wasm"))
     print("ok", len(answers))
 
 

@@ -93,6 +93,31 @@ def register_extern(ctx):
         ctx.add_host_function("extern", name, fn, np_, nr)
 
 
+# ---- the reference externref test's import module "extern_module"
+# (test/externref/ExternrefTest.cpp:20-70, registered at :172-211): the externref names a
+# host object the function calls. Handles as in the oracle: 1 = AddClass, 2 = MulFunc,
+# 3 = SquareStruct; a null or other handle fails the call (HostFuncFailed).
+EXT_ADD, EXT_MUL, EXT_SQUARE = 1, 2, 3
+
+
+def _ext_obj(kind, f, nargs):
+    def g(mem, a):
+        if a[0] & 0xFFFFFFFF != kind:
+            return HOST_FAILED, []
+        return 0, [f(*[x & 0xFFFFFFFF for x in a[1:1 + nargs]]) & 0xFFFFFFFF]
+    return g
+
+
+EXTERN_MODULE = {"class_add": (_ext_obj(EXT_ADD, lambda x, y: x + y, 2), 3, 1),
+                 "func_mul": (_ext_obj(EXT_MUL, lambda x, y: x * y, 2), 3, 1),
+                 "functor_square": (_ext_obj(EXT_SQUARE, lambda x: x * x, 1), 2, 1)}
+
+
+def register_extern_module(ctx):
+    for name, (fn, np_, nr) in EXTERN_MODULE.items():
+        ctx.add_host_function("extern_module", name, fn, np_, nr)
+
+
 def register(ctx):
     for name, (fn, np_, nr) in ENV.items():
         ctx.add_host_function("env", name, fn, np_, nr)
