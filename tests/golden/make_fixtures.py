@@ -10,6 +10,7 @@ answers):
   apitest.wasm      test/api/apiTestData/test.wasm
   externref_funcs.wasm  test/externref/externrefTestData/funcs.wasm
                     (answers in test/externref/ExternrefTest.cpp:308-356)
+  externref_stl.wasm    test/externref/externrefTestData/stl.wasm (:372-465)
 """
 import json
 import os
@@ -40,6 +41,8 @@ def main():
                 os.path.join(OUT, "apitest.wasm"))
     shutil.copy(os.path.join(REF, "test/externref/externrefTestData/funcs.wasm"),
                 os.path.join(OUT, "externref_funcs.wasm"))
+    shutil.copy(os.path.join(REF, "test/externref/externrefTestData/stl.wasm"),
+                os.path.join(OUT, "externref_stl.wasm"))
     print("ok", len(answers))
 
 

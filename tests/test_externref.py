@@ -95,3 +95,105 @@ def test_gpu_externref_per_lane_vs_oracle(built):
             assert compare(ref, got, st, cnt, None, [I32], check_hash=False) == [], fn
     finally:
         ctx.close()
+
+
+# ---- test/externref/externrefTestData/stl.wasm (ExternrefTest.cpp:360-465): externrefs
+# to host C++ containers; the host functions mutate them. Here every lane gets its own
+# containers in a host object registry (handle = index), and each lane must see exactly
+# the reference's expected contents after each call: one host call per lane, in order.
+
+class _Objects:
+    def __init__(self):
+        self.objs = []
+
+    def new(self, o):
+        self.objs.append(o)
+        return len(self.objs) - 1
+
+    def __getitem__(self, h):
+        return self.objs[h & 0xFFFFFFFF]
+
+
+def _stl_module(reg, calls):
+    def rec(name, f, nres):
+        def g(mem, a):
+            calls.append((name, mem.instance))
+            r = f(*a)
+            return 0, ([r & 0xFFFFFFFF] if nres else [])
+        return g
+
+    def vsum(b, e):
+        (vb, ib), (ve, ie) = reg[b], reg[e]
+        assert vb == ve
+        return sum(reg[vb][ib:ie])
+
+    return {
+        "stl_ostream_str": (rec("ostream_str", lambda s, x: reg[s].append(reg[x]), 0), 2, 0),
+        "stl_ostream_u32": (rec("ostream_u32", lambda s, v: reg[s].append(str(v & 0xFFFFFFFF)), 0), 2, 0),
+        "stl_map_insert": (rec("map_insert", lambda m, k, v: reg[m].__setitem__(reg[k], reg[v]), 0), 3, 0),
+        "stl_map_erase": (rec("map_erase", lambda m, k: reg[m].pop(reg[k], None), 0), 2, 0),
+        "stl_set_insert": (rec("set_insert", lambda s, v: reg[s].add(v & 0xFFFFFFFF), 0), 2, 0),
+        "stl_set_erase": (rec("set_erase", lambda s, v: reg[s].discard(v & 0xFFFFFFFF), 0), 2, 0),
+        "stl_vector_push": (rec("vector_push", lambda v, x: reg[v].append(x & 0xFFFFFFFF), 0), 2, 0),
+        "stl_vector_sum": (rec("vector_sum", vsum, 1), 2, 1),
+    }
+
+
+def test_externref_stl_oracle_counts():
+    m = O.Module(golden("externref_stl.wasm"))
+    inst = O.Instance(m)
+    assert inst.error == 0
+    for fn, args in [("call_ostream_str", [0, 1]), ("call_map_insert", [0, 1, 2]),
+                     ("call_vector_sum", [0, 1])]:
+        code, _, cnt, _ = inst.invoke(fn, args)
+        assert code == 0 and cnt == len(args) + 2, fn     # local.get x k, call, end
+
+
+@pytest.mark.gpu
+def test_gpu_externref_stl_reference_answers(built):
+    from wasmedge_amd import batch
+    n = 96
+    wasm = golden("externref_stl.wasm")
+    m = O.Module(wasm)
+    reg, calls = _Objects(), []
+    lanes = []
+    for i in range(n):
+        L = {"ss": reg.new([]), "str": reg.new("hello world!"), "key": reg.new("one"),
+             "val": reg.new("1"), "map": reg.new({}), "set": reg.new(set()),
+             "vec": reg.new([10, 20, 30, 40, 50, 60, 70, 80, 90])}
+        lanes.append(L)
+    ctx = batch.BatchContext(wasm, n, device=0)
+    E = EXTERNREF
+
+    def run(fn, rows, types, nres=0):
+        calls.clear()
+        ref = [O.Instance(m).invoke(fn, r) for r in rows]
+        rets, st, cnt = ctx.execute(fn, batch.make_values(rows, types), nres)
+        assert (st == 0).all(), fn
+        assert [int(c) for c in cnt] == [r[2] for r in ref], fn
+        assert sorted(c[1] for c in calls) == list(range(n)), fn   # once per lane
+        return rets
+
+    try:
+        for name, (fn, np_, nr) in _stl_module(reg, calls).items():
+            ctx.add_host_function("extern_module", name, fn, np_, nr)
+        run("call_ostream_str", [[L["ss"], L["str"]] for L in lanes], [E, E])
+        assert all("".join(reg[L["ss"]]) == "hello world!" for L in lanes)
+        run("call_ostream_u32", [[L["ss"], 123456] for L in lanes], [E, I32])
+        assert all("".join(reg[L["ss"]]) == "hello world!123456" for L in lanes)
+        run("call_map_insert", [[L["map"], L["key"], L["val"]] for L in lanes], [E, E, E])
+        assert all(reg[L["map"]] == {"one": "1"} for L in lanes)
+        run("call_map_erase", [[L["map"], L["key"]] for L in lanes], [E, E])
+        assert all(reg[L["map"]] == {} for L in lanes)
+        run("call_set_insert", [[L["set"], 123456] for L in lanes], [E, I32])
+        for L in lanes:
+            reg[L["set"]].add(3456)
+        run("call_set_erase", [[L["set"], 3456] for L in lanes], [E, I32])
+        assert all(reg[L["set"]] == {123456} for L in lanes)
+        run("call_vector_push", [[L["vec"], 100] for L in lanes], [E, I32])
+        assert all(len(reg[L["vec"]]) == 10 and reg[L["vec"]][9] == 100 for L in lanes)
+        rows = [[reg.new((L["vec"], 3)), reg.new((L["vec"], 8))] for L in lanes]
+        rets = run("call_vector_sum", rows, [E, E], 1)
+        assert [int(r[0]) for r in batch.ret_ints(rets)] == [40 + 50 + 60 + 70 + 80] * n
+    finally:
+        ctx.close()
