@@ -61,7 +61,9 @@ typedef struct WasmEdge_Result {
 typedef struct WasmEdge_BatchConfigure {
   /* Page budget per instance; plays RuntimeConfigure::MaxMemPage
    * (include/common/configure.h:123). 0 = the module's declared maximum, else its
-   * initial size. memory.grow beyond it returns -1 exactly like the reference. */
+   * initial size. memory.grow beyond it returns -1 exactly like the reference. A
+   * module whose initial size exceeds a non-zero budget fails WasmEdge_BatchCreate with
+   * MemoryOutOfBounds (0x88): the reference allocates no memory for it (memory.h:46-51). */
   uint32_t MaxMemoryPage;
   /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
   uint32_t CallStackCells;

@@ -130,6 +130,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
+  // MemoryInstance(MType, PageLimit) allocates nothing when the initial size exceeds the
+  // page limit (include/runtime/instance/memory.h:46-51, test/memlimit/MemLimitTest.cpp:16-18);
+  // such an instance is unusable, so the batch fails here instead of running without memory
+  if (P.has_mem && C->conf.MaxMemoryPage && P.mem_min > C->conf.MaxMemoryPage)
+    return C->fail(kMemoryOutOfBounds, "initial memory pages exceed MaxMemoryPage");
   if (C->conf.DeviceOrdinal >= 0) {
     if (!C->hip_ok(hipSetDevice(C->conf.DeviceOrdinal), "hipSetDevice")) return kRuntimeError;
   }
