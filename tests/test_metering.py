@@ -82,3 +82,24 @@ def test_gpu_interrupt(built):
         assert all(int(s) == 0x07 for s in st)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_interrupt_reference_module(built):
+    """The reference's interrupt test module (test/executor/ExecutorTest.cpp:118-146,
+    fixture tests/golden/executor_interrupt.wasm: `_start` = loop br 0): still running
+    after 1 ms, then cancelled -> every lane Interrupted (0x07)."""
+    from wasmedge_amd import batch
+    from conftest import golden
+    ctx = batch.BatchContext(golden("executor_interrupt.wasm"), 4096, device=0, time_limit=60.0)
+    try:
+        t = threading.Timer(0.5, ctx.interrupt)
+        t.start()
+        t0 = time.time()
+        rets, st, cnt = ctx.execute("_start", batch.make_values([[]] * 4096, []), 0)
+        t.join()
+        assert time.time() - t0 >= 0.001 and time.time() - t0 < 30
+        assert all(int(s) == 0x07 for s in st)
+        assert all(int(c) > 1000 for c in cnt)
+    finally:
+        ctx.close()
