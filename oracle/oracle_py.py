@@ -47,6 +47,8 @@ def lib():
         L.om_mem_hash.argtypes = [ctypes.c_void_p]
         L.om_hash_bytes.restype = ctypes.c_uint64
         L.om_hash_bytes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+        L.om_set_lazy_imports.restype = None
+        L.om_set_lazy_imports.argtypes = [ctypes.c_int]
         L.om_set_extern_value.restype = None
         L.om_set_extern_value.argtypes = [ctypes.c_uint32, ctypes.c_int32]
         L.om_table_set.restype = ctypes.c_int
@@ -214,6 +216,11 @@ class Instance:
         lo, hi = ctypes.c_uint64(0), ctypes.c_uint64(0)
         lib().om_global_get(self._h, g, ctypes.byref(lo), ctypes.byref(hi))
         return lo.value | (hi.value << 64)
+
+
+def set_lazy_imports(on):
+    """Instantiate modules with imports no test host module provides (calls fail)."""
+    lib().om_set_lazy_imports(1 if on else 0)
 
 
 def set_extern_value(handle, value):

@@ -50,6 +50,8 @@ int om_terminated(const OInst *i);
 
 /* Gas limit per invocation with unit costs (0 = none): statistics.h:69-91. */
 void om_set_cost_limit(OInst *i, uint64_t limit);
+/* Accept imports no test host module provides; calling one fails (test infrastructure). */
+void om_set_lazy_imports(int on);
 
 /* Test host module "extern" (the reference API test's): the int32 an externref handle
  * points to. Table entry write (ref: function index / handle, UINT64_MAX null) and a
