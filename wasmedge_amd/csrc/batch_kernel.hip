@@ -615,8 +615,9 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
     const uint32_t r1 = r0 + 1024u < rows ? r0 + 1024u : rows;
     if (r1 <= r0) continue;
     uint32_t *wm = mem + wave * mem_words * 64u;
-    for (uint32_t i = r0 * 64u + threadIdx.x; i < r1 * 64u; i += blockDim.x) {
-      const uint32_t word = i >> 6;
+    // size_t: rows past 2^26 (initial memories over 4096 pages) must not wrap
+    for (size_t i = (size_t)r0 * 64u + threadIdx.x; i < (size_t)r1 * 64u; i += blockDim.x) {
+      const uint32_t word = (uint32_t)(i >> 6);
       wm[i] = word < image_words ? image[word] : 0u;
     }
   }
