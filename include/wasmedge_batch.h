@@ -82,6 +82,9 @@ typedef struct WasmEdge_BatchConfigure {
    * CostLimitExceeded (0x03), its count = CostLimit + 1 as in engine.cpp:1616-1630.
    * Metered runs use the compiled step only (no threaded dispatch core). */
   uint64_t CostLimit;
+  /* Host threads serving lanes parked at host imports (0 = min(16, cores)). Waves are
+   * spread over the threads, so host functions must be reentrant. */
+  uint32_t HostThreads;
 } WasmEdge_BatchConfigure;
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
@@ -165,6 +168,29 @@ WasmEdge_BatchMemoryGetData(const WasmEdge_BatchMemoryContext *MemCxt, uint8_t *
 WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *MemCxt, const uint8_t *Data,
                             const uint32_t Offset, const uint32_t Length);
+
+/* ---- built-in WASI subset (wasi_snapshot_preview1) on the yield path -------------------
+ * Binds the module's imports args_get, args_sizes_get, environ_get, environ_sizes_get,
+ * fd_write, proc_exit and sched_yield (those with the WASI signature) to host functions
+ * inside the library, as WasmEdge_ImportObjectCreateWASI / InitWASI would
+ * (include/api/wasmedge/wasmedge.h:2719-2754, lib/host/wasi/wasifunc.cpp). Args/Envs are
+ * shared by every instance. fd_write to fd 1 / 2 is captured per instance (fd 0 gives
+ * NOTCAPABLE, other fds BADF: no preopened directories); proc_exit records the exit code
+ * and ends the instance with Terminated (0x01). Calling it again re-initialises the
+ * environment and clears the captured output and exit codes. Other WASI imports stay
+ * unbound (0xB1 when reached) unless registered with WasmEdge_BatchAddHostFunction. */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchInitWASI(WasmEdge_BatchContext *Cxt, const char *const *Args, const uint32_t ArgLen,
+                       const char *const *Envs, const uint32_t EnvLen);
+/* proc_exit code of instance Inst (0 if it never called it; WasmEdge_ImportObjectWASIGetExitCode,
+ * wasmedge.h:2754). */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetExitCode(const WasmEdge_BatchContext *Cxt,
+                                                          uint32_t Inst);
+/* Bytes instance Inst wrote to fd 1 (stdout) or 2 (stderr); copies at most Len of them into
+ * Buf (may be NULL) and returns the total size. */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetOutput(const WasmEdge_BatchContext *Cxt,
+                                                        uint32_t Inst, uint32_t Fd, uint8_t *Buf,
+                                                        uint32_t Len);
 
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */

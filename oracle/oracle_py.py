@@ -63,6 +63,13 @@ def lib():
         L.om_run_batch_mb.restype = ctypes.c_double
         L.om_run_batch_mb.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 6 + [ctypes.c_int]
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        L.om_set_wasi.restype = None
+        L.om_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
+        L.om_wasi_exit_code.restype = ctypes.c_uint32
+        L.om_wasi_exit_code.argtypes = [ctypes.c_void_p]
+        L.om_wasi_output.restype = ctypes.c_uint64
+        L.om_wasi_output.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
         _lib = L
     return _lib
 
@@ -207,6 +214,14 @@ class Instance:
         return code, vals, cnt.value, L.om_mem_hash(self._h)
 
 
+    def wasi_output(self, fd=1):
+        p = ctypes.c_void_p()
+        n = lib().om_wasi_output(self._h, fd, ctypes.byref(p))
+        return ctypes.string_at(p.value, n) if n else b""
+
+    def wasi_exit_code(self):
+        return lib().om_wasi_exit_code(self._h)
+
     def table_set(self, tab, off, ref):
         """Write one table entry (ref: function index / externref handle, None = null);
         returns the ErrCode (0x87 out of bounds)."""
@@ -221,6 +236,14 @@ class Instance:
 def set_lazy_imports(on):
     """Instantiate modules with imports no test host module provides (calls fail)."""
     lib().om_set_lazy_imports(1 if on else 0)
+
+
+def set_wasi(on, args=(), envs=()):
+    """Bind the WASI subset (wasi_snapshot_preview1) for later instantiations, with these
+    args/envs shared by every instance (the batched path's WasmEdge_BatchInitWASI)."""
+    def arr(v):
+        return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
+    lib().om_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
 
 
 def set_extern_value(handle, value):

@@ -110,6 +110,9 @@ struct OInst {
   uint64_t cost_limit;              /* unit-cost gas limit per invocation (statistics.h) */
   uint64_t mem_bytes;               /* linear-memory bytes the last invoke accessed (not
                                        in the reference: the roofline's algorithmic bytes) */
+  /* WASI subset (wasifunc.cpp): captured fd 1 / fd 2 bytes and the proc_exit code */
+  uint8_t *wasi_out[2]; uint64_t wasi_len[2], wasi_cap[2];
+  uint32_t wasi_exit;
 };
 
 /* ------------------------------------------------------------------ reader */

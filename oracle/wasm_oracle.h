@@ -53,6 +53,14 @@ void om_set_cost_limit(OInst *i, uint64_t limit);
 /* Accept imports no test host module provides; calling one fails (test infrastructure). */
 void om_set_lazy_imports(int on);
 
+/* WASI subset of the batched path (WasmEdge_BatchInitWASI): bind wasi_snapshot_preview1
+ * args/environ get+sizes, fd_write, proc_exit, sched_yield with these args/envs (shared
+ * by every instance). Per instance: captured fd 1/2 bytes and the proc_exit code. */
+void om_set_wasi(int on, const char *const *args, uint32_t nargs, const char *const *envs,
+                 uint32_t nenvs);
+uint32_t om_wasi_exit_code(const OInst *i);
+uint64_t om_wasi_output(const OInst *i, uint32_t fd, const uint8_t **data);
+
 /* Test host module "extern" (the reference API test's): the int32 an externref handle
  * points to. Table entry write (ref: function index / handle, UINT64_MAX null) and a
  * global's value bits, as the reference C API's TableInstanceSetData / GlobalInstanceGetValue. */

@@ -22,6 +22,12 @@ def emu_lib():
             [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         E.wb_emu_set_host.argtypes = [ctypes.c_void_p]
         E.wb_emu_set_cost_limit.argtypes = [ctypes.c_uint64]
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        E.wb_emu_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
+        E.wb_emu_wasi_output.restype = ctypes.c_uint32
+        E.wb_emu_wasi_output.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+        E.wb_emu_wasi_exit_code.restype = ctypes.c_uint32
+        E.wb_emu_wasi_exit_code.argtypes = [ctypes.c_uint32]
         E.wb_emu_disasm.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                     ctypes.c_uint32]
         _emu = E
@@ -72,6 +78,21 @@ def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_s
         raise RuntimeError("emu error 0x%x: %s" % (e, E.wb_emu_last_error().decode()))
     rets = [from_cells(res[i], rtypes) if st[i] == 0 else [] for i in range(n)]
     return rets, st, cnt, h
+
+
+def emu_set_wasi(on, args=(), envs=()):
+    """The emulator's copy of the library's WASI subset (wasi_impl.h)."""
+    def arr(v):
+        return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
+    emu_lib().wb_emu_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
+
+
+def emu_wasi_output(inst, fd):
+    E = emu_lib()
+    n = E.wb_emu_wasi_output(inst, fd, None, 0)
+    buf = ctypes.create_string_buffer(max(n, 1))
+    E.wb_emu_wasi_output(inst, fd, buf, n)
+    return buf.raw[:n]
 
 
 def disasm(wasm):

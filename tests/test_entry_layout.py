@@ -63,7 +63,8 @@ def test_oracle_chain_known_answers():
         assert code == 0 and vals == [(want + 100) & 0xFFFFFFFF], x
 
 
-@pytest.mark.parametrize("wasm,func,rows", [(NEXT, "a", [[]] * 4), (CHAIN, "run", ROWS)])
+@pytest.mark.parametrize("wasm,func,rows", [(NEXT, "a", [[]] * 4), (CHAIN, "run", ROWS)],
+                         ids=["next", "chain"])
 def test_emulator_matches_oracle(built, wasm, func, rows):
     m = O.Module(wasm)
     ref = [m.run(func, r) for r in rows]
@@ -72,7 +73,8 @@ def test_emulator_matches_oracle(built, wasm, func, rows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wasm,func,rows", [(NEXT, "a", [[]] * 64), (CHAIN, "run", ROWS)])
+@pytest.mark.parametrize("wasm,func,rows", [(NEXT, "a", [[]] * 64), (CHAIN, "run", ROWS)],
+                         ids=["next", "chain"])
 def test_gpu_matches_oracle(built, wasm, func, rows):
     m = O.Module(wasm)
     ref = [m.run(func, r) for r in rows]

@@ -98,8 +98,10 @@ def test_gpu_start_trap_fails_create(built):
 
 WRITER = assemble(r"""
 (module
+  (import "env" "mem_fill" (func $mem_fill (param i32 i32 i32)))
   (memory 2 3)
   (data (i32.const 16) "\11\22\33\44")
+  (data $p "\07\07\07\07\07\07")
   ;; poke: old word at a, then a store of each kind at a (selected by k)
   (func (export "poke") (param $a i32) (param $k i32) (result i32)
     (local $old i32)
@@ -112,22 +114,34 @@ WRITER = assemble(r"""
     (if (i32.eq (local.get $k) (i32.const 5)) (then (memory.copy (local.get $a) (i32.const 16) (i32.const 4))))
     (if (i32.eq (local.get $k) (i32.const 6))
       (then (drop (memory.grow (i32.const 1))) (i32.store (i32.const 131072) (i32.const 9))))
+    (if (i32.eq (local.get $k) (i32.const 7)) (then (i32.store16 (local.get $a) (i32.const 0x0707))))
+    (if (i32.eq (local.get $k) (i32.const 8))
+      (then (v128.store32_lane 2 (local.get $a) (v128.const i32x4 1 2 0x07070707 4))))
+    (if (i32.eq (local.get $k) (i32.const 9)) (then (memory.init $p (local.get $a) (i32.const 0) (i32.const 6))))
+    (if (i32.eq (local.get $k) (i32.const 10))
+      (then (call $mem_fill (local.get $a) (i32.const 9) (i32.const 7))))
     (local.get $old)))
 """)
 
 
 @pytest.mark.gpu
-def test_gpu_reset_restores_fresh_memory(built):
+@pytest.mark.parametrize("frames", ["lds", "vgpr"])
+def test_gpu_reset_restores_fresh_memory(built, monkeypatch, frames):
     """BatchReset re-instantiates memory: Reset rewrites only rows below each wave's write
-    mark (LS_HWM), so every store kind (scalar, i64, byte, v128, fill, copy, host
-    SetMemory, stores into grown pages) must raise the mark. After a Reset each lane reads
-    the fresh image again and the memory hash equals a freshly created context's."""
+    mark (LS_HWM), so every store kind (scalar, i64, byte, i16, v128, v128 lane, fill,
+    copy, memory.init, a host function's write, host SetMemory, stores into grown pages)
+    must raise the mark, in both frame kernels (LDS frames and VGPR frames, WB_VFRAME).
+    After a Reset each lane reads the fresh image again and the memory hash equals a
+    freshly created context's."""
+    import hostfuncs
     from wasmedge_amd import batch
+    monkeypatch.setenv("WB_VFRAME", "0" if frames == "lds" else "1")
     n = 256
-    rows = [[(i * 4093) % (2 * 65536 - 16) & ~15, i % 7] for i in range(n)]
+    rows = [[(i * 4093) % (2 * 65536 - 16) & ~15, i % 11] for i in range(n)]
     vals = batch.make_values(rows, [I32, I32])
     ctx = batch.BatchContext(WRITER, n, device=0)
     fresh = batch.BatchContext(WRITER, n, device=0)
+    hostfuncs.register(ctx)
     try:
         h0 = fresh.memory_hash()
         r0, st, _ = ctx.execute("poke", vals, 1)
@@ -135,7 +149,10 @@ def test_gpu_reset_restores_fresh_memory(built):
         ctx.set_memory(5, 100000, b"\x01\x02\x03\x04")        # host write, high offset
         r1, st, _ = ctx.execute("poke", vals, 1)              # state persists: sees its writes
         assert (st == 0).all()
-        assert any(int(a) != int(b) for a, b in zip(batch.ret_ints(r0)[:, 0], batch.ret_ints(r1)[:, 0]))
+        for k in range(11):                                   # every store kind wrote
+            assert any(int(a) != int(b) for i, (a, b) in
+                       enumerate(zip(batch.ret_ints(r0)[:, 0], batch.ret_ints(r1)[:, 0]))
+                       if rows[i][1] == k), k
         ctx.reset()
         assert list(ctx.memory_hash()) == list(h0)
         assert ctx.memory(5, 100000, 4) == b"\x00" * 4
@@ -145,3 +162,36 @@ def test_gpu_reset_restores_fresh_memory(built):
     finally:
         ctx.close()
         fresh.close()
+
+
+# an initial memory over 4096 pages puts image rows past 2^26 words,
+# whose interleaved index (row * 64) passes 2^32
+BIG = assemble(r"""
+(module
+  (memory 4097 4097)
+  (data (i32.const 268435556) "\5a\5b\5c\5d")
+  (func (export "touch") (param $x i32) (result i32)
+    (local $old i32)
+    (local.set $old (i32.load (i32.const 268435556)))
+    (i32.store (i32.const 268435556) (local.get $x))
+    (i32.store (i32.const 268500000) (local.get $x))
+    (local.get $old)))
+""")
+
+
+@pytest.mark.gpu
+def test_gpu_reset_memory_over_4096_pages(built):
+    from wasmedge_amd import batch
+    rows = [[0x11111111 * (i + 1)] for i in range(2)]
+    m = O.Module(BIG)
+    ref = [m.run("touch", r) for r in rows]
+    assert [r[1] for r in ref] == [[0x5D5C5B5A]] * 2
+    ctx = batch.BatchContext(BIG, 2, device=0)
+    try:
+        for _ in range(2):                      # fresh instantiation, then after a Reset
+            rets, st, cnt = ctx.execute("touch", batch.make_values(rows, [I32]), 1)
+            got = [[int(v)] for v in batch.ret_ints(rets)[:, 0]]
+            assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == []
+            ctx.reset()
+    finally:
+        ctx.close()

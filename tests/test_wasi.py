@@ -1,0 +1,176 @@
+"""WASI subset on the host-import yield path (VERDICT r1 "missing #8").
+
+The library binds wasi_snapshot_preview1's args_get, args_sizes_get, environ_get,
+environ_sizes_get, fd_write, proc_exit and sched_yield (WasmEdge_BatchInitWASI, the batched
+WasmEdge_ImportObjectCreateWASI). The oracle restates the same functions independently
+from lib/host/wasi/wasifunc.cpp and include/host/wasi/environ.h; the emulator runs the
+library's own wasi_impl.h on the CPU.
+
+Parity: status, return values, instruction count and memory hash per instance, plus each
+instance's captured stdout/stderr bytes and proc_exit code. Reference-held known answer:
+the compiled Rust example tools/wasmedge/examples/add.wasm panics on signed overflow,
+printing Rust's panic message to stderr through fd_write and then aborting (unreachable,
+0x89)."""
+import pytest
+
+import oracle_py as O
+from conftest import golden
+from helpers import compare, emu_run, emu_set_wasi, emu_wasi_output
+from wasmedge_amd.wat import assemble
+
+I32 = 0x7F
+ARGS = ["prog.wasm", "--flag", "", "last arg"]
+ENVS = ["A=1", "PATH=/usr/bin:/bin", "EMPTY="]
+PANIC = (b"thread '<unnamed>' panicked at 'attempt to add with overflow', src/lib.rs:3:10\n"
+         b"note: run with `RUST_BACKTRACE=1` environment variable to display a backtrace\n")
+
+WASI = assemble(r"""
+(module
+  (import "wasi_snapshot_preview1" "args_sizes_get" (func $args_sizes_get (param i32 i32) (result i32)))
+  (import "wasi_snapshot_preview1" "args_get" (func $args_get (param i32 i32) (result i32)))
+  (import "wasi_snapshot_preview1" "environ_sizes_get" (func $env_sizes_get (param i32 i32) (result i32)))
+  (import "wasi_snapshot_preview1" "environ_get" (func $env_get (param i32 i32) (result i32)))
+  (import "wasi_snapshot_preview1" "fd_write" (func $fd_write (param i32 i32 i32 i32) (result i32)))
+  (import "wasi_snapshot_preview1" "proc_exit" (func $proc_exit (param i32)))
+  (import "wasi_snapshot_preview1" "sched_yield" (func $sched_yield (result i32)))
+  (memory 1)
+  (data (i32.const 1024) "hello, lane 0123456789abcdef\n")
+  (func $write (param $fd i32) (param $iovs i32) (param $n i32) (param $nw i32) (result i32)
+    (call $fd_write (local.get $fd) (local.get $iovs) (local.get $n) (local.get $nw)))
+  (func (export "run") (param $x i32) (result i32)
+    (local $r i32) (local $m i32) (local $k i32)
+    (local.set $m (i32.rem_u (local.get $x) (i32.const 12)))
+    (local.set $r (call $args_sizes_get (i32.const 0) (i32.const 4)))
+    (local.set $r (i32.add (local.get $r) (call $args_get (i32.const 16) (i32.const 256))))
+    (local.set $r (i32.add (local.get $r) (call $env_sizes_get (i32.const 8) (i32.const 12))))
+    (local.set $r (i32.add (local.get $r) (call $env_get (i32.const 64) (i32.const 512))))
+    (local.set $r (i32.add (local.get $r) (call $sched_yield)))
+    ;; two iovecs: the greeting, then x%16 bytes of the hex digits
+    (i32.store (i32.const 2048) (i32.const 1024))
+    (i32.store (i32.const 2052) (i32.const 12))
+    (i32.store (i32.const 2056) (i32.const 1036))
+    (i32.store (i32.const 2060) (i32.and (local.get $x) (i32.const 15)))
+    (if (i32.eq (local.get $m) (i32.const 0))          ;; stdout, 1..3 rounds
+      (then (loop $l
+        (local.set $r (i32.add (local.get $r) (call $write (i32.const 1) (i32.const 2048) (i32.const 2) (i32.const 2100))))
+        (local.set $k (i32.add (local.get $k) (i32.const 1)))
+        (br_if $l (i32.lt_u (local.get $k) (i32.add (i32.rem_u (local.get $x) (i32.const 3)) (i32.const 1)))))))
+    (if (i32.eq (local.get $m) (i32.const 1))          ;; stderr
+      (then (local.set $r (i32.add (local.get $r) (call $write (i32.const 2) (i32.const 2048) (i32.const 2) (i32.const 2100))))))
+    (if (i32.eq (local.get $m) (i32.const 2))          ;; stdin: NOTCAPABLE
+      (then (local.set $r (call $write (i32.const 0) (i32.const 2048) (i32.const 2) (i32.const 2100)))))
+    (if (i32.eq (local.get $m) (i32.const 3))          ;; no such fd: BADF
+      (then (local.set $r (call $write (i32.const 7) (i32.const 2048) (i32.const 2) (i32.const 2100)))))
+    (if (i32.eq (local.get $m) (i32.const 4))          ;; more than kIOVMax: INVAL
+      (then (local.set $r (call $write (i32.const 1) (i32.const 2048) (i32.const 1025) (i32.const 2100)))))
+    (if (i32.eq (local.get $m) (i32.const 5))          ;; iovec array out of bounds: FAULT
+      (then (local.set $r (call $write (i32.const 1) (i32.const 65530) (i32.const 1) (i32.const 2100)))))
+    (if (i32.eq (local.get $m) (i32.const 6))          ;; nwritten out of bounds: FAULT
+      (then (local.set $r (call $write (i32.const 1) (i32.const 2048) (i32.const 2) (i32.const 65533)))))
+    (if (i32.eq (local.get $m) (i32.const 7))          ;; a buffer out of bounds: FAULT
+      (then (i32.store (i32.const 2056) (i32.const 65530))
+            (i32.store (i32.const 2060) (i32.const 7))
+            (local.set $r (call $write (i32.const 1) (i32.const 2048) (i32.const 2) (i32.const 2100)))))
+    (if (i32.eq (local.get $m) (i32.const 8))          ;; proc_exit: Terminated
+      (then (call $proc_exit (i32.add (local.get $x) (i32.const 3)))))
+    (if (i32.eq (local.get $m) (i32.const 9))          ;; argv array out of bounds: FAULT
+      (then (local.set $r (call $args_get (i32.const 65528) (i32.const 256)))))
+    (if (i32.eq (local.get $m) (i32.const 10))         ;; args into overlapping areas
+      (then (local.set $r (call $args_get (i32.const 300) (i32.const 296)))))
+    (if (i32.eq (local.get $m) (i32.const 11))         ;; env sizes through one pointer
+      (then (local.set $r (call $env_sizes_get (i32.const 40) (i32.const 40)))))
+    (i32.add (i32.mul (local.get $r) (i32.const 1000)) (i32.load (i32.const 2100)))))
+""")
+
+ROWS = [[x] for x in range(96)]
+
+
+def _oracle(wasm, rows, func="run", page_limit=65536):
+    O.set_wasi(True, ARGS, ENVS)
+    try:
+        m = O.Module(wasm, page_limit=page_limit)
+        out = []
+        for r in rows:
+            inst = O.Instance(m)
+            res = inst.invoke(func, r)
+            out.append((res, inst.wasi_output(1), inst.wasi_output(2), inst.wasi_exit_code()))
+        return out
+    finally:
+        O.set_wasi(False)
+
+
+def test_oracle_wasi_known_answers():
+    """args/env through the reference's layout rules, output bytes, errnos, exit code."""
+    ref = _oracle(WASI, ROWS[:12])
+    (code, vals, _, _), out, err, _ = ref[0]
+    assert code == 0 and out == b"hello, lane " and err == b""
+    assert vals == [0 * 1000 + 12]                    # every call SUCCESS, nwritten = 12 + 0
+    assert ref[1][2] == b"hello, lane 0" and ref[1][0][1] == [13]
+    assert ref[2][0][1][0] // 1000 == 76 and ref[3][0][1][0] // 1000 == 8     # NOTCAPABLE, BADF
+    assert ref[4][0][1][0] // 1000 == 28                                       # INVAL
+    assert [ref[k][0][1][0] // 1000 for k in (5, 6, 7, 9)] == [21] * 4          # FAULT
+    assert ref[8][0][0] == O.TERMINATED and ref[8][3] == 8 + 3
+
+
+def test_emulator_wasi_matches_oracle(built):
+    ref = _oracle(WASI, ROWS)
+    emu_set_wasi(True, ARGS, ENVS)
+    try:
+        got = emu_run(WASI, "run", ROWS, [I32], [I32])
+        outs = [(emu_wasi_output(i, 1), emu_wasi_output(i, 2)) for i in range(len(ROWS))]
+    finally:
+        emu_set_wasi(False)
+    assert compare([r[0] for r in ref], *got, [I32]) == []
+    assert outs == [(r[1], r[2]) for r in ref]
+
+
+def test_rust_panic_message_oracle_and_emulator(built):
+    rows = [[2, 2], [0x7FFFFFFF, 5], [1070428841, 1339305888]]
+    ref = _oracle(golden("rust_add.wasm"), rows, "add", page_limit=32)
+    assert [r[0][:3] for r in ref] == [(0, [4], 53), (0x89, [], 6464), (0x89, [], 6464)]
+    assert ref[1][2] == PANIC and ref[1][1] == b""
+    emu_set_wasi(True, ARGS, ENVS)
+    try:
+        got = emu_run(golden("rust_add.wasm"), "add", rows, [I32, I32], [I32], max_pages=32)
+        errs = [emu_wasi_output(i, 2) for i in range(3)]
+    finally:
+        emu_set_wasi(False)
+    assert compare([r[0] for r in ref], *got, [I32]) == []
+    assert errs == [r[2] for r in ref]
+
+
+def _gpu(wasm, rows, func, ptypes, host_threads=0, **kw):
+    from wasmedge_amd import batch
+    ctx = batch.BatchContext(wasm, len(rows), device=0, host_threads=host_threads, **kw)
+    try:
+        ctx.init_wasi(ARGS, ENVS)
+        rets, st, cnt = ctx.execute(func, batch.make_values(rows, ptypes), 1)
+        h = ctx.memory_hash()
+        ints = batch.ret_ints(rets)
+        vals = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
+        side = [(ctx.wasi_output(i, 1), ctx.wasi_output(i, 2), ctx.wasi_exit_code(i))
+                for i in range(len(rows))]
+        return (vals, st, cnt, h), side
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 0])
+def test_gpu_wasi_matches_oracle(built, threads):
+    """One service thread and the default pool (waves served concurrently)."""
+    rows = [[x] for x in range(640)]
+    ref = _oracle(WASI, rows)
+    got, side = _gpu(WASI, rows, "run", [I32], host_threads=threads)
+    assert compare([r[0] for r in ref], *got, [I32]) == []
+    assert side == [(r[1], r[2], r[3]) for r in ref]
+
+
+@pytest.mark.gpu
+def test_gpu_rust_panic_message(built):
+    rows = [[2, 2], [0x7FFFFFFF, 5], [1070428841, 1339305888]] * 64
+    ref = _oracle(golden("rust_add.wasm"), rows, "add", page_limit=32)
+    got, side = _gpu(golden("rust_add.wasm"), rows, "add", [I32, I32], max_memory_page=32)
+    assert compare([r[0] for r in ref], *got, [I32]) == []
+    assert side == [(r[1], r[2], r[3]) for r in ref]
+    assert side[1][1] == PANIC

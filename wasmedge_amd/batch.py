@@ -56,7 +56,8 @@ class WasmEdgeError(RuntimeError):
 class _Conf(ctypes.Structure):
     _fields_ = [("MaxMemoryPage", ctypes.c_uint32), ("CallStackCells", ctypes.c_uint32),
                 ("MaxSteps", ctypes.c_uint64), ("TimeLimitSeconds", ctypes.c_double),
-                ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64)]
+                ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64),
+                ("HostThreads", ctypes.c_uint32)]
 
 
 class _String(ctypes.Structure):
@@ -152,6 +153,13 @@ def lib():
         L.WasmEdge_BatchInterrupt.argtypes = [vp]
         L.WasmEdge_BatchMemoryGetInstance.restype = u32
         L.WasmEdge_BatchMemoryGetInstance.argtypes = [vp]
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        L.WasmEdge_BatchInitWASI.restype = _Result
+        L.WasmEdge_BatchInitWASI.argtypes = [vp, cpp, u32, cpp, u32]
+        L.WasmEdge_BatchWASIGetExitCode.restype = u32
+        L.WasmEdge_BatchWASIGetExitCode.argtypes = [vp, u32]
+        L.WasmEdge_BatchWASIGetOutput.restype = u32
+        L.WasmEdge_BatchWASIGetOutput.argtypes = [vp, u32, u32, vp, u32]
         _lib = L
     return _lib
 
@@ -190,9 +198,10 @@ class BatchContext:
     """N instances of one module on one GPU (WasmEdge_BatchContext)."""
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
-                 time_limit=0.0, device=-1, cost_limit=0):
+                 time_limit=0.0, device=-1, cost_limit=0, host_threads=0):
         L = lib()
-        conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit)
+        conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit,
+                     host_threads)
         res = _Result(0)
         self._h = L.WasmEdge_BatchCreate(ctypes.byref(conf), bytes(wasm), len(wasm), n,
                                          ctypes.byref(res))
@@ -329,6 +338,24 @@ class BatchContext:
         self._hosts = getattr(self, "_hosts", []) + [cb]   # keep the trampoline alive
         self._check(lib().WasmEdge_BatchAddHostFunction(self._h, self._name(module),
                                                         self._name(name), cb, None))
+
+
+    # built-in WASI subset (WasmEdge_BatchInitWASI): args/envs shared by every instance
+    def init_wasi(self, args=(), envs=()):
+        def arr(v):
+            a = (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
+            return a
+        a, e = arr(list(args)), arr(list(envs))
+        self._check(lib().WasmEdge_BatchInitWASI(self._h, a, len(args), e, len(envs)))
+
+    def wasi_exit_code(self, inst):
+        return lib().WasmEdge_BatchWASIGetExitCode(self._h, inst)
+
+    def wasi_output(self, inst, fd=1):
+        n = lib().WasmEdge_BatchWASIGetOutput(self._h, inst, fd, None, 0)
+        buf = ctypes.create_string_buffer(max(n, 1))
+        lib().WasmEdge_BatchWASIGetOutput(self._h, inst, fd, buf, n)
+        return buf.raw[:n]
 
 
 def ret_ints(rets):

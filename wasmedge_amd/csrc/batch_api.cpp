@@ -10,11 +10,8 @@
 #include <string>
 #include <vector>
 
-#include "../../include/wasmedge_batch.h"
-#include "frontend.h"
-#include "tc.h"
+#include "batch_ctx.h"
 #include "tc_slots.h"
-#include "kparams.h"
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s);
@@ -31,97 +28,8 @@ extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_
                                            uint32_t init_pages, uint32_t init_dropped,
                                            uint32_t nwaves, hipStream_t s);
 
-namespace {
 
-// ErrCodes (include/common/enum.inc)
-constexpr uint8_t kRuntimeError = 0x02, kWrongVMWorkflow = 0x04, kFuncNotFound = 0x05,
-                  kFuncSigMismatch = 0x83, kTableOutOfBounds = 0x87, kMemoryOutOfBounds = 0x88,
-                  kRefTypeMismatch = 0x8E;
-
-std::string g_last_create_error;
-
-WasmEdge_Result R(uint8_t c) { return WasmEdge_Result{c}; }
-
-std::string hexbyte(uint8_t c) {
-  const char *d = "0123456789ABCDEF";
-  return std::string(1, d[c >> 4]) + d[c & 15];
-}
-
-template <typename T>
-struct DevBuf {
-  T *ptr = nullptr;
-  size_t n = 0;
-  ~DevBuf() { if (ptr) (void)hipFree(ptr); }
-  bool alloc(size_t count) {
-    if (ptr) { (void)hipFree(ptr); ptr = nullptr; }
-    n = count;
-    if (count == 0) return true;
-    return hipMalloc(&ptr, sizeof(T) * count) == hipSuccess;
-  }
-  bool upload(const std::vector<T> &v, hipStream_t s) {
-    if (!alloc(v.size() ? v.size() : 1)) return false;
-    if (v.empty()) return true;
-    return hipMemcpyAsync(ptr, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s) == hipSuccess;
-  }
-};
-
-}  // namespace
-
-struct WasmEdge_BatchMemoryContext {   // one instance's linear memory, for host functions
-  WasmEdge_BatchContext *ctx;
-  uint32_t inst;
-};
-
-struct WasmEdge_BatchContext {
-  wb::Program prog;
-  WasmEdge_BatchConfigure conf{};
-  uint32_t n = 0, nwaves = 0;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t ctl_stream = nullptr;  // interrupt requests, while `stream` runs a kernel
-  uint32_t *stop = nullptr;          // uncached device word polled by the kernel
-  uint64_t *stats = nullptr;         // WB_STATS builds: per-wave counters (WB_STATS_OUT)
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::string last_error;
-  // module buffers
-  DevBuf<DInstr> code;
-  DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
-  bool threaded = true;
-  bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
-  uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
-  DevBuf<uint32_t> loops;         // Program::loops (scheduler)
-  DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
-  DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
-  DevBuf<DFunc> funcs;
-  DevBuf<uint8_t> data_pool;
-  // instance state
-  DevBuf<uint32_t> mem, gstack, lstate, params, results, ltab;
-  // host-import yield path (only allocated when the module imports functions)
-  DevBuf<uint32_t> fsave, hcall, hbuf;
-  uint32_t hb_cells = 0;
-  struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; };
-  std::vector<HostFn> hosts;      // per function index (imports only)
-  DevBuf<uint8_t> status;
-  DevBuf<uint64_t> counts, hashes;
-  uint32_t image_words = 0, init_dropped = 0;
-  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
-  // current invocation
-  int func = -1;
-  uint32_t param_cells = 0, result_cells = 0;
-  std::vector<uint8_t> result_types;
-  bool ran = false;         // a Run completed since the last Reset (results are valid)
-  bool mem_fresh = true;    // memory never initialised: the next Reset writes every page
-
-  uint8_t fail(uint8_t code, const std::string &m) {
-    last_error = m;
-    return code;
-  }
-  bool hip_ok(hipError_t e, const char *what) {
-    if (e == hipSuccess) return true;
-    last_error = std::string(what) + ": " + hipGetErrorString(e);
-    return false;
-  }
-};
+using namespace wbh;
 
 namespace {
 
@@ -262,39 +170,6 @@ uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
 
 // One interpreter launch over every instance: entry_pc with the staged params (or the
 // start function when is_start). Shared by BatchRun and BatchReset.
-// Read (dst) or write (src) bytes of one instance's linear memory: gather the lane's
-// interleaved words (word w of lane l in wave v at ((v*W + w)*64 + l)), patch, scatter.
-uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
-               uint8_t *Dst, const uint8_t *Src) {
-  if (Inst >= C->n) return C->fail(kRuntimeError, "instance index out of range");
-  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
-  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
-  if (Len == 0) return 0;
-  const uint32_t wave = Inst / 64, lane = Inst % 64;
-  const uint32_t w0 = Off / 4, w1 = uint32_t((uint64_t(Off) + Len + 3) / 4);
-  const size_t pitch = 64 * sizeof(uint32_t);
-  uint32_t *base = C->mem.ptr + (size_t(wave) * C->mem_words + w0) * 64 + lane;
-  std::vector<uint32_t> words(w1 - w0);
-  if (!C->hip_ok(hipMemcpy2D(words.data(), 4, base, pitch, 4, words.size(), hipMemcpyDeviceToHost), "memory"))
-    return kRuntimeError;
-  uint8_t *bytes = reinterpret_cast<uint8_t *>(words.data()) + (Off & 3);
-  if (Dst) { memcpy(Dst, bytes, Len); return 0; }
-  memcpy(bytes, Src, Len);
-  if (!C->hip_ok(hipMemcpy2D(base, pitch, words.data(), 4, 4, words.size(), hipMemcpyHostToDevice), "memory"))
-    return kRuntimeError;
-  // raise the lane's write mark (LS_HWM) so the next Reset re-initialises these bytes
-  uint32_t *mark = C->lstate.ptr + (size_t(wave) * C->ls_slots + LS_HWM) * 64 + lane;
-  uint32_t hw = 0;
-  if (!C->hip_ok(hipMemcpy(&hw, mark, 4, hipMemcpyDeviceToHost), "memory"))
-    return kRuntimeError;
-  const uint64_t end = uint64_t(Off) + Len;
-  if (end > hw) {
-    hw = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(end);
-    if (!C->hip_ok(hipMemcpy(mark, &hw, 4, hipMemcpyHostToDevice), "memory")) return kRuntimeError;
-  }
-  return 0;
-}
-
 uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, bool resume,
                     double *KernelSeconds) {
   const wb::Program &P = C->prog;
@@ -366,62 +241,6 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   return 0;
 }
 
-// Service every lane parked at a host import (helper.cpp:35-97 on the CPU executor):
-// call its host function with the args the kernel staged in hbuf, stage the results
-// (or end the lane with the host's ErrCode; Terminated 0x01 ends it too, engine.cpp:
-// 62-64). Returns the number of lanes to resume, or -1 on a device error.
-int64_t service_host_calls(WasmEdge_BatchContext *C) {
-  const wb::Program &P = C->prog;
-  const uint32_t n = C->n, hb = C->hb_cells;
-  std::vector<uint8_t> st(n);
-  if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, n, hipMemcpyDeviceToHost), "status"))
-    return -1;
-  std::vector<uint32_t> parked;
-  for (uint32_t i = 0; i < n; i++)
-    if (st[i] == WB_ERR_HOST_CALL) parked.push_back(i);
-  if (parked.empty()) return 0;
-  std::vector<uint32_t> hcall(n), hbuf(size_t(n) * hb);
-  if (!C->hip_ok(hipMemcpy(hcall.data(), C->hcall.ptr, size_t(n) * 4, hipMemcpyDeviceToHost), "hcall") ||
-      !C->hip_ok(hipMemcpy(hbuf.data(), C->hbuf.ptr, hbuf.size() * 4, hipMemcpyDeviceToHost), "hbuf"))
-    return -1;
-  int64_t resumed = 0;
-  std::vector<WasmEdge_Value> args, rets;
-  for (uint32_t i : parked) {
-    const uint32_t f = hcall[i];
-    const WasmEdge_BatchContext::HostFn h = f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
-    if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
-    const wb::FuncType &t = P.types[P.funcs[f].type];
-    uint32_t *cells = &hbuf[size_t(i) * hb];
-    args.assign(t.params.size(), WasmEdge_Value{});
-    rets.assign(t.results.size(), WasmEdge_Value{});
-    uint32_t at = 0;
-    for (size_t k = 0; k < t.params.size(); k++) {
-      uint128_t v = 0;
-      for (uint32_t q = 0; q < wb::cells_of(t.params[k]); q++) v |= uint128_t(cells[at++]) << (32 * q);
-      args[k].Value = v;
-      args[k].Type = static_cast<enum WasmEdge_ValType>(t.params[k]);
-    }
-    for (size_t k = 0; k < t.results.size(); k++) rets[k].Type = static_cast<enum WasmEdge_ValType>(t.results[k]);
-    WasmEdge_BatchMemoryContext mc{C, i};
-    const WasmEdge_Result r = h.fn(h.data, &mc, args.data(), rets.data());
-    if (r.Code) {            // host error or Terminated: the lane ends with that code
-      st[i] = r.Code;
-      hcall[i] = 0xFFFFFFFFu;
-      continue;
-    }
-    at = 0;
-    for (size_t k = 0; k < t.results.size(); k++)
-      for (uint32_t q = 0; q < wb::cells_of(t.results[k]); q++) cells[at++] = uint32_t(rets[k].Value >> (32 * q));
-    hcall[i] = at;
-    resumed++;
-  }
-  if (!C->hip_ok(hipMemcpy(C->status.ptr, st.data(), n, hipMemcpyHostToDevice), "status") ||
-      !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
-      !C->hip_ok(hipMemcpy(C->hbuf.ptr, hbuf.data(), hbuf.size() * 4, hipMemcpyHostToDevice), "hbuf"))
-    return -1;
-  return resumed;
-}
-
 // One interpreter invocation over every instance: entry_pc with the staged params (or the
 // start function when is_start), then host-import rounds until no lane is parked.
 // Shared by BatchRun and BatchReset.
@@ -456,6 +275,7 @@ WasmEdge_BatchContext *WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf,
   auto *C = new WasmEdge_BatchContext();
   if (Conf) C->conf = *Conf;
   else C->conf.DeviceOrdinal = -1;
+  C->host_threads = C->conf.HostThreads;
   C->n = NumInstances;
   uint8_t e = setup(C, WasmBuf, WasmLen);
   if (!e) e = WasmEdge_BatchReset(C, nullptr).Code;   // instantiate every instance
@@ -788,12 +608,14 @@ uint32_t WasmEdge_BatchMemoryGetInstance(const WasmEdge_BatchMemoryContext *M) {
 WasmEdge_Result WasmEdge_BatchMemoryGetData(const WasmEdge_BatchMemoryContext *M, uint8_t *Data,
                                             const uint32_t Offset, const uint32_t Length) {
   if (!M) return R(kWrongVMWorkflow);
+  if (M->view) return R(M->view->rw(M->inst % 64, Offset, Length, Data, nullptr));
   return R(mem_rw(M->ctx, M->inst, Offset, Length, Data, nullptr));
 }
 
 WasmEdge_Result WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *M, const uint8_t *Data,
                                             const uint32_t Offset, const uint32_t Length) {
   if (!M) return R(kWrongVMWorkflow);
+  if (M->view) return R(M->view->rw(M->inst % 64, Offset, Length, nullptr, Data));
   return R(mem_rw(M->ctx, M->inst, Offset, Length, nullptr, Data));
 }
 

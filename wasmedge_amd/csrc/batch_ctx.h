@@ -1,0 +1,153 @@
+// batch_ctx.h -- the batch context shared by the C-ABI translation units
+// (batch_api.cpp: create/run/results; hostcall.cpp: the host-import service rounds;
+// wasi.cpp: the built-in WASI subset). Host-only; never included by device code.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wasmedge_batch.h"
+#include "frontend.h"
+#include "tc.h"
+#include "kparams.h"
+#include "wasi_impl.h"
+
+namespace wbh {
+
+// ErrCodes (include/common/enum.inc)
+constexpr uint8_t kRuntimeError = 0x02, kWrongVMWorkflow = 0x04, kFuncNotFound = 0x05,
+                  kFuncSigMismatch = 0x83, kTableOutOfBounds = 0x87, kMemoryOutOfBounds = 0x88,
+                  kRefTypeMismatch = 0x8E;
+
+inline std::string g_last_create_error;
+
+inline WasmEdge_Result R(uint8_t c) { return WasmEdge_Result{c}; }
+
+inline std::string hexbyte(uint8_t c) {
+  const char *d = "0123456789ABCDEF";
+  return std::string(1, d[c >> 4]) + d[c & 15];
+}
+
+template <typename T>
+struct DevBuf {
+  T *ptr = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (ptr) (void)hipFree(ptr); }
+  bool alloc(size_t count) {
+    if (ptr) { (void)hipFree(ptr); ptr = nullptr; }
+    n = count;
+    if (count == 0) return true;
+    return hipMalloc(&ptr, sizeof(T) * count) == hipSuccess;
+  }
+  bool upload(const std::vector<T> &v, hipStream_t s) {
+    if (!alloc(v.size() ? v.size() : 1)) return false;
+    if (v.empty()) return true;
+    return hipMemcpyAsync(ptr, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  }
+};
+
+}  // namespace wbh
+
+namespace wbh { struct WaveView; }
+
+struct WasmEdge_BatchMemoryContext {   // one instance's linear memory, for host functions
+  WasmEdge_BatchContext *ctx;
+  uint32_t inst;
+  wbh::WaveView *view;                 // the service round's cached view of its wave (or NULL)
+};
+
+struct WasmEdge_BatchContext {
+  template <typename T> using DevBuf = wbh::DevBuf<T>;
+  wb::Program prog;
+  WasmEdge_BatchConfigure conf{};
+  uint32_t n = 0, nwaves = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t ctl_stream = nullptr;  // interrupt requests, while `stream` runs a kernel
+  uint32_t *stop = nullptr;          // uncached device word polled by the kernel
+  uint64_t *stats = nullptr;         // WB_STATS builds: per-wave counters (WB_STATS_OUT)
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string last_error;
+  // module buffers
+  DevBuf<DInstr> code;
+  DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
+  bool threaded = true;
+  bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
+  uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
+  DevBuf<uint32_t> loops;         // Program::loops (scheduler)
+  DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
+  DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
+  DevBuf<DFunc> funcs;
+  DevBuf<uint8_t> data_pool;
+  // instance state
+  DevBuf<uint32_t> mem, gstack, lstate, params, results, ltab;
+  // host-import yield path (only allocated when the module imports functions)
+  DevBuf<uint32_t> fsave, hcall, hbuf;
+  uint32_t hb_cells = 0;
+  struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; };
+  std::vector<HostFn> hosts;      // per function index (imports only)
+  uint32_t host_threads = 0;      // service-round worker threads (0 = min(16, cores))
+  // built-in WASI subset (wasi.cpp): args/envs shared by every instance, captured
+  // stdout/stderr and the proc_exit code per instance
+  struct WasiSlot { WasmEdge_BatchContext *ctx; int fn; };
+  wbw::Env wasi_env;
+  std::vector<wbw::Lane> wasi_lanes;
+  std::vector<WasiSlot> wasi_slots;   // per function index (Data of its HostFn)
+  DevBuf<uint8_t> status;
+  DevBuf<uint64_t> counts, hashes;
+  uint32_t image_words = 0, init_dropped = 0;
+  uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
+  // current invocation
+  int func = -1;
+  uint32_t param_cells = 0, result_cells = 0;
+  std::vector<uint8_t> result_types;
+  bool ran = false;         // a Run completed since the last Reset (results are valid)
+  bool mem_fresh = true;    // memory never initialised: the next Reset writes every page
+
+  uint8_t fail(uint8_t code, const std::string &m) {
+    last_error = m;
+    return code;
+  }
+  bool hip_ok(hipError_t e, const char *what) {
+    if (e == hipSuccess) return true;
+    last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return false;
+  }
+};
+
+namespace wbh {
+
+constexpr uint32_t kBlockWords = 1024;   // host-view block: 4 KiB of each of a wave's 64 lanes
+
+// Word `w` of instance `inst`'s linear memory in the lane-interleaved layout
+// (word w of lane l in wave v at ((v*W + w)*64 + l)).
+inline size_t mem_word(const WasmEdge_BatchContext *C, uint32_t inst, uint64_t w) {
+  return (size_t(inst / 64) * C->mem_words + w) * 64 + inst % 64;
+}
+
+// The host's view of one wave's linear memories during a host-call service round
+// (hostcall.cpp): blocks of kBlockWords rows (256 KiB, contiguous on the device) are
+// fetched on first touch and written back once at the end of the wave, and the lanes'
+// page counts and write marks come from one copy of the instance state per round.
+struct WaveView {
+  WasmEdge_BatchContext *C = nullptr;
+  uint32_t wave = 0;
+  const uint32_t *pages = nullptr;   // [64]
+  uint32_t *hwm = nullptr;           // [64], raised by writes
+  bool hwm_dirty = false, ok = true;
+  struct Block { std::vector<uint32_t> w; bool dirty = false; };
+  std::vector<std::pair<uint32_t, Block>> blocks;
+  Block *block(uint32_t b);
+  // bytes [off, off+len) of `lane`; 0 or MemoryOutOfBounds (0x88) / RuntimeError
+  uint8_t rw(uint32_t lane, uint32_t off, uint32_t len, uint8_t *dst, const uint8_t *src);
+  bool flush();
+};
+
+uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
+               uint8_t *Dst, const uint8_t *Src);
+int64_t service_host_calls(WasmEdge_BatchContext *C);
+uint64_t mem_size(const WasmEdge_BatchMemoryContext *M);   // bytes of the instance's memory
+
+}  // namespace wbh

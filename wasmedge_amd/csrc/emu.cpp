@@ -5,6 +5,7 @@
 // loads; the product path (libwasmedge_batch.so) has no CPU execution path.
 #define WB_MSHIFT 0
 #define WB_MARK(ea, n) ((void)0)   // the emulator re-creates memory per instance
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -13,6 +14,7 @@
 #include "dbc_ops.h"
 #include "frontend.h"
 #include "kparams.h"
+#include "wasi_impl.h"
 
 static std::string g_err;
 static uint64_t *g_hist = nullptr;   // optional per-op dispatch histogram (tuning aid)
@@ -26,6 +28,25 @@ typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
                              uint32_t *rets, uint8_t *mem, uint64_t mem_bytes);
 static wb_emu_host_t g_host = nullptr;
 static uint64_t g_cost_limit = ~0ull;   // exact unit-cost gas limit (0 = none)
+// the library's WASI subset (wasi_impl.h), bound before g_host when on
+static bool g_wasi = false;
+static wbw::Env g_wasi_env;
+static std::vector<wbw::Lane> g_wasi_lanes;
+struct EmuMem final : wbw::MemIO {
+  uint8_t *mb; uint64_t bytes; bool has;
+  bool present() override { return has; }
+  uint64_t size() override { return bytes; }
+  bool read(uint32_t off, uint32_t len, uint8_t *dst) override {
+    if (uint64_t(off) + len > bytes) return false;
+    memcpy(dst, mb + off, len);
+    return true;
+  }
+  bool write(uint32_t off, uint32_t len, const uint8_t *src) override {
+    if (uint64_t(off) + len > bytes) return false;
+    memcpy(mb + off, src, len);
+    return true;
+  }
+};
 
 extern "C" {
 
@@ -43,6 +64,23 @@ __attribute__((visibility("default"))) void wb_emu_set_pc_trace(uint32_t *buf, u
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
+// WASI subset on (args/envs shared by every instance) or off; outputs per instance of the
+// last wb_emu_execute
+__attribute__((visibility("default"))) void wb_emu_set_wasi(int on, const char *const *args, uint32_t nargs,
+                                                            const char *const *envs, uint32_t nenvs) {
+  g_wasi = on != 0;
+  g_wasi_env.args.assign(args, args + nargs);
+  g_wasi_env.envs.assign(envs, envs + nenvs);
+}
+__attribute__((visibility("default"))) uint32_t wb_emu_wasi_output(uint32_t inst, uint32_t fd, uint8_t *buf, uint32_t len) {
+  if (inst >= g_wasi_lanes.size() || (fd != 1 && fd != 2)) return 0;
+  const std::string &o = g_wasi_lanes[inst].out[fd - 1];
+  if (buf) memcpy(buf, o.data(), std::min<size_t>(len, o.size()));
+  return uint32_t(o.size());
+}
+__attribute__((visibility("default"))) uint32_t wb_emu_wasi_exit_code(uint32_t inst) {
+  return inst < g_wasi_lanes.size() ? g_wasi_lanes[inst].exit_code : 0;
+}
 
 // Returns ErrCode of the call; per-instance outputs like WasmEdge_BatchExecute.
 // params: [n][param cells] u32; results: [n][result cells] u32.
@@ -95,6 +133,13 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define EDROP edrop
   std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
   std::vector<uint32_t> memv;
+  // imports served by the WASI subset (wasi_impl.h), per function index
+  std::vector<int> wasi_fn(P.funcs.size(), -1);
+  g_wasi_lanes.assign(g_wasi ? n : 0, wbw::Lane{});
+  for (uint32_t f = 0; g_wasi && f < P.n_imported; f++)
+    if (P.funcs[f].import_module == "wasi_snapshot_preview1")
+      wasi_fn[f] = wbw::lookup(P.funcs[f].import_name, P.types[P.funcs[f].type].params,
+                               P.types[P.funcs[f].type].results);
   for (uint32_t inst = 0; inst < n; inst++) {
     // instantiate: memory image + globals
     memv.assign(size_t(budget) << 14, 0u);
@@ -169,11 +214,19 @@ __attribute__((visibility("default"))) int wb_emu_execute(
         }
         count += (int64_t)add;
         pc = npc;
-        if (status == WB_ERR_HOST_CALL && g_host) {   // run the host function inline
+        const int wfn = status == WB_ERR_HOST_CALL ? wasi_fn[ycall] : -1;
+        if (status == WB_ERR_HOST_CALL && (g_host || wfn >= 0)) {   // run the host function inline
           const wb::FuncType &ht = P.types[P.funcs[ycall].type];
           uint32_t rets[64] = {0}, nr = 0;
           for (uint8_t t : ht.results) nr += wb::cells_of(t);
-          const int e = g_host(inst, ycall, &fr[ybase], rets, mb, uint64_t(pages) << 16);
+          int e;
+          if (wfn >= 0) {
+            EmuMem em;
+            em.mb = mb; em.bytes = uint64_t(pages) << 16; em.has = P.has_mem;
+            e = wbw::call(wfn, g_wasi_env, g_wasi_lanes[inst], em, &fr[ybase], &rets[0]);
+          } else {
+            e = g_host(inst, ycall, &fr[ybase], rets, mb, uint64_t(pages) << 16);
+          }
           if (e) { status = uint32_t(e); break; }
           for (uint32_t k = 0; k < nr; k++) W32(ybase + k, rets[k]);
           status = WB_STATUS_RUNNING;

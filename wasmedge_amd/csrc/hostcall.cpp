@@ -1,0 +1,216 @@
+// hostcall.cpp -- the host side of the import yield path: lanes parked
+// at a host import are served on the CPU between kernel launches, the batched form of the
+// reference's host-function call (lib/executor/helper.cpp:35-97, hostfunc.h:25-40).
+//
+// A service round moves data in bulk, never per lane:
+//   * status, the import index (hcall) and the staged arguments (hbuf) of every lane:
+//     one copy each;
+//   * the page counts and write marks of every lane: one strided copy each (one 256-byte
+//     row per wave);
+//   * linear memory: a host function's reads and writes go to a WaveView, which fetches
+//     a 256 KiB block (4 KiB of each of the wave's 64 lanes, contiguous in the lane-
+//     interleaved layout) the first time any lane of the wave touches it and writes the
+//     dirty blocks back once, after the wave's last lane. 64K lanes calling fd_write on
+//     the same stack page thus cost 1024 block copies, not 64K x several strided ones.
+// Waves are served by a pool of host threads (a wave's lanes and blocks belong to one
+// thread), so host functions must be reentrant, as the reference's are under its
+// concurrent VM::execute (include/vm/vm.h:137-141).
+#include <algorithm>
+#include <atomic>
+#include <thread>
+
+#include "batch_ctx.h"
+
+namespace wbh {
+
+WaveView::Block *WaveView::block(uint32_t b) {
+  for (auto &e : blocks)
+    if (e.first == b) return &e.second;
+  const size_t rows = std::min<size_t>(kBlockWords, size_t(C->mem_words) - size_t(b) * kBlockWords);
+  Block blk;
+  blk.w.resize(rows * 64);
+  const uint32_t *src = C->mem.ptr + (size_t(wave) * C->mem_words + size_t(b) * kBlockWords) * 64;
+  if (hipMemcpy(blk.w.data(), src, blk.w.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+    ok = false;
+    return nullptr;
+  }
+  blocks.emplace_back(b, std::move(blk));
+  return &blocks.back().second;
+}
+
+uint8_t WaveView::rw(uint32_t lane, uint32_t off, uint32_t len, uint8_t *dst, const uint8_t *src) {
+  const uint64_t end = uint64_t(off) + len;
+  if (end > (uint64_t(pages[lane]) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
+  uint64_t a = off;
+  while (a < end) {
+    const uint32_t w = uint32_t(a >> 2), b = w / kBlockWords;
+    Block *blk = block(b);
+    if (!blk) return kRuntimeError;
+    // bytes of this block: up to the block's last word
+    const uint64_t bend = std::min<uint64_t>(end, uint64_t(b + 1) * kBlockWords * 4);
+    for (; a < bend; a++) {
+      uint32_t &word = blk->w[size_t((a >> 2) % kBlockWords) * 64 + lane];
+      const uint32_t sh = 8 * uint32_t(a & 3);
+      if (dst) *dst++ = uint8_t(word >> sh);
+      else word = (word & ~(0xFFu << sh)) | (uint32_t(*src++) << sh);
+    }
+    if (src) blk->dirty = true;
+  }
+  if (src && len && end > hwm[lane]) {   // raise the write mark: Reset re-inits these bytes
+    hwm[lane] = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(end);
+    hwm_dirty = true;
+  }
+  return 0;
+}
+
+bool WaveView::flush() {
+  for (auto &e : blocks) {
+    if (!e.second.dirty) continue;
+    uint32_t *dst = C->mem.ptr + (size_t(wave) * C->mem_words + size_t(e.first) * kBlockWords) * 64;
+    if (hipMemcpy(dst, e.second.w.data(), e.second.w.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      ok = false;
+  }
+  blocks.clear();
+  return ok;
+}
+
+uint64_t mem_size(const WasmEdge_BatchMemoryContext *M) {
+  if (M->view) return uint64_t(M->view->pages[M->inst % 64]) << 16;
+  return uint64_t(WasmEdge_BatchGetMemoryPages(M->ctx, M->inst)) << 16;
+}
+
+// Read (dst) or write (src) bytes of one instance's linear memory outside a service round
+// (WasmEdge_BatchGetMemory/SetMemory): gather the lane's interleaved words, patch, scatter.
+uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
+               uint8_t *Dst, const uint8_t *Src) {
+  if (Inst >= C->n) return C->fail(kRuntimeError, "instance index out of range");
+  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
+  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
+  if (Len == 0) return 0;
+  const uint32_t w0 = Off / 4, w1 = uint32_t((uint64_t(Off) + Len + 3) / 4);
+  const size_t pitch = 64 * sizeof(uint32_t);
+  uint32_t *base = C->mem.ptr + mem_word(C, Inst, w0);
+  std::vector<uint32_t> words(w1 - w0);
+  if (!C->hip_ok(hipMemcpy2D(words.data(), 4, base, pitch, 4, words.size(), hipMemcpyDeviceToHost), "memory"))
+    return kRuntimeError;
+  uint8_t *bytes = reinterpret_cast<uint8_t *>(words.data()) + (Off & 3);
+  if (Dst) { memcpy(Dst, bytes, Len); return 0; }
+  memcpy(bytes, Src, Len);
+  if (!C->hip_ok(hipMemcpy2D(base, pitch, words.data(), 4, 4, words.size(), hipMemcpyHostToDevice), "memory"))
+    return kRuntimeError;
+  // raise the lane's write mark (LS_HWM) so the next Reset re-initialises these bytes
+  uint32_t *mark = C->lstate.ptr + (size_t(Inst / 64) * C->ls_slots + LS_HWM) * 64 + Inst % 64;
+  uint32_t hw = 0;
+  if (!C->hip_ok(hipMemcpy(&hw, mark, 4, hipMemcpyDeviceToHost), "memory"))
+    return kRuntimeError;
+  const uint64_t end = uint64_t(Off) + Len;
+  if (end > hw) {
+    hw = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(end);
+    if (!C->hip_ok(hipMemcpy(mark, &hw, 4, hipMemcpyHostToDevice), "memory")) return kRuntimeError;
+  }
+  return 0;
+}
+
+// Serve every lane parked at a host import: call its host function with the args the
+// kernel staged in hbuf, stage the results (or end the lane with the host's ErrCode;
+// Terminated 0x01 ends it too, engine.cpp:62-64). Returns the number of lanes to resume,
+// or -1 on a device error.
+int64_t service_host_calls(WasmEdge_BatchContext *C) {
+  const wb::Program &P = C->prog;
+  const uint32_t n = C->n, hb = C->hb_cells, nw = C->nwaves;
+  std::vector<uint8_t> st(n);
+  if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, n, hipMemcpyDeviceToHost), "status"))
+    return -1;
+  // parked lanes grouped by wave: waves[k] = (wave, first index into `parked`)
+  std::vector<uint32_t> parked;
+  std::vector<std::pair<uint32_t, uint32_t>> waves;
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] == WB_ERR_HOST_CALL) {
+      if (waves.empty() || waves.back().first != i / 64) waves.emplace_back(i / 64, uint32_t(parked.size()));
+      parked.push_back(i);
+    }
+  if (parked.empty()) return 0;
+  waves.emplace_back(nw, uint32_t(parked.size()));   // sentinel
+  std::vector<uint32_t> hcall(n), hbuf(size_t(n) * hb);
+  if (!C->hip_ok(hipMemcpy(hcall.data(), C->hcall.ptr, size_t(n) * 4, hipMemcpyDeviceToHost), "hcall") ||
+      !C->hip_ok(hipMemcpy(hbuf.data(), C->hbuf.ptr, hbuf.size() * 4, hipMemcpyDeviceToHost), "hbuf"))
+    return -1;
+  // page counts and write marks: one 256-byte row per wave each
+  const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+  std::vector<uint32_t> pages(size_t(nw) * 64, 0), hwm(size_t(nw) * 64, 0);
+  if (P.has_mem &&
+      (!C->hip_ok(hipMemcpy2D(pages.data(), row, C->lstate.ptr + LS_PAGES * 64, pitch, row, nw,
+                              hipMemcpyDeviceToHost), "pages") ||
+       !C->hip_ok(hipMemcpy2D(hwm.data(), row, C->lstate.ptr + LS_HWM * 64, pitch, row, nw,
+                              hipMemcpyDeviceToHost), "write marks")))
+    return -1;
+
+  std::atomic<uint32_t> next{0};
+  std::atomic<int64_t> resumed{0};
+  std::atomic<bool> failed{false}, hwm_dirty{false};
+  auto worker = [&]() {
+    (void)hipSetDevice(C->device);   // the device is per host thread
+    std::vector<WasmEdge_Value> args, rets;
+    for (uint32_t k; (k = next.fetch_add(1)) + 1 < waves.size();) {
+      WaveView view;
+      view.C = C;
+      view.wave = waves[k].first;
+      view.pages = &pages[size_t(view.wave) * 64];
+      view.hwm = &hwm[size_t(view.wave) * 64];
+      for (uint32_t j = waves[k].second; j < waves[k + 1].second; j++) {
+        const uint32_t i = parked[j], f = hcall[i];
+        const WasmEdge_BatchContext::HostFn h =
+            f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
+        if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
+        const wb::FuncType &t = P.types[P.funcs[f].type];
+        uint32_t *cells = &hbuf[size_t(i) * hb];
+        args.assign(t.params.size(), WasmEdge_Value{});
+        rets.assign(t.results.size(), WasmEdge_Value{});
+        uint32_t at = 0;
+        for (size_t q = 0; q < t.params.size(); q++) {
+          uint128_t v = 0;
+          for (uint32_t c = 0; c < wb::cells_of(t.params[q]); c++) v |= uint128_t(cells[at++]) << (32 * c);
+          args[q].Value = v;
+          args[q].Type = static_cast<enum WasmEdge_ValType>(t.params[q]);
+        }
+        for (size_t q = 0; q < t.results.size(); q++)
+          rets[q].Type = static_cast<enum WasmEdge_ValType>(t.results[q]);
+        WasmEdge_BatchMemoryContext mc{C, i, &view};
+        const WasmEdge_Result r = h.fn(h.data, &mc, args.data(), rets.data());
+        if (r.Code) {            // host error or Terminated: the lane ends with that code
+          st[i] = r.Code;
+          hcall[i] = 0xFFFFFFFFu;
+          continue;
+        }
+        at = 0;
+        for (size_t q = 0; q < t.results.size(); q++)
+          for (uint32_t c = 0; c < wb::cells_of(t.results[q]); c++) cells[at++] = uint32_t(rets[q].Value >> (32 * c));
+        hcall[i] = at;
+        resumed.fetch_add(1);
+      }
+      if (!view.flush()) failed = true;
+      if (view.hwm_dirty) hwm_dirty = true;
+    }
+  };
+  uint32_t threads = C->host_threads ? C->host_threads
+                                     : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  threads = std::min<uint32_t>(threads, uint32_t(waves.size() - 1));
+  if (threads <= 1) {
+    worker();
+  } else {
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < threads; t++) pool.emplace_back(worker);
+    for (auto &th : pool) th.join();
+  }
+  if (failed) { C->last_error = "host-call memory view: device copy failed"; return -1; }
+  if (!C->hip_ok(hipMemcpy(C->status.ptr, st.data(), n, hipMemcpyHostToDevice), "status") ||
+      !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
+      !C->hip_ok(hipMemcpy(C->hbuf.ptr, hbuf.data(), hbuf.size() * 4, hipMemcpyHostToDevice), "hbuf"))
+    return -1;
+  if (hwm_dirty && !C->hip_ok(hipMemcpy2D(C->lstate.ptr + LS_HWM * 64, pitch, hwm.data(), row, row, nw,
+                                          hipMemcpyHostToDevice), "write marks"))
+    return -1;
+  return resumed.load();
+}
+
+}  // namespace wbh
