@@ -133,7 +133,10 @@ def gpu_run(wasm, func, arg_rows, ptypes, rtypes, **kw):
         ctx.close()
 
 
-def compare(oracle_rows, rets, st, cnt, h, rtypes, check_hash=True):
+def compare(oracle_rows, rets, st, cnt, h, rtypes, check_hash=True, exact=False):
+    """Differences between oracle rows (code, values, count, memhash) and a device /
+    emulator run. exact=True compares NaN return payloads bit for bit (no canon) and the
+    memory hash of trapped instances too (memory as the trap left it)."""
     bad = []
     for i, (code, vals, ocnt, oh) in enumerate(oracle_rows):
         if int(st[i]) != code:
@@ -142,10 +145,10 @@ def compare(oracle_rows, rets, st, cnt, h, rtypes, check_hash=True):
         if int(cnt[i]) != ocnt:
             bad.append((i, "count", ocnt, int(cnt[i])))
         if code == 0:
-            a = [canon(v, t) for v, t in zip(vals, rtypes)]
-            b = [canon(v, t) for v, t in zip(rets[i], rtypes)]
+            a = list(vals) if exact else [canon(v, t) for v, t in zip(vals, rtypes)]
+            b = list(rets[i]) if exact else [canon(v, t) for v, t in zip(rets[i], rtypes)]
             if a != b:
                 bad.append((i, "ret", vals, rets[i]))
-        if check_hash and code == 0 and int(h[i]) != oh:
+        if check_hash and (code == 0 or exact) and int(h[i]) != oh:
             bad.append((i, "memhash", oh, int(h[i])))
     return bad

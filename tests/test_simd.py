@@ -25,11 +25,11 @@ def test_simd_emulator_parity(built):
     ref = oracle_run(m, "simd", ROWS)
     assert all(r[0] == 0 for r in ref)
     rets, st, cnt, h = emu_run(wasm, "simd", ROWS, [I32], [I64])
-    assert compare(ref, rets, st, cnt, h, [I64]) == []
+    assert compare(ref, rets, st, cnt, h, [I64], exact=True) == []
     ref = oracle_run(m, "lane_oob", OOB_ROWS)
     assert {r[0] for r in ref} == {0, 0x88}
     rets, st, cnt, h = emu_run(wasm, "lane_oob", OOB_ROWS, [I32, I32], [I32])
-    assert compare(ref, rets, st, cnt, h, [I32]) == []
+    assert compare(ref, rets, st, cnt, h, [I32], exact=True) == []
 
 
 @pytest.mark.gpu
@@ -38,7 +38,7 @@ def test_gpu_simd_parity(built):
     m = O.Module(wasm)
     ref = oracle_run(m, "simd", ROWS)
     rets, st, cnt, h = gpu_run(wasm, "simd", ROWS, [I32], [I64])
-    assert compare(ref, rets, st, cnt, h, [I64]) == []
+    assert compare(ref, rets, st, cnt, h, [I64], exact=True) == []
     ref = oracle_run(m, "lane_oob", OOB_ROWS)
     rets, st, cnt, h = gpu_run(wasm, "lane_oob", OOB_ROWS, [I32, I32], [I32])
-    assert compare(ref, rets, st, cnt, h, [I32]) == []
+    assert compare(ref, rets, st, cnt, h, [I32], exact=True) == []

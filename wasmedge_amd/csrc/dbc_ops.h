@@ -57,6 +57,11 @@ WB_HD bool isnan32(uint32_t a) { return (a & 0x7FFFFFFFu) > 0x7F800000u; }
 WB_HD bool isnan64(uint64_t a) {
   return (a & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
 }
+// ceil/floor/trunc (unary_numeric.ipp:73-86, 358-398): g++ -O2 expands std::ceil/floor/trunc
+// inline with SSE2 (|x| >= 2^23 or unordered -> x), so a NaN operand comes back unchanged,
+// signalling ones included (tools/nan_probe.cpp); nearest calls libm roundeven, which quiets.
+WB_HD uint32_t nan_keep32(uint32_t r, uint32_t a) { return sel32(isnan32(a), a, r); }
+WB_HD uint64_t nan_keep64(uint64_t r, uint64_t a) { return sel64(isnan64(a), a, r); }
 
 // binary_numeric.ipp:155-191 (scalar min/max with its NaN/zero rules; raw NaN payload)
 WB_HD uint32_t fmin32(uint32_t a, uint32_t b) {
@@ -273,9 +278,9 @@ WB_HD void vunx(uint32_t sub, const uint32_t *x, uint32_t *r) {
     case 0x62: WB_LU(1, __builtin_popcount(a));
     case 0x80: WB_LU(2, as < 0 ? 0u - a : a);
     case 0x81: WB_LU(2, 0u - a);
-    case 0x67: WB_LU(4, nan_fix32(b32(ceilf(f32(a))), a, a));
-    case 0x68: WB_LU(4, nan_fix32(b32(floorf(f32(a))), a, a));
-    case 0x69: WB_LU(4, nan_fix32(b32(truncf(f32(a))), a, a));
+    case 0x67: WB_LU(4, nan_keep32(b32(ceilf(f32(a))), a));
+    case 0x68: WB_LU(4, nan_keep32(b32(floorf(f32(a))), a));
+    case 0x69: WB_LU(4, nan_keep32(b32(truncf(f32(a))), a));
     case 0x6A: WB_LU(4, nan_fix32(b32(rintf(f32(a))), a, a));
     case 0xF8: WB_LU(4, (uint32_t)trunc_sat((double)f32(a), true, true, false));
     case 0xF9: WB_LU(4, (uint32_t)trunc_sat((double)f32(a), true, false, false));
@@ -286,7 +291,7 @@ WB_HD void vunx(uint32_t sub, const uint32_t *x, uint32_t *r) {
         const uint64_t a = x[2 * k] | ((uint64_t)x[2 * k + 1] << 32);
         const double d = f64(a);
         const double t = sub == 0x74 ? ceil(d) : sub == 0x75 ? floor(d) : sub == 0x7A ? trunc(d) : rint(d);
-        const uint64_t v = nan_fix64(b64(t), a, a);
+        const uint64_t v = sub == 0x94 ? nan_fix64(b64(t), a, a) : nan_keep64(b64(t), a);
         o[2 * k] = (uint32_t)v; o[2 * k + 1] = (uint32_t)(v >> 32);
       }
       break;
