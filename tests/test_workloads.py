@@ -118,3 +118,85 @@ def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
         ref = oracle_run(O.Module(wasm), func, rows)
         rets, st, cnt, h = gpu_run(wasm, func, rows, pt, rt)
         assert compare(ref, rets, st, cnt, h, rt) == [], name
+
+
+def _oracle_batch(wasm, func, rows, page_limit=65536):
+    """The oracle on many instances at once (om_run_batch, host threads), as rows of
+    (code, values, count, memhash) for compare()."""
+    import os
+    m = O.Module(wasm, page_limit=page_limit)
+    rows = np.asarray(rows, dtype=np.int64)
+    params = np.zeros((len(rows), rows.shape[1], 2), np.uint64)
+    params[:, :, 0] = rows.astype(np.uint64)
+    out = m.run_batch(func, params, len(rows), threads=min(16, os.cpu_count() or 1))
+    res = []
+    for i in range(len(rows)):
+        code = int(out["codes"][i])
+        vals = [int(out["results"][i, 0, 0])] if code == 0 else []
+        res.append((code, vals, int(out["counts"][i]), int(out["hashes"][i])))
+    return res
+
+
+def _mask32(rets):
+    return [[v[0] & 0xFFFFFFFF] if v else [] for v in rets]
+
+
+@pytest.mark.gpu
+def test_gpu_c2_full_size(built):
+    """C2 exactly as configs[1] / bench.py: 64K instances x 1000 chained compressions;
+    every 61st instance checked against the oracle, all lanes against each other's
+    size-independent property (no traps, identical counts: the loop is data-independent)."""
+    wasm = W.blake3_wasm()
+    n = 65536
+    rows = [[i, 1000] for i in range(n)]
+    rets, st, cnt, h = gpu_run(wasm, "run", rows, [I32, I32], [I32])
+    assert all(int(s) == 0 for s in st) and len(set(int(c) for c in cnt)) == 1
+    idx = list(range(0, n, 61)) + [n - 1]
+    ref = _oracle_batch(wasm, "run", [rows[i] for i in idx])
+    sub = lambda a: [a[i] for i in idx]
+    assert compare(ref, _mask32(sub(rets)), sub(st), sub(cnt), sub(h), [I32]) == []
+
+
+@pytest.mark.gpu
+def test_gpu_c3_64k_x_16k(built):
+    """C3 at full width with 16,384 elements per instance (64 KiB of the 1 MiB region):
+    a sample of instances bit-exact against the oracle (status, checksum, count, memory
+    hash of the sorted region)."""
+    wasm = W.qsort_wasm()
+    n = 65536
+    rows = [[i, 16384] for i in range(n)]
+    rets, st, cnt, h = gpu_run(wasm, "sort", rows, [I32, I32], [I32], max_memory_page=17)
+    assert all(int(s) == 0 for s in st)
+    idx = list(range(0, n, 509)) + [n - 1]
+    ref = _oracle_batch(wasm, "sort", [rows[i] for i in idx], page_limit=17)
+    sub = lambda a: [a[i] for i in idx]
+    assert compare(ref, _mask32(sub(rets)), sub(st), sub(cnt), sub(h), [I32]) == []
+
+
+@pytest.mark.gpu
+def test_gpu_c3_full_size_sample(built):
+    """C3 at its configs[2] size, 262,144 i32 (1 MiB) per instance, on one wave of
+    instances (ids spread over the 64K range): bit-exact against the oracle. The 64K-wide
+    run at this size is bench.py --workload c3 (it checks its CPU-baseline sample too)."""
+    wasm = W.qsort_wasm()
+    ids = [i * 1021 for i in range(64)]
+    rows = [[i, 262144] for i in ids]
+    rets, st, cnt, h = gpu_run(wasm, "sort", rows, [I32, I32], [I32], max_memory_page=17)
+    ref = _oracle_batch(wasm, "sort", rows, page_limit=17)
+    assert compare(ref, _mask32(rets), st, cnt, h, [I32]) == []
+
+
+@pytest.mark.gpu
+def test_gpu_c5_full_size(built):
+    """C5 at its configs[4] size: 256K 8x8 tiles of a 4096^2 image, 50 iterations. This
+    batch (4096 waves) selects the LDS-frame threaded core. Every 7th tile against the
+    oracle exactly (f64 results, 64-bit masks, rendered bytes in the memory hash)."""
+    wasm = W.mandel_wasm()
+    n = 262144
+    rows = [[i, 4096, 50] for i in range(n)]
+    rets, st, cnt, h = gpu_run(wasm, "tile", rows, [I32, I32, I32], [I64])
+    assert all(int(s) == 0 for s in st)
+    idx = list(range(0, n, 7))
+    ref = _oracle_batch(wasm, "tile", [rows[i] for i in idx])
+    sub = lambda a: [a[i] for i in idx]
+    assert compare(ref, sub(rets), sub(st), sub(cnt), sub(h), [I64], exact=True) == []
