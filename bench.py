@@ -28,6 +28,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "aggregate Wasm instrs/sec at 64K instances, 1/2/4/8 GPUs vs host-core interp"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip-level parameters
+VALU_PEAK = 256 * 4 * 32 * 2.4e9   # VALU lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 INSTANCES = 65536
 ITERS = 1000                   # chained compressions per instance
 
@@ -107,50 +108,116 @@ class Dist:
         return float(t.item())
 
 
-def shard_ids(rank, n):
-    """Instance ids of this rank's shard: [rank*n, (rank+1)*n) -- every rank runs
-    different instances, so N GPUs process N*n distinct instances (weak scaling)."""
+def shard_ids(rank, n, world=1, scaling="weak"):
+    """Instance ids of this rank's shard. weak: [rank*n, (rank+1)*n) -- every rank runs n
+    instances of its own, N GPUs process N*n distinct instances. strong: the n instances
+    of the job split into contiguous blocks, [rank*n/N, (rank+1)*n/N)."""
+    if scaling == "strong":
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        return np.arange(lo, hi, dtype=np.int64)
     return np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(n, argv):
+    """`bench.py --gpus N` run directly (not under torch.distributed.run): start N worker
+    processes of this script, one per GPU (RANK = LOCAL_RANK = r, 127.0.0.1 rendezvous),
+    wait for all of them and return the worst exit status. This parent never touches the
+    GPU (no HIP call, no torch.cuda) and never execs; rank 0 prints the JSON line."""
+    import subprocess
+    env = dict(os.environ)
+    env.update(WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=env.get("MASTER_PORT") or str(_free_port()))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def host_cores():
+    """Host threads for the CPU baseline: the CPUs this process may run on, capped at 16
+    (the GPU box's CPU share per GPU; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     """The oracle (C restatement of the reference interpreter, oracle/) timed on the
     box's host cores over a bounded sample of the same workload: chunks of instances
-    (ids 0, 1, 2, ...) until about `budget_s` seconds of CPU work or every instance.
-    The oracle is the checker here too: the GPU's final state for the same instances
-    must match bit for bit (status, return value, count, memory hash). Returns the
-    baseline record and the sample's linear-memory bytes per wasm instruction."""
+    (ids 0, 1, 2, ...), first on ONE thread for about budget_s / 4 seconds, then on
+    `threads` threads for the rest of the budget (or until every instance ran). The
+    oracle is the checker here too: the GPU's final state for the same instances must
+    match bit for bit (status, return value, count, memory hash). Returns the baseline
+    record and the sample's linear-memory bytes per wasm instruction."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     m = oracle_py.Module(wasm)
     n_max = len(gpu["counts"])
-    # chunks of about budget_s / 4 at the oracle's ~2e8 instr/s per thread
+    # chunks of about a quarter of a phase at the oracle's ~2e8 instr/s per thread
     t_inst = float(gpu["counts"].mean()) / 2e8
-    chunk = int(max(threads, min(64 * threads, threads * budget_s / 4 / max(t_inst, 1e-9))))
-    done, instrs, secs, mbytes = 0, 0.0, 0.0, 0.0
     rmask = 0xFFFFFFFF if gpu["ret32"] else 0xFFFFFFFFFFFFFFFF
-    while secs < budget_s and done < n_max:
-        k = min(chunk, n_max - done)
-        ids = np.arange(done, done + k, dtype=np.int64)
-        rows = build_rows(ids)
-        params = np.zeros((k, len(ptypes), 2), np.uint64)
-        params[:, :, 0] = rows.astype(np.uint64)
-        out = m.run_batch(func, params, k, threads=threads)
-        lo = slice(done, done + k)
-        if not (np.array_equal(out["codes"], gpu["status"][lo])
-                and np.array_equal(out["counts"], gpu["counts"][lo])
-                and np.array_equal(out["hashes"], gpu["hashes"][lo])
-                and np.array_equal((out["results"][:, 0, 0] & rmask)[out["codes"] == 0],
-                                   (gpu["ret"][lo] & rmask)[out["codes"] == 0])):
-            raise SystemExit("GPU/oracle mismatch in instances [%d, %d)" % (done, done + k))
-        instrs += float(out["counts"].sum())
-        mbytes += float(out["mem_bytes"].sum())
-        secs += out["seconds"]
-        done += k
-    return ({"value": instrs / secs, "unit": "instr/s", "cores": threads, "kind": "port",
-             "sample": "%d %s instances (%.3g instrs) in %.2fs on %d threads; bit-exact vs "
-                       "the GPU run on those instances" % (done, what, instrs, secs, threads)},
-            mbytes / instrs)
+    state = {"done": 0, "mbytes": 0.0, "instrs": 0.0}
+
+    def phase(nthr, budget):
+        chunk = int(max(nthr, min(64 * nthr, nthr * budget / 4 / max(t_inst, 1e-9))))
+        instrs, secs, start = 0.0, 0.0, state["done"]
+        while secs < budget and state["done"] < n_max:
+            done = state["done"]
+            k = min(chunk, n_max - done)
+            ids = np.arange(done, done + k, dtype=np.int64)
+            rows = build_rows(ids)
+            params = np.zeros((k, len(ptypes), 2), np.uint64)
+            params[:, :, 0] = rows.astype(np.uint64)
+            out = m.run_batch(func, params, k, threads=nthr)
+            lo = slice(done, done + k)
+            if not (np.array_equal(out["codes"], gpu["status"][lo])
+                    and np.array_equal(out["counts"], gpu["counts"][lo])
+                    and np.array_equal(out["hashes"], gpu["hashes"][lo])
+                    and np.array_equal((out["results"][:, 0, 0] & rmask)[out["codes"] == 0],
+                                       (gpu["ret"][lo] & rmask)[out["codes"] == 0])):
+                raise SystemExit("GPU/oracle mismatch in instances [%d, %d)" % (done, done + k))
+            instrs += float(out["counts"].sum())
+            state["mbytes"] += float(out["mem_bytes"].sum())
+            secs += out["seconds"]
+            state["done"] = done + k
+        state["instrs"] += instrs
+        return instrs, secs, state["done"] - start
+
+    i1, s1, n1 = phase(1, budget_s / 4)
+    it, st, nt = phase(threads, budget_s - s1) if state["done"] < n_max else (i1, s1, n1)
+    rec = {"value": it / st, "unit": "instr/s", "cores": threads, "kind": "port",
+           "value_1thread": i1 / s1, "cpu_model": cpu_model(),
+           "sample": "%s instances: %d on 1 thread (%.3g instrs, %.2fs), then %d on %d threads "
+                     "(%.3g instrs, %.2fs); all bit-exact vs the GPU run on those instances"
+                     % (what, n1, i1, s1, nt, threads, it, st),
+           "calibration": "oracle vs the reference interpreter, same container, 1 thread: "
+                          "fib(30) 0.62x the reference's time, mt19937 1.7x (BASELINE.md 3)"}
+    return rec, state["mbytes"] / state["instrs"]
 
 
 def load_profile_traffic():
@@ -174,6 +241,10 @@ def elapsed_hint(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --instances per GPU; strong: --instances for the whole job")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rank plumbing only: shards, barrier and reductions, no GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--iters", type=int, default=ITERS)
@@ -184,13 +255,22 @@ def main():
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     args = ap.parse_args()
 
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
+    if world_env is not None and int(world_env) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, world_env))
     dist = Dist()
+    if args.dry_run:
+        return dry_run(args, dist)
     from wasmedge_amd import batch
     wasm, func, build_rows, ptypes, desc, extra = workload(args.workload, args)
     n = args.instances
     kw = {"max_memory_page": 17} if args.workload == "c3" else {}
     ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
-    rows = build_rows(shard_ids(dist.rank, n))
+    ids = shard_ids(dist.rank, n, dist.world, args.scaling)
+    n = len(ids)
+    rows = build_rows(ids)
     ctx.set_args(func, batch.make_values(rows, ptypes))
     nret = 1
     dist.init()
@@ -240,12 +320,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "i32" if args.workload != "c5" else "f64",
         "data": "synthetic: per-instance inputs derived from the instance id inside the "
                 "wasm module",
         "config": dict({"workload": desc, "instances_per_gpu": n,
+                        "instances": int(dist.sum(float(n))),
                         "instrs_per_instance": instrs_per_step / n,
                         "parallelism": "instance-sharded, 1 process per GPU"}, **extra),
         "memory_checksum": "%016x" % checksum,
@@ -261,13 +342,19 @@ def main():
                            "traffic": load_profile_traffic(),
                            "note": "algorithmic = linear-memory bytes the wasm program moves; "
                                    "the path is dispatch-issue bound, see issue_roofline"}
-        out["issue_roofline"] = {"achieved": total_instrs / elapsed / dist.world,
-                                 "unit": "wasm instr/s per GPU",
-                                 "dispatch_bound": "see DESIGN.md 'Roofline'"}
+
     else:
         out["data"] = "synthetic: per-instance inputs derived from the instance id"
+    # the bound that matters for a dispatch loop: vector issue. Every wasm instruction is
+    # at least one lane-op, so the VALU lane-op peak bounds wasm instr/s from above
+    per_gpu = total_instrs / elapsed / dist.world
+    out["issue_roofline"] = {"bound": "valu", "achieved": per_gpu, "peak": VALU_PEAK,
+                             "unit": "wasm instr/s per GPU vs VALU lane-op/s",
+                             "frac": per_gpu / VALU_PEAK,
+                             "basis": "DESIGN.md 'Roofline': 256 CU x 4 SIMD-32 x 32 lanes x "
+                                      "2.4 GHz (MI355X_MICROARCH.md)"}
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cores()
         out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
                                                 threads, gpu, args.workload.upper())
         if args.workload == "c3":
@@ -283,6 +370,27 @@ def main():
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
+
+
+def dry_run(args, dist):
+    """The multi-process plumbing without a GPU: each rank takes its shard, joins the
+    barrier and the max/sum reductions exactly as a measured run does; rank 0 prints the
+    resulting layout as the JSON line (no metric value)."""
+    dist.init()
+    ids = shard_ids(dist.rank, args.instances, dist.world, args.scaling)
+    dist.barrier()
+    t = dist.max(float(dist.rank + 1))
+    total = dist.sum(float(len(ids)))
+    lo = dist.sum(float(ids[0]) if dist.rank == 0 else 0.0)
+    hi = dist.max(float(ids[-1]))
+    dist.barrier()
+    if dist.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": dist.world, "scaling": args.scaling,
+                          "instances": int(total), "first_id": int(lo), "last_id": int(hi),
+                          "max_over_ranks": t}), flush=True)
+    if dist.td:
+        dist.td.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

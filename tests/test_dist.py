@@ -55,3 +55,43 @@ def test_single_rank_needs_no_process_group():
     d.init()
     assert d.td is None and d.max(3.0) == 3.0 and d.sum(2.0) == 2.0
     assert list(bench.shard_ids(0, 4)) == [0, 1, 2, 3]
+
+
+def _run_bench(*argv):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(argv),
+                         env=env, capture_output=True, text=True, timeout=240)
+    return out.returncode, [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+
+
+def test_bench_launcher_spawns_ranks_weak():
+    """`bench.py --gpus 2` run directly spawns one worker per GPU through its own launcher
+    (no torchrun); the ranks rendezvous on 127.0.0.1, shard by id and reduce."""
+    rc, lines = _run_bench("--gpus", "2", "--dry-run", "--instances", "65536")
+    assert rc == 0 and len(lines) == 1
+    assert lines[0] == {"dry_run": True, "n_gpus": 2, "scaling": "weak", "instances": 131072,
+                        "first_id": 0, "last_id": 131071, "max_over_ranks": 2.0}
+
+
+def test_bench_launcher_strong_scaling_splits_the_job():
+    rc, lines = _run_bench("--gpus", "2", "--dry-run", "--scaling", "strong", "--instances", "65536")
+    assert rc == 0 and lines[0]["instances"] == 65536 and lines[0]["last_id"] == 65535
+
+
+def test_bench_refuses_mismatched_world_size():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_strong_shards_cover_the_job():
+    import bench
+    for world in (1, 2, 4, 8):
+        ids = [bench.shard_ids(r, 65536, world, "strong") for r in range(world)]
+        assert sum(len(x) for x in ids) == 65536
+        assert all(int(a[-1]) + 1 == int(b[0]) for a, b in zip(ids, ids[1:]))
