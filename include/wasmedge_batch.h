@@ -76,15 +76,24 @@ typedef struct WasmEdge_BatchConfigure {
   double TimeLimitSeconds;
   /* HIP device ordinal (-1 = the current device). */
   int32_t DeviceOrdinal;
-  /* Gas limit per instance with the reference's default unit cost table
-   * (StatisticsConfigure::setCostLimit, statistics.h:32,69-91; 0 = none). Exact: an
-   * instance executes CostLimit wasm instructions and the next one fails with
-   * CostLimitExceeded (0x03), its count = CostLimit + 1 as in engine.cpp:1616-1630.
-   * Metered runs use the compiled step only (no threaded dispatch core). */
+  /* Gas limit per instance (StatisticsConfigure::setCostLimit, statistics.h:32,69-91;
+   * 0 = no metering). Every wasm instruction adds its cost to the instance's running
+   * total; the first one that would take the total past CostLimit fails with
+   * CostLimitExceeded (0x03), counted but not executed (engine.cpp:1616-1630). The total
+   * starts at instantiation, whose constant expressions and start function spend gas too,
+   * and runs on across Execute/Run calls until BatchReset, like the reference VM's
+   * Statistics::CostSum. Metered runs use the compiled step only (no threaded core). */
   uint64_t CostLimit;
   /* Host threads serving lanes parked at host imports (0 = min(16, cores)). Waves are
    * spread over the threads, so host functions must be reentrant. */
   uint32_t HostThreads;
+  /* Cost per instruction, indexed by the reference's OpCode (include/common/enum.inc:
+   * one-byte opcodes, 0xFCxx, 0xFDxx): CostTableLen entries, the rest 0 -- the batched
+   * WasmEdge_StatisticsSetCostTable (lib/api/wasmedge.cpp:878-882, statistics.h:59-66).
+   * NULL with length 0: the default table, every instruction costs 1. Copied at
+   * BatchCreate. */
+  const uint64_t *CostTable;
+  uint32_t CostTableLen;
 } WasmEdge_BatchConfigure;
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
@@ -191,6 +200,11 @@ WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetExitCode(const WasmEdge_BatchCo
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetOutput(const WasmEdge_BatchContext *Cxt,
                                                         uint32_t Inst, uint32_t Fd, uint8_t *Buf,
                                                         uint32_t Len);
+
+/* Each instance's gas total (WasmEdge_StatisticsGetTotalCost, wasmedge.h): Costs[N];
+ * all 0 when the context does not meter. */
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *Cxt,
+                                                               uint64_t *Costs);
 
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */

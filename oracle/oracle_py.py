@@ -37,6 +37,10 @@ def lib():
                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
         L.om_set_cost_limit.restype = None
         L.om_set_cost_limit.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.om_set_metering.restype = None
+        L.om_set_metering.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+        L.om_cost_sum.restype = ctypes.c_uint64
+        L.om_cost_sum.argtypes = [ctypes.c_void_p]
         L.om_terminated.restype = ctypes.c_int
         L.om_terminated.argtypes = [ctypes.c_void_p]
         L.om_mem_pages.restype = ctypes.c_uint32
@@ -182,14 +186,25 @@ class Instance:
     state -- memory, globals, tables -- across invoke() calls, like a module
     instantiated once in the reference VM and executed repeatedly."""
 
-    def __init__(self, module, cost_limit=0):
+    def __init__(self, module, cost_limit=0, cost_table=None):
+        """cost_limit / cost_table: gas metering from instantiation on (the constant
+        expressions and the start function spend gas too); cost_table = a list of costs
+        by OpCode (missing entries 0), None = unit costs."""
         L = lib()
         self.module = module
         err = ctypes.c_int(0)
-        self._h = L.om_instantiate(module._h, ctypes.byref(err))
+        tab = None
+        if cost_table is not None:
+            tab = (ctypes.c_uint64 * max(1, len(cost_table)))(*cost_table)
+        L.om_set_metering(cost_limit, tab, len(cost_table) if cost_table is not None else 0)
+        try:
+            self._h = L.om_instantiate(module._h, ctypes.byref(err))
+        finally:
+            L.om_set_metering(0, None, 0)
         self.error = err.value if not self._h else 0
-        if self._h and cost_limit:
-            L.om_set_cost_limit(self._h, cost_limit)
+
+    def cost_sum(self):
+        return lib().om_cost_sum(self._h) if self._h else 0
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -107,7 +107,12 @@ struct OInst {
   uint64_t fsp, fcap;
   uint64_t count;
   int terminated;                   /* the last invoke ended in Terminated (proc_exit) */
-  uint64_t cost_limit;              /* unit-cost gas limit per invocation (statistics.h) */
+  /* gas (statistics.h:32,69-91): Statistics::CostSum belongs to the VM and is never reset
+   * between executions, so it runs on from instantiation (constant expressions, start
+   * function) across every invocation of this instance */
+  int metered;
+  uint64_t cost_limit, cost_sum;
+  const uint64_t *cost_tab;         /* 65536 entries by OpCode; NULL = the unit table */
   uint64_t mem_bytes;               /* linear-memory bytes the last invoke accessed (not
                                        in the reference: the roofline's algorithmic bytes) */
   /* WASI subset (wasifunc.cpp): captured fd 1 / fd 2 bytes and the proc_exit code */

@@ -48,8 +48,14 @@ int om_invoke(OInst *i, uint32_t fidx, const uint64_t *params, uint64_t *results
  * reference treats it as success, engine.cpp:62-64, with unspecified return values). */
 int om_terminated(const OInst *i);
 
-/* Gas limit per invocation with unit costs (0 = none): statistics.h:69-91. */
+/* Gas (statistics.h:32,69-91). om_set_metering applies to instances created afterwards:
+ * limit 0 = off; tab NULL + len 0 = unit costs, else len entries by OpCode, the rest 0.
+ * The instance's gas total runs on from instantiation (constant expressions, start
+ * function) across its invocations, like the reference VM's Statistics::CostSum.
+ * om_set_cost_limit changes the limit of an existing instance. */
+void om_set_metering(uint64_t limit, const uint64_t *tab, uint32_t len);
 void om_set_cost_limit(OInst *i, uint64_t limit);
+uint64_t om_cost_sum(const OInst *i);
 /* Accept imports no test host module provides; calling one fails (test infrastructure). */
 void om_set_lazy_imports(int on);
 

@@ -22,6 +22,8 @@ def emu_lib():
             [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         E.wb_emu_set_host.argtypes = [ctypes.c_void_p]
         E.wb_emu_set_cost_limit.argtypes = [ctypes.c_uint64]
+        E.wb_emu_set_cost_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        E.wb_emu_get_costs.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         cpp = ctypes.POINTER(ctypes.c_char_p)
         E.wb_emu_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
         E.wb_emu_wasi_output.restype = ctypes.c_uint32
@@ -55,12 +57,18 @@ def from_cells(cells, types):
 
 
 def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0,
-            host=None, cost_limit=0):
+            host=None, cost_limit=0, cost_table=None, costs_out=None):
     """host: a wb_emu_host_t ctypes callback serving imports inline (hostfuncs.emu_host);
-    cost_limit: exact unit-cost gas limit (0 = none)."""
+    cost_limit: gas limit (0 = none) with cost_table (list by OpCode, None = unit costs);
+    costs_out: a list that receives each instance's gas total."""
     E = emu_lib()
     E.wb_emu_set_host(host)
     E.wb_emu_set_cost_limit(cost_limit)
+    if cost_table is None:
+        E.wb_emu_set_cost_table(None, 0)
+    else:
+        tab = np.ascontiguousarray(cost_table, np.uint64)
+        E.wb_emu_set_cost_table(tab.ctypes.data, len(tab))
     n = len(arg_rows)
     pc = sum(CELLS[t] for t in ptypes)
     rc = sum(CELLS[t] for t in rtypes)
@@ -76,6 +84,10 @@ def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_s
                          max_pages, gs_depth, max_steps)
     if e:
         raise RuntimeError("emu error 0x%x: %s" % (e, E.wb_emu_last_error().decode()))
+    if costs_out is not None:
+        c = np.zeros(n, np.uint64)
+        E.wb_emu_get_costs(c.ctypes.data, n)
+        costs_out[:] = [int(x) for x in c]
     rets = [from_cells(res[i], rtypes) if st[i] == 0 else [] for i in range(n)]
     return rets, st, cnt, h
 

@@ -51,15 +51,8 @@ def test_cost_limit_sweep_emulator(built, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_gpu_cost_limit(built, name):
-    from helpers import gpu_run
-    wasm, func, pt, rt, rows = CASES[name]
-    full = max(r[2] for r in _oracle(wasm, func, rows, 0))
-    for limit in sorted({1, 2, 3, full // 3, full // 2, full - 1, full, full + 5}):
-        if limit <= 0:
-            continue
-        ref = _oracle(wasm, func, rows, limit)
-        got = gpu_run(wasm, func, rows, pt, rt, cost_limit=limit)
-        assert compare(ref, *got, rt) == [], limit
+    """The default unit table (every instruction costs 1)."""
+    _gpu_sweep(name, None)
 
 
 @pytest.mark.gpu
@@ -101,5 +94,127 @@ def test_gpu_interrupt_reference_module(built):
         assert time.time() - t0 >= 0.001 and time.time() - t0 < 30
         assert all(int(s) == 0x07 for s in st)
         assert all(int(c) > 1000 for c in cnt)
+    finally:
+        ctx.close()
+
+
+# ---- custom cost tables (WasmEdge_StatisticsSetCostTable, statistics.h:32,59-66,
+# lib/api/wasmedge.cpp:878-882): every instruction adds CostTab[OpCode]; the first one that
+# would take the instance's running total past the limit fails with CostLimitExceeded,
+# counted and unpriced. The total runs on from instantiation across invocations.
+import random  # noqa: E402
+
+BIG = 1 << 62
+
+
+def _tables():
+    """The reference API test's table (test/api/APIUnitTest.cpp:1067-1072: 512 x 20, the
+    rest 0 -- every SIMD and most prefixed ops are free), and random tables with zeros."""
+    rng = random.Random(7)
+    out = {"apitest": [20] * 512}
+    for k in range(2):
+        t = [0] * 65536
+        for op in list(range(0x100)) + list(range(0xFC00, 0xFC12)) + list(range(0xFD00, 0xFE00)):
+            t[op] = rng.choice([0, 0, 1, 2, 3, 5, 17, 100])
+        out["random%d" % k] = t
+    return out
+
+
+TABLES = _tables()
+
+
+def _oracle_tab(wasm, func, rows, limit, table):
+    m = O.Module(wasm)
+    out, costs = [], []
+    for r in rows:
+        inst = O.Instance(m, cost_limit=limit, cost_table=table)
+        out.append(inst.invoke(func, r))
+        costs.append(inst.cost_sum() if not inst.error else None)   # None: instantiation failed
+    return out, costs
+
+
+@pytest.mark.parametrize("tab", sorted(TABLES))
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cost_table_sweep_emulator(built, name, tab):
+    wasm, func, pt, rt, rows = CASES[name]
+    table = TABLES[tab]
+    _, full = _oracle_tab(wasm, func, rows, BIG, table)
+    total = max(full)
+    step = max(1, total // 150)
+    for limit in sorted(set(list(range(1, total + 2, step)) + [total - 1, total, total + 1])):
+        if limit <= 0:
+            continue
+        ref, rcost = _oracle_tab(wasm, func, rows, limit, table)
+        costs = []
+        rets, st, cnt, h = emu_run(wasm, func, rows, pt, rt, cost_limit=limit, cost_table=table,
+                                   costs_out=costs)
+        bad = compare(ref, rets, st, cnt, h, rt)
+        assert bad == [], (limit, bad[:3])
+        assert [c for c, r in zip(costs, rcost) if r is not None] == \
+            [r for r in rcost if r is not None], limit
+
+
+def test_cost_accumulates_across_invocations(built):
+    """The gas total is the instance's, not the invocation's: a second run on the same
+    instance starts from where the first stopped (Statistics::CostSum is cleared only by
+    VM cleanup, lib/vm/vm.cpp:336-340)."""
+    m = O.Module(STATEFUL)
+    inst = O.Instance(m, cost_limit=BIG, cost_table=TABLES["random0"])
+    start = inst.cost_sum()
+    assert start > 0                                   # constant exprs + start function
+    a = inst.invoke("step", [4]); c1 = inst.cost_sum()
+    b = inst.invoke("step", [4]); c2 = inst.cost_sum()
+    assert a[0] == b[0] == 0 and c1 > start and c2 > c1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tab", sorted(TABLES))
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gpu_cost_table(built, name, tab):
+    """Device vs oracle under a custom cost table at limits across the program: status,
+    count, memory hash and each instance's gas total."""
+    _gpu_sweep(name, TABLES[tab])
+
+
+def _gpu_sweep(name, table):
+    from wasmedge_amd import batch
+    wasm, func, pt, rt, rows = CASES[name]
+    _, full = _oracle_tab(wasm, func, rows, BIG, table)
+    total = max(full)
+    for limit in sorted({1, 2, total // 3, total // 2, total - 1, total, total + 5, BIG}):
+        if limit <= 0:
+            continue
+        ref, rcost = _oracle_tab(wasm, func, rows, limit, table)
+        if any(c is None for c in rcost):     # instantiation itself runs out of gas
+            with pytest.raises(batch.WasmEdgeError) as e:
+                batch.BatchContext(wasm, len(rows), device=0, cost_limit=limit, cost_table=table)
+            assert e.value.code == 0x03
+            continue
+        ctx = batch.BatchContext(wasm, len(rows), device=0, cost_limit=limit, cost_table=table)
+        try:
+            rets, st, cnt = ctx.execute(func, batch.make_values(rows, pt), len(rt))
+            ints = batch.ret_ints(rets)
+            got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref, got, st, cnt, ctx.memory_hash(), rt) == [], limit
+            assert [int(c) for c in ctx.total_costs()] == rcost, limit
+        finally:
+            ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_cost_runs_on_across_invocations(built):
+    from wasmedge_amd import batch
+    table = TABLES["random1"]
+    rows = [[4], [1], [3]]
+    m = O.Module(STATEFUL)
+    insts = [O.Instance(m, cost_limit=BIG, cost_table=table) for _ in rows]
+    ctx = batch.BatchContext(STATEFUL, len(rows), device=0, cost_limit=BIG, cost_table=table)
+    try:
+        assert [int(c) for c in ctx.total_costs()] == [i.cost_sum() for i in insts]
+        for _ in range(3):
+            ctx.execute("step", batch.make_values(rows, [I32]), 1)
+            for i, r in zip(insts, rows):
+                i.invoke("step", r)
+            assert [int(c) for c in ctx.total_costs()] == [i.cost_sum() for i in insts]
     finally:
         ctx.close()

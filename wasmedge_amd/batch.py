@@ -57,7 +57,8 @@ class _Conf(ctypes.Structure):
     _fields_ = [("MaxMemoryPage", ctypes.c_uint32), ("CallStackCells", ctypes.c_uint32),
                 ("MaxSteps", ctypes.c_uint64), ("TimeLimitSeconds", ctypes.c_double),
                 ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64),
-                ("HostThreads", ctypes.c_uint32)]
+                ("HostThreads", ctypes.c_uint32), ("CostTable", ctypes.c_void_p),
+                ("CostTableLen", ctypes.c_uint32)]
 
 
 class _String(ctypes.Structure):
@@ -154,6 +155,8 @@ def lib():
         L.WasmEdge_BatchMemoryGetInstance.restype = u32
         L.WasmEdge_BatchMemoryGetInstance.argtypes = [vp]
         cpp = ctypes.POINTER(ctypes.c_char_p)
+        L.WasmEdge_BatchGetTotalCosts.restype = _Result
+        L.WasmEdge_BatchGetTotalCosts.argtypes = [vp, vp]
         L.WasmEdge_BatchInitWASI.restype = _Result
         L.WasmEdge_BatchInitWASI.argtypes = [vp, cpp, u32, cpp, u32]
         L.WasmEdge_BatchWASIGetExitCode.restype = u32
@@ -198,10 +201,16 @@ class BatchContext:
     """N instances of one module on one GPU (WasmEdge_BatchContext)."""
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
-                 time_limit=0.0, device=-1, cost_limit=0, host_threads=0):
+                 time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None):
+        """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
+        metering is on when cost_limit > 0."""
         L = lib()
+        tab = None
+        if cost_table is not None:
+            tab = np.ascontiguousarray(cost_table, np.uint64)
         conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit,
-                     host_threads)
+                     host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
+                     len(tab) if tab is not None else 0)
         res = _Result(0)
         self._h = L.WasmEdge_BatchCreate(ctypes.byref(conf), bytes(wasm), len(wasm), n,
                                          ctypes.byref(res))
@@ -261,6 +270,12 @@ class BatchContext:
         self.set_args(func, values)
         self.run()
         return self.results(nret)
+
+    def total_costs(self):
+        """Each instance's gas total (WasmEdge_BatchGetTotalCosts)."""
+        c = np.zeros(self.n, np.uint64)
+        self._check(lib().WasmEdge_BatchGetTotalCosts(self._h, c.ctypes.data))
+        return c
 
     def memory_hash(self):
         h = np.zeros(self.n, np.uint64)

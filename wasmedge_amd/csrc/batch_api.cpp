@@ -26,7 +26,7 @@ extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
                                            uint32_t global_cells, uint32_t ls_slots,
                                            uint32_t init_pages, uint32_t init_dropped,
-                                           uint32_t nwaves, hipStream_t s);
+                                           uint32_t nwaves, uint64_t init_cost, hipStream_t s);
 
 
 using namespace wbh;
@@ -38,6 +38,16 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
+  // gas tables (statistics.h:32: unit costs unless the caller set a table)
+  if (C->conf.CostLimit) {
+    std::vector<uint64_t> tab(65536, C->conf.CostTable || C->conf.CostTableLen ? 0ull : 1ull);
+    for (uint32_t k = 0; C->conf.CostTable && k < C->conf.CostTableLen && k < 65536; k++)
+      tab[k] = C->conf.CostTable[k];
+    C->init_cost = wb::build_cost_pool(P, tab.data(), C->conf.CostLimit, C->cost_off_h,
+                                       C->cost_pool_h, &C->init_exceeded);
+    C->cost_else = tab[0x05];
+  }
+  C->conf.CostTable = nullptr;   // copied: the caller's array need not outlive BatchCreate
   // MemoryInstance(MType, PageLimit) allocates nothing when the initial size exceeds the
   // page limit (include/runtime/instance/memory.h:46-51, test/memlimit/MemLimitTest.cpp:16-18);
   // such an instance is unusable, so the batch fails here instead of running without memory
@@ -126,6 +136,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
             C->tab_image.upload(P.tab_image, s) && C->tabinfo.upload(P.tabinfo, s) &&
             C->elem_pool.upload(P.elem_pool, s) && C->elem_off.upload(P.elem_off, s) &&
             C->elem_len.upload(P.elem_len, s) &&
+            (!C->conf.CostLimit || (C->cost_off.upload(C->cost_off_h, s) &&
+                                    C->cost_pool.upload(C->cost_pool_h, s))) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
             C->data_off.upload(doff, s) && C->data_len.upload(dlen, s);
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
@@ -179,8 +191,13 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
   // metered runs take the exact compiled step (the threaded core counts per run only)
   k.tcode = C->threaded && !C->conf.CostLimit ? C->tcode.ptr : nullptr;
-  // the gas limit applies per invocation; instantiation (start function) is not metered
-  k.cost_limit = C->conf.CostLimit && !is_start ? C->conf.CostLimit : ~0ull;
+  // gas: the instance's running total against the limit, start function included
+  k.cost_limit = C->conf.CostLimit ? C->conf.CostLimit : ~0ull;
+  if (C->conf.CostLimit) {
+    k.cost_off = C->cost_off.ptr;
+    k.cost_pool = C->cost_pool.ptr;
+    k.cost_else = C->cost_else;
+  }
   k.stop = C->stop;
   if (P.mut_tables) {
     k.ltab = C->ltab.ptr; k.tabinfo = C->tabinfo.ptr; k.elem_pool = C->elem_pool.ptr;
@@ -344,9 +361,13 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
       !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
                                     P.tab_words, C->nwaves, nullptr, 0, 1u, C->stream), "table init"))
     return R(kRuntimeError);
+  // gas: instantiation's constant expressions are priced first (module.cpp order); one
+  // past the limit fails the instantiation like the reference's VM::instantiate
+  if (C->conf.CostLimit && C->init_exceeded)
+    return R(C->fail(0x03, "instantiation exceeds the cost limit (constant expressions)"));
   if (!C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->global_init.ptr, P.global_cells,
                                       C->ls_slots, P.mem_min, C->init_dropped, C->nwaves,
-                                      C->stream), "state init"))
+                                      C->init_cost, C->stream), "state init"))
     return R(kRuntimeError);
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
@@ -440,6 +461,19 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "hash")) return R(kRuntimeError);
   if (!C->hip_ok(hipMemcpy(Hashes, C->hashes.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "hash"))
     return R(kRuntimeError);
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *Costs) {
+  if (!C || !Costs) return R(kWrongVMWorkflow);
+  const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+  std::vector<uint32_t> lo(size_t(C->nwaves) * 64), hi(lo.size());
+  if (!C->hip_ok(hipMemcpy2D(lo.data(), row, C->lstate.ptr + LS_COST * 64, pitch, row, C->nwaves,
+                             hipMemcpyDeviceToHost), "costs") ||
+      !C->hip_ok(hipMemcpy2D(hi.data(), row, C->lstate.ptr + (LS_COST + 1) * 64, pitch, row,
+                             C->nwaves, hipMemcpyDeviceToHost), "costs"))
+    return R(kRuntimeError);
+  for (uint32_t i = 0; i < C->n; i++) Costs[i] = C->conf.CostLimit ? (uint64_t(hi[i]) << 32) | lo[i] : 0;
   return R(0);
 }
 

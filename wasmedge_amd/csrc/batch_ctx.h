@@ -80,6 +80,14 @@ struct WasmEdge_BatchContext {
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;
   DevBuf<uint32_t> tab_image, tabinfo, elem_pool, elem_off, elem_len;   // per-lane tables
   DevBuf<DFunc> funcs;
+  // gas metering (conf.CostLimit): per-DBC cost prefix sums, the cost of instantiation's
+  // constant expressions, the manual `else` cost
+  std::vector<uint32_t> cost_off_h;
+  std::vector<uint64_t> cost_pool_h;
+  DevBuf<uint32_t> cost_off;
+  DevBuf<uint64_t> cost_pool;
+  uint64_t init_cost = 0, cost_else = 0;
+  bool init_exceeded = false;
   DevBuf<uint8_t> data_pool;
   // instance state
   DevBuf<uint32_t> mem, gstack, lstate, params, results, ltab;

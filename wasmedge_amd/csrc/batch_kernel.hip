@@ -243,6 +243,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   uint32_t hwm = LS(LS_HWM);
 #define WB_MARK(ea, n) (hwm = max(hwm, (uint32_t)min((uint64_t)(ea) + (uint64_t)(n), 0xFFFFFFFFull)))
   uint64_t count = 0;
+  // the running gas total (metered runs): kept in the instance state between launches
+  uint64_t cost = (uint64_t)LS(LS_COST) | ((uint64_t)LS(LS_COST + 1) << 32);
   const uint32_t istatus = LS(LS_ISTATUS);
   if (status == WB_STATUS_RUNNING && istatus) status = istatus;   // instance never came up
   for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, LS(LS_GLOBALS + c));
@@ -367,6 +369,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define HOST_YIELD(f, base) SLOW_OP()
       uint32_t sc = 0, tick = 1024, xpc = 0, xpost = 0, tcode = 0;
       int32_t xadj = 0;
+      uint64_t scost = 0;   // gas of the run so far (metered runs; wave-uniform)
       uint64_t asc = 0;     // instructions retired inside the threaded core
       w4 I = code[pcs];
       for (;;) {
@@ -402,15 +405,24 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
         WB_STAT_ADD(ST_CPP, 1);
-        // metered: a dispatch that may cross the gas limit runs in the exact slow step
-        // (the threaded core is off when metering, see launch_once)
-        if (p.cost_limit != ~0ull)
-          SLOW_IF(count + sc + cnt8 + (uint32_t)(tcnt > 0 ? tcnt : 0) > p.cost_limit);
+        // metered (the threaded core is off, see launch_once): only straight-line
+        // dispatches stay in the run, each priced at the full cost of the instructions it
+        // retires; one that branches or may trap, or whose cost could reach the limit (or
+        // wrap the sum), runs in the exact slow step
+        uint64_t dfull = 0;
+        if (p.cost_off) {
+          typedef __attribute__((address_space(4))) const uint32_t *cu32;
+          typedef __attribute__((address_space(4))) const uint64_t *cu64;
+          dfull = cnt8 ? ((cu64)p.cost_pool)[((cu32)p.cost_off)[pcs] + cnt8 - 1] : 0;
+          const uint64_t need = scost + dfull;
+          SLOW_IF((w0 & DBC_CTL) || need < scost || cost > p.cost_limit || p.cost_limit - cost < need);
+        }
         switch (op) {
 #include "dbc_step.inc"
         }
       k_next:
         sc += cnt8;
+        scost += dfull;
         pcs += 1;
         if (pcs >= other) { xpc = pcs; goto k_leave; }   // reached a waiting lane
         I = In;
@@ -446,6 +458,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_IF
 #undef HOST_YIELD
       count += (uint64_t)sc + asc;
+      cost += scost;
       if (tcode == 0) {
         pc = xpc;
         count += (int64_t)xadj;
@@ -468,9 +481,9 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define WB_FAST 0
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
 #define FINISH() (status = WB_STATUS_OK)
-#define JUMP(t, tc) do { npc = (t); add += (tc); goto s_next; } while (0)
+#define JUMP(t, tc) do { npc = (t); add += (tc); jtc = (tc); goto s_next; } while (0)
 #define JUMP_LANE(t, tc) JUMP(t, tc)
-#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); } goto s_next; } while (0)
+#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); jtc = (tc); } goto s_next; } while (0)
 #define EXIT_IF_TRAPPED(t) ((void)0)
 #define TRAP_CHECK() ((void)0)
 #define SLOW_OP() ((void)0)
@@ -483,24 +496,26 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
       const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
       uint32_t npc = pcs + 1;
-      int32_t add = (int32_t)cnt8;
-      // engine.cpp:1616-1630 with unit costs: an instruction is counted, then its cost
-      // is added; past the limit it fails with CostLimitExceeded before it executes
-      const bool metered = p.cost_limit != ~0ull;
-      if (metered && count + cnt8 - post8 > p.cost_limit) {
+      int32_t add = (int32_t)cnt8, jtc = 0;
+      const uint32_t coff = p.cost_off ? p.cost_off[pcs] : 0u;
+      // engine.cpp:1616-1630: an instruction is counted, then its cost is added; past the
+      // limit it fails with CostLimitExceeded before it executes. Here: the instructions
+      // up to the main op first, then (if it did not trap) the ones after it, then a
+      // taken branch's adjustment (gas_step in dbc_ops.h)
+      if (p.cost_off && gas_step(p.cost_pool + coff, 0, cnt8 - post8, p.cost_limit, cost, add)) {
         status = 0x03u;
-        add = (int32_t)(p.cost_limit + 1 - count);
-        goto s_next;
+        goto s_done;
       }
       switch (op) {
 #include "dbc_step.inc"
       }
     s_next:
-      if (metered && count + (int64_t)add > p.cost_limit &&
-          (status == WB_STATUS_RUNNING || status == WB_STATUS_OK)) {
-        status = 0x03u;   // the limit fell on a trailing folded / landing instruction
-        add = (int32_t)(p.cost_limit + 1 - count);
-      }
+      if (p.cost_off && (status == WB_STATUS_RUNNING || status == WB_STATUS_OK) &&
+          gas_tail(p.cost_pool + coff, cnt8 - post8, cnt8, jtc,
+                   jtc < 0 ? p.cost_pool + p.cost_off[npc] : nullptr, p.cost_else, p.cost_limit,
+                   cost, add))
+        status = 0x03u;
+    s_done:
       count += (int64_t)add;
       pc = npc;
 #undef WB_FAST
@@ -552,6 +567,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     LS(LS_PAGES) = pages;
     LS(LS_DROPPED) = dropped;
     LS(LS_HWM) = hwm;
+    LS(LS_COST) = (uint32_t)cost;
+    LS(LS_COST + 1) = (uint32_t)(cost >> 32);
     for (uint32_t c = 0; c < p.global_cells; c++) LS(LS_GLOBALS + c) = F.get(c);
     if (p.is_start && status != WB_STATUS_OK) LS(LS_ISTATUS) = status;
   }
@@ -628,7 +645,7 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
 extern "C" __global__ void __launch_bounds__(256)
 wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_cells,
                      uint32_t ls_slots, uint32_t init_pages, uint32_t init_dropped,
-                     uint32_t nwaves) {
+                     uint32_t nwaves, uint64_t init_cost) {
   const size_t total = (size_t)nwaves * ls_slots * 64u;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -637,6 +654,8 @@ wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_
     if (slot == LS_PAGES) v = init_pages;
     else if (slot == LS_DROPPED) v = init_dropped;
     else if (slot == LS_RPC) v = 0xFFFFFFFFu;
+    else if (slot == LS_COST) v = (uint32_t)init_cost;
+    else if (slot == LS_COST + 1) v = (uint32_t)(init_cost >> 32);
     else if (slot >= LS_GLOBALS) v = global_init[slot - LS_GLOBALS];
     ls[i] = v;
   }
@@ -701,11 +720,12 @@ extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
                                            uint32_t global_cells, uint32_t ls_slots,
                                            uint32_t init_pages, uint32_t init_dropped,
-                                           uint32_t nwaves, hipStream_t s) {
+                                           uint32_t nwaves, uint64_t init_cost, hipStream_t s) {
   const size_t total = (size_t)nwaves * ls_slots * 64u;
   size_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(wb_state_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ls,
-                     global_init, global_cells, ls_slots, init_pages, init_dropped, nwaves);
+                     global_init, global_cells, ls_slots, init_pages, init_dropped, nwaves,
+                     init_cost);
   return hipGetLastError();
 }

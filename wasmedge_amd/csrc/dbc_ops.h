@@ -63,6 +63,37 @@ WB_HD bool isnan64(uint64_t a) {
 WB_HD uint32_t nan_keep32(uint32_t r, uint32_t a) { return sel32(isnan32(a), a, r); }
 WB_HD uint64_t nan_keep64(uint64_t r, uint64_t a) { return sel64(isnan64(a), a, r); }
 
+// Gas metering (statistics.h:79-91 addCost): the sum Old + Cost (wrapping in 64 bits) past
+// the limit fails without being added. `pool[j]` = the cost of a DBC's first j+1
+// instructions (KParams::cost_pool). gas_step prices instructions [from, to) in order; on
+// CostLimitExceeded it sets `add` to the count through the failing instruction.
+WB_HD uint64_t gas_at(const uint64_t *pool, uint32_t j) { return j ? pool[j] - pool[j - 1] : pool[0]; }
+WB_HD bool gas_step(const uint64_t *pool, uint32_t from, uint32_t to, uint64_t limit,
+                    uint64_t &cost, int32_t &add) {
+  for (uint32_t j = from; j < to; j++) {
+    const uint64_t nc = cost + gas_at(pool, j);
+    if (nc > limit) { add = (int32_t)(j + 1); return true; }
+    cost = nc;
+  }
+  return false;
+}
+// After the main op: the instructions after it, then a taken branch's count correction --
+// tcnt = -k: its landing DBC re-prices its first k instructions (the landing list's prefix
+// is returned here); tcnt = +1: an if-false jump into an else arm also retires the `else`
+// (controlInstr.cpp:23-28).
+WB_HD bool gas_tail(const uint64_t *pool, uint32_t from, uint32_t cnt, int32_t jtc,
+                    const uint64_t *landing, uint64_t c_else, uint64_t limit, uint64_t &cost,
+                    int32_t &add) {
+  if (gas_step(pool, from, cnt, limit, cost, add)) return true;
+  if (jtc < 0) cost -= landing[(uint32_t)(-jtc) - 1u];
+  for (int32_t q = 0; q < jtc; q++) {
+    const uint64_t nc = cost + c_else;
+    if (nc > limit) { add = (int32_t)cnt + q + 1; return true; }
+    cost = nc;
+  }
+  return false;
+}
+
 // binary_numeric.ipp:155-191 (scalar min/max with its NaN/zero rules; raw NaN payload)
 WB_HD uint32_t fmin32(uint32_t a, uint32_t b) {
   const bool zz = ((a | b) & 0x7FFFFFFFu) == 0 && a != b;

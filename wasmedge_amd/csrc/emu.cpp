@@ -27,7 +27,9 @@ static uint64_t g_trace_cap = 0, g_trace_len = 0, *g_trace_lens = nullptr;
 typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
                              uint32_t *rets, uint8_t *mem, uint64_t mem_bytes);
 static wb_emu_host_t g_host = nullptr;
-static uint64_t g_cost_limit = ~0ull;   // exact unit-cost gas limit (0 = none)
+static uint64_t g_cost_limit = ~0ull;   // gas limit (0 = none)
+static std::vector<uint64_t> g_cost_tab;   // cost per OpCode (empty: the unit table)
+static std::vector<uint64_t> g_costs;      // per instance: its gas total after the last run
 // the library's WASI subset (wasi_impl.h), bound before g_host when on
 static bool g_wasi = false;
 static wbw::Env g_wasi_env;
@@ -64,6 +66,17 @@ __attribute__((visibility("default"))) void wb_emu_set_pc_trace(uint32_t *buf, u
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
+// WasmEdge_StatisticsSetCostTable (statistics.h:59-66): `len` entries, the rest 0;
+// tab = NULL and len = 0: back to the default unit table
+__attribute__((visibility("default"))) void wb_emu_set_cost_table(const uint64_t *tab, uint32_t len) {
+  g_cost_tab.clear();
+  if (!tab && !len) return;
+  g_cost_tab.assign(65536, 0ull);
+  for (uint32_t k = 0; k < len && k < 65536; k++) g_cost_tab[k] = tab[k];
+}
+__attribute__((visibility("default"))) void wb_emu_get_costs(uint64_t *out, uint32_t n) {
+  for (uint32_t k = 0; k < n && k < g_costs.size(); k++) out[k] = g_costs[k];
+}
 // WASI subset on (args/envs shared by every instance) or off; outputs per instance of the
 // last wb_emu_execute
 __attribute__((visibility("default"))) void wb_emu_set_wasi(int on, const char *const *args, uint32_t nargs,
@@ -133,6 +146,17 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define EDROP edrop
   std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
   std::vector<uint32_t> memv;
+  // gas metering: per DBC prefix sums of its instructions' costs (unit table by default)
+  const bool metered = g_cost_limit != ~0ull;
+  std::vector<uint64_t> unit, cpool;
+  std::vector<uint32_t> coff;
+  if (g_cost_tab.empty()) unit.assign(65536, 1ull);
+  const uint64_t *tab = g_cost_tab.empty() ? unit.data() : g_cost_tab.data();
+  bool init_exceeded = false;
+  const uint64_t init_cost = metered ? wb::build_cost_pool(P, tab, g_cost_limit, coff, cpool, &init_exceeded) : 0;
+  const uint64_t c_else = tab[0x05];
+  uint64_t cost = 0;
+  g_costs.assign(n, 0);
   // imports served by the WASI subset (wasi_impl.h), per function index
   std::vector<int> wasi_fn(P.funcs.size(), -1);
   g_wasi_lanes.assign(g_wasi ? n : 0, wbw::Lane{});
@@ -161,9 +185,9 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define GS_CPTR const uint32_t *const
 #define TRAP(code) do { status = (code); add = (int32_t)cnt8 - (int32_t)post8; } while (0)
 #define FINISH() (status = WB_STATUS_OK)
-#define JUMP(t, tc) do { npc = (t); add += (tc); goto e_next; } while (0)
+#define JUMP(t, tc) do { npc = (t); add += (tc); jtc = (tc); goto e_next; } while (0)
 #define JUMP_LANE(t, tc) JUMP(t, tc)
-#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); } goto e_next; } while (0)
+#define BRANCH(c, t, tc) do { if (c) { npc = (t); add += (tc); jtc = (tc); } goto e_next; } while (0)
 #define EXIT_IF_TRAPPED(t) ((void)0)
 #define TRAP_CHECK() ((void)0)
 #define SLOW_OP() ((void)0)
@@ -194,24 +218,24 @@ __attribute__((visibility("default"))) int wb_emu_execute(
         if (g_pchist && pcs < g_pchist_n) g_pchist[pcs]++;
         if (g_trace && g_trace_len < g_trace_cap) { g_trace[g_trace_len++] = pcs; g_trace_lens[inst]++; }
         const uint32_t cnt8 = (w0 >> 16) & 0xFFu, post8 = (w0 >> 24) & 0x7Fu;
-        int32_t add = (int32_t)cnt8;
+        int32_t add = (int32_t)cnt8, jtc = 0;
         uint32_t npc = pcs + 1;
         const int32_t tcnt = (int32_t)(int16_t)(w2 >> 16);
-        const bool metered = g_cost_limit != ~0ull;   // as the kernel's slow step
-        if (metered && count + cnt8 - post8 > g_cost_limit) {
+        // gas as the kernel's slow step (batch_kernel.hip, dbc_ops.h gas_step / gas_tail)
+        const uint64_t *cp = metered ? cpool.data() + coff[pcs] : nullptr;
+        if (metered && gas_step(cp, 0, cnt8 - post8, g_cost_limit, cost, add)) {
           status = 0x03u;
-          add = (int32_t)(g_cost_limit + 1 - count);
-          goto e_next;
+          goto e_done;
         }
         switch (op) {
 #include "dbc_step.inc"
         }
       e_next:
-        if (metered && count + (int64_t)add > g_cost_limit &&
-            (status == WB_STATUS_RUNNING || status == WB_STATUS_OK)) {
+        if (metered && (status == WB_STATUS_RUNNING || status == WB_STATUS_OK) &&
+            gas_tail(cp, cnt8 - post8, cnt8, jtc, jtc < 0 ? cpool.data() + coff[npc] : nullptr,
+                     c_else, g_cost_limit, cost, add))
           status = 0x03u;
-          add = (int32_t)(g_cost_limit + 1 - count);
-        }
+      e_done:
         count += (int64_t)add;
         pc = npc;
         const int wfn = status == WB_ERR_HOST_CALL ? wasi_fn[ycall] : -1;
@@ -238,18 +262,19 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     // not part of the invocation's
     uint64_t count = 0, start_count = 0;
     uint32_t status = WB_STATUS_OK;
-    if (P.start_func >= 0) {   // instantiation is not metered (limit per invocation)
-      const uint64_t lim = g_cost_limit;
-      g_cost_limit = ~0ull;
+    // instantiation spends gas too: its constant expressions, then the start function
+    cost = init_cost;
+    if (init_exceeded) status = 0x03u;
+    if (status == WB_STATUS_OK && P.start_func >= 0) {
       p.result_cells = 0;
       status = invoke(P.funcs[P.start_func].entry_pc, nullptr, 0, start_count);
       p.result_cells = rcells;
-      g_cost_limit = lim;
     }
     if (status == WB_STATUS_OK)
       status = invoke(F.entry_pc, params + size_t(inst) * pcells, pcells, count);
     statuses[inst] = uint8_t(status);
     counts[inst] = count;
+    g_costs[inst] = cost;
     if (hashes) {
       uint64_t h = 0, nw = uint64_t(pages) << 13;
       for (uint64_t i = 0; i < nw; i++) {

@@ -281,6 +281,7 @@ class Lowerer {
   std::vector<Entry> st;
   std::vector<Ctrl> ctrl;
   uint32_t pending = 0;
+  std::vector<uint16_t> pend_ops;   // the opcodes behind `pending`, in order (Program::dops)
   int64_t last_emit = -1;
   bool can_retarget = false;
   std::vector<CallFix> *callfix = nullptr;
@@ -331,6 +332,8 @@ class Lowerer {
       fail(E_UNSUPPORTED, "cell index out of range for the DBC encoding");
     while (pending > 255) {                  // cnt is 8 bits: spill into NOP_CNT
       P.code.push_back(DInstr{uint32_t(OP_NOP_CNT) | (255u << 16), 0, 0, 0});
+      P.dops.emplace_back(pend_ops.begin(), pend_ops.begin() + 255);
+      pend_ops.erase(pend_ops.begin(), pend_ops.begin() + 255);
       pending -= 255;
     }
     DInstr I;
@@ -341,6 +344,8 @@ class Lowerer {
     if (pending > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = pending;
     pending = 0;
     P.code.push_back(I);
+    P.dops.push_back(std::move(pend_ops));
+    pend_ops.clear();
     last_emit = int64_t(P.code.size()) - 1;
     can_retarget = true;
     return P.code.back();
@@ -534,6 +539,7 @@ class Lowerer {
     I.w2 = (I.w2 & 0xFFFF0000u) | dst;
     I.w0 = (I.w0 & (0xFFFFu | DBC_CTL)) | ((cnt + pending) << 16) | ((post + pending) << 24);
     pending = 0;
+    take_pending(last_emit);
     return true;
   }
 
@@ -552,8 +558,17 @@ class Lowerer {
     uint32_t cnt = ((I.w0 >> 16) & 0xFF) + pending;
     I.w0 = uint32_t(op) | (cnt << 16) | (is_ctl(op) ? DBC_CTL : 0u);
     pending = 0;
+    take_pending(&I - P.code.data());
     if (cnt > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = cnt;
   }
+  // the pending opcodes join an already emitted instruction's list (merged into it)
+  void take_pending(int64_t pc) {
+    auto &d = P.dops[size_t(pc)];
+    d.insert(d.end(), pend_ops.begin(), pend_ops.end());
+    pend_ops.clear();
+  }
+  void count_op(uint16_t op) { pending++; pend_ops.push_back(op); }
+  void drop_pending() { pending = 0; pend_ops.clear(); }
   bool try_fuse_simple(const SimpleOp &s, Entry *ops);
   bool try_fuse_branch(const Entry &cond, bool branch_if_true, Ctrl &f);
 
@@ -743,13 +758,15 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
   max_cell = cc;
   st.clear();
   ctrl.clear();
-  pending = 0;
+  drop_pending();
   last_emit = -1;
   can_retarget = false;
 
   F.entry_pc = uint32_t(P.code.size());
-  if (F.local_cells)   // prologue used by call_indirect / the kernel's first frame
+  if (F.local_cells) {   // prologue used by call_indirect / the kernel's first frame
     P.code.push_back(DInstr{OP_ZERO_LOCALS, (frame_base + F.param_cells) | (F.local_cells << 16), 0, 0});
+    P.dops.emplace_back();
+  }
   F.body_pc = uint32_t(P.code.size());
   push_ctrl(C_FUNC, {}, ft->results);
 
@@ -762,7 +779,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
       if (sub > 0xFF) fail(E_ILLEGAL_OPCODE, "illegal opcode");
       op = uint16_t(op << 8 | sub);
     }
-    if (op != 0x0B && op != 0x05 && op != 0x03) pending++;  // else/end/loop: at their labels
+    if (op != 0x0B && op != 0x05 && op != 0x03) count_op(op);  // else/end/loop: at their labels
     auto it = simple.find(op);
     if (it != simple.end()) { do_simple(it->second); continue; }
     switch (op) {
@@ -790,7 +807,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           place_label();
           int32_t tcnt = -int32_t(pending);
           uint32_t lpc = uint32_t(P.code.size());
-          pending++;
+          count_op(0x03);
           push_ctrl(C_LOOP, in, out);
           if (!ctrl.back().dead) resolve_label(ctrl.back(), lpc, tcnt);
         } else {
@@ -823,11 +840,11 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           if (st.size() != f.height) fail(E_TYPECHECK, "type mismatch at else");
           for (auto &e : vals) st.push_back(e);
           move_top_to(f.out.size(), f.cell_base);
-          pending++;                        // the `else` dispatch on the then-path
+          count_op(0x05);                   // the `else` dispatch on the then-path
           emit(OP_JMP);
           branch_fixup(f, false, uint32_t(last_emit), -1);  // end is not re-counted
         } else {
-          pending = 0;
+          drop_pending();
         }
         st.resize(f.height);
         for (uint8_t t : f.in) push_cell(t);
@@ -850,7 +867,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           for (auto &e : vals) st.push_back(e);
           move_top_to(f.out.size(), f.cell_base);
         } else {
-          pending = 0;
+          drop_pending();
         }
         if (f.kind == C_IF && !f.has_else) {
           if (f.in != f.out) fail(E_TYPECHECK, "if without else must not change the stack");
@@ -859,7 +876,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         place_label();
         int32_t tcnt = -int32_t(pending);
         uint32_t lpc = uint32_t(P.code.size());
-        pending++;                          // the `end` itself
+        count_op(0x0B);                     // the `end` itself
         if (f.kind != C_LOOP && !f.dead) resolve_label(f, lpc, tcnt);
         if (f.kind == C_FUNC) {
           uint32_t rc = 0;
@@ -1357,10 +1374,16 @@ struct ConstVal {
   uint32_t k[4];
 };
 
-ConstVal eval_const(Reader &r, const Program &P, const std::vector<ConstVal> &globals) {
+// `ops`: the expression's instructions (its `end` included) join Program::init_ops --
+// instantiation runs every constant expression through the interpreter loop, so each
+// one is counted and priced (engine.cpp:13-17; instantiate/global.cpp:42, elem.cpp:25,39,
+// data.cpp:27)
+ConstVal eval_const(Reader &r, const Program &P, const std::vector<ConstVal> &globals,
+                    std::vector<uint16_t> *ops) {
   ConstVal v{UNKNOWN, {0, 0, 0, 0}};
   for (;;) {
     uint8_t op = r.u8();
+    ops->push_back(op == 0xFD ? 0xFD0C : op);
     if (op == 0x0B) break;
     switch (op) {
       case 0x41: v.type = I32; v.k[0] = uint32_t(int32_t(r.sleb(32))); break;
@@ -1461,16 +1484,18 @@ void fuse_arx(Program &P) {
       I.w3 = y | (k << 16);
     }
     if (cnt > P.max_wasm_instrs_per_dispatch) P.max_wasm_instrs_per_dispatch = cnt;
+    P.dops[pc].insert(P.dops[pc].end(), P.dops[pc + 1].begin(), P.dops[pc + 1].end());
     drop[pc + 1] = 1;
     fused++;
   }
   if (!fused) return;
   std::vector<uint32_t> remap(n + 1);
   std::vector<DInstr> out;
+  std::vector<std::vector<uint16_t>> dout;
   out.reserve(n - fused);
   for (size_t pc = 0; pc < n; pc++) {
     remap[pc] = uint32_t(out.size());
-    if (!drop[pc]) out.push_back(P.code[pc]);
+    if (!drop[pc]) { out.push_back(P.code[pc]); dout.push_back(std::move(P.dops[pc])); }
   }
   remap[n] = uint32_t(out.size());
   for (DInstr &I : out) {
@@ -1482,6 +1507,7 @@ void fuse_arx(Program &P) {
   for (auto &f : P.funcs)
     if (!f.imported) { f.entry_pc = remap[f.entry_pc]; f.body_pc = remap[f.body_pc]; }
   P.code.swap(out);
+  P.dops.swap(dout);
 }
 
 void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
@@ -1569,7 +1595,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
         for (uint32_t k = 0; k < n; k++) {
           uint8_t t = s.u8();
           uint8_t mut = s.u8();
-          ConstVal v = eval_const(s, P, gvals);
+          ConstVal v = eval_const(s, P, gvals, &P.init_ops);
           if (v.type != t) throw Err{E_TYPECHECK, "type mismatch in global init"};
           gvals.push_back(v);
           P.global_types.push_back(t);
@@ -1602,7 +1628,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
           e.declarative = (flags & 3) == 3;
           if (e.active) {
             if (flags & 2) e.table = s.u32();
-            ConstVal off = eval_const(s, P, gvals);
+            ConstVal off = eval_const(s, P, gvals, &P.init_ops);
             e.offset = off.k[0];
           }
           if (flags & 3) {
@@ -1611,8 +1637,13 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
           }
           uint32_t m = s.u32();
           for (uint32_t q = 0; q < m; q++) {
-            if (flags & 4) e.items.push_back(eval_const(s, P, gvals).k[0]);
-            else e.items.push_back(s.u32());
+            if (flags & 4) {
+              e.items.push_back(eval_const(s, P, gvals, &P.init_ops).k[0]);
+            } else {   // a function index: the loader makes it `ref.func i; end` (segment.cpp:152-161)
+              e.items.push_back(s.u32());
+              P.init_ops.push_back(0xD2);
+              P.init_ops.push_back(0x0B);
+            }
           }
           P.elems.push_back(e);
         }
@@ -1650,7 +1681,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
           DataSeg d;
           d.active = !(flags & 1);
           if (flags == 2) s.u32();
-          if (d.active) d.offset = eval_const(s, P, gvals).k[0];
+          if (d.active) d.offset = eval_const(s, P, gvals, &P.init_ops).k[0];
           uint32_t m = s.u32();
           if (uint64_t(s.end - s.p) < m) throw Err{E_MALFORMED, "length out of bounds"};
           d.bytes.assign(s.p, s.p + m);
@@ -1754,10 +1785,36 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   }
   fuse_arx(P);
   find_loops(P);
+  // every instruction's opcode list holds exactly the `cnt` instructions it retires
+  if (P.dops.size() != P.code.size()) throw Err{E_UNSUPPORTED, "internal: opcode lists out of step"};
+  for (size_t pc = 0; pc < P.code.size(); pc++)
+    if (((P.code[pc].w0 >> 16) & 0xFFu) != P.dops[pc].size())
+      throw Err{E_UNSUPPORTED, "internal: opcode list of pc " + std::to_string(pc) + " does not match its count"};
   if (P.code.size() >= DBC_MAX_PC) throw Err{E_UNSUPPORTED, "module too large for 20-bit pcs"};
 }
 
 }  // namespace
+
+uint64_t build_cost_pool(const Program &P, const uint64_t *tab, uint64_t limit,
+                         std::vector<uint32_t> &off, std::vector<uint64_t> &pool, bool *exceeded) {
+  off.assign(P.code.size() + 1, 0);
+  pool.clear();
+  for (size_t pc = 0; pc < P.code.size(); pc++) {
+    off[pc] = uint32_t(pool.size());
+    uint64_t s = 0;
+    for (uint16_t op : P.dops[pc]) { s += tab[op]; pool.push_back(s); }
+  }
+  off[P.code.size()] = uint32_t(pool.size());
+  if (pool.empty()) pool.push_back(0);
+  uint64_t c = 0;
+  *exceeded = false;
+  for (uint16_t op : P.init_ops) {
+    const uint64_t n = c + tab[op];
+    if (n > limit) { *exceeded = true; break; }
+    c = n;
+  }
+  return c;
+}
 
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
                          bool exact_globals) {

@@ -96,6 +96,14 @@ struct Program {
   int64_t start_func = -1;
   // lowered code
   std::vector<DInstr> code;
+  // per DBC instruction: the wasm opcodes (reference OpCode numbering, 0xFCxx / 0xFDxx for
+  // prefixed ones) of the instructions it retires, in execution order -- its `cnt`
+  // entries, the last `post` of them after the main op. A taken branch with tcnt = -k
+  // retires its landing instruction's list from entry k on; tcnt = +1 (if-false to an
+  // else arm) also retires an `else` (controlInstr.cpp:23-28). Cost tables price these.
+  std::vector<std::vector<uint16_t>> dops;
+  std::vector<uint16_t> init_ops;      // instructions of every constant expression (counted
+                                       // and priced by instantiation, before the start function)
   std::vector<uint32_t> brtab;         // pairs (target pc, tcnt as int32)
   std::vector<uint32_t> loops;         // per pc: (head, end) of the innermost loop around
                                        // it (a backward branch end -> head), ~0 if none
@@ -114,6 +122,14 @@ std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t 
                          bool exact_globals = false);
 
 int find_export(const Program &p, const std::string &name);
+
+// Gas metering tables for a cost table `tab` (65536 entries, indexed by the reference's
+// OpCode; statistics.h:32 CostTab): off[pc] / pool hold each DBC's prefix sums of the
+// costs of the instructions it retires (KParams::cost_pool); the return value is the gas
+// instantiation's constant expressions spend, priced one by one against `limit` like
+// Statistics::addCost (*exceeded: one of them fails with CostLimitExceeded).
+uint64_t build_cost_pool(const Program &p, const uint64_t *tab, uint64_t limit,
+                         std::vector<uint32_t> &off, std::vector<uint64_t> &pool, bool *exceeded);
 
 const char *dop_name(uint16_t op);
 

@@ -44,7 +44,15 @@ struct KParams {
   uint32_t resume;              // continue the lanes parked at a host import
   uint32_t hb_cells;
   uint64_t max_steps;           // instruction budget per instance (Interrupted, coarse)
-  uint64_t cost_limit;          // exact unit-cost gas limit (CostLimitExceeded), ~0 = none
+  // gas metering (statistics.h:32,69-91): when cost_off is set, every retired wasm
+  // instruction adds its cost to the lane's running total (LS_COST) and the first one
+  // that would take it past cost_limit fails with CostLimitExceeded (0x03), counted.
+  // cost_pool[cost_off[pc] + j] = the cost of DBC pc's first j+1 instructions
+  // (Program::dops, prefix sums); cost_else = the cost of a manually counted `else`.
+  uint64_t cost_limit;
+  const uint32_t *cost_off;
+  const uint64_t *cost_pool;
+  uint64_t cost_else;
   // per-lane tables (frontend.h Program::mut_tables), else NULL / 0 and `table` serves
   uint32_t *ltab;               // [wave][tab_words][64] refs, ~0 = null
   const uint32_t *tabinfo;      // [ntables][2]: first word, capacity
@@ -65,7 +73,8 @@ struct KParams {
 // reference keeps it in ModuleInstance / MemoryInstance / GlobalInstance): memory size,
 // dropped data segments, instantiation status (a trapped start function fails the
 // instance, module.cpp:160-170), the resume point of a lane parked at a host import
-// (pc, call-stack depth, arg/result cell; pc ~0 = not parked), then the global cells,
+// (pc, call-stack depth, arg/result cell; pc ~0 = not parked), the write mark, the gas
+// total, then the global cells,
 // then (per-lane tables only) each table's size and the dropped-elem-segment mask.
 #define LS_PAGES 0u
 #define LS_DROPPED 1u
@@ -74,4 +83,6 @@ struct KParams {
 #define LS_GSP 4u
 #define LS_HBASE 5u
 #define LS_HWM 6u      // one past the highest linear-memory byte written since instantiation
-#define LS_GLOBALS 7u
+#define LS_COST 7u     // 2 slots: the instance's running gas total (lo, hi), kept from
+                       // instantiation on like the reference VM's Statistics::CostSum
+#define LS_GLOBALS 9u
