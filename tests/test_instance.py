@@ -125,8 +125,8 @@ WRITER = assemble(r"""
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("frames", ["lds", "vgpr"])
-def test_gpu_reset_restores_fresh_memory(built, monkeypatch, frames):
+@pytest.mark.parametrize("frames,granule", [("lds", 4), ("vgpr", 4), ("lds", 16), ("vgpr", 128)])
+def test_gpu_reset_restores_fresh_memory(built, monkeypatch, frames, granule):
     """BatchReset re-instantiates memory: Reset rewrites only rows below each wave's write
     mark (LS_HWM), so every store kind (scalar, i64, byte, i16, v128, v128 lane, fill,
     copy, memory.init, a host function's write, host SetMemory, stores into grown pages)
@@ -139,8 +139,8 @@ def test_gpu_reset_restores_fresh_memory(built, monkeypatch, frames):
     n = 256
     rows = [[(i * 4093) % (2 * 65536 - 16) & ~15, i % 11] for i in range(n)]
     vals = batch.make_values(rows, [I32, I32])
-    ctx = batch.BatchContext(WRITER, n, device=0)
-    fresh = batch.BatchContext(WRITER, n, device=0)
+    ctx = batch.BatchContext(WRITER, n, device=0, memory_granule=granule)
+    fresh = batch.BatchContext(WRITER, n, device=0, memory_granule=granule)
     hostfuncs.register(ctx)
     try:
         h0 = fresh.memory_hash()

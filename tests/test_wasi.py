@@ -156,12 +156,13 @@ def _gpu(wasm, rows, func, ptypes, host_threads=0, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1, 0])
-def test_gpu_wasi_matches_oracle(built, threads):
-    """One service thread and the default pool (waves served concurrently)."""
+@pytest.mark.parametrize("threads,granule", [(1, 4), (0, 4), (0, 16)])
+def test_gpu_wasi_matches_oracle(built, threads, granule):
+    """One service thread and the default pool (waves served concurrently); word and
+    16-byte memory interleave under the host's memory view."""
     rows = [[x] for x in range(640)]
     ref = _oracle(WASI, rows)
-    got, side = _gpu(WASI, rows, "run", [I32], host_threads=threads)
+    got, side = _gpu(WASI, rows, "run", [I32], host_threads=threads, memory_granule=granule)
     assert compare([r[0] for r in ref], *got, [I32]) == []
     assert side == [(r[1], r[2], r[3]) for r in ref]
 

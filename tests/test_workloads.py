@@ -200,3 +200,20 @@ def test_gpu_c5_full_size(built):
     ref = _oracle_batch(wasm, "tile", [rows[i] for i in idx])
     sub = lambda a: [a[i] for i in idx]
     assert compare(ref, sub(rets), sub(st), sub(cnt), sub(h), [I64], exact=True) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("granule", [4, 8, 16, 128])
+def test_gpu_memory_granules_bit_exact(built, granule):
+    """The memory interleave granule is layout only (MemoryGranule, dbc_ops.h GMem): every
+    workload -- uniform (BLAKE3, Mandelbrot) and per-lane (quicksort, Collatz) addresses,
+    i64 / v128 / byte accesses, memory.grow zeroing -- and the memory hash are identical
+    at every granule."""
+    cases = _cases()
+    wasm, func, pt, rt, _ = cases["qsort"]
+    cases["qsort"] = (wasm, func, pt, rt, [[i, (i * 37) % 700] for i in range(130)])
+    for name in ("blake3", "qsort", "collatz", "mandel"):
+        wasm, func, pt, rt, rows = cases[name]
+        ref = oracle_run(O.Module(wasm), func, rows)
+        got = gpu_run(wasm, func, rows, pt, rt, memory_granule=granule)
+        assert compare(ref, *got, rt, exact=True) == [], name

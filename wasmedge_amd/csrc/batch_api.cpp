@@ -19,10 +19,10 @@ extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
                                          const uint32_t *ls, uint32_t ls_slots, uint32_t full,
-                                         hipStream_t s);
+                                         uint32_t g, hipStream_t s);
 extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
-                                         uint32_t mem_words, uint32_t n, hipStream_t s);
+                                         uint32_t mem_words, uint32_t n, uint32_t g, hipStream_t s);
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
                                            uint32_t global_cells, uint32_t ls_slots,
                                            uint32_t init_pages, uint32_t init_dropped,
@@ -76,6 +76,15 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (!P.has_mem) budget = 0;
   C->mem_max_pages = budget;
   C->mem_words = budget << 14;
+  // interleave granule of the wave's linear memories (DESIGN.md "Linear memory"): 4-byte
+  // words when the module's addresses are wave-uniform, wider granules (a lane's
+  // consecutive words together) when they diverge per lane (Program::divergent_mem)
+  uint32_t gb = C->conf.MemoryGranule;
+  if (const char *e = getenv("WB_GRANULE")) gb = uint32_t(atoi(e));
+  if (gb == 0) gb = P.divergent_mem ? 16 : 4;
+  if (gb < 4 || gb > 128 || (gb & (gb - 1)))
+    return C->fail(kRuntimeError, "MemoryGranule must be 0 or a power of two in [4, 128]");
+  C->mlog = uint32_t(__builtin_ctz(gb)) - 2;
   C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
   C->nwaves = (C->n + 63) / 64;
   // module image: active data segments over the initial pages
@@ -218,6 +227,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.total_cells = P.total_cells() ? P.total_cells() : 1;
   k.table_size = uint32_t(P.table0.size());
   k.mem_words = C->mem_words;
+  k.mlog = C->mlog;
   k.init_pages = P.mem_min;
   k.mem_max_pages = C->mem_max_pages;
   k.gs_depth = C->gs_depth;
@@ -353,13 +363,13 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->lstate.ptr, C->ls_slots,
-                                    C->mem_fresh ? 1u : 0u, C->stream), "mem init"))
+                                    C->mem_fresh ? 1u : 0u, C->mlog, C->stream), "mem init"))
     return R(kRuntimeError);
   C->mem_fresh = false;   // from now on every lane's write mark (LS_HWM) is valid
   // per-lane tables (instantiate/table.cpp + elem.cpp): every lane starts from the image
   if (P.mut_tables &&
       !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
-                                    P.tab_words, C->nwaves, nullptr, 0, 1u, C->stream), "table init"))
+                                    P.tab_words, C->nwaves, nullptr, 0, 1u, 0u, C->stream), "table init"))
     return R(kRuntimeError);
   // gas: instantiation's constant expressions are priced first (module.cpp order); one
   // past the limit fails the instantiation like the reference's VM::instantiate
@@ -456,7 +466,7 @@ WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_S
 WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Hashes) {
   if (!C) return R(kWrongVMWorkflow);
   if (!C->hip_ok(wb_launch_mem_hash(C->mem.ptr, C->lstate.ptr, C->ls_slots, C->hashes.ptr,
-                                    C->mem_words, C->n, C->stream), "hash"))
+                                    C->mem_words, C->n, C->mlog, C->stream), "hash"))
     return R(kRuntimeError);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "hash")) return R(kRuntimeError);
   if (!C->hip_ok(hipMemcpy(Hashes, C->hashes.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "hash"))

@@ -107,6 +107,7 @@ struct WasmEdge_BatchContext {
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0;
   uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
+  uint32_t mlog = 0;              // log2(words per memory interleave granule), KParams::mlog
   // current invocation
   int func = -1;
   uint32_t param_cells = 0, result_cells = 0;
@@ -129,10 +130,10 @@ namespace wbh {
 
 constexpr uint32_t kBlockWords = 1024;   // host-view block: 4 KiB of each of a wave's 64 lanes
 
-// Word `w` of instance `inst`'s linear memory in the lane-interleaved layout
-// (word w of lane l in wave v at ((v*W + w)*64 + l)).
-inline size_t mem_word(const WasmEdge_BatchContext *C, uint32_t inst, uint64_t w) {
-  return (size_t(inst / 64) * C->mem_words + w) * 64 + inst % 64;
+// Word `w` of lane `lane` within its wave's memory region, granules of 2^g words
+// (dbc_ops.h GMem): ((w >> g) * 64 + lane) * 2^g + (w & (2^g - 1)).
+inline size_t lane_word(uint64_t w, uint32_t lane, uint32_t g) {
+  return (size_t(w >> g) << (6 + g)) + (size_t(lane) << g) + size_t(w & ((1u << g) - 1u));
 }
 
 // The host's view of one wave's linear memories during a host-call service round

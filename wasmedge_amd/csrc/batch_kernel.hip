@@ -135,6 +135,8 @@ struct LdsFrame {
       "v_mov_b32 v102, %[gsp]\n\t" \
       "v_mov_b32 v101, %[hwm]\n\t" \
       "v_mov_b32 v103, %[stk]\n\t" \
+      "v_mov_b32 v99, %[msh]\n\t" \
+      "v_add_u32_e32 v100, 6, v99\n\t" \
       "s_mov_b32 s93, %[slds]\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
       "s_mov_b32 s95, %[low]\n\t" \
@@ -154,12 +156,12 @@ struct LdsFrame {
       "v_mov_b32 %[hwm], v101" \
       : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm) \
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
-        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), \
+        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
-        "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 
@@ -178,13 +180,14 @@ struct LdsFrame {
   "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255"
 template <bool VF>
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other, uint32_t low,
-                                           uint32_t fr, uint32_t pages, const uint32_t *mem,
+                                           uint32_t fr, uint32_t pages, const uint32_t *mem, uint32_t g,
                                            uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
   const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
   const uint32_t lw = __builtin_amdgcn_readfirstlane(low >= (1u << 26) ? 0xFFFFFFFFu : low << 5);
   const uint64_t m = (uint64_t)(uintptr_t)mem;
+  const uint32_t msh = 2u + g;   // gen_tc.py MSH1 (MSH2 = MSH1 + 6)
   const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
   const uint64_t cp = (uint64_t)(uintptr_t)tcode;   // as two words: no aligned pair needed
   const uint32_t clo = (uint32_t)cp, chi = (uint32_t)(cp >> 32);
@@ -203,7 +206,7 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
 
 template <bool VF, class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
-                                       uint32_t *const gs, uint32_t *const mem,
+                                       uint32_t *const gs, const GMem mem,
                                        uint32_t *const ls, uint32_t *const fs,
                                        lds_u32 *const stk) {
   // the bytecode is read through the constant address space so every fetch is one
@@ -378,7 +381,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
-          pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem, gsp, hwm, stk_lds, S_lds,
+          pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
@@ -588,7 +591,7 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
   // LDS call-stack slots of this wave follow the frames of all the block's waves
   lds_u32 *const stk = (lds_u32 *)(lds + ((((blockDim.x >> 6) * p.total_cells) + wib * p.gs_lds) << 6) + lane);
   interp<VF>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
-         p.mem + (size_t)wave * p.mem_words * 64u + lane,
+         GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
          p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
          p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
 }
@@ -612,7 +615,7 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_vf_kernel(const KParam
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
                    uint32_t init_words, uint32_t mem_words, uint32_t nwaves,
-                   const uint32_t *ls, uint32_t ls_slots, uint32_t full) {
+                   const uint32_t *ls, uint32_t ls_slots, uint32_t full, uint32_t g) {
   const uint32_t chunks = (init_words + 1023u) / 1024u;
   __shared__ uint32_t smax;
   for (size_t b = blockIdx.x; b < (size_t)nwaves * chunks; b += gridDim.x) {
@@ -627,6 +630,10 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
       const uint64_t hw = ((uint64_t)smax + 3u) / 4u;
       rows = (uint32_t)(hw < init_words ? hw : init_words);
       if (rows < image_words && image_words <= init_words) rows = image_words;
+      // whole granules: words [0, rows) of the 64 lanes are the linear range [0, rows*64)
+      const uint32_t gm = (1u << g) - 1u;
+      rows = (rows + gm) & ~gm;
+      if (rows > init_words) rows = init_words;
       __syncthreads();   // smax is reused by the next iteration
     }
     const uint32_t r1 = r0 + 1024u < rows ? r0 + 1024u : rows;
@@ -634,7 +641,8 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
     uint32_t *wm = mem + wave * mem_words * 64u;
     // size_t: rows past 2^26 (initial memories over 4096 pages) must not wrap
     for (size_t i = (size_t)r0 * 64u + threadIdx.x; i < (size_t)r1 * 64u; i += blockDim.x) {
-      const uint32_t word = (uint32_t)(i >> 6);
+      // linear index -> word: granule i >> (6 + g), word (i & (2^g - 1)) within it
+      const uint32_t word = (uint32_t)(((i >> (6 + g)) << g) | (i & ((1u << g) - 1u)));
       wm[i] = word < image_words ? image[word] : 0u;
     }
   }
@@ -664,16 +672,17 @@ wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_
 // Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
-                   uint64_t *hashes, uint32_t mem_words, uint32_t n) {
+                   uint64_t *hashes, uint32_t mem_words, uint32_t n, uint32_t g) {
   const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
   if (inst >= n) return;
   const uint32_t wave = inst >> 6, lane = inst & 63u;
-  const uint32_t *m = mem + (size_t)wave * mem_words * 64u + lane;
+  const uint32_t *m = mem + (size_t)wave * mem_words * 64u + (lane << g);
   const uint32_t pages = ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + lane];
   const uint64_t nw = (uint64_t)pages << 13;
   uint64_t h = 0;
   for (uint64_t i = 0; i < nw; i++) {
-    const uint64_t w = (uint64_t)m[(2 * i) << 6] | ((uint64_t)m[(2 * i + 1) << 6] << 32);
+    const uint64_t w = (uint64_t)m[goff((uint32_t)(2 * i), g)] |
+                       ((uint64_t)m[goff((uint32_t)(2 * i + 1), g)] << 32);
     h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
   }
   hashes[inst] = h ^ fmix64((uint64_t)pages + 0x1234567ull);
@@ -701,20 +710,20 @@ extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
                                          const uint32_t *ls, uint32_t ls_slots, uint32_t full,
-                                         hipStream_t s) {
+                                         uint32_t g, hipStream_t s) {
   const size_t total = (size_t)nwaves * ((init_words + 1023u) / 1024u);
   if (total == 0) return hipSuccess;
   const size_t blocks = total < 262144 ? total : 262144;
   hipLaunchKernelGGL(wb_mem_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, mem, image,
-                     image_words, init_words, mem_words, nwaves, ls, ls_slots, full);
+                     image_words, init_words, mem_words, nwaves, ls, ls_slots, full, g);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
-                                         uint32_t mem_words, uint32_t n, hipStream_t s) {
+                                         uint32_t mem_words, uint32_t n, uint32_t g, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mem, ls,
-                     ls_slots, hashes, mem_words, n);
+                     ls_slots, hashes, mem_words, n, g);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,

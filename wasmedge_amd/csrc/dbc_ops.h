@@ -386,11 +386,24 @@ WB_HD void vunx(uint32_t sub, const uint32_t *x, uint32_t *r) {
 }
 
 // ------------------------------------------------------------- linear memory access
-// m points at word 0 of this lane (stride 64 words between consecutive words).
-WB_HD uint32_t mword(const uint32_t *m, uint32_t w) {
-  return m[(size_t)w << WB_MSHIFT];
+// A lane's linear memory as seen by the step code. The emulator passes a plain pointer
+// (its memory is contiguous per instance, WB_MSHIFT 0). The kernel passes a GMem: the
+// wave's 64 memories interleaved in granules of 2^g words -- word w of lane l at
+// ((w >> g) * 64 + l) * 2^g + (w & (2^g - 1)) words from the wave's base (g = 0: word
+// interleave; the kernel's `p` already includes the lane's l * 2^g).
+struct GMem {
+  uint32_t *p;
+  uint32_t g;
+};
+WB_HD uint32_t *mw(uint32_t *m, uint32_t w) { return &m[(size_t)w << WB_MSHIFT]; }
+WB_HD const uint32_t *mw(const uint32_t *m, uint32_t w) { return &m[(size_t)w << WB_MSHIFT]; }
+WB_HD size_t goff(uint32_t w, uint32_t g) {
+  return ((size_t)(w >> g) << (6 + g)) | (size_t)(w & ((1u << g) - 1u));
 }
-WB_HD uint64_t mload(const uint32_t *m, uint32_t ea, uint32_t n) {
+WB_HD uint32_t *mw(GMem m, uint32_t w) { return &m.p[goff(w, m.g)]; }
+
+template <class M> WB_HD uint32_t mword(M m, uint32_t w) { return *mw(m, w); }
+template <class M> WB_HD uint64_t mload(M m, uint32_t ea, uint32_t n) {
   const uint32_t w = ea >> 2, s = (ea & 3u) * 8u;
   if (s == 0) {
     if (n == 4) return mword(m, w);
@@ -408,7 +421,7 @@ WB_HD uint64_t mload(const uint32_t *m, uint32_t ea, uint32_t n) {
 }
 // Naturally aligned accesses (ea % min(n,4) == 0), branch-free per lane: n is uniform,
 // an access never straddles a 32-bit word except the two words of an 8-byte one.
-WB_HD uint64_t mload_aligned(const uint32_t *m, uint32_t ea, uint32_t n) {
+template <class M> WB_HD uint64_t mload_aligned(M m, uint32_t ea, uint32_t n) {
   const uint32_t w = ea >> 2;
   const uint32_t x = mword(m, w);
   if (n == 8) return (uint64_t)x | ((uint64_t)mword(m, w + 1) << 32);
@@ -416,33 +429,33 @@ WB_HD uint64_t mload_aligned(const uint32_t *m, uint32_t ea, uint32_t n) {
   const uint32_t y = x >> ((ea & 3u) * 8u);
   return n == 1 ? (y & 0xFFu) : (y & 0xFFFFu);
 }
-WB_HD void mstore_aligned(uint32_t *m, uint32_t ea, uint32_t n, uint64_t v) {
-  uint32_t *p = &m[(size_t)(ea >> 2) << WB_MSHIFT];
+template <class M> WB_HD void mstore_aligned(M m, uint32_t ea, uint32_t n, uint64_t v) {
+  uint32_t *p = mw(m, ea >> 2);
   if (n >= 4) {
     p[0] = (uint32_t)v;
-    if (n == 8) p[(size_t)1 << WB_MSHIFT] = (uint32_t)(v >> 32);
+    if (n == 8) *mw(m, (ea >> 2) + 1) = (uint32_t)(v >> 32);
   } else if (n == 2) {
     reinterpret_cast<uint16_t *>(p)[(ea & 3u) >> 1] = (uint16_t)v;
   } else {
     reinterpret_cast<uint8_t *>(p)[ea & 3u] = (uint8_t)v;
   }
 }
-WB_HD void mstore(uint32_t *m, uint32_t ea, uint32_t n, uint64_t v) {
+template <class M> WB_HD void mstore(M m, uint32_t ea, uint32_t n, uint64_t v) {
   if ((ea & 3u) == 0 && n >= 4) {
-    m[(size_t)(ea >> 2) << WB_MSHIFT] = (uint32_t)v;
-    if (n == 8) m[(size_t)((ea >> 2) + 1) << WB_MSHIFT] = (uint32_t)(v >> 32);
+    *mw(m, ea >> 2) = (uint32_t)v;
+    if (n == 8) *mw(m, (ea >> 2) + 1) = (uint32_t)(v >> 32);
     return;
   }
   for (uint32_t k = 0; k < n; k++) {
     const uint32_t a = ea + k;
-    reinterpret_cast<uint8_t *>(&m[(size_t)(a >> 2) << WB_MSHIFT])[a & 3u] = (uint8_t)(v >> (8 * k));
+    reinterpret_cast<uint8_t *>(mw(m, a >> 2))[a & 3u] = (uint8_t)(v >> (8 * k));
   }
 }
-WB_HD uint8_t mbyte(const uint32_t *m, uint32_t a) {
-  return reinterpret_cast<const uint8_t *>(&m[(size_t)(a >> 2) << WB_MSHIFT])[a & 3u];
+template <class M> WB_HD uint8_t mbyte(M m, uint32_t a) {
+  return reinterpret_cast<const uint8_t *>(mw(m, a >> 2))[a & 3u];
 }
-WB_HD void mbyte_set(uint32_t *m, uint32_t a, uint8_t v) {
-  reinterpret_cast<uint8_t *>(&m[(size_t)(a >> 2) << WB_MSHIFT])[a & 3u] = v;
+template <class M> WB_HD void mbyte_set(M m, uint32_t a, uint8_t v) {
+  reinterpret_cast<uint8_t *>(mw(m, a >> 2))[a & 3u] = v;
 }
 
 WB_HD uint32_t clz32(uint32_t x) { return x ? __builtin_clz(x) : 32; }

@@ -303,8 +303,8 @@ __attribute__((visibility("default"))) int wb_emu_disasm(const uint8_t *wasm, ui
              I.w1 >> 16, I.w2 & 0xFFFF, int(int16_t(I.w2 >> 16)), I.w3);
     s += buf;
   }
-  snprintf(buf, sizeof buf, "; globals=%u frame=%u code=%zu\n", P.global_cells, P.frame_cells,
-           P.code.size());
+  snprintf(buf, sizeof buf, "; globals=%u frame=%u code=%zu divergent_mem=%d\n", P.global_cells,
+           P.frame_cells, P.code.size(), int(P.divergent_mem));
   s += buf;
   if (out && outlen) {
     strncpy(out, s.c_str(), outlen - 1);

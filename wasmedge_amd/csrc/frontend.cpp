@@ -234,6 +234,7 @@ struct Entry {
   uint32_t local;       // K_LOCAL: local index
   uint32_t k[4];        // K_CONST: value words
   int64_t producer;     // index of the DInstr that wrote this cell as `c`, -1 if none
+  bool var = true;      // may differ between instances (Program::divergent_mem analysis)
 };
 
 struct Fixup {
@@ -264,15 +265,30 @@ struct CallFix {
   uint32_t callee;
 };
 
+// Which locals may hold per-instance values, by function (flow-insensitive): the
+// parameters of functions the host or call_indirect can call, every local ever set from
+// a parameter / loaded value / mutable global / call result, and (interprocedurally) the
+// parameters some call site passes such a value. Lowering repeats until it is stable;
+// Program::divergent_mem then says whether a load/store address can depend on one.
+struct VarInfo {
+  std::vector<std::vector<uint8_t>> locals;
+  bool changed = false;
+};
+
 class Lowerer {
  public:
-  Lowerer(Program &P, const uint8_t *bin) : P(P), bin(bin) {}
+  Lowerer(Program &P, const uint8_t *bin, VarInfo &vi) : P(P), bin(bin), vi(vi) {}
 
   void lower_function(uint32_t fi, std::vector<CallFix> &callfix);
 
  private:
   Program &P;
   const uint8_t *bin;
+  VarInfo &vi;
+  uint32_t cur_fn = 0;
+  void set_var_local(uint32_t f, uint32_t li) {
+    if (!vi.locals[f][li]) { vi.locals[f][li] = 1; vi.changed = true; }
+  }
   // per function
   const FuncType *ft = nullptr;
   std::vector<uint8_t> ltypes;
@@ -368,12 +384,14 @@ class Lowerer {
   void push_const(uint8_t t, const uint32_t *k) {
     Entry &e = push_cell(t);
     e.kind = K_CONST;
+    e.var = false;
     memcpy(e.k, k, sizeof e.k);
   }
   void push_local(uint32_t li) {
     Entry &e = push_cell(ltypes[li]);
     e.kind = K_LOCAL;
     e.local = li;
+    e.var = vi.locals[cur_fn][li] != 0;
   }
   Entry pop_any() {
     Ctrl &f = ctrl.back();
@@ -584,11 +602,13 @@ void Lowerer::do_simple(const SimpleOp &s) {
   Entry ops[3];
   for (int q = npop - 1; q >= 0; q--) ops[q] = pop_t(sigt(s.sig[q]));
   uint8_t rt = colon[1] ? sigt(colon[1]) : 0;
+  bool var = false;
+  for (int q = 0; q < npop; q++) var = var || ops[q].var;
   if (!live()) {
     if (rt) push_cell(rt);
     return;
   }
-  if (try_fuse_simple(s, ops)) { push_cell(rt, last_emit); return; }
+  if (try_fuse_simple(s, ops)) { push_cell(rt, last_emit).var = var; return; }
   uint32_t c = top_cell();  // result lands where the first operand was
   if (npop >= 1) c = ops[0].cell;
   if (npop == 2 && s.dop_imm >= 0) {
@@ -605,7 +625,7 @@ void Lowerer::do_simple(const SimpleOp &s) {
       if (fits) {
         uint32_t a = src(ops[1 - which]);
         emit(uint16_t(s.dop_imm), a, 0, c, 0, imm);
-        push_cell(rt, last_emit);
+        push_cell(rt, last_emit).var = var;
         return;
       }
     }
@@ -614,7 +634,7 @@ void Lowerer::do_simple(const SimpleOp &s) {
   uint32_t b = npop >= 2 ? src(ops[1]) : 0;
   uint32_t d = npop >= 3 ? src(ops[2]) : 0;
   emit(s.dop, a, b, c, d, s.imm);
-  if (rt) push_cell(rt, last_emit);
+  if (rt) push_cell(rt, last_emit).var = var;
 }
 
 // Superinstructions (merged into the previous DInstr; no label can intervene):
@@ -689,6 +709,7 @@ void Lowerer::do_load(uint16_t dop, uint8_t rtype, Reader &r) {
   uint32_t off = r.u32();
   if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
   Entry a = pop_t(I32);
+  if (a.var) P.divergent_mem = true;
   if (!live()) { push_cell(rtype); return; }
   uint32_t ac = src(a);
   emit(dop, ac, 0, a.cell, 0, off);
@@ -701,6 +722,7 @@ void Lowerer::do_store(uint16_t dop, uint8_t vtype, Reader &r) {
   if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
   Entry v = pop_t(vtype);
   Entry a = pop_t(I32);
+  if (a.var) P.divergent_mem = true;
   if (!live()) return;
   uint32_t ac = src(a), vc = src(v);
   emit(dop, ac, vc, 0, 0, off);
@@ -713,6 +735,9 @@ void Lowerer::do_call(uint32_t callee) {
   // type-check args
   std::vector<Entry> args(np);
   for (size_t k = np; k > 0; k--) args[k - 1] = pop_t(t.params[k - 1]);
+  if (!P.funcs[callee].imported)
+    for (size_t k = 0; k < np; k++)
+      if (args[k].var) set_var_local(callee, uint32_t(k));
   if (!live()) {
     for (uint8_t r : t.results) push_cell(r);
     return;
@@ -743,6 +768,7 @@ void Lowerer::do_call(uint32_t callee) {
 // ------------------------------------------------------------------ lower one function
 void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
   callfix = &cf;
+  cur_fn = fi;
   FuncInfo &F = P.funcs[fi];
   ft = &P.types[F.type];
   ltypes = ft->params;
@@ -1043,6 +1069,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         uint32_t li = r.u32();
         if (li >= ltypes.size()) fail(E_TYPECHECK, "unknown local");
         Entry v = pop_t(ltypes[li]);
+        if (v.var) set_var_local(cur_fn, li);
         if (!live()) { if (op == 0x22) push_cell(ltypes[li]); break; }
         if (v.kind == K_LOCAL && v.local == li) { if (op == 0x22) st.push_back(v); break; }
         materialize_locals(li);
@@ -1063,7 +1090,7 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           if (live()) {
             uint32_t dst = top_cell();
             emit(w == 1 ? OP_MOV32 : w == 2 ? OP_MOV64 : OP_MOV128, P.global_cell[gi], 0, dst);
-            push_cell(t, last_emit);
+            push_cell(t, last_emit).var = P.global_mut[gi] != 0;   // a constant global is uniform
           } else push_cell(t);
         } else {
           if (!P.global_mut[gi]) fail(E_TYPECHECK, "global is immutable");
@@ -1746,13 +1773,35 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
   }
   // lower
   const Program before = P;
-  for (;;) {
+  VarInfo vi;
+  vi.locals.resize(P.funcs.size());
+  {
+    // per-instance entry points: exported functions (the host passes per-instance
+    // arguments) and functions reachable through a table (call_indirect from anywhere)
+    std::vector<uint8_t> entry(P.funcs.size(), 0);
+    for (const auto &e : P.exports) if (e.func < entry.size()) entry[e.func] = 1;
+    for (const auto &e : P.elems) for (uint32_t f : e.items) if (f < entry.size()) entry[f] = 1;
+    for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) {
+      const FuncInfo &F = P.funcs[f];
+      const size_t np = P.types[F.type].params.size();
+      vi.locals[f].assign(np + F.local_types.size(), 0);
+      if (entry[f]) std::fill(vi.locals[f].begin(), vi.locals[f].begin() + np, 1);
+    }
+  }
+  for (int round = 0;; round++) {
     try {
-      Lowerer L(P, wasm);
+      vi.changed = false;
+      Lowerer L(P, wasm, vi);
       std::vector<CallFix> callfix;
       for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
       for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
-      break;
+      if (!vi.changed || round >= 16) {
+        if (vi.changed) P.divergent_mem = true;   // not settled: assume divergence
+        break;
+      }
+      const bool mt = P.mut_tables;
+      P = before;
+      P.mut_tables = mt;
     } catch (NeedMutTables &) {
       P = before;
       P.mut_tables = true;

@@ -114,6 +114,9 @@ struct Program {
   // metered lowering: global.set never retargets its producer, so a cost-limit trap
   // between a value and its global.set leaves the global unwritten as in the reference
   bool exact_globals = false;
+  // some load/store address depends on per-instance data (a parameter, a loaded value, a
+  // global): the batch then interleaves memory in wider granules (batch_api.cpp)
+  bool divergent_mem = false;
 };
 
 // Load + validate + lower. Returns empty string on success, else an error message;

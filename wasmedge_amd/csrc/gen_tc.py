@@ -66,6 +66,8 @@ Y = ("v120", "v121"); YP = "v[120:121]"
 AADDR, BADDR, DADDR, CADDR = "v122", "v123", "v124", "v125"
 Z = ("v126", "v127"); ZP = "v[126:127]"
 GSP = "v102"          # this lane's call-stack depth (slots), in/out
+MSH1 = "v99"          # linear-memory granule: 2 + g (the wave interleaves its lanes'
+MSH2 = "v100"         # memories in granules of 4 << g bytes); 8 + g (bytes per granule row)
 HWM = "v101"          # one past the highest memory byte written (LS_HWM), in/out
 SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
 SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
@@ -788,15 +790,17 @@ def specs():
                     "v_cmp_ne_u32_e64 vcc, %d, %s" % (m, Y[0]),
                     "s_or_b64 %s, %s, vcc" % (T2, T2)]
         out += ["s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh(),
-                # address = mem + (ea >> 2) * 256 (+ ea & 3 for sub-word)
-                "v_add_u32_e64 %s, %s, %s" % (Y[0], A[0], g.x(4)),
-                "v_lshrrev_b32_e32 %s, 2, %s" % (W[0], Y[0]),
-                "v_lshlrev_b64 %s, 8, %s" % (XP, WP),          # W[1] is always 0
-                "v_lshl_add_u64 %s, %s, 0, %s" % (XP, XP, MEM)]
-        if n < 4:   # byte within the lane's word
-            out += ["v_and_b32_e32 %s, 3, %s" % (W[0], Y[0]),
-                    "v_lshl_add_u64 %s, %s, 0, %s" % (XP, WP, XP)]
+                "v_add_u32_e64 %s, %s, %s" % (Y[0], A[0], g.x(4))] + gaddr(XP, Y[0])
         return out
+
+    # address of byte `ea` of this lane's memory: MEM (wave base + lane granule) +
+    # (ea >> (2+g)) granule rows of 256 << g bytes + the byte within the granule
+    def gaddr(dst, ea):
+        return ["v_lshrrev_b32_e32 %s, %s, %s" % (W[0], MSH1, ea),
+                "v_lshlrev_b64 %s, %s, %s" % (dst, MSH2, WP),  # W[1] is always 0
+                "v_lshl_add_u64 %s, %s, 0, %s" % (dst, dst, MEM),
+                "v_bfe_u32 %s, %s, 0, %s" % (W[0], ea, MSH1),
+                "v_lshl_add_u64 %s, %s, 0, %s" % (dst, WP, dst)]
 
     LOADS = {   # name -> (bytes, load instr, result width, sign-extend high word)
         "LD32": (4, "global_load_dword", 32, None),
@@ -820,9 +824,11 @@ def specs():
                 "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], R[0])
             return out + [hi] + g.w64() + g.next()
         add(nm, [nm], body)
-    add("LD64", ["LD64"], lambda g: mem_check(g, 8) + [
+    def word2():   # ZP = address of the second word (ea + 4: maybe another granule)
+        return ["v_add_u32_e32 %s, 4, %s" % (Y[1], Y[0])] + gaddr(ZP, Y[1])
+    add("LD64", ["LD64"], lambda g: mem_check(g, 8) + word2() + [
         "global_load_dword %s, %s, off" % (R[0], XP),
-        "global_load_dword %s, %s, off offset:256" % (R[1], XP),
+        "global_load_dword %s, %s, off" % (R[1], ZP),
         "s_waitcnt vmcnt(0)"] + g.w64() + g.next())
     STORES = {"ST8": (1, "global_store_byte"), "ST16": (2, "global_store_short"),
               "ST32": (4, "global_store_dword")}
@@ -832,9 +838,9 @@ def specs():
     for nm, (n, ins) in STORES.items():
         add(nm, [nm], lambda g, n=n, ins=ins: mem_check(g, n) + [
             "%s %s, %s, off" % (ins, XP, B[0])] + mark(n) + g.next())
-    add("ST64", ["ST64"], lambda g: mem_check(g, 8) + [
+    add("ST64", ["ST64"], lambda g: mem_check(g, 8) + word2() + [
         "global_store_dword %s, %s, off" % (XP, B[0]),
-        "global_store_dword %s, %s, off offset:256" % (XP, B[1])] + mark(8) + g.next())
+        "global_store_dword %s, %s, off" % (ZP, B[1])] + mark(8) + g.next())
     # ---- fused pairs (V blob, converged mode): the instruction at pc (a fall-through
     # op) and the one at pc + 1 in one handler, saving a dispatch. tc.cpp picks the slot
     # from the two instructions' own slots (tc_pair_slot); each half reads its own

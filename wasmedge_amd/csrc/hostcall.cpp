@@ -49,7 +49,7 @@ uint8_t WaveView::rw(uint32_t lane, uint32_t off, uint32_t len, uint8_t *dst, co
     // bytes of this block: up to the block's last word
     const uint64_t bend = std::min<uint64_t>(end, uint64_t(b + 1) * kBlockWords * 4);
     for (; a < bend; a++) {
-      uint32_t &word = blk->w[size_t((a >> 2) % kBlockWords) * 64 + lane];
+      uint32_t &word = blk->w[lane_word((a >> 2) % kBlockWords, lane, C->mlog)];
       const uint32_t sh = 8 * uint32_t(a & 3);
       if (dst) *dst++ = uint8_t(word >> sh);
       else word = (word & ~(0xFFu << sh)) | (uint32_t(*src++) << sh);
@@ -80,34 +80,29 @@ uint64_t mem_size(const WasmEdge_BatchMemoryContext *M) {
 }
 
 // Read (dst) or write (src) bytes of one instance's linear memory outside a service round
-// (WasmEdge_BatchGetMemory/SetMemory): gather the lane's interleaved words, patch, scatter.
+// (WasmEdge_BatchGetMemory/SetMemory): a one-lane WaveView over its wave's blocks.
 uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
                uint8_t *Dst, const uint8_t *Src) {
   if (Inst >= C->n) return C->fail(kRuntimeError, "instance index out of range");
-  uint32_t pages = WasmEdge_BatchGetMemoryPages(C, Inst);
-  if (uint64_t(Off) + Len > (uint64_t(pages) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
+  const uint32_t lane = Inst % 64;
+  uint32_t pages[64] = {0}, hwm[64] = {0};
+  pages[lane] = WasmEdge_BatchGetMemoryPages(C, Inst);
+  if (uint64_t(Off) + Len > (uint64_t(pages[lane]) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
   if (Len == 0) return 0;
-  const uint32_t w0 = Off / 4, w1 = uint32_t((uint64_t(Off) + Len + 3) / 4);
-  const size_t pitch = 64 * sizeof(uint32_t);
-  uint32_t *base = C->mem.ptr + mem_word(C, Inst, w0);
-  std::vector<uint32_t> words(w1 - w0);
-  if (!C->hip_ok(hipMemcpy2D(words.data(), 4, base, pitch, 4, words.size(), hipMemcpyDeviceToHost), "memory"))
+  uint32_t *mark = C->lstate.ptr + (size_t(Inst / 64) * C->ls_slots + LS_HWM) * 64 + lane;
+  if (Src && !C->hip_ok(hipMemcpy(&hwm[lane], mark, 4, hipMemcpyDeviceToHost), "memory"))
     return kRuntimeError;
-  uint8_t *bytes = reinterpret_cast<uint8_t *>(words.data()) + (Off & 3);
-  if (Dst) { memcpy(Dst, bytes, Len); return 0; }
-  memcpy(bytes, Src, Len);
-  if (!C->hip_ok(hipMemcpy2D(base, pitch, words.data(), 4, 4, words.size(), hipMemcpyHostToDevice), "memory"))
+  WaveView view;
+  view.C = C;
+  view.wave = Inst / 64;
+  view.pages = pages;
+  view.hwm = hwm;
+  const uint8_t e = view.rw(lane, Off, Len, Dst, Src);
+  if (!view.flush()) { C->last_error = "memory: device copy failed"; return kRuntimeError; }
+  if (e) return e;
+  // the raised write mark (LS_HWM): the next Reset re-initialises these bytes
+  if (view.hwm_dirty && !C->hip_ok(hipMemcpy(mark, &hwm[lane], 4, hipMemcpyHostToDevice), "memory"))
     return kRuntimeError;
-  // raise the lane's write mark (LS_HWM) so the next Reset re-initialises these bytes
-  uint32_t *mark = C->lstate.ptr + (size_t(Inst / 64) * C->ls_slots + LS_HWM) * 64 + Inst % 64;
-  uint32_t hw = 0;
-  if (!C->hip_ok(hipMemcpy(&hw, mark, 4, hipMemcpyDeviceToHost), "memory"))
-    return kRuntimeError;
-  const uint64_t end = uint64_t(Off) + Len;
-  if (end > hw) {
-    hw = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(end);
-    if (!C->hip_ok(hipMemcpy(mark, &hw, 4, hipMemcpyHostToDevice), "memory")) return kRuntimeError;
-  }
   return 0;
 }
 

@@ -35,6 +35,7 @@ struct KParams {
   uint32_t global_cells, total_cells;
   uint32_t table_size;
   uint32_t mem_words;           // words per lane reserved (= mem_max_pages * 16384)
+  uint32_t mlog;                // log2 of the words per interleave granule (dbc_ops.h GMem)
   uint32_t init_pages, mem_max_pages;
   uint32_t gs_depth;            // call-stack cells per lane
   uint32_t gs_lds;              // of which the first gs_lds live in LDS (after the frames)
