@@ -96,7 +96,7 @@ typedef struct WasmEdge_BatchConfigure {
   uint32_t CostTableLen;
   /* Bytes per granule in which the device interleaves the linear memories of a wave's 64
    * instances (4, 8, ..., 128; 0 = chosen from the module: 4 when its memory addresses
-   * are the same in every instance, 16 when they depend on per-instance data). Layout
+   * are the same in every instance, 128 when they depend on per-instance data). Layout
    * only: results never depend on it. */
   uint32_t MemoryGranule;
 } WasmEdge_BatchConfigure;

@@ -81,7 +81,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // consecutive words together) when they diverge per lane (Program::divergent_mem)
   uint32_t gb = C->conf.MemoryGranule;
   if (const char *e = getenv("WB_GRANULE")) gb = uint32_t(atoi(e));
-  if (gb == 0) gb = P.divergent_mem ? 16 : 4;
+  if (gb == 0) gb = P.divergent_mem ? 128 : 4;   // profiles/r02h_c3_granules.json
   if (gb < 4 || gb > 128 || (gb & (gb - 1)))
     return C->fail(kRuntimeError, "MemoryGranule must be 0 or a power of two in [4, 128]");
   C->mlog = uint32_t(__builtin_ctz(gb)) - 2;

@@ -115,7 +115,7 @@ struct Program {
   // between a value and its global.set leaves the global unwritten as in the reference
   bool exact_globals = false;
   // some load/store address depends on per-instance data (a parameter, a loaded value, a
-  // global): the batch then interleaves memory in wider granules (batch_api.cpp)
+  // global): the batch then interleaves memory in 128-byte granules (batch_api.cpp)
   bool divergent_mem = false;
 };
 
