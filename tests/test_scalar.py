@@ -16,7 +16,8 @@ binary (none can be built here): beyond that, parity unpinned.
 
 On the GPU each case runs through the three execution engines: the threaded core with
 frames in VGPRs (default at these sizes), the threaded core with LDS frames
-(WB_VFRAME=0), and the compiled per-op step (WB_THREADED=0)."""
+(WB_VFRAME=0), the compiled per-op step (WB_THREADED=0), and the compiled step over
+frames in HBM (WB_HBMFRAME=1, the mode of frames too large for LDS)."""
 import pytest
 
 import oracle_py as O
@@ -28,7 +29,7 @@ ROWS = [[i] for i in range(S.N * S.N)]
 TRAP_ROWS = [[op, i] for op in range(len(S.trap_ops())) for i in range(S.N * S.N)]
 CTRL_ROWS = [[c, x] for c in range(8) for x in list(range(12)) + [40, 100, 300, 1000]]
 ENGINES = {"vframe": {"WB_VFRAME": "1"}, "ldsframe": {"WB_VFRAME": "0"},
-           "step": {"WB_THREADED": "0"}}
+           "step": {"WB_THREADED": "0"}, "hbmframe": {"WB_HBMFRAME": "1"}}
 TRAP_CODES = {0x84, 0x85, 0x86}
 
 

@@ -118,6 +118,12 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // through the compiled step instead (A/B measurement aid)
   const char *thr = getenv("WB_THREADED");
   C->threaded = !(thr && thr[0] == '0');
+  // frames that LDS cannot hold (a 64-lane cell row is 256 B; ~640 cells per wave at one
+  // wave per block) live in HBM and run in the compiled step; WB_HBMFRAME=1 forces it
+  // (A/B and test aid)
+  const char *hfe = getenv("WB_HBMFRAME");
+  C->frame_hbm = (size_t(P.total_cells()) + 1) * 256 + 256 > 150 * 1024 || (hfe && hfe[0] == '1');
+  if (C->frame_hbm) C->threaded = false;
   std::vector<TInstr> tcv;
   // V frames (frame cells in VGPRs while the core runs) when the frame fits in
   // v128..v255 and the batch needs at most 2 waves per SIMD (the V kernel's 256 VGPRs
@@ -155,7 +161,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // LDS call-stack slots per lane: what the frames leave of the LDS share each wave gets
   // at the occupancy this batch reaches (nwaves over 256 CUs, at most 16 waves per CU)
   {
-    const uint32_t tc = P.total_cells() ? P.total_cells() : 1;
+    const uint32_t tc = C->frame_hbm ? 0 : P.total_cells() ? P.total_cells() : 1;
     const uint32_t per_cu = std::min<uint32_t>(16, std::max<uint32_t>(4, (C->nwaves + 255) / 256));
     const uint32_t wave_cells = (160 * 1024 - 1024) / 256 / per_cu;   // 256 B per cell row
     uint32_t s = wave_cells > tc + 1 ? wave_cells - tc - 1 : 0;
@@ -175,6 +181,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
       !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
+      (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
       (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
@@ -216,6 +223,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.ls_tab = LS_GLOBALS + P.global_cells;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
   k.fsave = C->fsave.ptr; k.hcall = C->hcall.ptr; k.hbuf = C->hbuf.ptr;
+  k.hframe = C->frame_hbm ? C->hframe.ptr : nullptr;
   k.params = is_start ? nullptr : C->params.ptr;
   k.results = is_start ? nullptr : C->results.ptr;
   k.status = C->status.ptr; k.counts = C->counts.ptr;
@@ -247,10 +255,9 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 14 + 1024) * sizeof(uint64_t), C->stream);
 #endif
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
-  size_t wave_lds = size_t(k.total_cells + k.gs_lds) * 64 * 4;
+  size_t wave_lds = size_t((C->frame_hbm ? 0 : k.total_cells) + k.gs_lds) * 64 * 4;
   if (wave_lds + 256 > 160 * 1024)
-    return C->fail(kRuntimeError, "frame of " + std::to_string(k.total_cells) +
-                                      " cells exceeds LDS (global-frame mode: next)");
+    return C->fail(kRuntimeError, "internal: LDS share of a wave exceeds 160 KiB");
   uint32_t wpb = 4;
   while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
   uint32_t blocks = (C->nwaves + wpb - 1) / wpb;

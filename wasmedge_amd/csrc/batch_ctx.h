@@ -75,6 +75,8 @@ struct WasmEdge_BatchContext {
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
   bool threaded = true;
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
+  bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
+  DevBuf<uint32_t> hframe;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
   DevBuf<uint32_t> loops;         // Program::loops (scheduler)
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;

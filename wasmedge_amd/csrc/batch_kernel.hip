@@ -113,6 +113,15 @@ struct LdsFrame {
   __device__ __forceinline__ uint32_t lds_addr() const { return (uint32_t)(uintptr_t)fr; }
 };
 
+// Frames too large for LDS (KParams::hframe): cell-major, lane-minor in HBM like linear
+// memory's word interleave, [wave][cell][64]; the compiled step only (no threaded core).
+struct HbmFrame {
+  uint32_t *fr;
+  __device__ __forceinline__ uint32_t get(uint32_t i) const { return fr[(size_t)i << 6]; }
+  __device__ __forceinline__ void set(uint32_t i, uint32_t v) { fr[(size_t)i << 6] = v; }
+  __device__ __forceinline__ uint32_t lds_addr() const { return 0u; }
+};
+
 // Run the threaded core from uniform pc `pc` for the lanes in EXEC until it meets an
 // instruction it cannot finish for all of them (reason 0: the C++ step executes that
 // instruction next), or reaches `other` / the count limit (reason 1: back to the
@@ -599,6 +608,19 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
 extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p) {
   exec_body<false>(p);
 }
+// HBM frames: LDS holds only the waves' call-stack slots
+extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KParams p) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t inst = wave * 64u + lane;
+  HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
+  lds_u32 *const stk = (lds_u32 *)(lds + ((wib * p.gs_lds) << 6) + lane);
+  interp<false>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
+                p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
+                p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+}
 extern "C" __global__ void __launch_bounds__(256) wb_exec_vf_kernel(const KParams p) {
   exec_body<true>(p);
 }
@@ -698,9 +720,13 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_vf_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_hbm_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (vframe)
+  if (p->hframe)
+    hipLaunchKernelGGL(wb_exec_hbm_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
+  else if (vframe)
     hipLaunchKernelGGL(wb_exec_vf_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
   else
     hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);

@@ -23,6 +23,8 @@ struct KParams {
   uint32_t *fsave;              // frames of lanes parked at a host import, [wave][cell][64]
   uint32_t *hcall;              // [n] import being called (out) / result cells (in, ~0: done)
   uint32_t *hbuf;               // [n][hb_cells] import args (out) / results (in)
+  uint32_t *hframe;             // frames in HBM, [wave][cell][64], when they exceed LDS
+                                // (else NULL: frames in LDS / VGPRs)
   // per-instance inputs / outputs
   const uint32_t *params;       // [n][param_cells]
   uint32_t *results;            // [n][result_cells]
