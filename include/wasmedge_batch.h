@@ -111,6 +111,39 @@ WASMEDGE_BATCH_API WasmEdge_BatchContext *
 WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf, const uint8_t *WasmBuf,
                      uint32_t WasmLen, uint32_t NumInstances, WasmEdge_Result *Res);
 
+/* A table, memory or global the embedder provides for the module's imports of that
+ * kind -- the batched form of creating it (WasmEdge_TableInstanceCreate /
+ * MemoryInstanceCreate / GlobalInstanceCreate, wasmedge.h) and adding it to an import
+ * object (WasmEdge_ImportObjectAddTable/AddMemory/AddGlobal). Every instance gets a copy
+ * of its own, as each reference VM has its own import object: a memory of Min zeroed
+ * pages, a table of Min null references, a global holding Value. Matching follows
+ * lib/executor/instantiate/import.cpp: an import with no provider fails with UnknownImport
+ * (0x62); a provider of another reference / value type or mutability, or whose limits do
+ * not fit the import's (Min >= the import's min; a Max when the import has one, no larger),
+ * fails with IncompatibleImportType (0x61). Function imports bind later, through
+ * WasmEdge_BatchAddHostFunction / WasmEdge_BatchInitWASI. */
+#define WASMEDGE_BATCH_IMPORT_TABLE 1u
+#define WASMEDGE_BATCH_IMPORT_MEMORY 2u
+#define WASMEDGE_BATCH_IMPORT_GLOBAL 3u
+typedef struct WasmEdge_BatchImport {
+  WasmEdge_String ModuleName;
+  WasmEdge_String ExternalName;
+  uint32_t Kind;                /* WASMEDGE_BATCH_IMPORT_* (the reference ExternalType) */
+  uint32_t Min, Max;            /* table / memory limits */
+  uint32_t HasMax;
+  enum WasmEdge_ValType Type;   /* table: FuncRef / ExternRef; global: its value type */
+  uint32_t Mutable;             /* global: 1 = var */
+  WasmEdge_Value Value;         /* global: its initial value (a funcref is a function
+                                   index of the module, null 0xFFFFFFFF) */
+} WasmEdge_BatchImport;
+
+/* WasmEdge_BatchCreate with the module's table / memory / global imports provided. */
+WASMEDGE_BATCH_API WasmEdge_BatchContext *
+WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfigure *Conf, const uint8_t *WasmBuf,
+                                uint32_t WasmLen, uint32_t NumInstances,
+                                const WasmEdge_BatchImport *Imports, uint32_t ImportLen,
+                                WasmEdge_Result *Res);
+
 /* Run `FuncName` on every instance (one instance per lane). Instance state -- linear
  * memory and its size, globals, dropped data segments -- persists from one Execute/Run
  * to the next until BatchReset, as an instantiated module does in the reference VM.

@@ -67,6 +67,10 @@ def lib():
         L.om_run_batch_mb.restype = ctypes.c_double
         L.om_run_batch_mb.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 6 + [ctypes.c_int]
+        L.om_clear_imports.restype = None
+        L.om_add_import.restype = None
+        L.om_add_import.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_uint32] * 5 + \
+            [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         cpp = ctypes.POINTER(ctypes.c_char_p)
         L.om_set_wasi.restype = None
         L.om_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
@@ -259,6 +263,20 @@ def set_wasi(on, args=(), envs=()):
     def arr(v):
         return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
     lib().om_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
+
+
+def set_imports(imports):
+    """Provided tables / memories / globals for modules loaded afterwards: dicts with
+    module, name, kind (1 table, 2 memory, 3 global), type, mut, min, max (None = no max),
+    value (global)."""
+    L = lib()
+    L.om_clear_imports()
+    for i in imports or []:
+        v = int(i.get("value", 0)) & ((1 << 128) - 1)
+        mx = i.get("max")
+        L.om_add_import(i["module"].encode(), i["name"].encode(), i["kind"], i.get("type", 0),
+                        1 if i.get("mut") else 0, i.get("min", 0), mx or 0, 0 if mx is None else 1,
+                        v & ((1 << 64) - 1), v >> 64)
 
 
 def set_extern_value(handle, value):

@@ -69,7 +69,7 @@ typedef struct {
 } Func;
 
 typedef struct { uint8_t reftype; uint32_t min, max; int has_max; } TableT;
-typedef struct { uint8_t type, mut; uint32_t init_start, init_len; } GlobalT;
+typedef struct { uint8_t type, mut; uint32_t init_start, init_len; int imported; uint64_t lo, hi; } GlobalT;
 typedef struct { char *name; uint8_t kind; uint32_t idx; } Export;
 typedef struct {
   int mode;                          /* 0 active, 1 passive, 2 declarative */
@@ -642,6 +642,61 @@ static int load_limits(Rd *r, uint32_t *mn, uint32_t *mx, int *has) {
   return r->err;
 }
 
+/* TEST INFRASTRUCTURE: the tables / memories / globals the batched path's embedder
+ * provides (WasmEdge_BatchCreateWithImports), for modules importing them. Matching
+ * follows instantiate/import.cpp:35-42 (isLimitMatched) and :137-190. */
+typedef struct { char mod[32], name[32]; uint8_t kind, type, mut; uint32_t min, max; int has_max;
+                 uint64_t lo, hi; } ProvidedImport;
+static ProvidedImport g_provided[64];
+static int g_nprovided;
+void om_clear_imports(void) { g_nprovided = 0; }
+void om_add_import(const char *mod, const char *name, uint32_t kind, uint32_t type, uint32_t mut,
+                   uint32_t min, uint32_t max, int has_max, uint64_t lo, uint64_t hi) {
+  if (g_nprovided >= 64) return;
+  ProvidedImport *p = &g_provided[g_nprovided++];
+  memset(p, 0, sizeof *p);
+  strncpy(p->mod, mod, 31); strncpy(p->name, name, 31);
+  p->kind = (uint8_t)kind; p->type = (uint8_t)type; p->mut = (uint8_t)mut;
+  p->min = min; p->max = max; p->has_max = has_max; p->lo = lo; p->hi = hi;
+}
+static int limits_ok(const ProvidedImport *p, uint32_t min, int has_max, uint32_t max) {
+  if (p->min < min || (!p->has_max && has_max)) return 0;
+  if (p->has_max && has_max && p->max > max) return 0;
+  return 1;
+}
+static int import_entity(OMod *m, Rd *s, uint8_t kind, const char *mod, const char *name) {
+  uint8_t ty = 0, mut = 0;
+  uint32_t mn = 0, mx = 0; int hm = 0;
+  if (kind == 1) { ty = rd_u8(s); load_limits(s, &mn, &mx, &hm); }
+  else if (kind == 2) load_limits(s, &mn, &mx, &hm);
+  else if (kind == 3) { ty = rd_u8(s); mut = rd_u8(s); }
+  else return E_MALFORMED;
+  const ProvidedImport *p = NULL;
+  for (int k = 0; k < g_nprovided; k++)
+    if (g_provided[k].kind == kind && !strcmp(g_provided[k].mod, mod) && !strcmp(g_provided[k].name, name)) {
+      p = &g_provided[k];
+      break;
+    }
+  if (!p) return E_UNKNOWN_IMPORT;
+  if (kind == 1) {
+    if (p->type != ty || !limits_ok(p, mn, hm, mx)) return 0x61;
+    m->tables = realloc(m->tables, sizeof(TableT) * (m->ntables + 2));
+    TableT *t = &m->tables[m->ntables++];
+    t->reftype = p->type; t->min = p->min; t->max = p->max; t->has_max = p->has_max;
+  } else if (kind == 2) {
+    if (m->has_mem) return 0x51;
+    if (!limits_ok(p, mn, hm, mx)) return 0x61;
+    m->has_mem = 1; m->mem_min = p->min; m->mem_max = p->max; m->mem_has_max = p->has_max;
+  } else {
+    if (p->type != ty || p->mut != mut) return 0x61;
+    m->globals = realloc(m->globals, sizeof(GlobalT) * (m->nglobals + 2));
+    GlobalT *g = &m->globals[m->nglobals++];
+    memset(g, 0, sizeof *g);
+    g->type = ty; g->mut = mut; g->imported = 1; g->lo = p->lo; g->hi = p->hi;
+  }
+  return 0;
+}
+
 OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) {
   OMod *m = calloc(1, sizeof(OMod));
   m->page_limit = page_limit ? page_limit : 65536;
@@ -683,7 +738,10 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
           s.p += l;
         }
         uint8_t kind = rd_u8(&s);
-        if (kind != 0) { *err = E_UNKNOWN_IMPORT; break; }
+        if (kind != 0) {            /* table / memory / global: instantiate/import.cpp */
+          if ((*err = import_entity(m, &s, kind, nm[0], nm[1]))) break;
+          continue;
+        }
         uint32_t ti = rd_u32(&s);
         m->funcs = realloc(m->funcs, sizeof(Func) * (m->nfuncs + 1));
         memset(&m->funcs[m->nfuncs], 0, sizeof(Func));
@@ -701,29 +759,34 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
       for (uint32_t k = 0; k < nfunc_decl; k++) func_types[k] = rd_u32(&s);
       break;
     }
-    case 4: {
-      m->ntables = rd_u32(&s);
-      m->tables = calloc(m->ntables + 1, sizeof(TableT));
-      for (uint32_t k = 0; k < m->ntables; k++) {
-        m->tables[k].reftype = rd_u8(&s);
-        load_limits(&s, &m->tables[k].min, &m->tables[k].max, &m->tables[k].has_max);
+    case 4: {                       /* after any imported tables */
+      uint32_t n = rd_u32(&s), t0 = m->ntables;
+      m->tables = realloc(m->tables, sizeof(TableT) * (t0 + n + 1));
+      for (uint32_t k = 0; k < n; k++) {
+        memset(&m->tables[t0 + k], 0, sizeof(TableT));
+        m->tables[t0 + k].reftype = rd_u8(&s);
+        load_limits(&s, &m->tables[t0 + k].min, &m->tables[t0 + k].max, &m->tables[t0 + k].has_max);
       }
+      m->ntables = t0 + n;
       break;
     }
     case 5: {
       uint32_t n = rd_u32(&s);
-      if (n > 1) { *err = 0x51; break; }
+      if (n > 1 || (n && m->has_mem)) { *err = 0x51; break; }
       if (n) { m->has_mem = 1; load_limits(&s, &m->mem_min, &m->mem_max, &m->mem_has_max); }
       break;
     }
-    case 6: {
-      m->nglobals = rd_u32(&s);
-      m->globals = calloc(m->nglobals + 1, sizeof(GlobalT));
-      for (uint32_t k = 0; k < m->nglobals && !*err; k++) {
-        m->globals[k].type = rd_u8(&s);
-        m->globals[k].mut = rd_u8(&s);
-        *err = load_const_expr(m, &s, &m->globals[k].init_start, &m->globals[k].init_len);
+    case 6: {                       /* after any imported globals */
+      uint32_t n = rd_u32(&s), g0 = m->nglobals;
+      m->globals = realloc(m->globals, sizeof(GlobalT) * (g0 + n + 1));
+      for (uint32_t k = 0; k < n && !*err; k++) {
+        GlobalT *g = &m->globals[g0 + k];
+        memset(g, 0, sizeof(GlobalT));
+        g->type = rd_u8(&s);
+        g->mut = rd_u8(&s);
+        *err = load_const_expr(m, &s, &g->init_start, &g->init_len);
       }
+      m->nglobals = g0 + n;
       break;
     }
     case 7: {

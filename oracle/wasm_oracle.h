@@ -67,6 +67,13 @@ void om_set_wasi(int on, const char *const *args, uint32_t nargs, const char *co
 uint32_t om_wasi_exit_code(const OInst *i);
 uint64_t om_wasi_output(const OInst *i, uint32_t fd, const uint8_t **data);
 
+/* Tables / memories / globals provided for non-function imports (kind 1 table, 2 memory,
+ * 3 global; the batched path's WasmEdge_BatchCreateWithImports), for modules loaded
+ * afterwards. */
+void om_clear_imports(void);
+void om_add_import(const char *mod, const char *name, uint32_t kind, uint32_t type, uint32_t mut,
+                   uint32_t min, uint32_t max, int has_max, uint64_t lo, uint64_t hi);
+
 /* Test host module "extern" (the reference API test's): the int32 an externref handle
  * points to. Table entry write (ref: function index / handle, UINT64_MAX null) and a
  * global's value bits, as the reference C API's TableInstanceSetData / GlobalInstanceGetValue. */

@@ -23,6 +23,8 @@ def emu_lib():
         E.wb_emu_set_host.argtypes = [ctypes.c_void_p]
         E.wb_emu_set_cost_limit.argtypes = [ctypes.c_uint64]
         E.wb_emu_set_cost_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        E.wb_emu_add_import.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_uint32] * 6 + \
+            [ctypes.c_void_p]
         E.wb_emu_get_costs.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         cpp = ctypes.POINTER(ctypes.c_char_p)
         E.wb_emu_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
@@ -90,6 +92,19 @@ def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_s
         costs_out[:] = [int(x) for x in c]
     rets = [from_cells(res[i], rtypes) if st[i] == 0 else [] for i in range(n)]
     return rets, st, cnt, h
+
+
+def emu_set_imports(imports):
+    """Provided tables / memories / globals for the emulator (dicts as oracle_py.set_imports)."""
+    E = emu_lib()
+    E.wb_emu_clear_imports()
+    for i in imports or []:
+        v = int(i.get("value", 0)) & ((1 << 128) - 1)
+        cells = (ctypes.c_uint32 * 4)(*[(v >> (32 * q)) & 0xFFFFFFFF for q in range(4)])
+        mx = i.get("max")
+        E.wb_emu_add_import(i["module"].encode(), i["name"].encode(), i["kind"], i.get("type", 0),
+                            1 if i.get("mut") else 0, i.get("min", 0), mx or 0,
+                            0 if mx is None else 1, ctypes.cast(cells, ctypes.c_void_p))
 
 
 def emu_set_wasi(on, args=(), envs=()):

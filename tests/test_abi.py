@@ -57,3 +57,28 @@ def test_create_rejects_malformed_module(built):
     with pytest.raises(batch.WasmEdgeError) as e:
         batch.BatchContext(b"\x00asn\x01\x00\x00\x00", 64)
     assert e.value.code == 0x23          # ErrCode::MalformedMagic (enum.inc:603)
+
+
+def test_ctypes_layouts_match_the_header(tmp_path):
+    """The Python mirror's structures have the C header's layout (gcc on the header):
+    a mismatch would hand the library garbage pointers."""
+    import ctypes
+    import subprocess
+    from wasmedge_amd import batch as b
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "%s/include/wasmedge_batch.h"\n'
+                   'int main(void) {\n'
+                   '  printf("%%zu %%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchConfigure),\n'
+                   '         offsetof(WasmEdge_BatchConfigure, CostTable), offsetof(WasmEdge_BatchConfigure, MemoryGranule),\n'
+                   '         offsetof(WasmEdge_BatchConfigure, HostThreads));\n'
+                   '  printf("%%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchImport), offsetof(WasmEdge_BatchImport, Value),\n'
+                   '         offsetof(WasmEdge_BatchImport, Mutable));\n'
+                   '  printf("%%zu\\n", sizeof(WasmEdge_Value));\n'
+                   '  return 0;\n}\n' % ROOT)
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-o", str(exe), str(src)])
+    got = [list(map(int, line.split())) for line in subprocess.check_output([str(exe)]).decode().splitlines()]
+    C, I = b._Conf, b._Import
+    assert got[0] == [ctypes.sizeof(C), C.CostTable.offset, C.MemoryGranule.offset, C.HostThreads.offset]
+    assert got[1] == [ctypes.sizeof(I), I.Value.offset, I.Mutable.offset]
+    assert got[2] == [ctypes.sizeof(b._Value)]

@@ -65,6 +65,15 @@ class _String(ctypes.Structure):
     _fields_ = [("Length", ctypes.c_uint32), ("Buf", ctypes.c_char_p)]
 
 
+class _Import(ctypes.Structure):
+    """WasmEdge_BatchImport: a provided table / memory / global."""
+    _fields_ = [("ModuleName", _String), ("ExternalName", _String), ("Kind", ctypes.c_uint32),
+                ("Min", ctypes.c_uint32), ("Max", ctypes.c_uint32), ("HasMax", ctypes.c_uint32),
+                ("Type", ctypes.c_uint32), ("Mutable", ctypes.c_uint32),
+                ("_align", ctypes.c_uint32 * 2),   # WasmEdge_Value is 16-byte aligned (uint128)
+                ("Value", _Value)]
+
+
 class _Result(ctypes.Structure):
     _fields_ = [("Code", ctypes.c_uint8)]
 
@@ -109,6 +118,10 @@ def lib():
         L.WasmEdge_BatchCreate.restype = vp
         L.WasmEdge_BatchCreate.argtypes = [ctypes.POINTER(_Conf), ctypes.c_char_p, u32, u32,
                                            ctypes.POINTER(_Result)]
+        L.WasmEdge_BatchCreateWithImports.restype = vp
+        L.WasmEdge_BatchCreateWithImports.argtypes = [ctypes.POINTER(_Conf), ctypes.c_char_p, u32, u32,
+                                                      ctypes.POINTER(_Import), u32,
+                                                      ctypes.POINTER(_Result)]
         for name, args in [
             ("WasmEdge_BatchExecute", [vp, _String, vp, u32, vp, u32, vp, vp]),
             ("WasmEdge_BatchSetArgs", [vp, _String, vp, u32]),
@@ -202,7 +215,7 @@ class BatchContext:
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
-                 memory_granule=0):
+                 memory_granule=0, imports=None):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
         metering is on when cost_limit > 0."""
         L = lib()
@@ -213,8 +226,19 @@ class BatchContext:
                      host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
                      len(tab) if tab is not None else 0, memory_granule)
         res = _Result(0)
-        self._h = L.WasmEdge_BatchCreate(ctypes.byref(conf), bytes(wasm), len(wasm), n,
-                                         ctypes.byref(res))
+        imps = imports or []
+        arr = (_Import * max(1, len(imps)))()
+        self._import_names = []
+        for k, i in enumerate(imps):
+            mod, nm = i["module"].encode(), i["name"].encode()
+            self._import_names += [mod, nm]
+            mx = i.get("max")
+            arr[k] = _Import(_String(len(mod), mod), _String(len(nm), nm), i["kind"], i.get("min", 0),
+                             mx or 0, 0 if mx is None else 1, i.get("type", 0),
+                             1 if i.get("mut") else 0, (ctypes.c_uint32 * 2)(),
+                             _Value.make(i.get("value", 0), i.get("type", 0)))
+        self._h = L.WasmEdge_BatchCreateWithImports(ctypes.byref(conf), bytes(wasm), len(wasm), n,
+                                                    arr, len(imps), ctypes.byref(res))
         if not self._h:
             raise WasmEdgeError(res.Code, L.WasmEdge_BatchGetLastError(None).decode())
         self.n = n

@@ -35,7 +35,7 @@ namespace {
 
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
-  std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0);
+  std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
   // gas tables (statistics.h:32: unit costs unless the caller set a table)
@@ -301,6 +301,14 @@ extern "C" {
 WasmEdge_BatchContext *WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf,
                                             const uint8_t *WasmBuf, uint32_t WasmLen,
                                             uint32_t NumInstances, WasmEdge_Result *Res) {
+  return WasmEdge_BatchCreateWithImports(Conf, WasmBuf, WasmLen, NumInstances, nullptr, 0, Res);
+}
+
+WasmEdge_BatchContext *WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfigure *Conf,
+                                                       const uint8_t *WasmBuf, uint32_t WasmLen,
+                                                       uint32_t NumInstances,
+                                                       const WasmEdge_BatchImport *Imports,
+                                                       uint32_t ImportLen, WasmEdge_Result *Res) {
   if (!WasmBuf || NumInstances == 0) {
     g_last_create_error = "null buffer or zero instances";
     if (Res) *Res = R(kWrongVMWorkflow);
@@ -311,6 +319,20 @@ WasmEdge_BatchContext *WasmEdge_BatchCreate(const WasmEdge_BatchConfigure *Conf,
   else C->conf.DeviceOrdinal = -1;
   C->host_threads = C->conf.HostThreads;
   C->n = NumInstances;
+  for (uint32_t k = 0; Imports && k < ImportLen; k++) {
+    const WasmEdge_BatchImport &I = Imports[k];
+    wb::HostImport h;
+    h.module.assign(I.ModuleName.Buf ? I.ModuleName.Buf : "", I.ModuleName.Length);
+    h.name.assign(I.ExternalName.Buf ? I.ExternalName.Buf : "", I.ExternalName.Length);
+    h.kind = uint8_t(I.Kind);
+    h.type = uint8_t(I.Type);
+    h.mut = I.Mutable != 0;
+    h.min = I.Min;
+    h.max = I.Max;
+    h.has_max = I.HasMax != 0;
+    for (uint32_t q = 0; q < 4; q++) h.value[q] = uint32_t(I.Value.Value >> (32 * q));
+    C->imports.push_back(h);
+  }
   uint8_t e = setup(C, WasmBuf, WasmLen);
   if (!e) e = WasmEdge_BatchReset(C, nullptr).Code;   // instantiate every instance
   if (e) {

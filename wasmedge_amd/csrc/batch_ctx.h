@@ -61,6 +61,7 @@ struct WasmEdge_BatchMemoryContext {   // one instance's linear memory, for host
 struct WasmEdge_BatchContext {
   template <typename T> using DevBuf = wbh::DevBuf<T>;
   wb::Program prog;
+  std::vector<wb::HostImport> imports;   // provided tables / memories / globals
   WasmEdge_BatchConfigure conf{};
   uint32_t n = 0, nwaves = 0;
   int device = 0;

@@ -30,6 +30,7 @@ static wb_emu_host_t g_host = nullptr;
 static uint64_t g_cost_limit = ~0ull;   // gas limit (0 = none)
 static std::vector<uint64_t> g_cost_tab;   // cost per OpCode (empty: the unit table)
 static std::vector<uint64_t> g_costs;      // per instance: its gas total after the last run
+static std::vector<wb::HostImport> g_imports;   // provided tables / memories / globals
 // the library's WASI subset (wasi_impl.h), bound before g_host when on
 static bool g_wasi = false;
 static wbw::Env g_wasi_env;
@@ -74,6 +75,17 @@ __attribute__((visibility("default"))) void wb_emu_set_cost_table(const uint64_t
   g_cost_tab.assign(65536, 0ull);
   for (uint32_t k = 0; k < len && k < 65536; k++) g_cost_tab[k] = tab[k];
 }
+__attribute__((visibility("default"))) void wb_emu_clear_imports() { g_imports.clear(); }
+__attribute__((visibility("default"))) void wb_emu_add_import(const char *mod, const char *name, uint32_t kind,
+                                                              uint32_t type, uint32_t mut, uint32_t min,
+                                                              uint32_t max, uint32_t has_max,
+                                                              const uint32_t *value) {
+  wb::HostImport h;
+  h.module = mod; h.name = name; h.kind = uint8_t(kind); h.type = uint8_t(type); h.mut = mut != 0;
+  h.min = min; h.max = max; h.has_max = has_max != 0;
+  for (int q = 0; q < 4; q++) h.value[q] = value ? value[q] : 0u;
+  g_imports.push_back(h);
+}
 __attribute__((visibility("default"))) void wb_emu_get_costs(uint64_t *out, uint32_t n) {
   for (uint32_t k = 0; k < n && k < g_costs.size(); k++) out[k] = g_costs[k];
 }
@@ -103,7 +115,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     uint32_t max_pages, uint32_t gs_depth, uint64_t max_steps) {
   wb::Program P;
   uint8_t ec = 0;
-  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull);
+  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull, &g_imports);
   if (!g_err.empty()) return ec ? ec : 2;
   int f = wb::find_export(P, func);
   if (f < 0) { g_err = "function not found"; return 0x05; }

@@ -1537,7 +1537,15 @@ void fuse_arx(Program &P) {
   P.dops.swap(dout);
 }
 
-void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
+// instantiate/import.cpp:35-42 isLimitMatched(provided, declared)
+static bool limits_match(const HostImport &h, uint32_t min, bool has_max, uint32_t max) {
+  if (h.min < min || (!h.has_max && has_max)) return false;
+  if (h.has_max && has_max && h.max > max) return false;
+  return true;
+}
+
+void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
+                     const std::vector<HostImport> *imports) {
   if (len < 8 || memcmp(wasm, "\0asm\1\0\0\0", 8)) throw Err{0x23, "magic header not detected"};
   Reader r{wasm + 8, wasm + len};
   std::vector<uint32_t> decl_types;
@@ -1568,7 +1576,55 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
         for (uint32_t k = 0; k < n; k++) {
           std::string mod = s.name(), nm = s.name();
           uint8_t kind = s.u8();
-          if (kind != 0) throw Err{E_UNSUPPORTED, "only function imports are supported"};
+          if (kind != 0) {
+            // a table / memory / global import (instantiate/import.cpp:137-190)
+            if (kind > 3) throw Err{E_MALFORMED, "malformed import kind"};
+            uint8_t ty = 0, mut = 0, fl = 0;
+            uint32_t mn = 0, mx = 0;
+            if (kind == 1) ty = s.u8();
+            if (kind == 1 || kind == 2) {
+              fl = s.u8();
+              mn = s.u32();
+              if (fl & 1) mx = s.u32();
+            } else {
+              ty = s.u8();
+              mut = s.u8();
+            }
+            const HostImport *h = nullptr;
+            if (imports)
+              for (const auto &x : *imports)
+                if (x.module == mod && x.name == nm && x.kind == kind) { h = &x; break; }
+            if (!h) throw Err{0x62, "unknown import " + mod + "." + nm};
+            if (kind == 1) {
+              if (h->type != ty || !limits_match(*h, mn, fl & 1, mx))
+                throw Err{0x61, "incompatible import type " + mod + "." + nm};
+              TableInfo t;
+              t.type = h->type;
+              t.min = h->min;
+              t.has_max = h->has_max;
+              t.max = h->max;
+              P.tables.push_back(t);
+              P.ntables = uint32_t(P.tables.size());
+            } else if (kind == 2) {
+              if (P.has_mem) throw Err{0x51, "multiple memories"};
+              if (!limits_match(*h, mn, fl & 1, mx))
+                throw Err{0x61, "incompatible import type " + mod + "." + nm};
+              if (h->min > 65536 || (h->has_max && h->max > 65536))
+                throw Err{0x53, "memory size must be at most 65536 pages (4GiB)"};
+              P.has_mem = true;
+              P.mem_min = h->min;
+              P.mem_has_max = h->has_max;
+              P.mem_max = h->has_max ? h->max : 65536;
+            } else {
+              if (h->type != ty || uint8_t(h->mut) != mut)
+                throw Err{0x61, "incompatible import type " + mod + "." + nm};
+              ConstVal v{ty, {h->value[0], h->value[1], h->value[2], h->value[3]}};
+              gvals.push_back(v);
+              P.global_types.push_back(ty);
+              P.global_mut.push_back(mut);
+            }
+            continue;
+          }
           FuncInfo f;
           f.type = s.u32();
           if (f.type >= P.types.size()) throw Err{E_TYPECHECK, "unknown type"};
@@ -1606,7 +1662,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P) {
       }
       case 5: {
         uint32_t n = s.u32();
-        if (n > 1) throw Err{0x51, "multiple memories"};
+        if (n > 1 || (n && P.has_mem)) throw Err{0x51, "multiple memories"};
         if (n) {
           uint8_t fl = s.u8();
           P.has_mem = true;
@@ -1866,11 +1922,11 @@ uint64_t build_cost_pool(const Program &P, const uint64_t *tab, uint64_t limit,
 }
 
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
-                         bool exact_globals) {
+                         bool exact_globals, const std::vector<HostImport> *imports) {
   try {
     out = Program();
     out.exact_globals = exact_globals;
-    parse_and_lower(wasm, len, out);
+    parse_and_lower(wasm, len, out, imports);
     *errcode = 0;
     return "";
   } catch (const Err &e) {

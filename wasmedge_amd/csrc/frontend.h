@@ -119,10 +119,26 @@ struct Program {
   bool divergent_mem = false;
 };
 
+// A table, memory or global import the embedder provides (WasmEdge_BatchImport). Every
+// instance gets a copy of its own, as each reference VM gets its own import object: a
+// memory of `min` zeroed pages, a table of `min` null references, a global = value.
+struct HostImport {
+  std::string module, name;
+  uint8_t kind = 0;                  // 1 table, 2 memory, 3 global (ExternalType)
+  uint8_t type = 0;                  // table: reference type; global: value type
+  bool mut = false;                  // global
+  uint32_t min = 0, max = 0;         // table / memory limits
+  bool has_max = false;
+  uint32_t value[4] = {0, 0, 0, 0};  // global: its value as cells
+};
+
 // Load + validate + lower. Returns empty string on success, else an error message;
-// *errcode receives the reference ErrCode byte (include/common/enum.inc).
+// *errcode receives the reference ErrCode byte (include/common/enum.inc). Non-function
+// imports resolve against `imports` like instantiate/import.cpp (UnknownImport 0x62,
+// IncompatibleImportType 0x61).
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
-                         bool exact_globals = false);
+                         bool exact_globals = false,
+                         const std::vector<HostImport> *imports = nullptr);
 
 int find_export(const Program &p, const std::string &name);
 

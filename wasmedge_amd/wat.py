@@ -230,6 +230,39 @@ class Assembler:
                     f.locals += [VALTYPES[t] for t in it[1:]]
         return rest
 
+    def _import_other(self, fld, desc):
+        """(import "m" "n" (memory $x? min max?)) / (table $x? min max? reftype) /
+        (global $x? type | (mut type)): takes the first indices of its kind."""
+        imp = (_strbytes(fld[1]), _strbytes(fld[2]))
+        rest = desc[1:]
+        name = None
+        if rest and isinstance(rest[0], str) and rest[0].startswith("$"):
+            name, rest = rest[0], rest[1:]
+        if desc[0] == "memory":
+            if name:
+                self.mem_names[name] = len(self.mems)
+            nums = [int(x) for x in rest]
+            self.mems.append((nums[0], nums[1] if len(nums) > 1 else None, imp))
+        elif desc[0] == "table":
+            if name:
+                self.table_names[name] = len(self.tables)
+            nums, rt = [], 0x70
+            for it in rest:
+                if it in VALTYPES:
+                    rt = VALTYPES[it]
+                else:
+                    nums.append(int(it))
+            self.tables.append((rt, nums[0], nums[1] if len(nums) > 1 else None, imp))
+        else:
+            if name:
+                self.global_names[name] = len(self.globals)
+            gt = rest[0]
+            if isinstance(gt, list) and gt[0] == "mut":
+                vt, mut = VALTYPES[gt[1]], 1
+            else:
+                vt, mut = VALTYPES[gt], 0
+            self.globals.append([vt, mut, None, imp])
+
     def _collect(self, sexpr):
         mod = sexpr[0] if len(sexpr) == 1 and isinstance(sexpr[0], list) else sexpr
         if mod and mod[0] == "module":
@@ -249,8 +282,11 @@ class Assembler:
         for fld in mod:
             if fld[0] == "import":
                 desc = fld[3]
+                if desc[0] in ("memory", "table", "global"):
+                    self._import_other(fld, desc)
+                    continue
                 if desc[0] != "func":
-                    raise NotImplementedError("only func imports")
+                    raise NotImplementedError("import kind " + desc[0])
                 f = _Func()
                 f.imported = (_strbytes(fld[1]), _strbytes(fld[2]))
                 rest = desc[1:]
@@ -682,7 +718,10 @@ class Assembler:
             body = lb + bytes(code)
             bodies.append(uleb(len(body)) + body)
         globals_enc = []
-        for vt, mut, init in self.globals:
+        for g in self.globals:
+            if len(g) == 4:      # imported
+                continue
+            vt, mut, init = g
             globals_enc.append(bytes([vt, mut]) + self._const_expr(init))
         out = bytearray(b"\x00asm\x01\x00\x00\x00")
 
@@ -693,18 +732,30 @@ class Assembler:
             section(1, _vec([b"\x60" + _vec([bytes([p]) for p in ps]) +
                              _vec([bytes([r]) for r in rs]) for ps, rs in self.types]))
         imps = [f for f in self.funcs if f.imported]
-        if imps:
+
+        def lim(mn, mx):
+            return b"\x00" + uleb(mn) if mx is None else b"\x01" + uleb(mn) + uleb(mx)
+        other = []
+        for t in self.tables:
+            if len(t) == 4:
+                other.append(_name(t[3][0]) + _name(t[3][1]) + b"\x01" + bytes([t[0]]) + lim(t[1], t[2]))
+        for m in self.mems:
+            if len(m) == 3:
+                other.append(_name(m[2][0]) + _name(m[2][1]) + b"\x02" + lim(m[0], m[1]))
+        for g in self.globals:
+            if len(g) == 4:
+                other.append(_name(g[3][0]) + _name(g[3][1]) + b"\x03" + bytes([g[0], g[1]]))
+        if imps or other:
             section(2, _vec([_name(f.imported[0]) + _name(f.imported[1]) + b"\x00" +
-                             uleb(f.typeidx) for f in imps]))
+                             uleb(f.typeidx) for f in imps] + other))
         if self.defs:
             section(3, _vec([uleb(f.typeidx) for f in self.defs]))
-        if self.tables:
-            section(4, _vec([bytes([rt]) + (b"\x00" + uleb(mn) if mx is None else
-                                            b"\x01" + uleb(mn) + uleb(mx))
-                             for rt, mn, mx in self.tables]))
-        if self.mems:
-            section(5, _vec([(b"\x00" + uleb(mn) if mx is None else b"\x01" + uleb(mn) + uleb(mx))
-                             for mn, mx in self.mems]))
+        tabs = [t for t in self.tables if len(t) == 3]
+        if tabs:
+            section(4, _vec([bytes([rt]) + lim(mn, mx) for rt, mn, mx in tabs]))
+        mems = [m for m in self.mems if len(m) == 2]
+        if mems:
+            section(5, _vec([lim(mn, mx) for mn, mx in mems]))
         if globals_enc:
             section(6, _vec(globals_enc))
         if self.exports:
