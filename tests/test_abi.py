@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "wasmedge_batch.h")
@@ -82,3 +84,82 @@ def test_ctypes_layouts_match_the_header(tmp_path):
     assert got[0] == [ctypes.sizeof(C), C.CostTable.offset, C.MemoryGranule.offset, C.HostThreads.offset]
     assert got[1] == [ctypes.sizeof(I), I.Value.offset, I.Mutable.offset]
     assert got[2] == [ctypes.sizeof(b._Value)]
+
+
+REF_API = "/root/reference/include"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_API), reason="reference tree absent (GPU box)")
+def test_integration_snippets_compile_after_the_reference_header(tmp_path):
+    """INTEGRATION.md's C snippets, with the reference's own C API header included first:
+    its WasmEdge_Value / String / Result then serve both APIs (the WASMEDGE_C_API_H guard
+    in include/wasmedge_batch.h). The header is used as installed: include/api/wasmedge/
+    wasmedge.h next to the C enum headers of include/common/ it includes, and version.h made
+    from version.h.in the way the reference's configure_file makes it. Compile only -- no
+    reference code is built or run."""
+    inc = tmp_path / "inc" / "wasmedge"
+    inc.mkdir(parents=True)
+    for f in ("enum_configure.h", "enum_errcode.h", "enum_types.h", "enum.inc"):
+        (inc / f).symlink_to(os.path.join(REF_API, "common", f))
+    for f in ("wasmedge.h", "int128.h"):
+        (inc / f).symlink_to(os.path.join(REF_API, "api", "wasmedge", f))
+    ver = open(os.path.join(REF_API, "api", "wasmedge", "version.h.in")).read()
+    for k, v in {"${CPACK_PACKAGE_VERSION}": "0.9.1", "${WASMEDGE_VERSION_MAJOR}": "0",
+                 "${WASMEDGE_VERSION_MINOR}": "9", "${WASMEDGE_VERSION_PATCH}": "1"}.items():
+        ver = ver.replace(k, v)
+    (inc / "version.h").write_text(ver)
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```c\n(.*?)```", doc, re.S)
+    assert len(blocks) >= 2
+    body, funcs = [], []
+    for b in blocks:
+        lines = [ln for ln in b.splitlines() if not ln.startswith("#include")]
+        text = "\n".join(lines)
+        # host-function definitions stay at file scope, statements go into a function
+        if "WasmEdge_Result MemSum(" in text:
+            head, _, rest = text.partition("WasmEdge_String mod")
+            funcs.append(head)
+            body.append("WasmEdge_String mod" + rest)
+        else:
+            body.append(text)
+    src = ("#include <stdio.h>\n#include <stdlib.h>\n#include <wasmedge/wasmedge.h>\n"
+           '#include "wasmedge_batch.h"\n' + "\n".join(funcs) +
+           "\nint use(const uint8_t *wasm_bytes, uint32_t wasm_len) {\n" + "\n".join(body) +
+           "\nreturn 0;\n}\n")
+    c = tmp_path / "snippet.c"
+    c.write_text(src)
+    r = subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-Wno-unused-variable", "-c",
+                        "-I", str(tmp_path / "inc"), "-I", os.path.join(ROOT, "include"),
+                        str(c), "-o", str(tmp_path / "snippet.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_gpu_boundary_errors(built):
+    """Call-level errors of WasmEdge_BatchExecute / SetArgs, as the reference VM reports
+    them (executor.cpp:88-100, vm.cpp): FuncNotFound (0x05) for an unknown export,
+    FuncSigMismatch (0x83) for a wrong parameter count or type, WrongVMWorkflow (0x04) for
+    Results before a Run; per-instance traps never surface here."""
+    import numpy as np
+    from wasmedge_amd import batch
+    with open(os.path.join(ROOT, "tests", "golden", "fibonacci.wasm"), "rb") as f:
+        fib = f.read()
+    ctx = batch.BatchContext(fib, 64, device=0)
+    try:
+        with pytest.raises(batch.WasmEdgeError) as e:
+            ctx.results(1)
+        assert e.value.code == 0x04
+        with pytest.raises(batch.WasmEdgeError) as e:
+            ctx.execute("nope", batch.make_values([[1]] * 64, [batch.I32]), 1)
+        assert e.value.code == 0x05
+        with pytest.raises(batch.WasmEdgeError) as e:
+            ctx.execute("fib", batch.make_values([[1, 2]] * 64, [batch.I32, batch.I32]), 1)
+        assert e.value.code == 0x83
+        with pytest.raises(batch.WasmEdgeError) as e:
+            ctx.execute("fib", batch.make_values([[1]] * 64, [batch.I64]), 1)
+        assert e.value.code == 0x83
+        rets, st, cnt = ctx.execute("fib", batch.make_values([[10]] * 64, [batch.I32]), 1)
+        assert (st == 0).all() and list(set(batch.ret_ints(rets)[:, 0])) == [55]
+        assert np.all(cnt == cnt[0])
+    finally:
+        ctx.close()
