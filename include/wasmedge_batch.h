@@ -244,6 +244,12 @@ WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetOutput(const WasmEdge_BatchCont
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *Cxt,
                                                                uint64_t *Costs);
 
+/* Straight-line runs of the module that the context compiled to machine code for the
+ * V-frame threaded core (DESIGN.md "Compiled runs"; 0 when it runs them interpreted: LDS
+ * frames, metering, WB_JIT=0, or a compile failure, whose message WasmEdge_BatchGetLastError
+ * then returns until the next error). Results never depend on it. */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *Cxt);
+
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */
 WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *Cxt,

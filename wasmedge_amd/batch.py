@@ -176,6 +176,8 @@ def lib():
         L.WasmEdge_BatchWASIGetExitCode.argtypes = [vp, u32]
         L.WasmEdge_BatchWASIGetOutput.restype = u32
         L.WasmEdge_BatchWASIGetOutput.argtypes = [vp, u32, u32, vp, u32]
+        L.WasmEdge_BatchGetCompiledRuns.restype = u32
+        L.WasmEdge_BatchGetCompiledRuns.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -317,6 +319,10 @@ class BatchContext:
 
     def code_size(self):
         return lib().WasmEdge_BatchGetCodeSize(self._h)
+
+    def compiled_runs(self):
+        """Straight-line runs compiled for the V-frame core (WasmEdge_BatchGetCompiledRuns)."""
+        return lib().WasmEdge_BatchGetCompiledRuns(self._h)
 
     def interrupt(self):
         lib().WasmEdge_BatchInterrupt(self._h)

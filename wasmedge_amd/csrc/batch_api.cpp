@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "batch_ctx.h"
+#include "jit.h"
 #include "tc_slots.h"
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
@@ -138,6 +139,28 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
   C->vframe = vf_fit && (vfe ? vfe[0] == '1' : C->nwaves <= 2 * 1024);
   if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);
+  // compiled runs (jit.h) for the V-frame core; WB_JIT=0 interprets them instead. A
+  // compile failure is not fatal (the core interprets) but is kept as the last error.
+  const char *jte = getenv("WB_JIT");
+  if (C->threaded && C->vframe && !C->conf.CostLimit && !(jte && jte[0] == '0')) {
+    const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv);
+    if (!runs.empty()) {
+      std::vector<uint8_t> start(P.code.size() + 1, 0);
+      for (const auto &r : runs) start[r.pc] = 1;
+      std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
+      std::vector<uint64_t> addr;
+      const std::string src = wb::jit_source(P, runs, C->mlog);
+      const std::string err = src.empty() ? std::string("compiled runs: no source")
+                                          : wb::jit_load(src, runs.size(), C->device, &addr);
+      if (err.empty()) {
+        wb::jit_patch(tcj, runs, addr);
+        tcv.swap(tcj);
+        C->jit_runs = uint32_t(runs.size());
+      } else {
+        C->last_error = err;
+      }
+    }
+  }
   // LS image from slot LS_GLOBALS on: globals, then (per-lane tables) table sizes and
   // the dropped-elem mask
   std::vector<uint32_t> ls_init = P.global_init;
@@ -502,6 +525,8 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
     return R(kRuntimeError);
   return R(0);
 }
+
+uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) { return C ? C->jit_runs : 0; }
 
 WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *Costs) {
   if (!C || !Costs) return R(kWrongVMWorkflow);

@@ -76,6 +76,7 @@ struct WasmEdge_BatchContext {
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
   bool threaded = true;
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
+  uint32_t jit_runs = 0;          // compiled straight-line runs (jit.h)
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
   DevBuf<uint32_t> hframe;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)

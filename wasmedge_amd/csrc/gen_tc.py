@@ -33,6 +33,7 @@ import re
 import sys
 
 SLOT = 256                         # bytes per handler slot
+JIT_XS = 64                        # offset of the xs exit stub in slot 0 (V blob)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 # ---------------------------------------------------------------- register conventions
@@ -841,6 +842,22 @@ def specs():
     add("ST64", ["ST64"], lambda g: mem_check(g, 8) + word2() + [
         "global_store_dword %s, %s, off" % (XP, B[0]),
         "global_store_dword %s, %s, off" % (ZP, B[1])] + mark(8) + g.next())
+    # ---- compiled blocks (jit.cpp): a straight-line run of instructions compiled for
+    # this module, entered here. Fields: w1/w2 = the block's code address, w5 = (run
+    # length - 1) * 32. The block reloads both banks for the instruction after the run
+    # and dispatches it itself (bank A), or leaves through slot 0 (xh at +0, xs at
+    # +JIT_XS). Diverged mode: a run that would pass the lowest waiting pc is left to
+    # the C++ step (it never does in practice: runs hold no jump target).
+    def jit_body(g):
+        if not g.vf:
+            return g.exit_here()
+        out = [SELF]
+        if g.mode == "D":
+            out += ["s_add_u32 s68, %s, %s" % (PCOFF, g.x(5)),
+                    "s_cmp_ge_u32 s68, %s" % OTHER, "s_cbranch_scc1 %s" % g.xh()]
+        return out + ["s_mov_b32 s68, %s" % g.x(1), "s_mov_b32 s69, %s" % g.x(2),
+                      "s_setpc_b64 s[68:69]"]
+    add("JIT", [], jit_body)
     # ---- fused pairs (V blob, converged mode): the instruction at pc (a fall-through
     # op) and the one at pc + 1 in one handler, saving a dispatch. tc.cpp picks the slot
     # from the two instructions' own slots (tc_pair_slot); each half reads its own
@@ -1029,6 +1046,11 @@ def blob(S, names, vf):
                         body = []
                         for stub, why in ((g.xh(), 0), (g.xs(), 1)):
                             pcl = g.lab("so")
+                            if why:   # compiled runs leave through slot 0 + JIT_XS
+                                # (the xh stub is 36 bytes; checked below)
+                                body += ["s_nop 0"] * ((JIT_XS - 36) // 4) + [
+                                    ".if (. - %s) != %d" % (lab, JIT_XS),
+                                    '.error "xs stub not at JIT_XS"', ".endif"]
                             body += ["%s:" % stub, "s_mov_b32 %s, %d" % (REASON, why),
                                      "s_getpc_b64 s[68:69]", "%s:" % pcl,
                                      "s_add_u32 s68, s68, Lvf_so_base - %s" % pcl,
@@ -1078,7 +1100,8 @@ def main():
     with open(os.path.join(HERE, "tc_slots.h"), "w") as f:
         f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
         f.write("#pragma once\n#include \"dbc.h\"\n\n")
-        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n#define TC_VF_CELLS %d\n\n" % (SLOT, nslots, VMAX))
+        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n#define TC_VF_CELLS %d\n#define TC_JIT_XS %d\n\n"
+                % (SLOT, nslots, VMAX, JIT_XS))
         for si, (nm, ops, body) in enumerate(S, start=1):
             if body is not None:
                 f.write("#define TC_SLOT_%s %d\n" % (nm, si))

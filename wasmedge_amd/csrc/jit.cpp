@@ -1,0 +1,686 @@
+// jit.cpp -- compiled straight-line runs for the V-frame threaded core (jit.h).
+//
+// Register contract (gen_tc.py): frame cell i = v[128 + i]; PAGES v105, MEM v[106:107],
+// HWM v101, v117 = 0; temps v108-v121, v126-v127, s68-s69, s[74:75]; PCOFF s62, OTHER
+// s63, CNT s65, the code base s[60:61], bank A s[76:83] / bank B s[84:91], bank-A
+// handler base s[70:71] (slot 0 = the xh exit stub, +TC_JIT_XS = xs). Every instruction
+// below does what its threaded-core handler does (gen_tc.py specs), with the cell
+// numbers and immediates folded in; instruction semantics: dbc_step.inc.
+#include "jit.h"
+
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+#include "frontend.h"
+#include "tc_slots.h"
+
+namespace wb {
+
+namespace {
+
+constexpr uint32_t kMinRun = 3;   // shorter runs gain less than the entry/exit costs
+
+const char *const PAGES = "v105", *const MEM = "v[106:107]", *const HWM = "v101";
+const char *const A0 = "v108", *const A1 = "v109", *const AP = "v[108:109]";
+const char *const B0 = "v110", *const B1 = "v111", *const BP = "v[110:111]";
+const char *const R0 = "v114", *const R1 = "v115", *const RP = "v[114:115]";
+const char *const W0 = "v116", *const WP = "v[116:117]";   // v117 stays 0
+const char *const X0 = "v118", *const X1 = "v119", *const XP = "v[118:119]";
+const char *const Y0 = "v120", *const Y1 = "v121";
+const char *const Z0 = "v126", *const Z1 = "v127", *const ZP = "v[126:127]";
+const char *const T2 = "s[74:75]";
+
+uint16_t op_of(const DInstr &I) { return uint16_t(I.w0 & 0x7FFFu); }
+
+uint32_t mem_bytes(uint16_t op) {
+  switch (op) {
+    case OP_LD8S32: case OP_LD8U32: case OP_LD8S64: case OP_LD8U64: case OP_ST8: return 1;
+    case OP_LD16S32: case OP_LD16U32: case OP_LD16S64: case OP_LD16U64: case OP_ST16: return 2;
+    case OP_LD32: case OP_LD32S64: case OP_LD32U64: case OP_ST32: return 4;
+    case OP_LD64: case OP_ST64: return 8;
+    default: return 0;
+  }
+}
+
+// compare ops: VOPC suffix (32-bit form; the 64-bit form appends "64" to the type)
+const char *cmp_kind(uint16_t k) {   // k: 0 EQ, 1 NE, 2 LT_S, 3 LT_U, 4 GT_S, 5 GT_U, 6 LE_S, 7 LE_U, 8 GE_S, 9 GE_U
+  static const char *const n[] = {"eq_u", "ne_u", "lt_i", "lt_u", "gt_i", "gt_u", "le_i", "le_u", "ge_i", "ge_u"};
+  return n[k];
+}
+uint16_t cmp_swap(uint16_t k) {   // a CMP b == b CMP' a
+  static const uint16_t s[] = {0, 1, 4, 5, 2, 3, 8, 9, 6, 7};
+  return s[k];
+}
+
+struct Em {
+  std::string o;
+  uint32_t g = 0;        // granule log
+  uint32_t run = 0;      // run index (label suffix)
+  uint32_t pc = 0;       // instruction being compiled
+  uint32_t done = 0;     // wasm instructions retired before it (within the run)
+  bool pend[256] = {};   // cells with a global load in flight
+  bool any = false;
+  struct Stub { std::string lab; uint32_t pc, done; };
+  std::vector<Stub> stubs;
+
+  void l(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    o += buf;
+    o += '\n';
+  }
+  static std::string V(uint32_t c) { return "v" + std::to_string(128 + c); }
+  static std::string P(uint32_t c) {
+    return "v[" + std::to_string(128 + c) + ":" + std::to_string(129 + c) + "]";
+  }
+  const char *v(uint32_t c) {   // (short-lived: valid until the next call)
+    static thread_local std::string s[8];
+    static thread_local int k = 0;
+    k = (k + 1) & 7;
+    s[k] = V(c);
+    return s[k].c_str();
+  }
+  const char *p(uint32_t c) {
+    static thread_local std::string s[8];
+    static thread_local int k = 0;
+    k = (k + 1) & 7;
+    s[k] = P(c);
+    return s[k].c_str();
+  }
+  // wait for loads in flight into any of these cells (read after load, write after load)
+  void sync(std::initializer_list<uint32_t> cells) {
+    if (!any) return;
+    for (uint32_t c : cells)
+      if (c < 256 && pend[c]) { drain(); return; }
+  }
+  void drain() {
+    if (!any) return;
+    l("s_waitcnt vmcnt(0)");
+    for (bool &b : pend) b = false;
+    any = false;
+  }
+  // a 64-bit operand as an aligned VGPR pair (gfx9 tuples start at even registers)
+  const char *src64(uint32_t c, const char *lo, const char *hi, const char *pair) {
+    if (!(c & 1)) return p(c);
+    l("v_mov_b32 %s, %s", lo, v(c));
+    l("v_mov_b32 %s, %s", hi, v(c + 1));
+    return pair;
+  }
+  // cells c, c+1 = R
+  void put64(uint32_t c) {
+    if (!(c & 1)) {
+      l("v_mov_b64 %s, %s", p(c), RP);
+    } else {
+      l("v_mov_b32 %s, %s", v(c), R0);
+      l("v_mov_b32 %s, %s", v(c + 1), R1);
+    }
+  }
+  // leave before instruction pc (the C++ step executes it) when any active lane's T2 bit
+  // is set
+  void leave_if_t2() {
+    const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(pc);
+    l("s_and_b64 %s, %s, exec", T2, T2);
+    l("s_cbranch_scc1 %s", lab.c_str());
+    stubs.push_back(Stub{lab, pc, done});
+  }
+};
+
+// ---------------------------------------------------------------- linear memory
+// Bounds and alignment as the handlers (gen_tc.py mem_check): the last byte
+// ea + n - 1 = a + (offset + n - 1) must not carry and must lie below pages * 64 KiB;
+// 2- and >= 4-byte accesses must be naturally aligned (4 for 8 bytes). Leaves XP = the
+// address of the first word (granule layout, batch_ctx.h); a store (mark) also raises
+// the write mark (LS_HWM) to one past its last byte, saturating.
+void mem_addr(Em &e, uint32_t a, uint32_t imm, uint32_t n, bool mark) {
+  const uint32_t last = imm + n - 1;   // < 2^32 (jit_ok)
+  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, last, e.v(a));
+  e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
+  e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  const uint32_t m = n >= 4 ? 3 : n - 1;
+  if (m) {
+    e.l("v_and_b32_e32 %s, %u, %s", Y0, m, X0);
+    e.l("v_cmp_ne_u32_e32 vcc, %u, %s", m, Y0);
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  }
+  e.leave_if_t2();
+  if (mark) {
+    e.l("v_add_u32_e64 %s, %s, 1 clamp", Y1, X0);
+    e.l("v_max_u32_e32 %s, %s, %s", HWM, HWM, Y1);
+  }
+  // ea -> W0 (g = 0, aligned word: the byte address is MEM + ea * 64)
+  if (e.g == 0 && n >= 4) {
+    if (imm) e.l("v_add_u32_e32 %s, 0x%x, %s", W0, imm, e.v(a));
+    else e.l("v_mov_b32 %s, %s", W0, e.v(a));
+    e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+    return;
+  }
+  // granule rows of 256 << g bytes, (ea >> (2 + g)) of them, + the byte in the granule
+  std::string ea = e.V(a);
+  if (imm) { e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, imm, e.v(a)); ea = Y0; }
+  e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, ea.c_str());
+  e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+  e.l("v_bfe_u32 %s, %s, 0, %u", W0, ea.c_str(), 2 + e.g);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  if (n == 8) {   // ZP = address of the second word (ea + 4: maybe the next granule)
+    e.l("v_add_u32_e32 %s, 4, %s", Y1, ea.c_str());
+    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y1);
+    e.l("v_lshlrev_b64 %s, %u, %s", ZP, 8 + e.g, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, ZP, MEM);
+    e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y1, 2 + e.g);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, WP, ZP);
+  }
+}
+
+// second word of an 8-byte access: 256 bytes on in the word interleave, else ZP
+std::string word2(const Em &e) { return e.g == 0 ? std::string(XP) + ", off offset:256" : std::string(ZP) + ", off"; }
+
+bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
+  const uint32_t n = mem_bytes(op);
+  const char *ins = n == 1 ? (op == OP_LD8S32 || op == OP_LD8S64 ? "global_load_sbyte" : "global_load_ubyte")
+                    : n == 2 ? (op == OP_LD16S32 || op == OP_LD16S64 ? "global_load_sshort" : "global_load_ushort")
+                             : "global_load_dword";
+  const bool wide = op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
+                    op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
+  e.sync({a, c, wide ? c + 1 : c});
+  mem_addr(e, a, imm, n, false);
+  e.l("%s %s, %s, off", ins, e.v(c), XP);
+  e.pend[c] = e.any = true;
+  if (op == OP_LD64) {
+    e.l("global_load_dword %s, %s", e.v(c + 1), word2(e).c_str());
+    e.pend[c + 1] = true;
+  } else if (op == OP_LD8U64 || op == OP_LD16U64 || op == OP_LD32U64) {
+    e.l("v_mov_b32 %s, 0", e.v(c + 1));
+  } else if (wide) {   // sign extension needs the loaded word
+    e.drain();
+    e.l("v_ashrrev_i32_e32 %s, 31, %s", e.v(c + 1), e.v(c));
+  }
+  return true;
+}
+
+bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm) {
+  const uint32_t n = mem_bytes(op);
+  e.drain();   // a store never overtakes a load of this run (same-address ordering)
+  mem_addr(e, a, imm, n, true);
+  const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
+  e.l("%s %s, %s, off", ins, XP, e.v(b));
+  if (n == 8) {
+    const std::string w2 = word2(e);
+    const size_t k = w2.find(", off");
+    e.l("global_store_dword %s, %s%s", w2.substr(0, k).c_str(), e.v(b + 1), w2.substr(k).c_str());
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- one instruction
+// Returns false when the instruction has no compiled form (the run ends before it).
+bool emit(Em &e, const DInstr &I) {
+  const uint16_t op = op_of(I);
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16, imm = I.w3;
+  // i32 binary ops: (register form, immediate form); SUB_I as a - imm
+  struct Bin { uint16_t rr, ri; const char *ins; int form; };   // form 0 VOP2, 1 shift, 2 VOP3
+  static const Bin bins[] = {
+      {OP_I32_ADD, OP_I32_ADD_I, "v_add_u32_e32", 0}, {OP_I32_SUB, OP_I32_SUB_I, "v_sub_u32_e32", 0},
+      {OP_I32_MUL, OP_I32_MUL_I, "v_mul_lo_u32", 2}, {OP_I32_AND, OP_I32_AND_I, "v_and_b32_e32", 0},
+      {OP_I32_OR, OP_I32_OR_I, "v_or_b32_e32", 0}, {OP_I32_XOR, OP_I32_XOR_I, "v_xor_b32_e32", 0},
+      {OP_I32_SHL, OP_I32_SHL_I, "v_lshlrev_b32_e32", 1}, {OP_I32_SHR_S, OP_I32_SHR_S_I, "v_ashrrev_i32_e32", 1},
+      {OP_I32_SHR_U, OP_I32_SHR_U_I, "v_lshrrev_b32_e32", 1}};
+  for (const Bin &x : bins) {
+    if (op == x.rr) {
+      e.sync({a, b, c});
+      if (x.form == 1) e.l("%s %s, %s, %s", x.ins, e.v(c), e.v(b), e.v(a));
+      else e.l("%s %s, %s, %s", x.ins, e.v(c), e.v(a), e.v(b));
+      return true;
+    }
+    if (op == x.ri) {
+      e.sync({a, c});
+      if (x.form == 1) {
+        e.l("%s %s, %u, %s", x.ins, e.v(c), imm & 31u, e.v(a));
+      } else if (x.form == 2) {
+        e.l("s_mov_b32 s68, 0x%x", imm);
+        e.l("%s %s, %s, s68", x.ins, e.v(c), e.v(a));
+      } else if (op == OP_I32_SUB_I) {
+        e.l("v_subrev_u32_e32 %s, 0x%x, %s", e.v(c), imm, e.v(a));
+      } else {
+        e.l("%s %s, 0x%x, %s", x.ins, e.v(c), imm, e.v(a));
+      }
+      return true;
+    }
+  }
+  // compares: I32_EQ..I32_GE_U, *_I; I64 likewise
+  if ((op >= OP_I32_EQ && op <= OP_I32_GE_U) || (op >= OP_I32_EQ_I && op <= OP_I32_GE_U_I)) {
+    const bool ri = op >= OP_I32_EQ_I;
+    const uint16_t k = uint16_t(op - (ri ? OP_I32_EQ_I : OP_I32_EQ));
+    if (ri) {
+      e.sync({a, c});
+      e.l("v_cmp_%s32_e32 vcc, 0x%x, %s", cmp_kind(cmp_swap(k)), imm, e.v(a));
+    } else {
+      e.sync({a, b, c});
+      e.l("v_cmp_%s32_e32 vcc, %s, %s", cmp_kind(k), e.v(a), e.v(b));
+    }
+    e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+    return true;
+  }
+  if ((op >= OP_I64_EQ && op <= OP_I64_GE_U) || (op >= OP_I64_EQ_I && op <= OP_I64_GE_U_I)) {
+    const bool ri = op >= OP_I64_EQ_I;
+    const uint16_t k = uint16_t(op - (ri ? OP_I64_EQ_I : OP_I64_EQ));
+    e.sync({a, a + 1, b, b + 1, c});
+    const char *x = e.src64(a, A0, A1, AP);
+    const char *y;
+    if (ri) {
+      e.l("v_mov_b32 %s, 0x%x", Z0, imm);
+      e.l("v_ashrrev_i32_e32 %s, 31, %s", Z1, Z0);
+      y = ZP;
+    } else {
+      y = e.src64(b, B0, B1, BP);
+    }
+    e.l("v_cmp_%s64_e64 vcc, %s, %s", cmp_kind(k), x, y);
+    e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+    return true;
+  }
+  switch (op) {
+    case OP_NOP_CNT:
+      return true;
+    case OP_MOV32:
+      e.sync({a, c});
+      if (a != c) e.l("v_mov_b32 %s, %s", e.v(c), e.v(a));
+      return true;
+    case OP_MOV64:
+      e.sync({a, a + 1, c, c + 1});
+      if (a == c) return true;
+      if (!(a & 1) && !(c & 1)) {
+        e.l("v_mov_b64 %s, %s", e.p(c), e.p(a));
+      } else if (c > a) {   // overlapping copies: the word that would be overwritten first
+        e.l("v_mov_b32 %s, %s", e.v(c + 1), e.v(a + 1));
+        e.l("v_mov_b32 %s, %s", e.v(c), e.v(a));
+      } else {
+        e.l("v_mov_b32 %s, %s", e.v(c), e.v(a));
+        e.l("v_mov_b32 %s, %s", e.v(c + 1), e.v(a + 1));
+      }
+      return true;
+    case OP_CONST32:
+      e.sync({c});
+      e.l("v_mov_b32 %s, 0x%x", e.v(c), imm);
+      return true;
+    case OP_CONST64:
+      e.sync({c, c + 1});
+      e.l("v_mov_b32 %s, 0x%x", e.v(c), imm);
+      e.l("v_mov_b32 %s, 0x%x", e.v(c + 1), I.w1);
+      return true;
+    case OP_SELECT32:
+      e.sync({a, b, c, d});
+      e.l("v_cmp_ne_u32_e32 vcc, 0, %s", e.v(d));
+      e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", e.v(c), e.v(b), e.v(a));
+      return true;
+    case OP_SELECT64:
+      e.sync({a, a + 1, b, b + 1, c, c + 1, d});
+      e.l("v_cmp_ne_u32_e32 vcc, 0, %s", e.v(d));
+      e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", R0, e.v(b), e.v(a));
+      e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", R1, e.v(b + 1), e.v(a + 1));
+      e.put64(c);
+      return true;
+    case OP_I32_ROTR:
+      e.sync({a, b, c});
+      e.l("v_alignbit_b32 %s, %s, %s, %s", e.v(c), e.v(a), e.v(a), e.v(b));
+      return true;
+    case OP_I32_ROTL:
+      e.sync({a, b, c});
+      e.l("v_sub_u32_e32 %s, 0, %s", X0, e.v(b));
+      e.l("v_alignbit_b32 %s, %s, %s, %s", e.v(c), e.v(a), e.v(a), X0);
+      return true;
+    case OP_I32_ROTR_I: case OP_I32_ROTL_I: {
+      e.sync({a, c});
+      const uint32_t k = op == OP_I32_ROTR_I ? imm & 31u : (32u - (imm & 31u)) & 31u;
+      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(c), e.v(a), e.v(a), k);
+      return true;
+    }
+    case OP_I32_EQZ:
+      e.sync({a, c});
+      e.l("v_cmp_eq_u32_e32 vcc, 0, %s", e.v(a));
+      e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+      return true;
+    case OP_I32_CLZ: case OP_I32_CTZ:
+      e.sync({a, c});
+      e.l("%s %s, %s", op == OP_I32_CLZ ? "v_ffbh_u32_e32" : "v_ffbl_b32_e32", X0, e.v(a));
+      e.l("v_min_u32_e32 %s, 32, %s", e.v(c), X0);
+      return true;
+    case OP_I32_POPCNT:
+      e.sync({a, c});
+      e.l("v_bcnt_u32_b32 %s, %s, 0", e.v(c), e.v(a));
+      return true;
+    case OP_I32_EXT8S: case OP_I32_EXT16S:
+      e.sync({a, c});
+      e.l("v_bfe_i32 %s, %s, 0, %u", e.v(c), e.v(a), op == OP_I32_EXT8S ? 8u : 16u);
+      return true;
+    case OP_I32_ADD3:
+      e.sync({a, b, c, d});
+      e.l("v_add3_u32 %s, %s, %s, %s", e.v(c), e.v(a), e.v(b), e.v(d));
+      return true;
+    case OP_I32_XOR_ROTR_I: case OP_I32_XOR_ROTL_I: {
+      e.sync({a, b, c});
+      const uint32_t k = op == OP_I32_XOR_ROTR_I ? imm & 31u : (32u - (imm & 31u)) & 31u;
+      e.l("v_xor_b32_e32 %s, %s, %s", X0, e.v(a), e.v(b));
+      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(c), X0, X0, k);
+      return true;
+    }
+    case OP_I32_ADD_XROTR_I: case OP_I32_ADD3_XROTR_I: {
+      // s = a + b (+ d); c = s; y = rotr(y ^ s, k) with y read before c is written
+      const bool three = op == OP_I32_ADD3_XROTR_I;
+      const uint32_t y = three ? imm & 0xFFFFu : d, k = (three ? imm >> 16 : imm) & 31u;
+      e.sync({a, b, c, d, y});
+      const std::string s = c == y ? std::string(R0) : e.V(c);
+      if (three) e.l("v_add3_u32 %s, %s, %s, %s", s.c_str(), e.v(a), e.v(b), e.v(d));
+      else e.l("v_add_u32_e32 %s, %s, %s", s.c_str(), e.v(a), e.v(b));
+      e.l("v_xor_b32_e32 %s, %s, %s", X0, e.v(y), s.c_str());
+      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(y), X0, X0, k);
+      return true;
+    }
+    // ---- i64 (b operand of *_I: imm sign-extended)
+    case OP_I64_ADD: case OP_I64_ADD_I: case OP_I64_SUB: case OP_I64_SUB_I:
+    case OP_I64_MUL: case OP_I64_MUL_I: case OP_I64_AND: case OP_I64_AND_I:
+    case OP_I64_OR: case OP_I64_OR_I: case OP_I64_XOR: case OP_I64_XOR_I: {
+      const bool ri = op == OP_I64_ADD_I || op == OP_I64_SUB_I || op == OP_I64_MUL_I ||
+                      op == OP_I64_AND_I || op == OP_I64_OR_I || op == OP_I64_XOR_I;
+      e.sync({a, a + 1, b, b + 1, c, c + 1});
+      // operands as word registers; the b operand of *_I in Z
+      std::string bl = e.V(b), bh = e.V(b + 1);
+      if (ri) {
+        e.l("v_mov_b32 %s, 0x%x", Z0, imm);
+        e.l("v_ashrrev_i32_e32 %s, 31, %s", Z1, Z0);
+        bl = Z0;
+        bh = Z1;
+      }
+      const std::string al = e.V(a), ah = e.V(a + 1);
+      if (op == OP_I64_ADD || op == OP_I64_ADD_I) {
+        const char *x = e.src64(a, A0, A1, AP);
+        const char *y = ri ? ZP : e.src64(b, B0, B1, BP);
+        e.l("v_lshl_add_u64 %s, %s, 0, %s", RP, x, y);
+      } else if (op == OP_I64_SUB || op == OP_I64_SUB_I) {
+        e.l("v_sub_co_u32_e32 %s, vcc, %s, %s", R0, al.c_str(), bl.c_str());
+        e.l("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc", R1, ah.c_str(), bh.c_str());
+      } else if (op == OP_I64_MUL || op == OP_I64_MUL_I) {
+        e.l("v_mul_hi_u32 %s, %s, %s", X0, al.c_str(), bl.c_str());
+        e.l("v_mul_lo_u32 %s, %s, %s", X1, al.c_str(), bh.c_str());
+        e.l("v_mul_lo_u32 %s, %s, %s", Y0, ah.c_str(), bl.c_str());
+        e.l("v_mul_lo_u32 %s, %s, %s", R0, al.c_str(), bl.c_str());
+        e.l("v_add3_u32 %s, %s, %s, %s", R1, X0, X1, Y0);
+      } else {
+        const char *ins = (op == OP_I64_AND || op == OP_I64_AND_I) ? "v_and_b32_e32"
+                          : (op == OP_I64_OR || op == OP_I64_OR_I) ? "v_or_b32_e32" : "v_xor_b32_e32";
+        e.l("%s %s, %s, %s", ins, R0, al.c_str(), bl.c_str());
+        e.l("%s %s, %s, %s", ins, R1, ah.c_str(), bh.c_str());
+      }
+      e.put64(c);
+      return true;
+    }
+    case OP_I64_SHL: case OP_I64_SHR_S: case OP_I64_SHR_U:
+    case OP_I64_SHL_I: case OP_I64_SHR_S_I: case OP_I64_SHR_U_I: {
+      const bool ri = op == OP_I64_SHL_I || op == OP_I64_SHR_S_I || op == OP_I64_SHR_U_I;
+      const uint16_t base = ri ? uint16_t(op - OP_I64_SHL_I) : uint16_t(op - OP_I64_SHL);
+      const char *ins = base == 0 ? "v_lshlrev_b64" : base == 1 ? "v_ashrrev_i64" : "v_lshrrev_b64";
+      e.sync({a, a + 1, b, c, c + 1});
+      const char *x = e.src64(a, A0, A1, AP);
+      const std::string amt = ri ? std::to_string(imm & 63u) : e.V(b);
+      e.l("%s %s, %s, %s", ins, RP, amt.c_str(), x);
+      e.put64(c);
+      return true;
+    }
+    case OP_I64_ROTL: case OP_I64_ROTR: case OP_I64_ROTL_I: case OP_I64_ROTR_I: {
+      const bool left = op == OP_I64_ROTL || op == OP_I64_ROTL_I;
+      const bool ri = op == OP_I64_ROTL_I || op == OP_I64_ROTR_I;
+      e.sync({a, a + 1, b, c, c + 1});
+      const char *x = e.src64(a, A0, A1, AP);
+      if (ri) e.l("v_mov_b32 %s, %u", Z0, imm & 63u);
+      else e.l("v_mov_b32 %s, %s", Z0, e.v(b));
+      e.l("v_sub_u32_e32 %s, 0, %s", Y0, Z0);
+      e.l("%s %s, %s, %s", left ? "v_lshlrev_b64" : "v_lshrrev_b64", XP, Z0, x);
+      e.l("%s %s, %s, %s", left ? "v_lshrrev_b64" : "v_lshlrev_b64", RP, Y0, x);
+      e.l("v_or_b32_e32 %s, %s, %s", R0, R0, X0);
+      e.l("v_or_b32_e32 %s, %s, %s", R1, R1, X1);
+      e.put64(c);
+      return true;
+    }
+    case OP_I64_EQZ: {
+      e.sync({a, a + 1, c});
+      const char *x = e.src64(a, A0, A1, AP);
+      e.l("v_cmp_eq_u64_e64 vcc, 0, %s", x);
+      e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+      return true;
+    }
+    case OP_I64_EXTEND_I32_S: case OP_I64_EXT32S:
+      e.sync({a, c, c + 1});
+      e.l("v_ashrrev_i32_e32 %s, 31, %s", X0, e.v(a));
+      if (c != a) e.l("v_mov_b32 %s, %s", e.v(c), e.v(a));
+      e.l("v_mov_b32 %s, %s", e.v(c + 1), X0);
+      return true;
+    case OP_I64_EXTEND_I32_U:
+      e.sync({a, c, c + 1});
+      if (c != a) e.l("v_mov_b32 %s, %s", e.v(c), e.v(a));
+      e.l("v_mov_b32 %s, 0", e.v(c + 1));
+      return true;
+    case OP_I64_EXT8S: case OP_I64_EXT16S:
+      e.sync({a, c, c + 1});
+      e.l("v_bfe_i32 %s, %s, 0, %u", R0, e.v(a), op == OP_I64_EXT8S ? 8u : 16u);
+      e.l("v_ashrrev_i32_e32 %s, 31, %s", R1, R0);
+      e.put64(c);
+      return true;
+    default:
+      break;
+  }
+  if (mem_bytes(op)) {
+    if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64) return emit_store(e, op, a, b, imm);
+    return emit_load(e, op, a, c, imm);
+  }
+  return false;
+}
+
+// can instruction I be compiled (dry run)
+bool jit_ok(const Program &P, const DInstr &I) {
+  const uint16_t op = op_of(I);
+  if (const uint32_t n = mem_bytes(op))
+    if (uint64_t(I.w3) + n - 1 > 0xFFFFFFFFull) return false;
+  Em e;
+  (void)P;
+  return emit(e, I);
+}
+
+}  // namespace
+
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
+  std::vector<JitRun> runs;
+  const size_t n = P.code.size();
+  if (P.total_cells() > TC_VF_CELLS) return runs;
+  const std::vector<uint8_t> target = jump_targets(P);
+  std::vector<uint8_t> ok(n, 0);
+  for (size_t pc = 0; pc < n; pc++) ok[pc] = tc[pc].w[0] != 0 && jit_ok(P, P.code[pc]);
+  for (size_t pc = 0; pc < n;) {
+    if (!ok[pc]) { pc++; continue; }
+    size_t end = pc + 1;
+    while (end < n && ok[end] && !target[end]) end++;
+    if (end - pc >= kMinRun) {
+      uint32_t cnt = 0;
+      for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
+      runs.push_back(JitRun{uint32_t(pc), uint32_t(end - pc), cnt});
+    }
+    pc = end;
+  }
+  return runs;
+}
+
+std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog) {
+  std::string src =
+      "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
+      "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out) {\n"
+      "  unsigned lo, hi;\n";
+  for (size_t k = 0; k < runs.size(); k++) {
+    const JitRun &r = runs[k];
+    Em e;
+    e.g = glog;
+    e.run = uint32_t(k);
+    const std::string K = std::to_string(k);
+    e.l("s_getpc_b64 s[6:7]");
+    e.l("Lp%s:", K.c_str());
+    e.l("s_add_u32 s6, s6, Lb%s - Lp%s", K.c_str(), K.c_str());
+    e.l("s_addc_u32 s7, s7, 0");
+    e.l("s_mov_b32 %%0, s6");
+    e.l("s_mov_b32 %%1, s7");
+    e.l("s_branch Le%s", K.c_str());
+    e.l(".p2align 6");
+    e.l("Lb%s:", K.c_str());
+    // the successor prefetch in flight must land before both banks are reloaded for the
+    // instruction after the run (SMEM returns out of order); that reload then overlaps
+    // the run's own work
+    const uint32_t next = (r.pc + r.len) * 32u;
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_mov_b32 s68, 0x%x", next);
+    e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
+    e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
+    for (uint32_t i = 0; i < r.len; i++) {
+      const DInstr &I = P.code[r.pc + i];
+      e.pc = r.pc + i;
+      if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
+      e.done += (I.w0 >> 16) & 0xFFu;
+    }
+    e.drain();
+    e.l("s_mov_b32 s62, 0x%x", next);
+    e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+    e.l("s_cmp_ge_u32 s62, s63");   // diverged: a waiting lane's pc reached -> scheduler
+    e.l("s_cbranch_scc1 Lxs%s", K.c_str());
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_add_u32 s68, s70, s76");
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    e.l("Lxs%s:", K.c_str());
+    e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    for (const auto &s : e.stubs) {   // leave before instruction s.pc
+      e.l("%s:", s.lab.c_str());
+      e.l("s_mov_b32 s62, 0x%x", s.pc * 32u);
+      e.l("s_add_u32 s65, s65, 0x%x", s.done);
+      e.l("s_setpc_b64 s[70:71]");
+    }
+    e.l("Le%s:", K.c_str());
+    src += "  asm volatile(\n";
+    size_t at = 0;
+    while (at < e.o.size()) {
+      const size_t nl = e.o.find('\n', at);
+      src += "      \"" + e.o.substr(at, nl - at) + "\\n\"\n";
+      at = nl + 1;
+    }
+    src += "      : \"=s\"(lo), \"=s\"(hi) : : \"s6\", \"s7\", \"scc\");\n";
+    src += "  if (threadIdx.x == 0) out[" + K + "] = ((unsigned long long)hi << 32) | lo;\n";
+  }
+  src += "}\n";
+  return src;
+}
+
+std::string jit_compile(const std::string &src, std::vector<char> *code) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "wbjit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    return "hiprtcCreateProgram failed";
+  const char *opts[] = {"--offload-arch=gfx950", "-O1"};
+  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n + 1, '\0');
+    hiprtcGetProgramLog(prog, log.data());
+    hiprtcDestroyProgram(&prog);
+    return "compiled-run assembly failed: " + log.substr(0, 2000);
+  }
+  size_t sz = 0;
+  hiprtcGetCodeSize(prog, &sz);
+  code->assign(sz, 0);
+  hiprtcGetCode(prog, code->data());
+  hiprtcDestroyProgram(&prog);
+  return "";
+}
+
+std::string jit_load(const std::string &src, size_t nruns, int device, std::vector<uint64_t> *addr) {
+  // one code object per (device, source) for the life of the process: contexts of the
+  // same module share it
+  static std::mutex mu;
+  static std::map<std::pair<int, std::string>, std::vector<uint64_t>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({device, src});
+  if (it != cache.end()) { *addr = it->second; return ""; }
+  std::vector<char> code;
+  std::string err = jit_compile(src, &code);
+  if (!err.empty()) return err;
+  hipModule_t mod;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) return "hipModuleLoadData failed";
+  hipFunction_t fn;
+  if (hipModuleGetFunction(&fn, mod, "wbjit_addrs") != hipSuccess) return "hipModuleGetFunction failed";
+  uint64_t *dout = nullptr;
+  if (hipMalloc(&dout, std::max<size_t>(1, nruns) * 8) != hipSuccess) return "hipMalloc failed";
+  void *args[] = {&dout};
+  std::vector<uint64_t> a(nruns, 0);
+  const bool ok = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) == hipSuccess &&
+                  hipDeviceSynchronize() == hipSuccess &&
+                  hipMemcpy(a.data(), dout, nruns * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(dout);
+  if (!ok) return "compiled-run address query failed";
+  for (uint64_t x : a)
+    if (x == 0 || (x & 63)) return "compiled-run address query returned a bad address";
+  cache[{device, src}] = a;   // the module stays loaded: its code is jumped to
+  *addr = a;
+  return "";
+}
+
+void jit_patch(std::vector<TInstr> &tc, const std::vector<JitRun> &runs, const std::vector<uint64_t> &addr) {
+  for (size_t k = 0; k < runs.size(); k++) {
+    uint32_t *w = tc[runs[k].pc].w;
+    w[0] = TC_SLOT_JIT * TC_SLOT_BYTES;
+    w[1] = uint32_t(addr[k]);
+    w[2] = uint32_t(addr[k] >> 32);
+    w[3] = w[4] = w[6] = w[7] = 0;
+    w[5] = (runs[k].len - 1) * 32u;
+  }
+}
+
+}  // namespace wb
+
+// TEST hook (tests/test_jit.py, CPU): lower a module, pick its runs and assemble them for
+// gfx950 without a device. Returns the number of runs, or -1 with the error in err.
+extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t *wasm, uint32_t len,
+                                                                   uint32_t glog, uint32_t *instrs,
+                                                                   char *err, uint32_t errlen) {
+  wb::Program P;
+  uint8_t ec = 0;
+  std::string e = wb::load_program(wasm, len, P, &ec);
+  std::vector<wb::JitRun> runs;
+  if (e.empty() && P.total_cells() > TC_VF_CELLS) e = "frame too large for V frames";
+  if (e.empty()) {
+    std::vector<DInstr> code = P.code;
+    code.push_back(DInstr{0, 0, 0, 0});
+    const std::vector<TInstr> tc = wb::build_threaded(P, code, true);
+    runs = wb::jit_runs(P, tc);
+    if (instrs) {
+      *instrs = 0;
+      for (const auto &r : runs) *instrs += r.len;
+    }
+    if (!runs.empty()) {
+      std::vector<char> obj;
+      const std::string src = wb::jit_source(P, runs, glog);
+      if (const char *dump = getenv("WB_JIT_DUMP"))
+        if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
+      e = src.empty() ? "no source" : wb::jit_compile(src, &obj);
+    }
+  }
+  if (!e.empty()) {
+    if (err && errlen) snprintf(err, errlen, "%s", e.c_str());
+    return -1;
+  }
+  return int(runs.size());
+}

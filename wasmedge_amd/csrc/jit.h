@@ -1,0 +1,50 @@
+// jit.h -- per-module compiled runs for the V-frame threaded core.
+//
+// The threaded core (gen_tc.py) spends most of a dispatch on the dispatch itself: the
+// s_load of the next TInstr, the s_setpc, the GPR-index moves that name frame cells by
+// an SGPR field. For a straight-line run of instructions (no jump target inside, every
+// instruction one the compiler below knows) all of that is known when the module is
+// loaded, so jit.cpp writes the run as plain CDNA4 assembly over the frame VGPRs
+// (cell i = v[128 + i], the V-frame blob's layout), compiles it with hiprtc into a code
+// object of its own and patches the run's first TInstr to the core's JIT slot, which
+// jumps there. The run's code retires the run and dispatches the instruction after it
+// through the core's bank-A handlers, or leaves through the core's exit stubs (slot 0)
+// when a memory access fails its bounds or alignment check (the C++ step then executes
+// that instruction, exactly as when a handler leaves). Results never depend on it:
+// WB_JIT=0 turns it off, and the parity tests run both ways.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "tc.h"
+
+namespace wb {
+struct Program;
+
+struct JitRun {
+  uint32_t pc;    // first instruction
+  uint32_t len;   // instructions
+  uint32_t cnt;   // wasm instructions retired by the whole run
+};
+
+// Runs worth compiling: maximal straight-line stretches of compilable instructions with
+// no jump target past their first, at least kMinRun long. `tc`: build_threaded's array
+// (an instruction without a handler there is never compiled).
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc);
+
+// The hiprtc source: one kernel, wbjit_addrs(uint64_t *out), that writes the address of
+// run k's code to out[k]; the runs' code sits inside it behind branches. glog: linear-
+// memory granule = 4 << glog bytes (batch_ctx.h lane_word).
+std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog);
+
+// Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
+std::string jit_compile(const std::string &src, std::vector<char> *code);
+
+// Compile (cached per device and source), load on the current device and read back the
+// runs' code addresses. Returns "" or an error.
+std::string jit_load(const std::string &src, size_t nruns, int device, std::vector<uint64_t> *addr);
+
+// Point each run's first TInstr at its code (the core's JIT slot).
+void jit_patch(std::vector<TInstr> &tc, const std::vector<JitRun> &runs, const std::vector<uint64_t> &addr);
+}  // namespace wb

@@ -22,7 +22,25 @@ static bool is_branch(uint16_t op) {
          (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
 
-std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe) {
+std::vector<uint8_t> jump_targets(const Program &P) {
+  const size_t n = P.code.size();
+  std::vector<uint8_t> target(n + 1, 0);
+  for (size_t pc = 0; pc < n; pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
+    if ((is_branch(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2 || op == OP_CALL) && I.w3 < n)
+      target[I.w3] = 1;
+    if (op == OP_CALL || op == OP_CALL_INDIRECT || op == OP_HOST_CALL) target[pc + 1] = 1;
+  }
+  for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
+    if (P.brtab[k] < n) target[P.brtab[k]] = 1;
+  for (const auto &f : P.funcs)
+    if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
+  return target;
+}
+
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe,
+                                   const std::vector<uint8_t> *run_start) {
   const uint32_t T = P.total_cells();
   // operand fields: LDS byte offsets (cell * 256) for the LDS-frame blob, cell indices
   // (= VGPR index past v128) for the V-frame blob
@@ -99,18 +117,7 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
   // fall-through: not a jump/call/return target, and not an entry point of the core
   // (DBC_HOT cleared: a run that stops in front of it resumes in the C++ step).
   const size_t n = P.code.size();
-  std::vector<uint8_t> target(n + 1, 0);
-  for (size_t pc = 0; pc < n; pc++) {
-    const DInstr &I = P.code[pc];
-    const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
-    if ((is_branch(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2 || op == OP_CALL) && I.w3 < n)
-      target[I.w3] = 1;
-    if (op == OP_CALL || op == OP_CALL_INDIRECT) target[pc + 1] = 1;
-  }
-  for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
-    if (P.brtab[k] < n) target[P.brtab[k]] = 1;
-  for (const auto &f : P.funcs)
-    if (!f.imported) { target[f.entry_pc] = 1; target[f.body_pc] = 1; }
+  const std::vector<uint8_t> target = jump_targets(P);
   // V blob: fused pair handlers (gen_tc.py PAIRS) for an instruction and the one after
   // it; the instruction at pc + 1 keeps its own handler for jumps and resumes
   if (vframe) {
@@ -118,7 +125,8 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
     for (size_t pc = 0; pc < n; pc++) sl[pc] = int(tc[pc].w[0] / TC_SLOT_BYTES);
     for (size_t pc = 0; pc < n; pc++) {
       size_t m = 0;   // handled instructions from pc on (a tuple only covers those)
-      while (pc + m < n && m < 8 && sl[pc + m]) m++;
+      // a tuple never covers the start of a compiled run (jit.cpp replaces that TInstr)
+      while (pc + m < n && m < 8 && sl[pc + m] && !(m && run_start && (*run_start)[pc + m])) m++;
       int len = 0;
       const int ps = m >= 2 ? tc_tuple_slot(&sl[pc], int(m), &len) : 0;
       if (ps) tc[pc].w[0] = uint32_t(ps) * TC_SLOT_BYTES;

@@ -27,5 +27,11 @@ struct Program;
 // Build the TInstr array for P (size = code + 2 padding entries for the core's
 // successor prefetch) and mark DBC_HOT on the device copy `code` of P.code. vframe:
 // fields for the V-frame blob (frame cells in VGPRs; needs total cells <= TC_VF_CELLS).
-std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe);
+// run_start (optional): pcs where a compiled run will begin (jit.h); no fused tuple
+// handler covers one of them past its first instruction.
+std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe,
+                                   const std::vector<uint8_t> *run_start = nullptr);
+// Jump targets and resume points of P (index pc; size code + 1): branch/br_table/call
+// targets, the instruction after every call, function entries and bodies.
+std::vector<uint8_t> jump_targets(const Program &P);
 }  // namespace wb
