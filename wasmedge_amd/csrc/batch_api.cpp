@@ -154,6 +154,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
                                           : wb::jit_load(src, runs.size(), C->device, &addr);
       if (err.empty()) {
         wb::jit_patch(tcj, runs, addr);
+        for (const auto &r : runs) codepad[r.pc].w0 |= DBC_HOT;   // the core is entered there
         tcv.swap(tcj);
         C->jit_runs = uint32_t(runs.size());
       } else {

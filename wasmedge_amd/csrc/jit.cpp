@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -68,6 +69,7 @@ struct Em {
   bool any = false;
   struct Stub { std::string lab; uint32_t pc, done; };
   std::vector<Stub> stubs;
+  const struct MemGroup *group = nullptr;   // set on a group's first access (group_check)
 
   void l(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
     char buf[256];
@@ -135,34 +137,68 @@ struct Em {
 };
 
 // ---------------------------------------------------------------- linear memory
-// Bounds and alignment as the handlers (gen_tc.py mem_check): the last byte
-// ea + n - 1 = a + (offset + n - 1) must not carry and must lie below pages * 64 KiB;
-// 2- and >= 4-byte accesses must be naturally aligned (4 for 8 bytes). Leaves XP = the
-// address of the first word (granule layout, batch_ctx.h); a store (mark) also raises
-// the write mark (LS_HWM) to one past its last byte, saturating.
-void mem_addr(Em &e, uint32_t a, uint32_t imm, uint32_t n, bool mark) {
-  const uint32_t last = imm + n - 1;   // < 2^32 (jit_ok)
-  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, last, e.v(a));
+// Accesses are checked in groups: consecutive loads/stores of a run through the same
+// address cell a, which nothing in between writes (jit_groups). The group's first
+// access checks all of them at once, as the handlers check one (gen_tc.py mem_check):
+// the highest last byte a + (offset + n - 1) must not carry and must lie below
+// pages * 64 KiB, and each access must be naturally aligned (4 for 8 bytes). If any
+// active lane fails, the run leaves before the group (the C++ step and the handlers then
+// meet the failing access themselves). Stores raise the write mark (LS_HWM) once, to one
+// past the group's highest stored byte. In the word interleave (g = 0) an aligned word
+// access is at MEM + ea * 64: the group computes MEM + a * 64 once (BASE) and each access
+// adds offset * 64 in its instruction's offset field.
+const char *const BASE = "v[122:123]", *const BASE0 = "v122", *const BASE1 = "v123";
+
+struct MemGroup {
+  uint32_t base = 0;                // address cell
+  uint32_t maxlast = 0;             // highest offset + n - 1
+  uint64_t store_end = 0;           // highest offset + n of a store (0: no store)
+  std::vector<std::pair<uint32_t, uint32_t>> aligns;   // distinct (offset & m, m)
+};
+
+void group_check(Em &e, const MemGroup &G) {
+  const uint32_t a = G.base;
+  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, G.maxlast, e.v(a));
   e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
   e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
   e.l("s_or_b64 %s, %s, vcc", T2, T2);
-  const uint32_t m = n >= 4 ? 3 : n - 1;
-  if (m) {
-    e.l("v_and_b32_e32 %s, %u, %s", Y0, m, X0);
-    e.l("v_cmp_ne_u32_e32 vcc, %u, %s", m, Y0);
+  for (const auto &am : G.aligns) {
+    if (am.first) {
+      e.l("v_add_u32_e32 %s, %u, %s", Y0, am.first, e.v(a));
+      e.l("v_and_b32_e32 %s, %u, %s", Y0, am.second, Y0);
+    } else {
+      e.l("v_and_b32_e32 %s, %u, %s", Y0, am.second, e.v(a));
+    }
+    e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y0);
     e.l("s_or_b64 %s, %s, vcc", T2, T2);
   }
   e.leave_if_t2();
-  if (mark) {
-    e.l("v_add_u32_e64 %s, %s, 1 clamp", Y1, X0);
+  if (G.store_end) {   // (cannot carry past 2^32 once the bounds hold; clamp the sum)
+    e.l("s_mov_b32 s69, 0x%x", uint32_t(G.store_end));
+    e.l("v_add_u32_e64 %s, %s, s69 clamp", Y1, e.v(a));
     e.l("v_max_u32_e32 %s, %s, %s", HWM, HWM, Y1);
   }
-  // ea -> W0 (g = 0, aligned word: the byte address is MEM + ea * 64)
+  if (e.g == 0) {
+    e.l("v_mov_b32 %s, %s", W0, e.v(a));
+    e.l("v_lshlrev_b64 %s, 6, %s", BASE, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", BASE, BASE, MEM);
+  }
+}
+
+// Address operand(s) of the access at offset imm (n bytes) of the current group: the
+// first word's "vaddr, off[ offset:k]" and, for n = 8, the second word's.
+void mem_ea(Em &e, uint32_t a, uint32_t imm, uint32_t n, std::string *w1, std::string *w2) {
   if (e.g == 0 && n >= 4) {
-    if (imm) e.l("v_add_u32_e32 %s, 0x%x, %s", W0, imm, e.v(a));
-    else e.l("v_mov_b32 %s, %s", W0, e.v(a));
-    e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+    const uint64_t k = uint64_t(imm) * 64u;
+    if (k + (n == 8 ? 256 : 0) <= 4095) {
+      *w1 = std::string(BASE) + ", off offset:" + std::to_string(k);
+      *w2 = std::string(BASE) + ", off offset:" + std::to_string(k + 256);
+    } else {
+      e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(k), BASE0);
+      e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(k >> 32), BASE1);
+      *w1 = std::string(XP) + ", off";
+      *w2 = std::string(XP) + ", off offset:256";
+    }
     return;
   }
   // granule rows of 256 << g bytes, (ea >> (2 + g)) of them, + the byte in the granule
@@ -173,6 +209,7 @@ void mem_addr(Em &e, uint32_t a, uint32_t imm, uint32_t n, bool mark) {
   e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
   e.l("v_bfe_u32 %s, %s, 0, %u", W0, ea.c_str(), 2 + e.g);
   e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  *w1 = std::string(XP) + ", off";
   if (n == 8) {   // ZP = address of the second word (ea + 4: maybe the next granule)
     e.l("v_add_u32_e32 %s, 4, %s", Y1, ea.c_str());
     e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y1);
@@ -180,11 +217,9 @@ void mem_addr(Em &e, uint32_t a, uint32_t imm, uint32_t n, bool mark) {
     e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, ZP, MEM);
     e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y1, 2 + e.g);
     e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, WP, ZP);
+    *w2 = std::string(ZP) + ", off";
   }
 }
-
-// second word of an 8-byte access: 256 bytes on in the word interleave, else ZP
-std::string word2(const Em &e) { return e.g == 0 ? std::string(XP) + ", off offset:256" : std::string(ZP) + ", off"; }
 
 bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
   const uint32_t n = mem_bytes(op);
@@ -194,11 +229,13 @@ bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
   const bool wide = op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
                     op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
   e.sync({a, c, wide ? c + 1 : c});
-  mem_addr(e, a, imm, n, false);
-  e.l("%s %s, %s, off", ins, e.v(c), XP);
+  if (e.group) group_check(e, *e.group);
+  std::string w1, w2;
+  mem_ea(e, a, imm, n, &w1, &w2);
+  e.l("%s %s, %s", ins, e.v(c), w1.c_str());
   e.pend[c] = e.any = true;
   if (op == OP_LD64) {
-    e.l("global_load_dword %s, %s", e.v(c + 1), word2(e).c_str());
+    e.l("global_load_dword %s, %s", e.v(c + 1), w2.c_str());
     e.pend[c + 1] = true;
   } else if (op == OP_LD8U64 || op == OP_LD16U64 || op == OP_LD32U64) {
     e.l("v_mov_b32 %s, 0", e.v(c + 1));
@@ -212,14 +249,13 @@ bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
 bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm) {
   const uint32_t n = mem_bytes(op);
   e.drain();   // a store never overtakes a load of this run (same-address ordering)
-  mem_addr(e, a, imm, n, true);
+  if (e.group) group_check(e, *e.group);
+  std::string w1, w2;
+  mem_ea(e, a, imm, n, &w1, &w2);
   const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
-  e.l("%s %s, %s, off", ins, XP, e.v(b));
-  if (n == 8) {
-    const std::string w2 = word2(e);
-    const size_t k = w2.find(", off");
-    e.l("global_store_dword %s, %s%s", w2.substr(0, k).c_str(), e.v(b + 1), w2.substr(k).c_str());
-  }
+  const size_t k1 = w1.find(", off"), k2 = w2.find(", off");
+  e.l("%s %s, %s%s", ins, w1.substr(0, k1).c_str(), e.v(b), w1.substr(k1).c_str());
+  if (n == 8) e.l("global_store_dword %s, %s%s", w2.substr(0, k2).c_str(), e.v(b + 1), w2.substr(k2).c_str());
   return true;
 }
 
@@ -291,6 +327,13 @@ bool emit(Em &e, const DInstr &I) {
   }
   switch (op) {
     case OP_NOP_CNT:
+      return true;
+    case OP_ZERO_LOCALS:   // a = first cell, b = count
+      if (uint64_t(a) + b > TC_VF_CELLS) return false;
+      for (uint32_t k = 0; k < b; k++) {
+        e.sync({a + k});
+        e.l("v_mov_b32 %s, 0", e.v(a + k));
+      }
       return true;
     case OP_MOV32:
       e.sync({a, c});
@@ -485,6 +528,57 @@ bool emit(Em &e, const DInstr &I) {
   return false;
 }
 
+// cells an instruction writes (for the access groups: a write to the address cell ends
+// its group)
+void written(const DInstr &I, std::vector<uint32_t> *out) {
+  const uint16_t op = op_of(I);
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
+  out->clear();
+  if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64 || op == OP_NOP_CNT) return;
+  if (op == OP_ZERO_LOCALS) {
+    for (uint32_t k = 0; k < b; k++) out->push_back(a + k);
+    return;
+  }
+  out->push_back(c);
+  out->push_back(c + 1);   // (over-approximates 32-bit results)
+  if (op == OP_I32_ADD_XROTR_I) out->push_back(d);
+  if (op == OP_I32_ADD3_XROTR_I) out->push_back(I.w3 & 0xFFFFu);
+}
+
+// The access groups of a run (see "linear memory"): lead[i] = group index of the access
+// at pc + i that checks its group, -1 otherwise.
+std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<int> *lead) {
+  std::vector<MemGroup> G;
+  lead->assign(r.len, -1);
+  int open = -1;
+  std::vector<uint32_t> wr;
+  for (uint32_t i = 0; i < r.len; i++) {
+    const DInstr &I = P.code[r.pc + i];
+    const uint16_t op = op_of(I);
+    if (const uint32_t n = mem_bytes(op)) {
+      const uint32_t a = I.w1 & 0xFFFFu, imm = I.w3;
+      if (open < 0 || G[size_t(open)].base != a) {
+        open = int(G.size());
+        G.emplace_back();
+        G.back().base = a;
+        (*lead)[i] = open;
+      }
+      MemGroup &g = G[size_t(open)];
+      g.maxlast = std::max(g.maxlast, imm + n - 1);
+      if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64)
+        g.store_end = std::max<uint64_t>(g.store_end, uint64_t(imm) + n);
+      const uint32_t m = n >= 4 ? 3 : n - 1;
+      if (m) {
+        const std::pair<uint32_t, uint32_t> am{imm & m, m};
+        if (std::find(g.aligns.begin(), g.aligns.end(), am) == g.aligns.end()) g.aligns.push_back(am);
+      }
+    }
+    written(I, &wr);
+    if (open >= 0 && std::find(wr.begin(), wr.end(), G[size_t(open)].base) != wr.end()) open = -1;
+  }
+  return G;
+}
+
 // can instruction I be compiled (dry run)
 bool jit_ok(const Program &P, const DInstr &I) {
   const uint16_t op = op_of(I);
@@ -503,7 +597,8 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
   if (P.total_cells() > TC_VF_CELLS) return runs;
   const std::vector<uint8_t> target = jump_targets(P);
   std::vector<uint8_t> ok(n, 0);
-  for (size_t pc = 0; pc < n; pc++) ok[pc] = tc[pc].w[0] != 0 && jit_ok(P, P.code[pc]);
+  (void)tc;
+  for (size_t pc = 0; pc < n; pc++) ok[pc] = jit_ok(P, P.code[pc]);
   for (size_t pc = 0; pc < n;) {
     if (!ok[pc]) { pc++; continue; }
     size_t end = pc + 1;
@@ -546,9 +641,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.l("s_mov_b32 s68, 0x%x", next);
     e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
     e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
+    std::vector<int> lead;
+    const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
     for (uint32_t i = 0; i < r.len; i++) {
       const DInstr &I = P.code[r.pc + i];
       e.pc = r.pc + i;
+      e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
       if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
     }
