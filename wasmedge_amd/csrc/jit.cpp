@@ -12,6 +12,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -70,6 +71,7 @@ struct Em {
   struct Stub { std::string lab; uint32_t pc, done; };
   std::vector<Stub> stubs;
   const struct MemGroup *group = nullptr;   // set on a group's first access (group_check)
+  uint32_t fb = 0;                          // frame base (Program::global_cells)
 
   void l(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
     char buf[256];
@@ -128,11 +130,12 @@ struct Em {
   }
   // leave before instruction pc (the C++ step executes it) when any active lane's T2 bit
   // is set
-  void leave_if_t2() {
-    const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(pc);
+  std::string leave_if_t2() {
+    const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(stubs.size());
     l("s_and_b64 %s, %s, exec", T2, T2);
     l("s_cbranch_scc1 %s", lab.c_str());
     stubs.push_back(Stub{lab, pc, done});
+    return lab;
   }
 };
 
@@ -328,6 +331,29 @@ bool emit(Em &e, const DInstr &I) {
   switch (op) {
     case OP_NOP_CNT:
       return true;
+    case OP_POST_CALL: {   // gen_tc.py post_call_body_v: results fb.. -> L.., restore [fb, L)
+      const uint32_t L = a, r = b, fb = e.fb;
+      if (L < e.fb || uint64_t(L) + r > TC_VF_CELLS) return false;
+      e.drain();
+      e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);   // call stack slots past LDS: the C++ step
+      e.leave_if_t2();
+      for (uint32_t k = r; k-- > 0;)
+        if (L != fb) e.l("v_mov_b32 %s, %s", e.v(L + k), e.v(fb + k));
+      if (L > fb) {
+        e.l("v_subrev_u32_e32 v102, %u, v102", L - fb);
+        e.l("v_lshl_add_u32 %s, v102, 8, v103", X0);
+        for (uint32_t k = 0; k < L - fb; k++) e.l("ds_read_b32 %s, %s offset:%u", e.v(fb + k), X0, k * 256u);
+        e.l("s_waitcnt lgkmcnt(0)");
+      }
+      return true;
+    }
+    case OP_CALL: {   // the last instruction of a run (emit_call)
+      const uint32_t L = a, nargs = b, nloc = c, fb = e.fb;
+      return L >= fb && L < TC_VF_CELLS && imm < (1u << 26) && uint64_t(L) + nargs <= TC_VF_CELLS &&
+             uint64_t(fb) + nargs + nloc <= TC_VF_CELLS && L - fb < 255;
+    }
+    case OP_RET:    // the last instruction of a run (emit_ret)
+      return e.fb < TC_VF_CELLS && uint64_t(a) + b <= TC_VF_CELLS;
     case OP_ZERO_LOCALS:   // a = first cell, b = count
       if (uint64_t(a) + b > TC_VF_CELLS) return false;
       for (uint32_t k = 0; k < b; k++) {
@@ -413,8 +439,8 @@ bool emit(Em &e, const DInstr &I) {
     case OP_I32_XOR_ROTR_I: case OP_I32_XOR_ROTL_I: {
       e.sync({a, b, c});
       const uint32_t k = op == OP_I32_XOR_ROTR_I ? imm & 31u : (32u - (imm & 31u)) & 31u;
-      e.l("v_xor_b32_e32 %s, %s, %s", X0, e.v(a), e.v(b));
-      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(c), X0, X0, k);
+      e.l("v_xor_b32_e32 %s, %s, %s", e.v(c), e.v(a), e.v(b));
+      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(c), e.v(c), e.v(c), k);
       return true;
     }
     case OP_I32_ADD_XROTR_I: case OP_I32_ADD3_XROTR_I: {
@@ -425,8 +451,9 @@ bool emit(Em &e, const DInstr &I) {
       const std::string s = c == y ? std::string(R0) : e.V(c);
       if (three) e.l("v_add3_u32 %s, %s, %s, %s", s.c_str(), e.v(a), e.v(b), e.v(d));
       else e.l("v_add_u32_e32 %s, %s, %s", s.c_str(), e.v(a), e.v(b));
-      e.l("v_xor_b32_e32 %s, %s, %s", X0, e.v(y), s.c_str());
-      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(y), X0, X0, k);
+      // (no temporaries when c != y: the scheduler below then sees only frame cells)
+      e.l("v_xor_b32_e32 %s, %s, %s", e.v(y), e.v(y), s.c_str());
+      e.l("v_alignbit_b32 %s, %s, %s, %u", e.v(y), e.v(y), e.v(y), k);
       return true;
     }
     // ---- i64 (b operand of *_I: imm sign-extended)
@@ -528,6 +555,149 @@ bool emit(Em &e, const DInstr &I) {
   return false;
 }
 
+// ---------------------------------------------------------------- scheduling
+// One wave per SIMD (64K instances fill the chip) hides no latency: a VALU instruction
+// that needs the result of the one before waits for it (measured: ~12 cycles per
+// instruction along a dependent chain against 4 for independent ones). The run's code is
+// therefore list-scheduled between barriers (anything but a VALU instruction: scalar
+// code, branches, memory, waits), on the registers each instruction names: true, anti
+// and output dependences kept, independent chains (BLAKE3's four column / diagonal G
+// functions) interleaved.
+struct SIns {
+  std::string text;
+  std::vector<int> defs, uses;
+};
+
+void regs_of(const std::string &tok, std::vector<int> *out) {
+  // vN, v[N:M], sN, s[N:M], vcc (VGPR k -> k, SGPR k -> 1000 + k, vcc -> 2000)
+  size_t i = 0;
+  while (i < tok.size()) {
+    const char ch = tok[i];
+    const bool word_start = i == 0 || !(isalnum((unsigned char)tok[i - 1]) || tok[i - 1] == '_');
+    if (word_start && tok.compare(i, 3, "vcc") == 0) { out->push_back(2000); i += 3; continue; }
+    if (word_start && (ch == 'v' || ch == 's') && i + 1 < tok.size()) {
+      const int base = ch == 'v' ? 0 : 1000;
+      if (tok[i + 1] == '[') {
+        int lo = 0, hi = 0;
+        if (sscanf(tok.c_str() + i + 2, "%d:%d", &lo, &hi) == 2)
+          for (int r = lo; r <= hi; r++) out->push_back(base + r);
+        i = tok.find(']', i) + 1;
+        continue;
+      }
+      if (isdigit((unsigned char)tok[i + 1])) {
+        out->push_back(base + atoi(tok.c_str() + i + 1));
+        i++;
+        while (i < tok.size() && isdigit((unsigned char)tok[i])) i++;
+        continue;
+      }
+    }
+    i++;
+  }
+}
+
+bool parse_valu(const std::string &line, SIns *ins) {
+  ins->text = line;
+  if (line.compare(0, 2, "v_") != 0) return false;
+  const size_t sp = line.find(' ');
+  if (sp == std::string::npos) return false;
+  const std::string mn = line.substr(0, sp);
+  std::vector<std::string> ops;
+  for (size_t at = sp + 1; at <= line.size();) {
+    size_t cm = line.find(", ", at);
+    if (cm == std::string::npos) cm = line.size();
+    ops.push_back(line.substr(at, cm - at));
+    at = cm + 2;
+  }
+  const size_t ndef = mn.find("_co_") != std::string::npos ? 2 : 1;   // v_add_co: vdst, sdst
+  for (size_t k = 0; k < ops.size(); k++) regs_of(ops[k], k < ndef ? &ins->defs : &ins->uses);
+  return true;
+}
+
+std::string schedule(const std::string &body) {
+  std::vector<std::string> lines;
+  for (size_t at = 0; at < body.size();) {
+    const size_t nl = body.find('\n', at);
+    lines.push_back(body.substr(at, nl - at));
+    at = nl + 1;
+  }
+  std::string out;
+  std::vector<SIns> seg;
+  auto flush = [&]() {
+    const size_t n = seg.size();
+    if (n > 1) {
+      // dependences: j -> i (j earlier) with a latency in cycles
+      constexpr int kIssue = 4, kLat = 12;
+      std::vector<std::vector<std::pair<int, int>>> pred(n), succ(n);
+      std::map<int, int> last_def;
+      std::map<int, std::vector<int>> readers;
+      for (size_t i = 0; i < n; i++) {
+        std::map<int, int> dep;   // pred -> latency
+        for (int r : seg[i].uses) {
+          auto it = last_def.find(r);
+          if (it != last_def.end()) dep[it->second] = std::max(dep[it->second], kLat);
+        }
+        for (int r : seg[i].defs) {
+          auto it = last_def.find(r);
+          if (it != last_def.end()) dep[it->second] = std::max(dep[it->second], 1);
+          for (int j : readers[r])
+            if (j != int(i)) dep[j] = std::max(dep[j], 1);
+        }
+        for (auto &d : dep) {
+          pred[i].push_back({d.first, d.second});
+          succ[size_t(d.first)].push_back({int(i), d.second});
+        }
+        for (int r : seg[i].uses) readers[r].push_back(int(i));
+        for (int r : seg[i].defs) { last_def[r] = int(i); readers[r].clear(); }
+      }
+      std::vector<int> height(n, 0);   // longest latency path to the segment's end
+      for (size_t i = n; i-- > 0;)
+        for (auto &s : succ[i]) height[i] = std::max(height[i], height[size_t(s.first)] + s.second);
+      std::vector<int> npred(n), at(n, 0);
+      for (size_t i = 0; i < n; i++) npred[i] = int(pred[i].size());
+      std::vector<int> ready;
+      for (size_t i = 0; i < n; i++)
+        if (!npred[i]) ready.push_back(int(i));
+      int clock = 0;
+      while (!ready.empty()) {
+        size_t best = 0;
+        for (size_t k = 1; k < ready.size(); k++) {
+          const int a = ready[k], b = ready[best];
+          const int ta = std::max(at[size_t(a)], clock), tb = std::max(at[size_t(b)], clock);
+          if (ta < tb || (ta == tb && (height[size_t(a)] > height[size_t(b)] ||
+                                       (height[size_t(a)] == height[size_t(b)] && a < b))))
+            best = k;
+        }
+        const int i = ready[best];
+        ready.erase(ready.begin() + long(best));
+        const int t = std::max(at[size_t(i)], clock);
+        clock = t + kIssue;
+        out += seg[size_t(i)].text;
+        out += '\n';
+        for (auto &s : succ[size_t(i)]) {
+          at[size_t(s.first)] = std::max(at[size_t(s.first)], t + s.second);
+          if (--npred[size_t(s.first)] == 0) ready.push_back(s.first);
+        }
+      }
+    } else if (n == 1) {
+      out += seg[0].text;
+      out += '\n';
+    }
+    seg.clear();
+  };
+  for (const auto &ln : lines) {
+    SIns ins;
+    if (parse_valu(ln, &ins)) {
+      seg.push_back(std::move(ins));
+    } else {
+      flush();
+      out += ln;
+      out += '\n';
+    }
+  }
+  flush();
+  return out;
+}
+
 // cells an instruction writes (for the access groups: a write to the address cell ends
 // its group)
 void written(const DInstr &I, std::vector<uint32_t> *out) {
@@ -579,15 +749,81 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
   return G;
 }
 
+// After a taken transfer (PCOFF = s62 set, CNT counted): the core's taken() checks --
+// the count limit, and in diverged mode a jump to or below the lowest waiting pc re-aims
+// OTHER -- then the instruction at PCOFF is dispatched (bank A) or the core leaves for
+// the scheduler (xs).
+void taken_dispatch(Em &e, const std::string &xs, bool banks_loaded) {
+  e.l("s_cmp_ge_u32 s65, s64");
+  e.l("s_cbranch_scc1 %s", xs.c_str());
+  e.l("s_cmp_le_u32 s62, s95");
+  e.l("s_cselect_b32 s63, s95, s63");
+  e.l("s_cmp_ge_u32 s62, s63");
+  e.l("s_cbranch_scc1 %s", xs.c_str());
+  e.l("s_waitcnt lgkmcnt(0)");
+  if (!banks_loaded) {
+    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+    e.l("s_waitcnt lgkmcnt(0)");
+  }
+  e.l("s_add_u32 s68, s70, s76");
+  e.l("s_addc_u32 s69, s71, 0");
+  e.l("s_setpc_b64 s[68:69]");
+}
+
+// CALL (gen_tc.py call_body_v): spill [fb, L) and the return record to the LDS call
+// stack, args L.. -> fb.., zero the callee's locals, jump to the callee.
+void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::string &xs) {
+  const uint32_t L = I.w1 & 0xFFFFu, nargs = I.w1 >> 16, nloc = I.w2 & 0xFFFFu, fb = e.fb;
+  const uint32_t n = L - fb;
+  e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
+  e.l("v_cmp_lt_u32_e64 %s, s93, %s", T2, X0);   // would pass the LDS part: the C++ step
+  e.leave_if_t2();
+  e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+  for (uint32_t k = 0; k < n; k++) e.l("ds_write_b32 %s, %s offset:%u", X1, e.v(fb + k), k * 256u);
+  e.l("v_mov_b32 %s, 0x%x", Y1, ((pc + 1) & 0xFFFFFu) | (L << 20));
+  e.l("ds_write_b32 %s, %s offset:%u", X1, Y1, n * 256u);
+  e.l("v_add_u32_e32 v102, %u, v102", n + 1);
+  for (uint32_t k = 0; k < nargs; k++)
+    if (L != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(L + k));
+  for (uint32_t k = 0; k < nloc; k++) e.l("v_mov_b32 %s, 0", e.v(fb + nargs + k));
+}
+
+// RET (gen_tc.py ret_body_v): pop the return record (it must agree across the lanes and
+// not be the entry frame's), results a.. -> fb.., jump to the return pc.
+void emit_ret(Em &e, const DInstr &I) {
+  const uint32_t a = I.w1 & 0xFFFFu, nres = I.w1 >> 16, fb = e.fb;
+  e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
+  const std::string out = e.leave_if_t2();
+  e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+  e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
+  e.l("ds_read_b32 %s, %s", Y1, X1);
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("v_readfirstlane_b32 s68, %s", Y1);
+  e.l("s_nop 1");
+  e.l("v_cmp_ne_u32_e64 %s, s68, %s", T2, Y1);
+  e.l("s_and_b64 %s, %s, exec", T2, T2);
+  e.l("s_cbranch_scc1 %s", out.c_str());
+  e.l("s_and_b32 s68, s68, 0xfffff");
+  e.l("s_cmp_eq_u32 s68, 0xfffff");
+  e.l("s_cbranch_scc1 %s", out.c_str());
+  e.l("v_subrev_u32_e32 v102, 1, v102");
+  for (uint32_t k = 0; k < nres; k++)
+    if (a != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(a + k));
+  e.l("s_lshl_b32 s62, s68, 5");
+}
+
 // can instruction I be compiled (dry run)
 bool jit_ok(const Program &P, const DInstr &I) {
   const uint16_t op = op_of(I);
   if (const uint32_t n = mem_bytes(op))
     if (uint64_t(I.w3) + n - 1 > 0xFFFFFFFFull) return false;
   Em e;
-  (void)P;
+  e.fb = P.global_cells;
   return emit(e, I);
 }
+
+bool is_xfer(uint16_t op) { return op == OP_CALL || op == OP_RET; }
 
 }  // namespace
 
@@ -601,9 +837,19 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
   for (size_t pc = 0; pc < n; pc++) ok[pc] = jit_ok(P, P.code[pc]);
   for (size_t pc = 0; pc < n;) {
     if (!ok[pc]) { pc++; continue; }
+    // a run ends after a call or return (the run's code makes the transfer itself)
     size_t end = pc + 1;
-    while (end < n && ok[end] && !target[end]) end++;
-    if (end - pc >= kMinRun) {
+    if (!is_xfer(op_of(P.code[pc])))
+      while (end < n && ok[end] && !target[end]) {
+        end++;
+        if (is_xfer(op_of(P.code[end - 1]))) break;
+      }
+    bool calls = false;   // the call protocol's handlers are long: worth a run of any length
+    for (size_t k = pc; k < end; k++) {
+      const uint16_t o = op_of(P.code[k]);
+      calls |= is_xfer(o) || o == OP_POST_CALL;
+    }
+    if (end - pc >= kMinRun || calls) {
       uint32_t cnt = 0;
       for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
       runs.push_back(JitRun{uint32_t(pc), uint32_t(end - pc), cnt});
@@ -614,6 +860,8 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
 }
 
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog) {
+  const char *se = getenv("WB_JIT_SCHED");   // 0: keep program order (A/B measurement aid)
+  const bool sched = !(se && se[0] == '0');
   std::string src =
       "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
       "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out) {\n"
@@ -636,29 +884,48 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     // the successor prefetch in flight must land before both banks are reloaded for the
     // instruction after the run (SMEM returns out of order); that reload then overlaps
     // the run's own work
-    const uint32_t next = (r.pc + r.len) * 32u;
-    e.l("s_waitcnt lgkmcnt(0)");
-    e.l("s_mov_b32 s68, 0x%x", next);
-    e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
-    e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
+    const DInstr &last = P.code[r.pc + r.len - 1];
+    const uint16_t lop = op_of(last);
+    // the next instruction: after the run, or a call's target (a return's is dynamic)
+    const uint32_t next = (lop == OP_CALL ? last.w3 : r.pc + r.len) * 32u;
+    e.fb = P.global_cells;
+    if (lop != OP_RET) {
+      e.l("s_waitcnt lgkmcnt(0)");
+      e.l("s_mov_b32 s68, 0x%x", next);
+      e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
+      e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
+    }
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
+    const size_t body_at = e.o.size();
+    const std::string xs = "Lxs" + K;
     for (uint32_t i = 0; i < r.len; i++) {
       const DInstr &I = P.code[r.pc + i];
       e.pc = r.pc + i;
       e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
-      if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
+      if (i + 1 == r.len && is_xfer(op_of(I))) {
+        e.drain();
+        if (op_of(I) == OP_CALL) emit_call(e, I, e.pc, xs);
+        else emit_ret(e, I);
+      } else if (!emit(e, I)) {
+        return "";   // jit_runs only picks compilable instructions
+      }
       e.done += (I.w0 >> 16) & 0xFFu;
     }
     e.drain();
-    e.l("s_mov_b32 s62, 0x%x", next);
+    if (sched) e.o = e.o.substr(0, body_at) + schedule(e.o.substr(body_at));
+    if (lop != OP_RET) e.l("s_mov_b32 s62, 0x%x", next);
     e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
-    e.l("s_cmp_ge_u32 s62, s63");   // diverged: a waiting lane's pc reached -> scheduler
-    e.l("s_cbranch_scc1 Lxs%s", K.c_str());
-    e.l("s_waitcnt lgkmcnt(0)");
-    e.l("s_add_u32 s68, s70, s76");
-    e.l("s_addc_u32 s69, s71, 0");
-    e.l("s_setpc_b64 s[68:69]");
+    if (is_xfer(lop)) {
+      taken_dispatch(e, xs, lop == OP_CALL);
+    } else {
+      e.l("s_cmp_ge_u32 s62, s63");   // diverged: a waiting lane's pc reached -> scheduler
+      e.l("s_cbranch_scc1 %s", xs.c_str());
+      e.l("s_waitcnt lgkmcnt(0)");
+      e.l("s_add_u32 s68, s70, s76");
+      e.l("s_addc_u32 s69, s71, 0");
+      e.l("s_setpc_b64 s[68:69]");
+    }
     e.l("Lxs%s:", K.c_str());
     e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
     e.l("s_addc_u32 s69, s71, 0");
