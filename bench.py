@@ -220,16 +220,21 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     return rec, state["mbytes"] / state["instrs"]
 
 
-def load_profile_traffic():
-    """HBM bytes per interpreter launch from the committed rocprofv3 PMC summary
-    (profiles/), when present (see DESIGN.md 'Measurement')."""
+def load_profile():
+    """The committed rocprofv3 PMC summary of this bench command (profiles/traffic_c2.json,
+    tools/prof_summary.py): HBM bytes and VALU instructions per interpreter launch, when
+    it matches the configuration (see DESIGN.md 'Measurement')."""
     p = os.path.join(ROOT, "profiles", "traffic_c2.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
         if d.get("iters") == ITERS and d.get("instances") == INSTANCES:
-            return d.get("hbm_bytes_per_launch")
-    return None
+            return d
+    return {}
+
+
+def load_profile_traffic():
+    return load_profile().get("hbm_bytes_per_launch")
 
 
 def elapsed_hint(args):
@@ -345,14 +350,26 @@ def main():
 
     else:
         out["data"] = "synthetic: per-instance inputs derived from the instance id"
-    # the bound that matters for a dispatch loop: vector issue. Every wasm instruction is
-    # at least one lane-op, so the VALU lane-op peak bounds wasm instr/s from above
+    # the bound that matters for the interpreter: vector issue at one wave per SIMD. The
+    # achieved rate is the VALU lane-ops the kernel issues (SQ_INSTS_VALU x 64 from the
+    # committed PMC pass of this same command) over this run's measured kernel time
     per_gpu = total_instrs / elapsed / dist.world
-    out["issue_roofline"] = {"bound": "valu", "achieved": per_gpu, "peak": VALU_PEAK,
-                             "unit": "wasm instr/s per GPU vs VALU lane-op/s",
-                             "frac": per_gpu / VALU_PEAK,
-                             "basis": "DESIGN.md 'Roofline': 256 CU x 4 SIMD-32 x 32 lanes x "
-                                      "2.4 GHz (MI355X_MICROARCH.md)"}
+    prof = load_profile() if (args.workload == "c2" and args.iters == ITERS and n == INSTANCES) else {}
+    if prof.get("valu_insts_per_launch"):
+        valu = prof["valu_insts_per_launch"] * 64.0 / kernel_avg
+        out["issue_roofline"] = {
+            "bound": "valu", "achieved": valu, "peak": VALU_PEAK, "unit": "VALU lane-op/s",
+            "frac": valu / VALU_PEAK,
+            "wasm_instr_per_valu_lane_op": (total_instrs / args.steps / dist.world) /
+                                           (prof["valu_insts_per_launch"] * 64.0),
+            "source": "SQ_INSTS_VALU per launch, profiles/%s_counters.md" % prof.get("source"),
+            "basis": "DESIGN.md 'Roofline': 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
+                     "(MI355X_MICROARCH.md)"}
+    else:
+        out["issue_roofline"] = {
+            "bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "VALU lane-op/s",
+            "frac": None, "wasm_instr_per_s_per_gpu": per_gpu,
+            "note": "no PMC summary for this configuration (tools/prof_bench.sh)"}
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads = host_cores()
         out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,

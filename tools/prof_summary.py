@@ -85,7 +85,10 @@ def main():
     open(os.path.join(prof, tag + "_counters.md"), "w").write("\n".join(lines) + "\n")
     json.dump({"iters": iters, "instances": inst, "hbm_bytes_per_launch": fetch + write,
                "fetch_bytes": fetch, "write_bytes": write, "fetch_factor": fetch_factor,
-               "kernel_avg_ns": avg_ns, "source": tag},
+               "kernel_avg_ns": avg_ns, "source": tag,
+               "valu_insts_per_launch": C[(K, "SQ_INSTS_VALU")],
+               "salu_insts_per_launch": C[(K, "SQ_INSTS_SALU")],
+               "wave_quad_cycles_per_launch": wc, "waves": waves},
               open(os.path.join(prof, "traffic_c2.json" if label is None else
                                 "traffic_%s.json" % tag), "w"), indent=1)
     print("\n".join(lines))

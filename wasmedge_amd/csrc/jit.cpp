@@ -352,6 +352,13 @@ bool emit(Em &e, const DInstr &I) {
       return L >= fb && L < TC_VF_CELLS && imm < (1u << 26) && uint64_t(L) + nargs <= TC_VF_CELLS &&
              uint64_t(fb) + nargs + nloc <= TC_VF_CELLS && L - fb < 255;
     }
+    case OP_JMP: case OP_BR_IF: case OP_BR_UNLESS:
+    case OP_BR_EQ: case OP_BR_NE: case OP_BR_LT_S: case OP_BR_LT_U: case OP_BR_GT_S: case OP_BR_GT_U:
+    case OP_BR_LE_S: case OP_BR_LE_U: case OP_BR_GE_S: case OP_BR_GE_U:
+    case OP_BR_EQ_I: case OP_BR_NE_I: case OP_BR_LT_S_I: case OP_BR_LT_U_I: case OP_BR_GT_S_I:
+    case OP_BR_GT_U_I: case OP_BR_LE_S_I: case OP_BR_LE_U_I: case OP_BR_GE_S_I: case OP_BR_GE_U_I:
+      // the last instruction of a run (emit_branch); as tc.cpp: a taken count >= 0
+      return int32_t((I.w0 >> 16) & 0xFFu) + int32_t(int16_t(d)) >= 0 && imm < (1u << 26);
     case OP_RET:    // the last instruction of a run (emit_ret)
       return e.fb < TC_VF_CELLS && uint64_t(a) + b <= TC_VF_CELLS;
     case OP_ZERO_LOCALS:   // a = first cell, b = count
@@ -749,31 +756,9 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
   return G;
 }
 
-// After a taken transfer (PCOFF = s62 set, CNT counted): the core's taken() checks --
-// the count limit, and in diverged mode a jump to or below the lowest waiting pc re-aims
-// OTHER -- then the instruction at PCOFF is dispatched (bank A) or the core leaves for
-// the scheduler (xs).
-void taken_dispatch(Em &e, const std::string &xs, bool banks_loaded) {
-  e.l("s_cmp_ge_u32 s65, s64");
-  e.l("s_cbranch_scc1 %s", xs.c_str());
-  e.l("s_cmp_le_u32 s62, s95");
-  e.l("s_cselect_b32 s63, s95, s63");
-  e.l("s_cmp_ge_u32 s62, s63");
-  e.l("s_cbranch_scc1 %s", xs.c_str());
-  e.l("s_waitcnt lgkmcnt(0)");
-  if (!banks_loaded) {
-    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
-    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
-    e.l("s_waitcnt lgkmcnt(0)");
-  }
-  e.l("s_add_u32 s68, s70, s76");
-  e.l("s_addc_u32 s69, s71, 0");
-  e.l("s_setpc_b64 s[68:69]");
-}
-
 // CALL (gen_tc.py call_body_v): spill [fb, L) and the return record to the LDS call
 // stack, args L.. -> fb.., zero the callee's locals, jump to the callee.
-void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::string &xs) {
+void emit_call(Em &e, const DInstr &I, uint32_t pc) {
   const uint32_t L = I.w1 & 0xFFFFu, nargs = I.w1 >> 16, nloc = I.w2 & 0xFFFFu, fb = e.fb;
   const uint32_t n = L - fb;
   e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
@@ -824,6 +809,27 @@ bool jit_ok(const Program &P, const DInstr &I) {
 }
 
 bool is_xfer(uint16_t op) { return op == OP_CALL || op == OP_RET; }
+bool is_branch_op(uint16_t op) {
+  return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
+}
+bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op); }
+
+// The compare of a branch into vcc (true = taken).
+void branch_cond(Em &e, const DInstr &I) {
+  const uint16_t op = op_of(I);
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16;
+  if (op == OP_BR_IF) {
+    e.l("v_cmp_ne_u32_e32 vcc, 0, %s", e.v(a));
+  } else if (op == OP_BR_UNLESS) {
+    e.l("v_cmp_eq_u32_e32 vcc, 0, %s", e.v(a));
+  } else if (op >= OP_BR_EQ_I) {   // b: a signed imm16
+    const uint16_t k = uint16_t(op - OP_BR_EQ_I);
+    e.l("v_cmp_%s32_e32 vcc, %d, %s", cmp_kind(cmp_swap(k)), int32_t(int16_t(b)), e.v(a));
+  } else {
+    const uint16_t k = uint16_t(op - OP_BR_EQ);
+    e.l("v_cmp_%s32_e32 vcc, %s, %s", cmp_kind(k), e.v(a), e.v(b));
+  }
+}
 
 }  // namespace
 
@@ -837,18 +843,19 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
   for (size_t pc = 0; pc < n; pc++) ok[pc] = jit_ok(P, P.code[pc]);
   for (size_t pc = 0; pc < n;) {
     if (!ok[pc]) { pc++; continue; }
-    // a run ends after a call or return (the run's code makes the transfer itself)
+    // a run ends after a call, return or branch (the run's code makes the transfer)
     size_t end = pc + 1;
-    if (!is_xfer(op_of(P.code[pc])))
+    if (!ends_run(op_of(P.code[pc])))
       while (end < n && ok[end] && !target[end]) {
         end++;
-        if (is_xfer(op_of(P.code[end - 1]))) break;
+        if (ends_run(op_of(P.code[end - 1]))) break;
       }
     bool calls = false;   // the call protocol's handlers are long: worth a run of any length
     for (size_t k = pc; k < end; k++) {
       const uint16_t o = op_of(P.code[k]);
       calls |= is_xfer(o) || o == OP_POST_CALL;
     }
+    if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = false;   // a lone branch
     if (end - pc >= kMinRun || calls) {
       uint32_t cnt = 0;
       for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
@@ -866,6 +873,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
       "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out) {\n"
       "  unsigned lo, hi;\n";
+  // run index by start pc: a transfer to one jumps straight to its code
+  std::map<uint32_t, size_t> start;
+  for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
   for (size_t k = 0; k < runs.size(); k++) {
     const JitRun &r = runs[k];
     Em e;
@@ -881,17 +891,20 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.l("s_branch Le%s", K.c_str());
     e.l(".p2align 6");
     e.l("Lb%s:", K.c_str());
-    // the successor prefetch in flight must land before both banks are reloaded for the
-    // instruction after the run (SMEM returns out of order); that reload then overlaps
-    // the run's own work
     const DInstr &last = P.code[r.pc + r.len - 1];
     const uint16_t lop = op_of(last);
-    // the next instruction: after the run, or a call's target (a return's is dynamic)
-    const uint32_t next = (lop == OP_CALL ? last.w3 : r.pc + r.len) * 32u;
+    // Where the run goes on: the instruction after it (fall-through, untaken branch), a
+    // call's or branch's target, or (return) the popped return pc. The instruction after
+    // the run is prefetched into both banks while the run works, unless it starts a
+    // compiled run itself (then the code jumps there) or the run calls.
+    const uint32_t fall = r.pc + r.len;
+    const uint32_t tgt = (lop == OP_CALL || is_branch_op(lop)) ? last.w3 : 0;
+    const uint32_t pre = lop == OP_CALL ? tgt : fall;
+    const bool preload = lop != OP_RET && lop != OP_JMP && !start.count(pre);
     e.fb = P.global_cells;
-    if (lop != OP_RET) {
+    if (preload) {
       e.l("s_waitcnt lgkmcnt(0)");
-      e.l("s_mov_b32 s68, 0x%x", next);
+      e.l("s_mov_b32 s68, 0x%x", pre * 32u);
       e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
       e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
     }
@@ -899,32 +912,96 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
     const size_t body_at = e.o.size();
     const std::string xs = "Lxs" + K;
-    for (uint32_t i = 0; i < r.len; i++) {
+    const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
+    for (uint32_t i = 0; i < nbody; i++) {
       const DInstr &I = P.code[r.pc + i];
       e.pc = r.pc + i;
       e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
-      if (i + 1 == r.len && is_xfer(op_of(I))) {
-        e.drain();
-        if (op_of(I) == OP_CALL) emit_call(e, I, e.pc, xs);
-        else emit_ret(e, I);
-      } else if (!emit(e, I)) {
-        return "";   // jit_runs only picks compilable instructions
-      }
+      if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
     }
     e.drain();
     if (sched) e.o = e.o.substr(0, body_at) + schedule(e.o.substr(body_at));
-    if (lop != OP_RET) e.l("s_mov_b32 s62, 0x%x", next);
-    e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
-    if (is_xfer(lop)) {
-      taken_dispatch(e, xs, lop == OP_CALL);
-    } else {
-      e.l("s_cmp_ge_u32 s62, s63");   // diverged: a waiting lane's pc reached -> scheduler
-      e.l("s_cbranch_scc1 %s", xs.c_str());
+    e.pc = r.pc + r.len - 1;
+    e.group = nullptr;
+    // go to pc `to` (PCOFF and CNT set): straight into its compiled run when it has one
+    // (in diverged mode only if that run stops short of the lowest waiting pc, as the
+    // JIT slot would check), else through its TInstr (banks: already loaded for it)
+    int lab = 0;
+    auto go = [&](uint32_t to, bool banks) {
+      auto it = start.find(to);
+      const std::string disp = "Ld" + K + "_" + std::to_string(lab++);
+      if (it != start.end()) {
+        e.l("s_add_u32 s68, s62, 0x%x", (runs[it->second].len - 1) * 32u);
+        e.l("s_cmp_ge_u32 s68, s63");
+        e.l("s_cbranch_scc1 %s", disp.c_str());
+        e.l("s_branch Lb%zu", it->second);
+        e.l("%s:", disp.c_str());
+        banks = false;
+      }
       e.l("s_waitcnt lgkmcnt(0)");
+      if (!banks) {
+        e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+        e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+        e.l("s_waitcnt lgkmcnt(0)");
+      }
       e.l("s_add_u32 s68, s70, s76");
       e.l("s_addc_u32 s69, s71, 0");
       e.l("s_setpc_b64 s[68:69]");
+    };
+    // a taken transfer: the core's taken() checks (count limit; diverged: a jump to or
+    // below the lowest waiting pc re-aims OTHER, reaching OTHER goes to the scheduler)
+    auto taken_checks = [&]() {
+      e.l("s_cmp_ge_u32 s65, s64");
+      e.l("s_cbranch_scc1 %s", xs.c_str());
+      e.l("s_cmp_le_u32 s62, s95");
+      e.l("s_cselect_b32 s63, s95, s63");
+      e.l("s_cmp_ge_u32 s62, s63");
+      e.l("s_cbranch_scc1 %s", xs.c_str());
+    };
+    auto fallthrough = [&](uint32_t cnt) {   // next(): stop at the lowest waiting pc
+      e.l("s_mov_b32 s62, 0x%x", fall * 32u);
+      e.l("s_add_u32 s65, s65, 0x%x", cnt);
+      e.l("s_cmp_ge_u32 s62, s63");
+      e.l("s_cbranch_scc1 %s", xs.c_str());
+      go(fall, preload);
+    };
+    if (lop == OP_CALL) {
+      emit_call(e, last, e.pc);
+      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
+      e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+      taken_checks();
+      go(tgt, preload);
+    } else if (lop == OP_RET) {
+      emit_ret(e, last);
+      e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+      taken_checks();
+      go(~0u, false);
+    } else if (is_branch_op(lop)) {
+      const uint32_t bcnt = (last.w0 >> 16) & 0xFFu;
+      const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
+      const uint32_t taken_cnt = uint32_t(int32_t(r.cnt) + tcnt);   // (cnt + tcnt >= 0)
+      const std::string nt = "Lnt" + K;
+      if (lop != OP_JMP) {
+        branch_cond(e, last);
+        e.l("s_and_b64 %s, vcc, exec", T2);
+        e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
+        e.l("s_cmp_eq_u64 %s, exec", T2);
+        const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
+        e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done});
+        e.l("s_cbranch_scc0 %s", lab_split.c_str());   // lanes disagree: the C++ step splits
+      }
+      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
+      e.l("s_add_u32 s65, s65, 0x%x", taken_cnt);
+      taken_checks();
+      go(tgt, false);
+      if (lop != OP_JMP) {
+        e.l("%s:", nt.c_str());
+        (void)bcnt;
+        fallthrough(r.cnt);
+      }
+    } else {
+      fallthrough(r.cnt);
     }
     e.l("Lxs%s:", K.c_str());
     e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
