@@ -184,39 +184,40 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     state = {"done": 0, "mbytes": 0.0, "instrs": 0.0}
 
     def phase(nthr, budget):
+        # ids wrap round: a phase that runs out of instances starts over (checked again)
         chunk = int(max(nthr, min(64 * nthr, nthr * budget / 4 / max(t_inst, 1e-9))))
-        instrs, secs, start = 0.0, 0.0, state["done"]
-        while secs < budget and state["done"] < n_max:
-            done = state["done"]
-            k = min(chunk, n_max - done)
-            ids = np.arange(done, done + k, dtype=np.int64)
+        instrs, secs, ran = 0.0, 0.0, 0
+        while secs < budget and (nthr > 1 or ran < n_max):
+            k = min(chunk, n_max)
+            ids = (state["done"] + np.arange(k, dtype=np.int64)) % n_max
             rows = build_rows(ids)
             params = np.zeros((k, len(ptypes), 2), np.uint64)
             params[:, :, 0] = rows.astype(np.uint64)
             out = m.run_batch(func, params, k, threads=nthr)
-            lo = slice(done, done + k)
-            if not (np.array_equal(out["codes"], gpu["status"][lo])
-                    and np.array_equal(out["counts"], gpu["counts"][lo])
-                    and np.array_equal(out["hashes"], gpu["hashes"][lo])
+            if not (np.array_equal(out["codes"], gpu["status"][ids])
+                    and np.array_equal(out["counts"], gpu["counts"][ids])
+                    and np.array_equal(out["hashes"], gpu["hashes"][ids])
                     and np.array_equal((out["results"][:, 0, 0] & rmask)[out["codes"] == 0],
-                                       (gpu["ret"][lo] & rmask)[out["codes"] == 0])):
-                raise SystemExit("GPU/oracle mismatch in instances [%d, %d)" % (done, done + k))
+                                       (gpu["ret"][ids] & rmask)[out["codes"] == 0])):
+                raise SystemExit("GPU/oracle mismatch in instances %d..%d" % (ids[0], ids[-1]))
             instrs += float(out["counts"].sum())
             state["mbytes"] += float(out["mem_bytes"].sum())
             secs += out["seconds"]
-            state["done"] = done + k
+            state["done"] = int((ids[-1] + 1) % n_max)
+            ran += k
         state["instrs"] += instrs
-        return instrs, secs, state["done"] - start
+        return instrs, secs, ran
 
     i1, s1, n1 = phase(1, budget_s / 4)
-    it, st, nt = phase(threads, budget_s - s1) if state["done"] < n_max else (i1, s1, n1)
+    it, st, nt = phase(threads, budget_s - s1)
     rec = {"value": it / st, "unit": "instr/s", "cores": threads, "kind": "port",
            "value_1thread": i1 / s1, "cpu_model": cpu_model(),
            "sample": "%s instances: %d on 1 thread (%.3g instrs, %.2fs), then %d on %d threads "
-                     "(%.3g instrs, %.2fs); all bit-exact vs the GPU run on those instances"
+                     "(%.3g instrs, %.2fs), ids from 0 wrapping round; all bit-exact vs the GPU run "
+                     "on those instances"
                      % (what, n1, i1, s1, nt, threads, it, st),
-           "calibration": "oracle vs the reference interpreter, same container, 1 thread: "
-                          "fib(30) 0.62x the reference's time, mt19937 1.7x (BASELINE.md 3)"}
+           "calibration": "the oracle on 1 thread takes 0.9-1.4x the reference interpreter's "
+                          "time on fib(30) and 3.5x on mt19937 (BASELINE.md 3)"}
     return rec, state["mbytes"] / state["instrs"]
 
 
@@ -258,6 +259,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
+    ap.add_argument("--cost-limit", type=int, default=0,
+                    help="meter gas with the unit cost table up to this limit (measures the "
+                         "cost of exact metering; not the headline configuration)")
     args = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -272,6 +276,8 @@ def main():
     wasm, func, build_rows, ptypes, desc, extra = workload(args.workload, args)
     n = args.instances
     kw = {"max_memory_page": 17} if args.workload == "c3" else {}
+    if args.cost_limit:
+        kw["cost_limit"] = args.cost_limit
     ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
     ids = shard_ids(dist.rank, n, dist.world, args.scaling)
     n = len(ids)
@@ -339,6 +345,8 @@ def main():
     }
     if args.workload == "c4":
         out["config"]["trapped_instances"] = traps
+    if args.cost_limit:
+        out["config"]["cost_limit"] = args.cost_limit
     if args.workload == "c2":
         bytes_launch = float(c2_mem_bytes(args.iters)) * n
         achieved = bytes_launch / kernel_avg / 1e9
