@@ -218,3 +218,43 @@ def test_gpu_cost_runs_on_across_invocations(built):
             assert [int(c) for c in ctx.total_costs()] == [i.cost_sum() for i in insts]
     finally:
         ctx.close()
+
+
+METER_JIT = {
+    "blake3": (W.blake3_wasm(), "run", [I32, I32], [I32], [[5, 2], [9, 1]]),
+    "fib": CASES["fib"][:4] + ([[7], [9]],),
+    "qsort": CASES["qsort"],
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tab", [None, "random0"])
+@pytest.mark.parametrize("name", sorted(METER_JIT))
+def test_gpu_metered_compiled_runs(built, name, tab):
+    """Metered contexts run the module's compiled runs (jit.cpp prices each run at entry
+    against the limit and adds the exact price of the way it leaves): a dense limit sweep
+    so the limit falls inside, at the start and at the end of runs, calls and returns."""
+    from wasmedge_amd import batch
+    wasm, func, pt, rt, rows = METER_JIT[name]
+    table = TABLES[tab] if tab else None
+    _, full = _oracle_tab(wasm, func, rows, BIG, table)
+    total = max(full)
+    runs = 0
+    limits = sorted(set(list(range(1, total + 2, max(1, total // 60))) + [total - 1, total, total + 1]))
+    for limit in limits:
+        if limit <= 0:
+            continue
+        ref, rcost = _oracle_tab(wasm, func, rows, limit, table)
+        if any(c is None for c in rcost):
+            continue
+        ctx = batch.BatchContext(wasm, len(rows), device=0, cost_limit=limit, cost_table=table)
+        try:
+            runs = max(runs, ctx.compiled_runs())
+            rets, st, cnt = ctx.execute(func, batch.make_values(rows, pt), len(rt))
+            ints = batch.ret_ints(rets)
+            got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref, got, st, cnt, ctx.memory_hash(), rt) == [], limit
+            assert [int(c) for c in ctx.total_costs()] == rcost, limit
+        finally:
+            ctx.close()
+    assert runs > 0

@@ -142,17 +142,25 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // compiled runs (jit.h) for the V-frame core; WB_JIT=0 interprets them instead. A
   // compile failure is not fatal (the core interprets) but is kept as the last error.
   const char *jte = getenv("WB_JIT");
-  if (C->threaded && C->vframe && !C->conf.CostLimit && !(jte && jte[0] == '0')) {
+  // Metered contexts run only the compiled runs in the core (they price themselves,
+  // JitCost); every other instruction stays in the exact compiled / per-lane step.
+  if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
     const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv);
     if (!runs.empty()) {
       std::vector<uint8_t> start(P.code.size() + 1, 0);
       for (const auto &r : runs) start[r.pc] = 1;
       std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
       std::vector<uint64_t> addr;
-      const std::string src = wb::jit_source(P, runs, C->mlog);
+      const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
+      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr);
       const std::string err = src.empty() ? std::string("compiled runs: no source")
                                           : wb::jit_load(src, runs.size(), C->device, &addr);
       if (err.empty()) {
+        if (C->conf.CostLimit)   // metered: the core holds the runs and nothing else
+          for (size_t pc = 0; pc < P.code.size(); pc++) {
+            tcj[pc].w[0] = 0;
+            codepad[pc].w0 &= ~DBC_HOT;
+          }
         wb::jit_patch(tcj, runs, addr);
         for (const auto &r : runs) codepad[r.pc].w0 |= DBC_HOT;   // the core is entered there
         tcv.swap(tcj);
@@ -230,7 +238,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.funcs = C->funcs.ptr; k.table = C->table.ptr; k.global_init = C->global_init.ptr;
   k.data_pool = C->data_pool.ptr; k.data_off = C->data_off.ptr; k.data_len = C->data_len.ptr;
   // metered runs take the exact compiled step (the threaded core counts per run only)
-  k.tcode = C->threaded && !C->conf.CostLimit ? C->tcode.ptr : nullptr;
+  k.tcode = C->threaded && (!C->conf.CostLimit || C->jit_runs) ? C->tcode.ptr : nullptr;
   // gas: the instance's running total against the limit, start function included
   k.cost_limit = C->conf.CostLimit ? C->conf.CostLimit : ~0ull;
   if (C->conf.CostLimit) {

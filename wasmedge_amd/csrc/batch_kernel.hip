@@ -147,6 +147,10 @@ struct HbmFrame {
       "v_mov_b32 v99, %[msh]\n\t" \
       "v_add_u32_e32 v100, 6, v99\n\t" \
       "s_mov_b32 s93, %[slds]\n\t" \
+      "v_mov_b32 v94, %[llo]\n\t" \
+      "v_mov_b32 v95, %[lhi]\n\t" \
+      "v_mov_b32 v96, %[glo]\n\t" \
+      "v_mov_b32 v97, %[ghi]\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
       "s_mov_b32 s95, %[low]\n\t" \
       "s_getpc_b64 s[66:67]\n" \
@@ -162,15 +166,18 @@ struct HbmFrame {
       "s_mov_b32 %[cnt], s65\n\t" \
       "s_mov_b32 %[why], s92\n\t" \
       "v_mov_b32 %[gsp], v102\n\t" \
+      "v_mov_b32 %[glo], v96\n\t" \
+      "v_mov_b32 %[ghi], v97\n\t" \
       "v_mov_b32 %[hwm], v101" \
-      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm) \
+      : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm), \
+        [glo] "+v"(glo), [ghi] "+v"(ghi) \
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
-        [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw) \
+        [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
-        "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v94", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 
@@ -191,8 +198,14 @@ template <bool VF>
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other, uint32_t low,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem, uint32_t g,
                                            uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
-                                           uint32_t vsync, uint32_t *ncnt, uint32_t *reason) {
+                                           uint32_t vsync, uint64_t &gas, uint64_t gas_limit,
+                                           uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
+  // metered contexts: the lane's gas total in v[96:97] and the limit in v[94:95] for the
+  // compiled runs (jit.cpp), which price themselves; handlers never touch them
+  uint32_t glo = (uint32_t)gas, ghi = (uint32_t)(gas >> 32);
+  const uint32_t llo = __builtin_amdgcn_readfirstlane((uint32_t)gas_limit);
+  const uint32_t lhi = __builtin_amdgcn_readfirstlane((uint32_t)(gas_limit >> 32));
   const uint32_t oth = __builtin_amdgcn_readfirstlane(other >= (1u << 26) ? 0xFFFFFFFFu : other << 5);
   const uint32_t lw = __builtin_amdgcn_readfirstlane(low >= (1u << 26) ? 0xFFFFFFFFu : low << 5);
   const uint64_t m = (uint64_t)(uintptr_t)mem;
@@ -208,6 +221,7 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
   } else {
     TC_RUN_ASM("wb_tc_entry");
   }
+  gas = (uint64_t)glo | ((uint64_t)ghi << 32);
   *ncnt = cnt;
   *reason = why;
   return npc;
@@ -390,8 +404,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
+          // (metered: the run's gas so far joins the lanes' totals first, jit.cpp prices
+          // the compiled runs against the limit itself)
+          cost += scost;
+          scost = 0;
           pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
-                            (TC_VF_CELLS - p.total_cells) * 8u, &ncnt, &why);
+                            (TC_VF_CELLS - p.total_cells) * 8u, cost,
+                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why);
           asc += ncnt;
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
           I = code[pcs];

@@ -66,9 +66,11 @@ struct Em {
   uint32_t run = 0;      // run index (label suffix)
   uint32_t pc = 0;       // instruction being compiled
   uint32_t done = 0;     // wasm instructions retired before it (within the run)
+  uint64_t cdone = 0;    // their gas (metered contexts)
+  bool metered = false;
   bool pend[256] = {};   // cells with a global load in flight
   bool any = false;
-  struct Stub { std::string lab; uint32_t pc, done; };
+  struct Stub { std::string lab; uint32_t pc, done; uint64_t cdone; };
   std::vector<Stub> stubs;
   const struct MemGroup *group = nullptr;   // set on a group's first access (group_check)
   uint32_t fb = 0;                          // frame base (Program::global_cells)
@@ -112,6 +114,13 @@ struct Em {
     for (bool &b : pend) b = false;
     any = false;
   }
+  // the lanes' gas total (v[96:97]) += c
+  void gas_add(uint64_t c) {
+    if (!metered || !c) return;
+    l("s_mov_b32 s68, 0x%x", uint32_t(c));
+    l("s_mov_b32 s69, 0x%x", uint32_t(c >> 32));
+    l("v_lshl_add_u64 v[96:97], v[96:97], 0, s[68:69]");
+  }
   // a 64-bit operand as an aligned VGPR pair (gfx9 tuples start at even registers)
   const char *src64(uint32_t c, const char *lo, const char *hi, const char *pair) {
     if (!(c & 1)) return p(c);
@@ -134,7 +143,7 @@ struct Em {
     const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(stubs.size());
     l("s_and_b64 %s, %s, exec", T2, T2);
     l("s_cbranch_scc1 %s", lab.c_str());
-    stubs.push_back(Stub{lab, pc, done});
+    stubs.push_back(Stub{lab, pc, done, cdone});
     return lab;
   }
 };
@@ -808,6 +817,20 @@ bool jit_ok(const Program &P, const DInstr &I) {
   return emit(e, I);
 }
 
+}  // namespace
+
+uint64_t JitCost::full(const Program &P, uint32_t pc) const {
+  const uint32_t cnt = (P.code[pc].w0 >> 16) & 0xFFu;
+  return cnt ? (*pool)[(*off)[pc] + cnt - 1] : 0;
+}
+
+int64_t JitCost::taken(uint32_t to, int32_t jtc) const {
+  if (jtc < 0) return -int64_t((*pool)[(*off)[to] + uint32_t(-jtc) - 1u]);
+  return int64_t(c_else) * jtc;
+}
+
+namespace {
+
 bool is_xfer(uint16_t op) { return op == OP_CALL || op == OP_RET; }
 bool is_branch_op(uint16_t op) {
   return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
@@ -866,7 +889,8 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
   return runs;
 }
 
-std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog) {
+std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
+                       const JitCost *cost) {
   const char *se = getenv("WB_JIT_SCHED");   // 0: keep program order (A/B measurement aid)
   const bool sched = !(se && se[0] == '0');
   std::string src =
@@ -908,6 +932,23 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
       e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
     }
+    // metered: the price of each way out, and the entry check against the dearest
+    uint64_t c_fall = 0;
+    int64_t c_adj = 0;
+    if (cost) {
+      e.metered = true;
+      for (uint32_t i = 0; i < r.len; i++) c_fall += cost->full(P, r.pc + i);
+      if (is_branch_op(lop)) c_adj = cost->taken(tgt, int32_t(int16_t(last.w2 >> 16)));
+      const uint64_t c_max = c_adj > 0 ? c_fall + uint64_t(c_adj) : c_fall;
+      e.pc = r.pc;
+      e.l("s_mov_b32 s68, 0x%x", uint32_t(c_max));
+      e.l("s_mov_b32 s69, 0x%x", uint32_t(c_max >> 32));
+      e.l("v_lshl_add_u64 %s, v[96:97], 0, s[68:69]", XP);
+      e.l("v_cmp_gt_u64_e64 %s, %s, v[94:95]", T2, XP);   // past the limit
+      e.l("v_cmp_lt_u64_e32 vcc, %s, v[96:97]", XP);      // or wrapped
+      e.l("s_or_b64 %s, %s, vcc", T2, T2);
+      e.leave_if_t2();
+    }
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
     const size_t body_at = e.o.size();
@@ -919,6 +960,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
       if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
+      if (cost) e.cdone += cost->full(P, r.pc + i);
     }
     e.drain();
     if (sched) e.o = e.o.substr(0, body_at) + schedule(e.o.substr(body_at));
@@ -960,6 +1002,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_cbranch_scc1 %s", xs.c_str());
     };
     auto fallthrough = [&](uint32_t cnt) {   // next(): stop at the lowest waiting pc
+      e.gas_add(c_fall);
       e.l("s_mov_b32 s62, 0x%x", fall * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", cnt);
       e.l("s_cmp_ge_u32 s62, s63");
@@ -968,12 +1011,14 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     };
     if (lop == OP_CALL) {
       emit_call(e, last, e.pc);
+      e.gas_add(c_fall);
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       taken_checks();
       go(tgt, preload);
     } else if (lop == OP_RET) {
       emit_ret(e, last);
+      e.gas_add(c_fall);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       taken_checks();
       go(~0u, false);
@@ -988,9 +1033,10 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
         e.l("s_cmp_eq_u64 %s, exec", T2);
         const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
-        e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done});
+        e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done, e.cdone});
         e.l("s_cbranch_scc0 %s", lab_split.c_str());   // lanes disagree: the C++ step splits
       }
+      e.gas_add(uint64_t(int64_t(c_fall) + c_adj));
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", taken_cnt);
       taken_checks();
@@ -1009,6 +1055,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.l("s_setpc_b64 s[68:69]");
     for (const auto &s : e.stubs) {   // leave before instruction s.pc
       e.l("%s:", s.lab.c_str());
+      e.gas_add(s.cdone);
       e.l("s_mov_b32 s62, 0x%x", s.pc * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", s.done);
       e.l("s_setpc_b64 s[70:71]");

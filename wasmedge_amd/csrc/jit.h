@@ -33,10 +33,24 @@ struct JitRun {
 // (an instruction without a handler there is never compiled).
 std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc);
 
+// Gas prices of a metered context (batch_ctx.h cost_off_h / cost_pool_h): per DBC
+// instruction its cost list's prefix sums. A compiled run checks at entry that every lane
+// can pay its most expensive exit (else it leaves to the exact per-lane step) and adds
+// the exact price of the exit it takes (the same sums as gas_step / gas_tail).
+struct JitCost {
+  const std::vector<uint32_t> *off;
+  const std::vector<uint64_t> *pool;
+  uint64_t c_else;   // price of an `else` a taken if-false branch retires
+  uint64_t full(const Program &P, uint32_t pc) const;
+  // a taken branch's correction (tcnt = jtc) landing at pc `to`
+  int64_t taken(uint32_t to, int32_t jtc) const;
+};
+
 // The hiprtc source: one kernel, wbjit_addrs(uint64_t *out), that writes the address of
 // run k's code to out[k]; the runs' code sits inside it behind branches. glog: linear-
-// memory granule = 4 << glog bytes (batch_ctx.h lane_word).
-std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog);
+// memory granule = 4 << glog bytes (batch_ctx.h lane_word). cost: metered contexts.
+std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
+                       const JitCost *cost = nullptr);
 
 // Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
 std::string jit_compile(const std::string &src, std::vector<char> *code);
