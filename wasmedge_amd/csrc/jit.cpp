@@ -74,6 +74,7 @@ struct Em {
   std::vector<Stub> stubs;
   const struct MemGroup *group = nullptr;   // set on a group's first access (group_check)
   uint32_t fb = 0;                          // frame base (Program::global_cells)
+  const Program *prog = nullptr;
 
   void l(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
     char buf[256];
@@ -136,6 +137,22 @@ struct Em {
       l("v_mov_b32 %s, %s", v(c), R0);
       l("v_mov_b32 %s, %s", v(c + 1), R1);
     }
+  }
+  // cells c..c+3 = the four registers (results computed into temporaries first)
+  void put128(uint32_t c, const char *const r[4]) {
+    for (int k = 0; k < 4; k++) l("v_mov_b32 %s, %s", v(c + k), r[k]);
+  }
+  // leave before this instruction when any active lane's result is a NaN: the handlers'
+  // rule (gen_tc.py nan_exit); the C++ step then produces the reference's payload.
+  // regs: result registers or pairs, w: 32 / 64
+  void nan_leave(std::initializer_list<const char *> regs, int w) {
+    bool first = true;
+    for (const char *r : regs) {
+      l("v_cmp_u_f%d_e64 %s, %s, %s", w, first ? T2 : "vcc", r, r);
+      if (!first) l("s_or_b64 %s, %s, vcc", T2, T2);
+      first = false;
+    }
+    leave_if_t2();
   }
   // leave before instruction pc (the C++ step executes it) when any active lane's T2 bit
   // is set
@@ -340,6 +357,206 @@ bool emit(Em &e, const DInstr &I) {
   switch (op) {
     case OP_NOP_CNT:
       return true;
+    // ---- floating point (results exact IEEE; a NaN result leaves to the C++ step)
+    case OP_F32_ADD: case OP_F32_SUB: case OP_F32_MUL: {
+      e.sync({a, b, c});
+      const char *ins = op == OP_F32_MUL ? "v_mul_f32_e32" : op == OP_F32_SUB ? "v_sub_f32_e32" : "v_add_f32_e32";
+      e.l("%s %s, %s, %s", ins, R0, e.v(a), e.v(b));
+      e.nan_leave({R0}, 32);
+      e.l("v_mov_b32 %s, %s", e.v(c), R0);
+      return true;
+    }
+    case OP_F64_ADD: case OP_F64_SUB: case OP_F64_MUL: {
+      e.sync({a, a + 1, b, b + 1, c, c + 1});
+      const char *x = e.src64(a, A0, A1, AP), *y = e.src64(b, B0, B1, BP);
+      if (op == OP_F64_MUL) e.l("v_mul_f64 %s, %s, %s", RP, x, y);
+      else e.l("v_add_f64 %s, %s, %s%s", RP, x, op == OP_F64_SUB ? "-" : "", y);
+      e.nan_leave({RP}, 64);
+      e.put64(c);
+      return true;
+    }
+    case OP_F32_EQ: case OP_F32_NE: case OP_F32_LT: case OP_F32_GT: case OP_F32_LE: case OP_F32_GE: {
+      static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
+      e.sync({a, b, c});
+      e.l("v_cmp_%s_f32_e32 vcc, %s, %s", k[op - OP_F32_EQ], e.v(a), e.v(b));
+      e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+      return true;
+    }
+    case OP_F64_EQ: case OP_F64_NE: case OP_F64_LT: case OP_F64_GT: case OP_F64_LE: case OP_F64_GE: {
+      static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
+      e.sync({a, a + 1, b, b + 1, c});
+      const char *x = e.src64(a, A0, A1, AP), *y = e.src64(b, B0, B1, BP);
+      e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_F64_EQ], x, y);
+      e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+      return true;
+    }
+    case OP_F32_ABS: case OP_F32_NEG:
+      e.sync({a, c});
+      e.l("%s %s, 0x%x, %s", op == OP_F32_ABS ? "v_and_b32_e32" : "v_xor_b32_e32", e.v(c),
+          op == OP_F32_ABS ? 0x7FFFFFFFu : 0x80000000u, e.v(a));
+      return true;
+    case OP_F64_ABS: case OP_F64_NEG:
+      e.sync({a, a + 1, c, c + 1});
+      e.l("%s %s, 0x%x, %s", op == OP_F64_ABS ? "v_and_b32_e32" : "v_xor_b32_e32", R1,
+          op == OP_F64_ABS ? 0x7FFFFFFFu : 0x80000000u, e.v(a + 1));
+      e.l("v_mov_b32 %s, %s", R0, e.v(a));
+      e.put64(c);
+      return true;
+    case OP_F32_COPYSIGN:
+      e.sync({a, b, c});
+      e.l("s_mov_b32 s68, 0x7fffffff");
+      e.l("v_bfi_b32 %s, s68, %s, %s", e.v(c), e.v(a), e.v(b));
+      return true;
+    case OP_F64_COPYSIGN:
+      e.sync({a, a + 1, b, b + 1, c, c + 1});
+      e.l("s_mov_b32 s68, 0x7fffffff");
+      e.l("v_bfi_b32 %s, s68, %s, %s", R1, e.v(a + 1), e.v(b + 1));
+      e.l("v_mov_b32 %s, %s", R0, e.v(a));
+      e.put64(c);
+      return true;
+    case OP_F64_CONVERT_I32_S: case OP_F64_CONVERT_I32_U:
+      e.sync({a, c, c + 1});
+      e.l("%s %s, %s", op == OP_F64_CONVERT_I32_S ? "v_cvt_f64_i32_e32" : "v_cvt_f64_u32_e32", RP, e.v(a));
+      e.put64(c);
+      return true;
+    case OP_F32_CONVERT_I32_S: case OP_F32_CONVERT_I32_U:
+      e.sync({a, c});
+      e.l("%s %s, %s", op == OP_F32_CONVERT_I32_S ? "v_cvt_f32_i32_e32" : "v_cvt_f32_u32_e32", e.v(c), e.v(a));
+      return true;
+    // ---- SIMD128 (4 cells; results through temporaries R0 R1 Z0 Z1)
+    case OP_MOV128: case OP_CONST128: case OP_V_I32X4_SPLAT: case OP_V_F32X4_SPLAT:
+    case OP_V_I64X2_SPLAT: case OP_V_F64X2_SPLAT: {
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      if (op == OP_CONST128) {
+        if (!e.prog || uint64_t(imm) * 4 + 4 > e.prog->vconst.size()) return false;
+        e.sync({c, c + 1, c + 2, c + 3});
+        for (int k = 0; k < 4; k++) e.l("v_mov_b32 %s, 0x%x", e.v(c + k), e.prog->vconst[imm * 4 + k]);
+        return true;
+      }
+      e.sync({a, a + 1, a + 2, a + 3, c, c + 1, c + 2, c + 3});
+      for (int k = 0; k < 4; k++) {
+        const uint32_t src = op == OP_MOV128 ? a + k
+                             : (op == OP_V_I32X4_SPLAT || op == OP_V_F32X4_SPLAT) ? a : a + (k & 1);
+        e.l("v_mov_b32 %s, %s", r[k], e.v(src));
+      }
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_AND: case OP_V_OR: case OP_V_XOR: case OP_V_I32X4_ADD: case OP_V_I32X4_SUB:
+    case OP_V_I32X4_MUL: {
+      const char *ins = op == OP_V_AND ? "v_and_b32_e32" : op == OP_V_OR ? "v_or_b32_e32"
+                        : op == OP_V_XOR ? "v_xor_b32_e32" : op == OP_V_I32X4_ADD ? "v_add_u32_e32"
+                        : op == OP_V_I32X4_SUB ? "v_sub_u32_e32" : "v_mul_lo_u32";
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_I64X2_ADD: case OP_V_I64X2_SUB: case OP_V_I64X2_EQ: {
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      for (int k = 0; k < 2; k++) {
+        const uint32_t x = a + 2 * k, y = b + 2 * k;
+        if (op == OP_V_I64X2_SUB) {
+          e.l("v_sub_co_u32_e32 %s, vcc, %s, %s", r[2 * k], e.v(x), e.v(y));
+          e.l("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc", r[2 * k + 1], e.v(x + 1), e.v(y + 1));
+        } else if (op == OP_V_I64X2_ADD) {
+          e.l("v_add_co_u32_e32 %s, vcc, %s, %s", r[2 * k], e.v(x), e.v(y));
+          e.l("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc", r[2 * k + 1], e.v(x + 1), e.v(y + 1));
+        } else {
+          const char *xx = e.src64(x, A0, A1, AP), *yy = e.src64(y, B0, B1, BP);
+          e.l("v_cmp_eq_u64_e64 vcc, %s, %s", xx, yy);
+          e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[2 * k]);
+          e.l("v_mov_b32 %s, %s", r[2 * k + 1], r[2 * k]);
+        }
+      }
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_F32X4_ADD: case OP_V_F32X4_SUB: case OP_V_F32X4_MUL: {
+      const char *ins = op == OP_V_F32X4_MUL ? "v_mul_f32_e32" : op == OP_V_F32X4_SUB ? "v_sub_f32_e32" : "v_add_f32_e32";
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
+      e.nan_leave({R0, R1, Z0, Z1}, 32);
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_F64X2_ADD: case OP_V_F64X2_SUB: case OP_V_F64X2_MUL: {
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const res[2] = {RP, ZP};
+      for (int k = 0; k < 2; k++) {
+        const char *x = e.src64(a + 2 * k, A0, A1, AP), *y = e.src64(b + 2 * k, B0, B1, BP);
+        if (op == OP_V_F64X2_MUL) e.l("v_mul_f64 %s, %s, %s", res[k], x, y);
+        else e.l("v_add_f64 %s, %s, %s%s", res[k], x, op == OP_V_F64X2_SUB ? "-" : "", y);
+      }
+      e.nan_leave({RP, ZP}, 64);
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_F32X4_EQ: case OP_V_F32X4_NE: case OP_V_F32X4_LT: case OP_V_F32X4_GT:
+    case OP_V_F32X4_LE: case OP_V_F32X4_GE: {
+      static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      for (int q = 0; q < 4; q++) {
+        e.l("v_cmp_%s_f32_e32 vcc, %s, %s", k[op - OP_V_F32X4_EQ], e.v(a + q), e.v(b + q));
+        e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[q]);
+      }
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_F64X2_EQ: case OP_V_F64X2_NE: case OP_V_F64X2_LT: case OP_V_F64X2_GT:
+    case OP_V_F64X2_LE: case OP_V_F64X2_GE: {
+      static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      for (int q = 0; q < 2; q++) {
+        const char *x = e.src64(a + 2 * q, A0, A1, AP), *y = e.src64(b + 2 * q, B0, B1, BP);
+        e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
+        e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[2 * q]);
+        e.l("v_mov_b32 %s, %s", r[2 * q + 1], r[2 * q]);
+      }
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_ANY_TRUE:
+      e.sync({a, a + 1, a + 2, a + 3, c});
+      e.l("v_or3_b32 %s, %s, %s, %s", R0, e.v(a), e.v(a + 1), e.v(a + 2));
+      e.l("v_or_b32_e32 %s, %s, %s", R0, R0, e.v(a + 3));
+      e.l("v_cmp_ne_u32_e32 vcc, 0, %s", R0);
+      e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
+      return true;
+    case OP_V_I32X4_BITMASK:
+      e.sync({a, a + 1, a + 2, a + 3, c});
+      e.l("v_lshrrev_b32_e32 %s, 31, %s", R0, e.v(a));
+      for (uint32_t q = 1; q < 4; q++) {
+        e.l("v_lshrrev_b32_e32 %s, 31, %s", R1, e.v(a + q));
+        e.l("v_lshl_or_b32 %s, %s, %u, %s", R0, R1, q, R0);
+      }
+      e.l("v_mov_b32 %s, %s", e.v(c), R0);
+      return true;
+    case OP_V_EXTRACT32:
+      e.sync({a + d, c});
+      if (a + d != c) e.l("v_mov_b32 %s, %s", e.v(c), e.v(a + d));
+      return true;
+    case OP_V_EXTRACT64:
+      e.sync({a + 2 * d, a + 2 * d + 1, c, c + 1});
+      e.l("v_mov_b32 %s, %s", R0, e.v(a + 2 * d));
+      e.l("v_mov_b32 %s, %s", R1, e.v(a + 2 * d + 1));
+      e.put64(c);
+      return true;
+    case OP_V_REPLACE64: {
+      if (d > 1) return false;
+      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, c, c + 1, c + 2, c + 3});
+      for (uint32_t q = 0; q < 4; q++)
+        e.l("v_mov_b32 %s, %s", r[q], e.v(q / 2 == d ? b + (q & 1) : a + q));
+      e.put128(c, r);
+      return true;
+    }
     case OP_POST_CALL: {   // gen_tc.py post_call_body_v: results fb.. -> L.., restore [fb, L)
       const uint32_t L = a, r = b, fb = e.fb;
       if (L < e.fb || uint64_t(L) + r > TC_VF_CELLS) return false;
@@ -814,6 +1031,7 @@ bool jit_ok(const Program &P, const DInstr &I) {
     if (uint64_t(I.w3) + n - 1 > 0xFFFFFFFFull) return false;
   Em e;
   e.fb = P.global_cells;
+  e.prog = &P;
   return emit(e, I);
 }
 
@@ -926,6 +1144,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const uint32_t pre = lop == OP_CALL ? tgt : fall;
     const bool preload = lop != OP_RET && lop != OP_JMP && !start.count(pre);
     e.fb = P.global_cells;
+    e.prog = &P;
     if (preload) {
       e.l("s_waitcnt lgkmcnt(0)");
       e.l("s_mov_b32 s68, 0x%x", pre * 32u);
