@@ -1118,6 +1118,21 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // run index by start pc: a transfer to one jumps straight to its code
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
+  // a return's likely targets: the instruction after each direct call of its function
+  // (functions are laid out in order of entry pc)
+  std::map<uint32_t, uint32_t> fentry;   // entry pc -> function index
+  for (uint32_t f = 0; f < P.funcs.size(); f++)
+    if (!P.funcs[f].imported) fentry[P.funcs[f].entry_pc] = f;
+  auto func_of = [&](uint32_t pc) -> int64_t {
+    auto it = fentry.upper_bound(pc);
+    return it == fentry.begin() ? -1 : int64_t(std::prev(it)->second);
+  };
+  std::map<uint32_t, std::vector<uint32_t>> ret_sites;   // function -> return pcs
+  for (uint32_t pc = 0; pc < P.code.size(); pc++)
+    if (op_of(P.code[pc]) == OP_CALL) {
+      const int64_t f = func_of(P.code[pc].w3);
+      if (f >= 0) ret_sites[uint32_t(f)].push_back(pc + 1);
+    }
   for (size_t k = 0; k < runs.size(); k++) {
     const JitRun &r = runs[k];
     Em e;
@@ -1240,7 +1255,21 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.gas_add(c_fall);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       taken_checks();
+      // straight into the code after a known call site of this function, else dispatch
+      std::vector<uint32_t> sites;
+      const int64_t f = func_of(e.pc);
+      if (f >= 0)
+        for (uint32_t rs : ret_sites[uint32_t(f)])
+          if (start.count(rs) && sites.size() < 6) sites.push_back(rs);
+      for (size_t q = 0; q < sites.size(); q++) {
+        e.l("s_cmp_eq_u32 s62, 0x%x", sites[q] * 32u);
+        e.l("s_cbranch_scc1 Lrt%s_%zu", K.c_str(), q);
+      }
       go(~0u, false);
+      for (size_t q = 0; q < sites.size(); q++) {
+        e.l("Lrt%s_%zu:", K.c_str(), q);
+        go(sites[q], false);
+      }
     } else if (is_branch_op(lop)) {
       const uint32_t bcnt = (last.w0 >> 16) & 0xFFu;
       const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
