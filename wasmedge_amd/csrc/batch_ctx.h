@@ -7,6 +7,10 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
 
 #include "../../include/wasmedge_batch.h"
 #include "frontend.h"
@@ -140,11 +144,41 @@ inline size_t lane_word(uint64_t w, uint32_t lane, uint32_t g) {
   return (size_t(w >> g) << (6 + g)) + (size_t(lane) << g) + size_t(w & ((1u << g) - 1u));
 }
 
+// One service round's copy of linear-memory rows across all parked waves (hostcall.cpp):
+// row b = words [64b, 64b + 64) of every lane, 16 KiB per wave, contiguous on the device
+// in each wave's region; the first touch by ANY wave fetches the row of every wave with
+// one 2D copy, and a dirty row goes back with one 2D copy. Host functions of a SIMT batch
+// touch the same few addresses in every instance, so a round moves a few rows, not 64K
+// small pieces. Past a byte budget a row is left to the per-wave blocks of WaveView.
+struct RoundCache {
+  static constexpr uint32_t kRowWords = 64;
+  WasmEdge_BatchContext *C = nullptr;
+  uint32_t w0 = 0, nw = 0;             // waves [w0, w0 + nw)
+  size_t budget = size_t(1) << 30;     // host bytes for rows
+  struct Row {
+    std::once_flag once;
+    bool cached = false, ok = true;
+    std::atomic<bool> dirty{false};
+    std::vector<uint32_t> w;           // [nw][64 lanes * kRowWords]
+  };
+  std::mutex mu;
+  std::unordered_map<uint32_t, std::unique_ptr<Row>> rows;
+  std::atomic<size_t> used{0};
+  // the wave's part of row b (4096 words, lane-interleaved), or nullptr (not cached)
+  uint32_t *get(uint32_t b, uint32_t wave, bool *fail);
+  void mark_dirty(uint32_t b);
+  bool flush();
+};
+
 // The host's view of one wave's linear memories during a host-call service round
-// (hostcall.cpp): blocks of kBlockWords rows (256 KiB, contiguous on the device) are
-// fetched on first touch and written back once at the end of the wave, and the lanes'
-// page counts and write marks come from one copy of the instance state per round.
+// (hostcall.cpp): through the round's RoundCache when it holds the row, else blocks of
+// kBlockWords rows (256 KiB, contiguous on the device) fetched on first touch and written
+// back once at the end of the wave; the lanes' page counts and write marks come from one
+// copy of the instance state per round.
 struct WaveView {
+  RoundCache *rc = nullptr;
+  struct RowRef { uint32_t b; uint32_t *p; bool dirty; };
+  std::vector<RowRef> rows;          // this wave's rows of rc, looked up once each
   WasmEdge_BatchContext *C = nullptr;
   uint32_t wave = 0;
   const uint32_t *pages = nullptr;   // [64]

@@ -7,11 +7,12 @@
 //     one copy each;
 //   * the page counts and write marks of every lane: one strided copy each (one 256-byte
 //     row per wave);
-//   * linear memory: a host function's reads and writes go to a WaveView, which fetches
-//     a 256 KiB block (4 KiB of each of the wave's 64 lanes, contiguous in the lane-
-//     interleaved layout) the first time any lane of the wave touches it and writes the
-//     dirty blocks back once, after the wave's last lane. 64K lanes calling fd_write on
-//     the same stack page thus cost 1024 block copies, not 64K x several strided ones.
+//   * linear memory: a host function's reads and writes go through the round's
+//     RoundCache: the first touch of a 256-byte row by any lane fetches that row of every
+//     parked wave with one 2D copy (16 KiB per wave, contiguous in the lane-interleaved
+//     layout), and dirty rows go back with one 2D copy each. 64K lanes calling fd_write
+//     thus cost a handful of copies. Past the cache's byte budget (a host function that
+//     reads a lot of memory) a wave's WaveView fetches 256 KiB per-wave blocks instead.
 // Waves are served by a pool of host threads (a wave's lanes and blocks belong to one
 // thread), so host functions must be reentrant, as the reference's are under its
 // concurrent VM::execute (include/vm/vm.h:137-141).
@@ -22,6 +23,48 @@
 #include "batch_ctx.h"
 
 namespace wbh {
+
+void RoundCache::mark_dirty(uint32_t b) {
+  std::lock_guard<std::mutex> lock(mu);
+  rows[b]->dirty = true;
+}
+
+uint32_t *RoundCache::get(uint32_t b, uint32_t wave, bool *fail) {
+  if (wave < w0 || wave >= w0 + nw) return nullptr;
+  Row *r;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto &slot = rows[b];
+    if (!slot) slot.reset(new Row);
+    r = slot.get();
+  }
+  std::call_once(r->once, [&]() {
+    const size_t row = size_t(64) * kRowWords;   // words per wave
+    const size_t bytes = size_t(nw) * row * 4;
+    if (used.fetch_add(bytes) + bytes > budget) return;   // left to the per-wave blocks
+    r->w.resize(size_t(nw) * row);
+    const size_t pitch = size_t(C->mem_words) * 64 * 4;   // one wave's memories
+    const uint32_t *src = C->mem.ptr + (size_t(w0) * C->mem_words + size_t(b) * kRowWords) * 64;
+    r->ok = hipMemcpy2D(r->w.data(), row * 4, src, pitch, row * 4, nw, hipMemcpyDeviceToHost) == hipSuccess;
+    r->cached = true;
+  });
+  if (!r->cached) return nullptr;
+  if (!r->ok) { *fail = true; return nullptr; }
+  return r->w.data() + size_t(wave - w0) * 64 * kRowWords;
+}
+
+bool RoundCache::flush() {
+  bool ok = true;
+  const size_t row = size_t(64) * kRowWords, pitch = size_t(C->mem_words) * 64 * 4;
+  for (auto &e : rows) {
+    Row &r = *e.second;
+    if (!r.cached || !r.ok || !r.dirty) continue;
+    uint32_t *dst = C->mem.ptr + (size_t(w0) * C->mem_words + size_t(e.first) * kRowWords) * 64;
+    ok &= hipMemcpy2D(dst, pitch, r.w.data(), row * 4, row * 4, nw, hipMemcpyHostToDevice) == hipSuccess;
+  }
+  rows.clear();
+  return ok;
+}
 
 WaveView::Block *WaveView::block(uint32_t b) {
   for (auto &e : blocks)
@@ -43,7 +86,31 @@ uint8_t WaveView::rw(uint32_t lane, uint32_t off, uint32_t len, uint8_t *dst, co
   if (end > (uint64_t(pages[lane]) << 16)) return kMemoryOutOfBounds;   // memory.h:74-78
   uint64_t a = off;
   while (a < end) {
-    const uint32_t w = uint32_t(a >> 2), b = w / kBlockWords;
+    const uint32_t w = uint32_t(a >> 2);
+    if (rc) {   // the round's rows first
+      bool fail = false;
+      const uint32_t rb = w / RoundCache::kRowWords;
+      RowRef *ref = nullptr;
+      for (auto &x : rows)
+        if (x.b == rb) { ref = &x; break; }
+      if (!ref) {
+        rows.push_back(RowRef{rb, rc->get(rb, wave, &fail), false});
+        ref = &rows.back();
+      }
+      if (uint32_t *row = ref->p) {
+        if (src && !ref->dirty) { rc->mark_dirty(rb); ref->dirty = true; }
+        const uint64_t rend = std::min<uint64_t>(end, uint64_t(rb + 1) * RoundCache::kRowWords * 4);
+        for (; a < rend; a++) {
+          uint32_t &word = row[lane_word((a >> 2) % RoundCache::kRowWords, lane, C->mlog)];
+          const uint32_t sh = 8 * uint32_t(a & 3);
+          if (dst) *dst++ = uint8_t(word >> sh);
+          else word = (word & ~(0xFFu << sh)) | (uint32_t(*src++) << sh);
+        }
+        continue;
+      }
+      if (fail) return kRuntimeError;
+    }
+    const uint32_t b = w / kBlockWords;
     Block *blk = block(b);
     if (!blk) return kRuntimeError;
     // bytes of this block: up to the block's last word
@@ -140,14 +207,20 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
                               hipMemcpyDeviceToHost), "write marks")))
     return -1;
 
+  RoundCache rc;
+  rc.C = C;
+  rc.w0 = waves.front().first;
+  rc.nw = waves[waves.size() - 2].first - rc.w0 + 1;   // (the last entry is the sentinel)
   std::atomic<uint32_t> next{0};
   std::atomic<int64_t> resumed{0};
   std::atomic<bool> failed{false}, hwm_dirty{false};
   auto worker = [&]() {
     (void)hipSetDevice(C->device);   // the device is per host thread
     std::vector<WasmEdge_Value> args, rets;
+    int64_t mine = 0;   // lanes this thread resumes (one atomic add at the end)
     for (uint32_t k; (k = next.fetch_add(1)) + 1 < waves.size();) {
       WaveView view;
+      view.rc = P.has_mem ? &rc : nullptr;
       view.C = C;
       view.wave = waves[k].first;
       view.pages = &pages[size_t(view.wave) * 64];
@@ -181,11 +254,12 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
         for (size_t q = 0; q < t.results.size(); q++)
           for (uint32_t c = 0; c < wb::cells_of(t.results[q]); c++) cells[at++] = uint32_t(rets[q].Value >> (32 * c));
         hcall[i] = at;
-        resumed.fetch_add(1);
+        mine++;
       }
       if (!view.flush()) failed = true;
       if (view.hwm_dirty) hwm_dirty = true;
     }
+    resumed.fetch_add(mine);
   };
   uint32_t threads = C->host_threads ? C->host_threads
                                      : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
@@ -197,6 +271,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
     for (uint32_t t = 0; t < threads; t++) pool.emplace_back(worker);
     for (auto &th : pool) th.join();
   }
+  if (!rc.flush()) failed = true;
   if (failed) { C->last_error = "host-call memory view: device copy failed"; return -1; }
   if (!C->hip_ok(hipMemcpy(C->status.ptr, st.data(), n, hipMemcpyHostToDevice), "status") ||
       !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
