@@ -69,8 +69,11 @@ def _addr(r, n):
     return "(i32.and %s (i32.const %d))" % (_g32(r), 0x1FFFC), 0
 
 
-def _stmt(r):
-    k = r.randrange(15)
+def _stmt(r, calls=True):
+    k = r.randrange(16 if calls else 15)
+    if k == 15:   # a call: the callee's locals start at zero (some read before written)
+        return "(local.set $b%d (call $h (local.get $a%d) (local.get $b%d)))" % (
+            r.randrange(N64), r.randrange(N32), r.randrange(N64))
     d32, d64 = "$a%d" % r.randrange(N32), "$b%d" % r.randrange(N64)
     if k == 0:
         return "(local.set %s (i32.%s %s %s))" % (d32, r.choice(I32_BIN), _g32(r), _g32(r))
@@ -133,9 +136,20 @@ def random_module(seed, n=40):
     fold = " ".join(["(i64.xor"] * (N32 + N64 - 1))
     parts = ["(local.get $b0)"] + ["(local.get $b%d))" % i for i in range(1, N64)] + \
         ["(i64.extend_i32_u (local.get $a%d)))" % i for i in range(N32)]
+    # the callee: params $a0 $b0, locals $a1.. $b1..; its straight-line body reads some
+    # locals before writing them (zero) and writes others first
+    hbody = "\n    ".join(_stmt(r, calls=False) for _ in range(12))
+    hlocs = " ".join("(local $a%d i32)" % i for i in range(1, N32)) + " " + \
+        " ".join("(local $b%d i64)" % i for i in range(1, N64))
+    hfold = "(i64.xor (local.get $b1) (i64.xor (local.get $b0) (i64.extend_i32_u (i32.add (local.get $a0) (local.get $a1)))))"
     return assemble("""
 (module
   (memory 1)
+  (func $h (param $a0 i32) (param $b0 i64) (result i64)
+    %s
+    (local.set $a2 (i32.const 5)) (local.set $b2 (i64.const 7))
+    %s
+    %s)
   (func (export "run") (param $a0 i32) (result i64)
     %s (local $it i32)
     %s
@@ -149,7 +163,7 @@ def random_module(seed, n=40):
       (br_if $l (i32.lt_u (local.get $it) (i32.const 2))))
     %s
     %s %s))
-""" % (locs, init, body(), body(), body(), body(), body(), fold, " ".join(parts)))
+""" % (hlocs, hbody, hfold, locs, init, body(), body(), body(), body(), body(), fold, " ".join(parts)))
 
 
 SEEDS = list(range(12))

@@ -984,7 +984,49 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
 
 // CALL (gen_tc.py call_body_v): spill [fb, L) and the return record to the LDS call
 // stack, args L.. -> fb.., zero the callee's locals, jump to the callee.
-void emit_call(Em &e, const DInstr &I, uint32_t pc) {
+// Zeroing a callee local is dead when the callee's first compiled run writes it before
+// anything could read it: on every path from the body start the run's instructions come
+// first in program order (the interpreter resumes a run that leaves mid-way at the same
+// instruction), so the zero is never observed. Writes are taken only from instructions
+// whose destination is certain; any operand field that names the cell counts as a read.
+bool is_xfer(uint16_t op);
+bool is_branch_op(uint16_t op);
+std::vector<uint8_t> dead_zeros(const Program &P, const JitRun &r) {
+  std::vector<uint8_t> dead(TC_VF_CELLS, 0), seen(TC_VF_CELLS, 0);
+  for (uint32_t i = 0; i < r.len; i++) {
+    const DInstr &I = P.code[r.pc + i];
+    const uint16_t op = op_of(I);
+    const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
+    auto rd = [&](uint32_t x, uint32_t n) {
+      for (uint32_t k = 0; k < n; k++)
+        if (x + k < TC_VF_CELLS) seen[x + k] = 1;
+    };
+    rd(a, 4); rd(b, 4); rd(d, 4);
+    if (op == OP_I32_ADD3_XROTR_I) rd(I.w3 & 0xFFFFu, 1);
+    if (op == OP_ZERO_LOCALS || op == OP_POST_CALL || is_xfer(op) || is_branch_op(op)) {
+      rd(0, TC_VF_CELLS);   // (no claims past these)
+      continue;
+    }
+    uint32_t w = 0;   // certain 32-bit words written at c
+    switch (op) {
+      case OP_LD32: case OP_LD8S32: case OP_LD8U32: case OP_LD16S32: case OP_LD16U32:
+      case OP_CONST32: case OP_MOV32: case OP_I32_ADD: case OP_I32_SUB: case OP_I32_MUL:
+      case OP_I32_AND: case OP_I32_OR: case OP_I32_XOR: case OP_I32_ADD_I: case OP_I32_SUB_I:
+      case OP_I32_AND_I: case OP_I32_OR_I: case OP_I32_XOR_I: case OP_I32_SHL_I:
+      case OP_I32_SHR_U_I: case OP_I32_SHR_S_I:
+        w = 1; break;
+      case OP_CONST64: case OP_MOV64: case OP_LD64: case OP_LD32U64: case OP_LD32S64:
+        w = 2; break;
+      default: break;
+    }
+    for (uint32_t k = 0; k < w; k++)
+      if (c + k < TC_VF_CELLS && !seen[c + k]) dead[c + k] = 1;
+    rd(c, w ? w : 4);
+  }
+  return dead;
+}
+
+void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *dead) {
   const uint32_t L = I.w1 & 0xFFFFu, nargs = I.w1 >> 16, nloc = I.w2 & 0xFFFFu, fb = e.fb;
   const uint32_t n = L - fb;
   e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
@@ -997,7 +1039,8 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc) {
   e.l("v_add_u32_e32 v102, %u, v102", n + 1);
   for (uint32_t k = 0; k < nargs; k++)
     if (L != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(L + k));
-  for (uint32_t k = 0; k < nloc; k++) e.l("v_mov_b32 %s, 0", e.v(fb + nargs + k));
+  for (uint32_t k = 0; k < nloc; k++)
+    if (!dead || !(*dead)[fb + nargs + k]) e.l("v_mov_b32 %s, 0", e.v(fb + nargs + k));
 }
 
 // RET (gen_tc.py ret_body_v): pop the return record (it must agree across the lanes and
@@ -1244,7 +1287,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       go(fall, preload);
     };
     if (lop == OP_CALL) {
-      emit_call(e, last, e.pc);
+      std::vector<uint8_t> dead;
+      if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
+      emit_call(e, last, e.pc, dead.empty() ? nullptr : &dead);
       e.gas_add(c_fall);
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
