@@ -246,3 +246,12 @@ def test_gpu_blake3_compiled(built):
         ctx.close()
     got = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
     assert compare(ref, got[:512], st[:512], cnt[:512], h[:512], [I32], exact=True) == []
+
+
+def test_large_module_assembles(built):
+    """The reference's 1.7 MB Rust example compiles to ~2,000 runs spread over a code
+    object far beyond s_branch's +-128 KiB: run-to-run jumps are long jumps, and the
+    address table keeps the compile to a couple of seconds."""
+    from conftest import golden
+    n, ins = _jit_check(golden("rust_add.wasm"), 0)
+    assert n > 1000 and ins > 5000

@@ -27,6 +27,7 @@ namespace wb {
 namespace {
 
 constexpr uint32_t kMinRun = 3;   // shorter runs gain less than the entry/exit costs
+constexpr uint32_t kMaxRun = 1500;   // keeps a run's branches to its exit stubs in range
 
 const char *const PAGES = "v105", *const MEM = "v[106:107]", *const HWM = "v101";
 const char *const A0 = "v108", *const A1 = "v109", *const AP = "v[108:109]";
@@ -1130,7 +1131,7 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
     // a run ends after a call, return or branch (the run's code makes the transfer)
     size_t end = pc + 1;
     if (!ends_run(op_of(P.code[pc])))
-      while (end < n && ok[end] && !target[end]) {
+      while (end < n && ok[end] && !target[end] && end - pc < kMaxRun) {
         end++;
         if (ends_run(op_of(P.code[end - 1]))) break;
       }
@@ -1154,10 +1155,13 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
                        const JitCost *cost) {
   const char *se = getenv("WB_JIT_SCHED");   // 0: keep program order (A/B measurement aid)
   const bool sched = !(se && se[0] == '0');
-  std::string src =
-      "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
-      "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out) {\n"
-      "  unsigned lo, hi;\n";
+  // One asm statement holds every run (behind a jump) and a table of their offsets from
+  // the table itself; the kernel reads the table and writes the absolute addresses.
+  std::string body;
+  body += "s_getpc_b64 s[6:7]\nLpt:\ns_add_u32 s6, s6, Ltab - Lpt\ns_addc_u32 s7, s7, 0\n"
+          "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
+          "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
+          "s_setpc_b64 s[8:9]\n";
   // run index by start pc: a transfer to one jumps straight to its code
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
@@ -1182,13 +1186,6 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.g = glog;
     e.run = uint32_t(k);
     const std::string K = std::to_string(k);
-    e.l("s_getpc_b64 s[6:7]");
-    e.l("Lp%s:", K.c_str());
-    e.l("s_add_u32 s6, s6, Lb%s - Lp%s", K.c_str(), K.c_str());
-    e.l("s_addc_u32 s7, s7, 0");
-    e.l("s_mov_b32 %%0, s6");
-    e.l("s_mov_b32 %%1, s7");
-    e.l("s_branch Le%s", K.c_str());
     e.l(".p2align 6");
     e.l("Lb%s:", K.c_str());
     const DInstr &last = P.code[r.pc + r.len - 1];
@@ -1254,7 +1251,13 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("s_add_u32 s68, s62, 0x%x", (runs[it->second].len - 1) * 32u);
         e.l("s_cmp_ge_u32 s68, s63");
         e.l("s_cbranch_scc1 %s", disp.c_str());
-        e.l("s_branch Lb%zu", it->second);
+        // (a long jump: the code object can outgrow s_branch's +-128 KiB)
+        const std::string q = "Lq" + K + "_" + std::to_string(lab);
+        e.l("s_getpc_b64 s[68:69]");
+        e.l("%s:", q.c_str());
+        e.l("s_add_u32 s68, s68, Lb%zu - %s", it->second, q.c_str());
+        e.l("s_addc_u32 s69, s69, (Lb%zu - %s) >> 32", it->second, q.c_str());
+        e.l("s_setpc_b64 s[68:69]");
         e.l("%s:", disp.c_str());
         banks = false;
       }
@@ -1353,18 +1356,26 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_add_u32 s65, s65, 0x%x", s.done);
       e.l("s_setpc_b64 s[70:71]");
     }
-    e.l("Le%s:", K.c_str());
-    src += "  asm volatile(\n";
-    size_t at = 0;
-    while (at < e.o.size()) {
-      const size_t nl = e.o.find('\n', at);
-      src += "      \"" + e.o.substr(at, nl - at) + "\\n\"\n";
-      at = nl + 1;
-    }
-    src += "      : \"=s\"(lo), \"=s\"(hi) : : \"s6\", \"s7\", \"scc\");\n";
-    src += "  if (threadIdx.x == 0) out[" + K + "] = ((unsigned long long)hi << 32) | lo;\n";
+    body += e.o;
   }
-  src += "}\n";
+  body += ".p2align 3\nLtab:\n";
+  for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
+  body += "Lend:\n";
+  std::string src =
+      "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
+      "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out, unsigned n) {\n"
+      "  unsigned lo, hi;\n"
+      "  asm volatile(\n";
+  for (size_t at = 0; at < body.size();) {
+    const size_t nl = body.find('\n', at);
+    src += "      \"" + body.substr(at, nl - at) + "\\n\"\n";
+    at = nl + 1;
+  }
+  src += "      : \"=s\"(lo), \"=s\"(hi) : : \"s6\", \"s7\", \"s8\", \"s9\", \"scc\", \"memory\");\n"
+         "  const long long *tab = (const long long *)(((unsigned long long)hi << 32) | lo);\n"
+         "  for (unsigned k = threadIdx.x; k < n; k += blockDim.x)\n"
+         "    out[k] = (unsigned long long)tab + (unsigned long long)tab[k];\n"
+         "}\n";
   return src;
 }
 
@@ -1406,7 +1417,8 @@ std::string jit_load(const std::string &src, size_t nruns, int device, std::vect
   if (hipModuleGetFunction(&fn, mod, "wbjit_addrs") != hipSuccess) return "hipModuleGetFunction failed";
   uint64_t *dout = nullptr;
   if (hipMalloc(&dout, std::max<size_t>(1, nruns) * 8) != hipSuccess) return "hipMalloc failed";
-  void *args[] = {&dout};
+  unsigned nr = unsigned(nruns);
+  void *args[] = {&dout, &nr};
   std::vector<uint64_t> a(nruns, 0);
   const bool ok = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) == hipSuccess &&
                   hipDeviceSynchronize() == hipSuccess &&
