@@ -151,8 +151,6 @@ struct HbmFrame {
       "v_mov_b32 v95, %[lhi]\n\t" \
       "v_mov_b32 v96, %[glo]\n\t" \
       "v_mov_b32 v97, %[ghi]\n\t" \
-      "v_mov_b32 v92, -1\n\t" \
-      "v_mov_b32 v93, 0\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
       "s_mov_b32 s95, %[low]\n\t" \
       "s_getpc_b64 s[66:67]\n" \
@@ -169,19 +167,17 @@ struct HbmFrame {
       "s_mov_b32 %[why], s92\n\t" \
       "v_mov_b32 %[gsp], v102\n\t" \
       "v_mov_b32 %[glo], v96\n\t" \
-      "v_mov_b32 %[park], v92\n\t" \
-      "v_mov_b32 %[cbase], v93\n\t" \
       "v_mov_b32 %[ghi], v97\n\t" \
       "v_mov_b32 %[hwm], v101" \
       : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm), \
-        [glo] "+v"(glo), [ghi] "+v"(ghi), [park] "=v"(park), [cbase] "=v"(cbase) \
+        [glo] "+v"(glo), [ghi] "+v"(ghi) \
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
-        "s96", "s97", "v92", "v93", "v94", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v94", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 
@@ -203,7 +199,6 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
                                            uint32_t fr, uint32_t pages, const uint32_t *mem, uint32_t g,
                                            uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint64_t &gas, uint64_t gas_limit,
-                                           uint32_t &park, uint32_t &cbase,
                                            uint32_t *ncnt, uint32_t *reason) {
   uint32_t npc, cnt, why;
   // metered contexts: the lane's gas total in v[96:97] and the limit in v[94:95] for the
@@ -402,8 +397,6 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       int32_t xadj = 0;
       uint64_t scost = 0;   // gas of the run so far (metered runs; wave-uniform)
       uint64_t asc = 0;     // instructions retired inside the threaded core
-      uint32_t ppc = 0xFFFFFFFFu, park, cbase;   // a lane parked inside the core: its pc
-      int64_t padj = 0;                          // and its count correction
       w4 I = code[pcs];
       for (;;) {
         if (p.tcode && (I.x & DBC_HOT)) {
@@ -417,17 +410,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           scost = 0;
           pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, cost,
-                            p.cost_off ? p.cost_limit : ~0ull, park, cbase, &ncnt, &why);
+                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why);
           asc += ncnt;
-          padj += (int64_t)cbase;   // per-lane count base (compiled SIMT loops)
-          if (__ballot(park != 0xFFFFFFFFu)) {
-            // lanes a compiled loop parked at its exit wait at their own pc (their count
-            // frozen at cbase): the run ends; the others stand at pcs, which the slow step
-            // executes for them when the core left for the C++ step (reason 0)
-            if (park != 0xFFFFFFFFu) { ppc = park; padj -= (int64_t)ncnt; }
-            else if (!why) slow = true;
-            xpc = pcs; tcode = 0; xadj = 0; break;
-          }
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
           I = code[pcs];
 #ifdef WB_STATS
@@ -504,10 +488,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_OP
 #undef SLOW_IF
 #undef HOST_YIELD
-      count += (uint64_t)sc + asc + (uint64_t)padj;
+      count += (uint64_t)sc + asc;
       cost += scost;
       if (tcode == 0) {
-        pc = ppc != 0xFFFFFFFFu ? ppc : xpc;
+        pc = xpc;
         count += (int64_t)xadj;
       } else if (tcode == WB_TCODE_DONE) {
         status = WB_STATUS_OK;

@@ -1141,11 +1141,7 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
       calls |= is_xfer(o) || o == OP_POST_CALL;
     }
     if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = false;   // a lone branch
-    // a loop of its own (SIMT loop: its lanes stay in the core until all leave)
-    const DInstr &lst = P.code[end - 1];
-    const bool self_loop = end - pc >= 2 && is_branch_op(op_of(lst)) && op_of(lst) != OP_JMP &&
-                           lst.w3 == pc;
-    if (end - pc >= kMinRun || calls || self_loop) {
+    if (end - pc >= kMinRun || calls) {
       uint32_t cnt = 0;
       for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
       runs.push_back(JitRun{uint32_t(pc), uint32_t(end - pc), cnt});
@@ -1210,16 +1206,6 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_load_dwordx8 s[76:83], s[60:61], s68");
       e.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
     }
-    // A SIMT loop: a run that ends in a conditional branch back to its own start. When
-    // its lanes disagree, the exiting ones park at the exit (v92 = the exit pc, v93 = their
-    // count so far, mask s[96:97]) and the rest loop on; once none loops, the parked lanes
-    // resume together at the exit with their counts in v93 (CNT restarts at 0). A run that
-    // leaves while lanes are parked hands the kernel per-lane pcs (batch_kernel.hip).
-    const bool simt = is_branch_op(lop) && lop != OP_JMP && tgt == r.pc && !cost;
-    if (simt) {
-      e.l("s_mov_b64 s[96:97], 0");
-      e.l("Ll%s:", K.c_str());
-    }
     // metered: the price of each way out, and the entry check against the dearest
     uint64_t c_fall = 0;
     int64_t c_adj = 0;
@@ -1262,8 +1248,6 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       auto it = start.find(to);
       const std::string disp = "Ld" + K + "_" + std::to_string(lab++);
       if (it != start.end()) {
-        // (a SIMT loop's back edge skips its entry's mask reset)
-        const std::string tl = (simt && to == r.pc) ? "Ll" + K : "Lb" + std::to_string(it->second);
         e.l("s_add_u32 s68, s62, 0x%x", (runs[it->second].len - 1) * 32u);
         e.l("s_cmp_ge_u32 s68, s63");
         e.l("s_cbranch_scc1 %s", disp.c_str());
@@ -1271,8 +1255,8 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         const std::string q = "Lq" + K + "_" + std::to_string(lab);
         e.l("s_getpc_b64 s[68:69]");
         e.l("%s:", q.c_str());
-        e.l("s_add_u32 s68, s68, %s - %s", tl.c_str(), q.c_str());
-        e.l("s_addc_u32 s69, s69, (%s - %s) >> 32", tl.c_str(), q.c_str());
+        e.l("s_add_u32 s68, s68, Lb%zu - %s", it->second, q.c_str());
+        e.l("s_addc_u32 s69, s69, (Lb%zu - %s) >> 32", it->second, q.c_str());
         e.l("s_setpc_b64 s[68:69]");
         e.l("%s:", disp.c_str());
         banks = false;
@@ -1339,28 +1323,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
       const uint32_t taken_cnt = uint32_t(int32_t(r.cnt) + tcnt);   // (cnt + tcnt >= 0)
       const std::string nt = "Lnt" + K;
-      const std::string res = "Lres" + K;
-      if (simt) {
-        branch_cond(e, last);
-        e.l("s_and_b64 %s, vcc, exec", T2);                 // lanes looping on
-        e.l("s_cmp_eq_u64 %s, exec", T2);
-        e.l("s_cbranch_scc1 Ltk%s", K.c_str());            // all of them
-        e.l("s_cmp_eq_u64 s[96:97], 0");
-        e.l("s_cbranch_scc0 Lsp%s", K.c_str());            // lanes parked already
-        e.l("s_cmp_eq_u64 %s, 0", T2);
-        e.l("s_cbranch_scc1 %s", nt.c_str());              // all leave, none parked
-        e.l("Lsp%s:", K.c_str());
-        e.l("s_andn2_b64 s[68:69], exec, %s", T2);          // the leaving lanes park
-        e.l("s_or_b64 s[96:97], s[96:97], s[68:69]");
-        e.l("s_mov_b64 exec, s[68:69]");
-        e.l("v_add_u32_e32 v93, s65, v93");
-        e.l("v_add_u32_e32 v93, 0x%x, v93", r.cnt);
-        e.l("v_mov_b32 v92, 0x%x", fall);
-        e.l("s_mov_b64 exec, %s", T2);
-        e.l("s_cmp_eq_u64 exec, 0");
-        e.l("s_cbranch_scc1 %s", res.c_str());             // nobody loops on
-        e.l("Ltk%s:", K.c_str());
-      } else if (lop != OP_JMP) {
+      if (lop != OP_JMP) {
         branch_cond(e, last);
         e.l("s_and_b64 %s, vcc, exec", T2);
         e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
@@ -1374,14 +1337,6 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_add_u32 s65, s65, 0x%x", taken_cnt);
       taken_checks();
       go(tgt, false);
-      if (simt) {   // every lane left: resume them all at the exit, counts in v93
-        e.l("%s:", res.c_str());
-        e.l("s_mov_b64 exec, s[96:97]");
-        e.l("v_mov_b32 v92, -1");
-        e.l("s_mov_b32 s65, 0");
-        e.l("s_mov_b64 s[96:97], 0");
-        fallthrough(0);
-      }
       if (lop != OP_JMP) {
         e.l("%s:", nt.c_str());
         (void)bcnt;
