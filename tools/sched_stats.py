@@ -18,7 +18,8 @@ _i = _src.index("#define DBC_OPS(X)")
 import re  # noqa: E402
 OPS = re.findall(r"X\((\w+)\)", _src[_i:_src.index("enum DOp", _i)])
 NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow",
-         "x_call", "x_ret", "x_post", "x_br", "x_other"]
+         "x_call", "x_ret", "x_post", "x_br", "x_other", "cyc_tc", "tc_sched"]
+NST = len(NAMES)
 
 
 def run(name, wasm, func, rows, types):
@@ -32,10 +33,10 @@ def run(name, wasm, func, rows, types):
     t = ctx.run()
     _, st, cnt = ctx.results(1)
     nw = (n + 63) // 64
-    raw = np.zeros(nw * 14 + 1024, np.uint64)
+    raw = np.zeros(nw * NST + 1024, np.uint64)
     L.wb_stats_read(ctx._h, raw.ctypes.data)
-    buf = raw[:nw * 14].reshape(nw, 14)
-    hist = raw[nw * 14:]
+    buf = raw[:nw * NST].reshape(nw, NST)
+    hist = raw[nw * NST:]
     m = buf.astype(np.float64).mean(0)
     d = dict(zip(NAMES, m))
     cyc = (d["cyc_sched"] + d["cyc_fast"] + d["cyc_slow"]) * 16
@@ -47,6 +48,8 @@ def run(name, wasm, func, rows, types):
              cyc / max(d["rounds"], 1)), flush=True)
     print("           core exits at: call=%.3e ret=%.3e post_call=%.3e branch=%.3e other=%.3e"
           % (d["x_call"], d["x_ret"], d["x_post"], d["x_br"], d["x_other"]), flush=True)
+    print("           inside the core %.0f%% of cycles; core returns for the scheduler %.3e per wave"
+          % (100 * 16 * d["cyc_tc"] / cyc, d["tc_sched"]), flush=True)
     top = np.argsort(hist)[::-1][:8]
     print("           exit ops (per wave): " + " ".join(
         "%s=%.3g" % (OPS[k] if k < len(OPS) else k, hist[k] / nw) for k in top if hist[k]), flush=True)
@@ -62,3 +65,4 @@ run("fib-uni", fib, "fib", [[22] for i in range(N)], [I32])
 run("c3-4k", W.qsort_wasm(), "sort", [[i, 4096] for i in range(N)], [I32, I32])
 run("c4", W.collatz_wasm(), "collatz", [[i, 10000] for i in range(N)], [I32, I32])
 run("c5", W.mandel_wasm(), "tile", [[i, 4096, 50] for i in range(N)], [I32, I32, I32])
+run("c5-256k", W.mandel_wasm(), "tile", [[i, 4096, 50] for i in range(4 * N)], [I32, I32, I32])

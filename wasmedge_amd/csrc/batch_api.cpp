@@ -144,6 +144,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const char *jte = getenv("WB_JIT");
   // Metered contexts run only the compiled runs in the core (they price themselves,
   // JitCost); every other instruction stays in the exact compiled / per-lane step.
+  // SIMT scheduling inside the compiled runs (KParams::simt): for modules the kernel
+  // schedules by plain min pc (the scan-loop policy lives in the kernel's scheduler), not
+  // for metered contexts; WB_SIMT=0 / 1 forces it off / on (A/B measurement aid)
+  const char *sme = getenv("WB_SIMT");
+  const bool want_simt = !C->conf.CostLimit && (sme ? sme[0] == '1' : C->sched == 0);
   if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
     const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv);
     if (!runs.empty()) {
@@ -152,7 +157,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
       std::vector<uint64_t> addr;
       const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
-      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr);
+      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt);
       const std::string err = src.empty() ? std::string("compiled runs: no source")
                                           : wb::jit_load(src, runs.size(), C->device, &addr);
       if (err.empty()) {
@@ -165,6 +170,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
         for (const auto &r : runs) codepad[r.pc].w0 |= DBC_HOT;   // the core is entered there
         tcv.swap(tcj);
         C->jit_runs = uint32_t(runs.size());
+        C->simt = want_simt;
       } else {
         C->last_error = err;
       }
@@ -220,7 +226,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
 #ifdef WB_STATS
-  if (!C->hip_ok(hipMalloc(&C->stats, (nw * 14 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
+  if (!C->hip_ok(hipMalloc(&C->stats, (nw * 16 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
 #endif
   if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
   return 0;
@@ -282,9 +288,10 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.max_ticks = uint64_t(tl * 1e8);
   k.sched = C->sched;
   k.loops = C->loops.ptr;
+  k.simt = C->simt && k.tcode ? 1u : 0u;
   k.stats = C->stats;
 #ifdef WB_STATS
-  (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 14 + 1024) * sizeof(uint64_t), C->stream);
+  (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 16 + 1024) * sizeof(uint64_t), C->stream);
 #endif
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
   size_t wave_lds = size_t((C->frame_hbm ? 0 : k.total_cells) + k.gs_lds) * 64 * 4;
@@ -738,11 +745,11 @@ const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
 }
 
 #ifdef WB_STATS
-// profiling builds only: per-wave counters of the last launch, [waves][14] (batch_kernel.hip)
+// profiling builds only: per-wave counters of the last launch, [waves][16] (batch_kernel.hip)
 __attribute__((visibility("default"))) uint32_t wb_stats_read(WasmEdge_BatchContext *C,
                                                               uint64_t *out) {
   if (!C || !C->stats) return 0;
-  (void)hipMemcpy(out, C->stats, (size_t(C->nwaves) * 14 + 1024) * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out, C->stats, (size_t(C->nwaves) * 16 + 1024) * sizeof(uint64_t), hipMemcpyDeviceToHost);
   return C->nwaves;
 }
 #endif

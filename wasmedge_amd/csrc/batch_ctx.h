@@ -81,6 +81,7 @@ struct WasmEdge_BatchContext {
   bool threaded = true;
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
   uint32_t jit_runs = 0;          // compiled straight-line runs (jit.h)
+  bool simt = false;              // KParams::simt: the compiled runs schedule diverged lanes
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
   DevBuf<uint32_t> hframe;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)

@@ -90,7 +90,8 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // entries, compiled-step dispatches, slow steps, and shader cycles per phase.
 #ifdef WB_STATS
 enum { ST_ROUNDS, ST_FAST, ST_LANES, ST_TC, ST_CPP, ST_SLOW, ST_CYC_SCHED, ST_CYC_FAST,
-       ST_CYC_SLOW, ST_X_CALL, ST_X_RET, ST_X_POST, ST_X_BR, ST_X_OTHER, ST_N };
+       ST_CYC_SLOW, ST_X_CALL, ST_X_RET, ST_X_POST, ST_X_BR, ST_X_OTHER, ST_CYC_TC, ST_TC_SCHED,
+       ST_N };
 // one relaxed atomic add per event from the first active lane (also inside divergent
 // regions, where a per-wave count must be taken once); cycles in units of 16 clocks
 #define WB_STAT_ADD(k, v)                                                              \
@@ -181,8 +182,78 @@ struct HbmFrame {
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 
-// VF: the V-frame core (wb_vf_entry): it loads the frame into v128.. on entry and stores
-// it back on exit (vsync = (TC_VF_CELLS - frame cells) * 8, gen_tc.py VSYNC).
+// VF: the V-frame core (wb_vf_entry): it loads the frames of the lanes in ALL (s[96:97])
+// into v128.. on entry, runs the group in s[74:75], and stores the frames back on exit
+// (vsync = (TC_VF_CELLS - frame cells) * 8, gen_tc.py VSYNC). It returns the group that
+// left in s[74:75] and, for every lane in ALL, its pc (v92) and the wasm instructions it
+// retired (v93): in SIMT mode (KParams::simt) the compiled runs schedule the lanes among
+// themselves (jit.cpp Lsched), otherwise ALL = the group = EXEC throughout. The caller's
+// EXEC (`ex`) is restored at the end.
+#define TC_RUN_VF_ASM(...) \
+  asm volatile( \
+      "s_mov_b32 s60, %[clo]\n\t" \
+      "s_mov_b32 s61, %[chi]\n\t" \
+      "s_lshl_b32 s62, %[pc], 5\n\t" \
+      "s_mov_b32 s63, %[oth]\n\t" \
+      "s_mov_b32 s64, %[lim]\n\t" \
+      "s_mov_b32 s65, 0\n\t" \
+      "s_mov_b64 s[96:97], %[all]\n\t" \
+      "s_mov_b64 s[74:75], %[grp]\n\t" \
+      "v_mov_b32 v104, %[fr]\n\t" \
+      "v_mov_b32 v105, %[pages]\n\t" \
+      "v_mov_b32 v106, %[mlo]\n\t" \
+      "v_mov_b32 v107, %[mhi]\n\t" \
+      "v_mov_b32 v102, %[gsp]\n\t" \
+      "v_mov_b32 v101, %[hwm]\n\t" \
+      "v_mov_b32 v103, %[stk]\n\t" \
+      "v_mov_b32 v99, %[msh]\n\t" \
+      "v_add_u32_e32 v100, 6, v99\n\t" \
+      "v_mov_b32 v92, %[vpc]\n\t" \
+      "v_mov_b32 v93, 0\n\t" \
+      "s_mov_b32 s93, %[slds]\n\t" \
+      "v_mov_b32 v94, %[llo]\n\t" \
+      "v_mov_b32 v95, %[lhi]\n\t" \
+      "v_mov_b32 v96, %[glo]\n\t" \
+      "v_mov_b32 v97, %[ghi]\n\t" \
+      "s_mov_b32 s94, %[vsync]\n\t" \
+      "s_mov_b32 s95, %[low]\n\t" \
+      "s_mov_b64 exec, s[96:97]\n\t" \
+      "s_getpc_b64 s[66:67]\n" \
+      "Ltc_ret_%=:\n\t" \
+      "s_add_u32 s66, s66, Ltc_back_%= - Ltc_ret_%=\n\t" \
+      "s_addc_u32 s67, s67, 0\n\t" \
+      "s_getpc_b64 s[68:69]\n\t" \
+      "s_add_u32 s68, s68, wb_vf_entry@rel32@lo+4\n\t" \
+      "s_addc_u32 s69, s69, wb_vf_entry@rel32@hi+12\n\t" \
+      "s_setpc_b64 s[68:69]\n" \
+      "Ltc_back_%=:\n\t" \
+      "s_lshr_b32 %[npc], s62, 5\n\t" \
+      "s_mov_b32 %[cnt], s65\n\t" \
+      "s_mov_b32 %[why], s92\n\t" \
+      "s_mov_b32 %[noth], s63\n\t" \
+      "s_mov_b32 %[nlow], s95\n\t" \
+      "s_mov_b64 %[ngrp], s[74:75]\n\t" \
+      "v_mov_b32 %[gsp], v102\n\t" \
+      "v_mov_b32 %[glo], v96\n\t" \
+      "v_mov_b32 %[ghi], v97\n\t" \
+      "v_mov_b32 %[vpc], v92\n\t" \
+      "v_mov_b32 %[vcnt], v93\n\t" \
+      "v_mov_b32 %[hwm], v101\n\t" \
+      "s_mov_b64 exec, %[ex]" \
+      /* (early-clobber outputs: they are written before `ex` is read) */ \
+      : [npc] "=&s"(npc), [cnt] "=&s"(cnt), [why] "=&s"(why), [noth] "=&s"(noth), [nlow] "=&s"(nlow), \
+        [ngrp] "=&s"(ngrp), [gsp] "+v"(gsp), [hwm] "+v"(hwm), [glo] "+v"(glo), [ghi] "+v"(ghi), \
+        [vpc] "+v"(vpc), [vcnt] "=&v"(vcnt) \
+      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
+        [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
+        [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi), \
+        [all] "s"(all), [grp] "s"(grp), [ex] "s"(ex) \
+      : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
+        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
+        "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", \
+        "v92", "v93", "v94", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
+        "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 #define TC_VREGS "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", \
   "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", \
   "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", \
@@ -194,12 +265,19 @@ struct HbmFrame {
   "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", \
   "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", \
   "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255"
+// What a SIMT-mode core call (VF) hands back besides the group's pc: the group, its
+// stop pcs, and for every lane in ALL its pc and retired instructions.
+struct SimtOut {
+  uint64_t grp;
+  uint32_t oth, low, vpc, vcnt;
+};
 template <bool VF>
 __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint32_t other, uint32_t low,
                                            uint32_t fr, uint32_t pages, const uint32_t *mem, uint32_t g,
                                            uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint64_t &gas, uint64_t gas_limit,
-                                           uint32_t *ncnt, uint32_t *reason) {
+                                           uint32_t *ncnt, uint32_t *reason, SimtOut *so = nullptr,
+                                           uint64_t all = 0, uint64_t grp = 0, uint32_t vpc = 0) {
   uint32_t npc, cnt, why;
   // metered contexts: the lane's gas total in v[96:97] and the limit in v[94:95] for the
   // compiled runs (jit.cpp), which price themselves; handlers never touch them
@@ -217,7 +295,13 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
   // compiler's divergence analysis cannot prove it (profiling builds)
   pc = __builtin_amdgcn_readfirstlane(pc);
   if constexpr (VF) {
-    TC_RUN_ASM("wb_vf_entry", TC_VREGS);
+    // (the caller's EXEC; without SIMT the core runs exactly it: ALL = the group = EXEC)
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if (!so) all = grp = ex;
+    uint32_t noth, nlow, vcnt;
+    uint64_t ngrp;
+    TC_RUN_VF_ASM(TC_VREGS);
+    if (so) *so = SimtOut{ngrp, noth, nlow, vpc, vcnt};
   } else {
     TC_RUN_ASM("wb_tc_entry");
   }
@@ -357,6 +441,37 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       }
     }
     bool slow = false;   // the run stopped at an instruction that needs the slow step
+    bool first = false;  // SIMT: the core left the group before a HOT instruction
+    if constexpr (VF) {
+      if (p.simt && (code[pcs].x & DBC_HOT)) {
+        // SIMT mode: every running lane enters the core (EXEC is the whole wave here);
+        // the compiled runs pick groups themselves and hand back each lane's pc and
+        // retired instructions, and the group (if any) whose next instruction the C++
+        // step must execute (reason 0)
+        WB_STAT_ADD(ST_TC, 1);
+        [[maybe_unused]] const uint64_t tt0 = WB_NOW();
+        SimtOut so;
+        uint32_t ncnt, why;
+        const uint32_t gpc = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm,
+                                        stk_lds, S_lds, (TC_VF_CELLS - p.total_cells) * 8u, cost, ~0ull,
+                                        &ncnt, &why, &so, runmask, act, pc);
+        WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
+        if (status == WB_STATUS_RUNNING) {
+          pc = so.vpc;
+          count += so.vcnt;
+        }
+        if (why) {   // the core's budget is spent: nothing for the C++ step this round
+          WB_STAT_ADD(ST_TC_SCHED, 1);
+          act = 0;
+        } else {
+          act = so.grp;
+          pcs = gpc;
+          other = so.oth == 0xFFFFFFFFu ? 0xFFFFFFFFu : so.oth >> 5;
+          low = so.low == 0xFFFFFFFFu ? 0xFFFFFFFFu : so.low >> 5;
+          first = true;
+        }
+      }
+    }
     [[maybe_unused]] const uint64_t ts1 = WB_NOW();
     WB_STAT_ADD(ST_CYC_SCHED, ts1 - ts0);
     WB_STAT_ADD(ST_FAST, 1);
@@ -399,11 +514,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       uint64_t asc = 0;     // instructions retired inside the threaded core
       w4 I = code[pcs];
       for (;;) {
-        if (p.tcode && (I.x & DBC_HOT)) {
+        if (!(VF && p.simt) && p.tcode && (I.x & DBC_HOT)) {
           // hand the run to the threaded core; it returns at an instruction this
           // C++ step must execute (reason 0), or for the scheduler (reason 1)
           uint32_t ncnt, why;
           WB_STAT_ADD(ST_TC, 1);
+          [[maybe_unused]] const uint64_t tt0 = WB_NOW();
           // (metered: the run's gas so far joins the lanes' totals first, jit.cpp prices
           // the compiled runs against the limit itself)
           cost += scost;
@@ -412,6 +528,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
                             (TC_VF_CELLS - p.total_cells) * 8u, cost,
                             p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why);
           asc += ncnt;
+          WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
+          if (why) WB_STAT_ADD(ST_TC_SCHED, 1);
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
           I = code[pcs];
 #ifdef WB_STATS
@@ -448,6 +566,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           const uint64_t need = scost + dfull;
           SLOW_IF((w0 & DBC_CTL) || need < scost || cost > p.cost_limit || p.cost_limit - cost < need);
         }
+        // SIMT: a HOT instruction goes back to the core (with every running lane), but
+        // the one the core left the group before runs here
+        if (VF && p.simt && (w0 & DBC_HOT) && !first) goto k_leave;
+        first = false;
         switch (op) {
 #include "dbc_step.inc"
         }
@@ -624,7 +746,7 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
          p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
 }
 
-extern "C" __global__ void __launch_bounds__(256) wb_exec_kernel(const KParams p) {
+extern "C" __global__ void __launch_bounds__(256, 4) wb_exec_kernel(const KParams p) {
   exec_body<false>(p);
 }
 // HBM frames: LDS holds only the waves' call-stack slots
@@ -640,7 +762,7 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KPara
                 p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
                 p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
 }
-extern "C" __global__ void __launch_bounds__(256) wb_exec_vf_kernel(const KParams p) {
+extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_kernel(const KParams p) {
   exec_body<true>(p);
 }
 

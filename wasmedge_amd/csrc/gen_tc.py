@@ -74,6 +74,14 @@ SB0 = "v103"          # LDS byte address of this lane's call-stack slot 0
 SLDS = "s93"          # call-stack slots held in LDS (the fast path stays below this)
 VSYNC = "s94"         # V frames: (VMAX - frame cells) * 8, the frame-sync jump offset
 LOW = "s95"           # lowest waiting pc * 32 (<= OTHER; a jump to or below it re-aims OTHER)
+# V frames only: the lanes in the core (ALL, their frames are in v128..) and, at entry and
+# exit, the group that runs (GROUP, = the T2 temp pair); VPC / VCNT: per-lane pc of the
+# lanes waiting in the core and per-lane wasm-instruction count not yet in CNT (SIMT mode,
+# jit.cpp Lsched; both are outputs of every core call)
+ALL = "s[96:97]"
+GROUP = T2
+VPC = "v92"
+VCNT = "v93"
 
 
 def sreg(bank, k):
@@ -1018,6 +1026,9 @@ def blob(S, names, vf):
         for i in range(VMAX - 1, -1, -1):
             e("ds_read_b32 v%d, %s offset:%d" % (VB + i, FR, i * 256))
         e("s_waitcnt lgkmcnt(0)")
+        # the frames of every lane in the core (ALL) are loaded; the group runs (SIMT
+        # mode: batch_kernel.hip tc_run, jit.cpp Lsched; otherwise GROUP = ALL = EXEC)
+        e("s_mov_b64 exec, %s" % GROUP)
         for ln in g0.dispatch("A"):
             e(ln)
     else:
@@ -1047,15 +1058,23 @@ def blob(S, names, vf):
                         for stub, why in ((g.xh(), 0), (g.xs(), 1)):
                             pcl = g.lab("so")
                             if why:   # compiled runs leave through slot 0 + JIT_XS
-                                # (the xh stub is 36 bytes; checked below)
-                                body += ["s_nop 0"] * ((JIT_XS - 36) // 4) + [
+                                # (the xh stub is 56 bytes; checked below)
+                                body += ["s_nop 0"] * ((JIT_XS - 56) // 4) + [
                                     ".if (. - %s) != %d" % (lab, JIT_XS),
                                     '.error "xs stub not at JIT_XS"', ".endif"]
+                            # the group's lanes record where they stand (VPC) and what
+                            # they retired since their last flush (VCNT), the group mask
+                            # goes out in GROUP, then every lane in the core (ALL) stores
+                            # its frame (Lvf_so_base + VSYNC: only the frame's cells)
                             body += ["%s:" % stub, "s_mov_b32 %s, %d" % (REASON, why),
                                      "s_getpc_b64 s[68:69]", "%s:" % pcl,
                                      "s_add_u32 s68, s68, Lvf_so_base - %s" % pcl,
                                      "s_addc_u32 s69, s69, 0",
                                      "s_add_u32 s68, s68, %s" % VSYNC, "s_addc_u32 s69, s69, 0",
+                                     "v_lshrrev_b32_e64 %s, 5, %s" % (VPC, PCOFF),
+                                     "v_add_u32_e32 %s, %s, %s" % (VCNT, CNT, VCNT),
+                                     "s_mov_b64 %s, exec" % GROUP,
+                                     "s_mov_b64 exec, %s" % ALL,
                                      "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_setpc_b64 s[68:69]"]
                     else:
                         body = ["%s:" % g.xh(), "s_mov_b32 %s, 0" % REASON,
@@ -1100,8 +1119,9 @@ def main():
     with open(os.path.join(HERE, "tc_slots.h"), "w") as f:
         f.write("// GENERATED by gen_tc.py -- do not edit. DBC op -> threaded-core slot.\n")
         f.write("#pragma once\n#include \"dbc.h\"\n\n")
-        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n#define TC_VF_CELLS %d\n#define TC_JIT_XS %d\n\n"
-                % (SLOT, nslots, VMAX, JIT_XS))
+        f.write("#define TC_SLOT_BYTES %d\n#define TC_NUM_SLOTS %d\n#define TC_VF_CELLS %d\n#define TC_JIT_XS %d\n"
+                "#define TC_BANK_BYTES %d   // one bank; banks CA CB DA DB follow each other\n\n"
+                % (SLOT, nslots, VMAX, JIT_XS, nslots * SLOT))
         for si, (nm, ops, body) in enumerate(S, start=1):
             if body is not None:
                 f.write("#define TC_SLOT_%s %d\n" % (nm, si))

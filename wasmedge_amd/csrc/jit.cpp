@@ -141,7 +141,29 @@ struct Em {
   }
   // cells c..c+3 = the four registers (results computed into temporaries first)
   void put128(uint32_t c, const char *const r[4]) {
-    for (int k = 0; k < 4; k++) l("v_mov_b32 %s, %s", v(c + k), r[k]);
+    for (int k = 0; k < 4; k++)
+      if (r[k] != dst[k]) l("v_mov_b32 %s, %s", v(c + k), r[k]);
+  }
+  // Result registers of a 4-cell result at c whose sources are the cell ranges in `src`
+  // ({first, count}): the cells themselves when no source overlaps them (nothing read
+  // after the first write can then see it, and a run that leaves before the instruction
+  // re-executes it from intact sources), else the temporaries R0 R1 Z0 Z1 (put128 copies
+  // them). pair64: the two 64-bit halves as aligned pairs (c even) for f64 / u64 ops.
+  std::string dst[4], dstp[2];
+  const char *const *res128(uint32_t c, std::initializer_list<std::pair<uint32_t, uint32_t>> src,
+                            bool pair64 = false) {
+    static const char *const tmp[4] = {R0, R1, Z0, Z1};
+    static thread_local const char *out[4];
+    bool direct = !(pair64 && (c & 1));
+    for (const auto &r : src)
+      if (r.first < c + 4 && c < r.first + r.second) direct = false;
+    for (int k = 0; k < 4; k++) {
+      dst[k] = direct ? V(c + k) : "";
+      out[k] = direct ? dst[k].c_str() : tmp[k];
+    }
+    dstp[0] = direct ? P(c) : RP;
+    dstp[1] = direct ? P(c + 2) : ZP;
+    return out;
   }
   // leave before this instruction when any active lane's result is a NaN: the handlers'
   // rule (gen_tc.py nan_exit); the C++ step then produces the reference's payload.
@@ -427,7 +449,6 @@ bool emit(Em &e, const DInstr &I) {
     // ---- SIMD128 (4 cells; results through temporaries R0 R1 Z0 Z1)
     case OP_MOV128: case OP_CONST128: case OP_V_I32X4_SPLAT: case OP_V_F32X4_SPLAT:
     case OP_V_I64X2_SPLAT: case OP_V_F64X2_SPLAT: {
-      const char *const r[4] = {R0, R1, Z0, Z1};
       if (op == OP_CONST128) {
         if (!e.prog || uint64_t(imm) * 4 + 4 > e.prog->vconst.size()) return false;
         e.sync({c, c + 1, c + 2, c + 3});
@@ -435,12 +456,20 @@ bool emit(Em &e, const DInstr &I) {
         return true;
       }
       e.sync({a, a + 1, a + 2, a + 3, c, c + 1, c + 2, c + 3});
+      if (op == OP_MOV128 && a == c) return true;
+      if (op != OP_MOV128 && a == c) {   // a splat in place: copy the lane into the rest
+        const uint32_t w = (op == OP_V_I32X4_SPLAT || op == OP_V_F32X4_SPLAT) ? 1 : 2;
+        for (uint32_t k = w; k < 4; k++) e.l("v_mov_b32 %s, %s", e.v(c + k), e.v(a + (k % w)));
+        return true;
+      }
+      const uint32_t na = op == OP_MOV128 ? 4 : (op == OP_V_I32X4_SPLAT || op == OP_V_F32X4_SPLAT) ? 1 : 2;
+      const char *const *rr = e.res128(c, {{a, na}});
       for (int k = 0; k < 4; k++) {
         const uint32_t src = op == OP_MOV128 ? a + k
                              : (op == OP_V_I32X4_SPLAT || op == OP_V_F32X4_SPLAT) ? a : a + (k & 1);
-        e.l("v_mov_b32 %s, %s", r[k], e.v(src));
+        e.l("v_mov_b32 %s, %s", rr[k], e.v(src));
       }
-      e.put128(c, r);
+      e.put128(c, rr);
       return true;
     }
     case OP_V_AND: case OP_V_OR: case OP_V_XOR: case OP_V_I32X4_ADD: case OP_V_I32X4_SUB:
@@ -448,15 +477,15 @@ bool emit(Em &e, const DInstr &I) {
       const char *ins = op == OP_V_AND ? "v_and_b32_e32" : op == OP_V_OR ? "v_or_b32_e32"
                         : op == OP_V_XOR ? "v_xor_b32_e32" : op == OP_V_I32X4_ADD ? "v_add_u32_e32"
                         : op == OP_V_I32X4_SUB ? "v_sub_u32_e32" : "v_mul_lo_u32";
-      const char *const r[4] = {R0, R1, Z0, Z1};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
       e.put128(c, r);
       return true;
     }
     case OP_V_I64X2_ADD: case OP_V_I64X2_SUB: case OP_V_I64X2_EQ: {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const r[4] = {R0, R1, Z0, Z1};
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int k = 0; k < 2; k++) {
         const uint32_t x = a + 2 * k, y = b + 2 * k;
         if (op == OP_V_I64X2_SUB) {
@@ -477,31 +506,31 @@ bool emit(Em &e, const DInstr &I) {
     }
     case OP_V_F32X4_ADD: case OP_V_F32X4_SUB: case OP_V_F32X4_MUL: {
       const char *ins = op == OP_V_F32X4_MUL ? "v_mul_f32_e32" : op == OP_V_F32X4_SUB ? "v_sub_f32_e32" : "v_add_f32_e32";
-      const char *const r[4] = {R0, R1, Z0, Z1};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
-      e.nan_leave({R0, R1, Z0, Z1}, 32);
+      e.nan_leave({r[0], r[1], r[2], r[3]}, 32);
       e.put128(c, r);
       return true;
     }
     case OP_V_F64X2_ADD: case OP_V_F64X2_SUB: case OP_V_F64X2_MUL: {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const res[2] = {RP, ZP};
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, true);
+      const std::string res[2] = {e.dstp[0], e.dstp[1]};
       for (int k = 0; k < 2; k++) {
         const char *x = e.src64(a + 2 * k, A0, A1, AP), *y = e.src64(b + 2 * k, B0, B1, BP);
-        if (op == OP_V_F64X2_MUL) e.l("v_mul_f64 %s, %s, %s", res[k], x, y);
-        else e.l("v_add_f64 %s, %s, %s%s", res[k], x, op == OP_V_F64X2_SUB ? "-" : "", y);
+        if (op == OP_V_F64X2_MUL) e.l("v_mul_f64 %s, %s, %s", res[k].c_str(), x, y);
+        else e.l("v_add_f64 %s, %s, %s%s", res[k].c_str(), x, op == OP_V_F64X2_SUB ? "-" : "", y);
       }
-      e.nan_leave({RP, ZP}, 64);
-      const char *const r[4] = {R0, R1, Z0, Z1};
+      e.nan_leave({res[0].c_str(), res[1].c_str()}, 64);
       e.put128(c, r);
       return true;
     }
     case OP_V_F32X4_EQ: case OP_V_F32X4_NE: case OP_V_F32X4_LT: case OP_V_F32X4_GT:
     case OP_V_F32X4_LE: case OP_V_F32X4_GE: {
       static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
-      const char *const r[4] = {R0, R1, Z0, Z1};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int q = 0; q < 4; q++) {
         e.l("v_cmp_%s_f32_e32 vcc, %s, %s", k[op - OP_V_F32X4_EQ], e.v(a + q), e.v(b + q));
         e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[q]);
@@ -512,8 +541,8 @@ bool emit(Em &e, const DInstr &I) {
     case OP_V_F64X2_EQ: case OP_V_F64X2_NE: case OP_V_F64X2_LT: case OP_V_F64X2_GT:
     case OP_V_F64X2_LE: case OP_V_F64X2_GE: {
       static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
-      const char *const r[4] = {R0, R1, Z0, Z1};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int q = 0; q < 2; q++) {
         const char *x = e.src64(a + 2 * q, A0, A1, AP), *y = e.src64(b + 2 * q, B0, B1, BP);
         e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
@@ -551,8 +580,8 @@ bool emit(Em &e, const DInstr &I) {
       return true;
     case OP_V_REPLACE64: {
       if (d > 1) return false;
-      const char *const r[4] = {R0, R1, Z0, Z1};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 2}});
       for (uint32_t q = 0; q < 4; q++)
         e.l("v_mov_b32 %s, %s", r[q], e.v(q / 2 == d ? b + (q & 1) : a + q));
       e.put128(c, r);
@@ -1046,7 +1075,9 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *
 
 // RET (gen_tc.py ret_body_v): pop the return record (it must agree across the lanes and
 // not be the entry frame's), results a.. -> fb.., jump to the return pc.
-void emit_ret(Em &e, const DInstr &I) {
+// split: (SIMT) where the lanes' return records disagree, go there (Y1 = the records);
+// else leave before the return. Returns the leave stub's label.
+std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
   const uint32_t a = I.w1 & 0xFFFFu, nres = I.w1 >> 16, fb = e.fb;
   e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
   const std::string out = e.leave_if_t2();
@@ -1058,7 +1089,7 @@ void emit_ret(Em &e, const DInstr &I) {
   e.l("s_nop 1");
   e.l("v_cmp_ne_u32_e64 %s, s68, %s", T2, Y1);
   e.l("s_and_b64 %s, %s, exec", T2, T2);
-  e.l("s_cbranch_scc1 %s", out.c_str());
+  e.l("s_cbranch_scc1 %s", split.empty() ? out.c_str() : split.c_str());
   e.l("s_and_b32 s68, s68, 0xfffff");
   e.l("s_cmp_eq_u32 s68, 0xfffff");
   e.l("s_cbranch_scc1 %s", out.c_str());
@@ -1066,6 +1097,7 @@ void emit_ret(Em &e, const DInstr &I) {
   for (uint32_t k = 0; k < nres; k++)
     if (a != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(a + k));
   e.l("s_lshl_b32 s62, s68, 5");
+  return out;
 }
 
 // can instruction I be compiled (dry run)
@@ -1151,8 +1183,119 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
   return runs;
 }
 
+// ---------------------------------------------------------------- SIMT scheduling
+// (KParams::simt) Every running lane of the wave is in the core: ALL = s[96:97], their
+// frames in v128.. . The group in EXEC runs at PCOFF; every other lane in ALL waits at its
+// own pc in VPC (v92). VCNT (v93) holds each lane's retired instructions not yet counted
+// in CNT (s65), which only the group advances. Where the group's lanes part ways (a split
+// branch or return) or it reaches OTHER (the lowest waiting pc: lanes merge there), it
+// records its lanes' pcs and counts (a "flush": CNT moves into VCNT and comes off the
+// budget LIM) and Lsched picks the next group: the lanes at the lowest pc (min-pc
+// reconvergence, as the kernel's scheduler), OTHER/LOW = the lowest pc of the rest, the
+// handler banks of the matching mode (converged C / diverged D: gen_tc.py), and
+// dispatches its TInstr. Lanes never leave the core here; the core returns to the kernel
+// (the group's next instruction in the C++ step, or LIM spent) with VPC/VCNT for all.
+const char *const VPC = "v92", *const VCNT = "v93";
+
+// CNT into VCNT for the group, off the budget LIM
+void flush(Em &e) {
+  e.l("v_add_u32_e32 %s, s65, %s", VCNT, VCNT);
+  e.l("s_sub_u32 s64, s64, s65");
+  e.l("s_cselect_b32 s64, 0, s64");
+  e.l("s_mov_b32 s65, 0");
+}
+
+// jump to label `to` from anywhere in the code object
+void long_jump(Em &e, const std::string &to, const std::string &tag) {
+  e.l("s_getpc_b64 s[68:69]");
+  e.l("%s:", tag.c_str());
+  e.l("s_add_u32 s68, s68, %s - %s", to.c_str(), tag.c_str());
+  e.l("s_addc_u32 s69, s69, (%s - %s) >> 32", to.c_str(), tag.c_str());
+  e.l("s_setpc_b64 s[68:69]");
+}
+
+// min over the lanes of `mask` (an SGPR pair) of VPC into SGPR `dst` (~0 when none);
+// EXEC = all 64 lanes on entry and exit
+void wave_min_vpc(Em &e, const char *mask, const char *dst) {
+  e.l("v_cndmask_b32_e64 %s, -1, %s, %s", X0, VPC, mask);
+  static const char *const steps[6] = {"row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf",
+                                       "row_shr:4 row_mask:0xf", "row_shr:8 row_mask:0xf",
+                                       "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"};
+  for (const char *st : steps) {
+    e.l("s_nop 1");
+    e.l("v_min_u32_dpp %s, %s, %s %s bank_mask:0xf", X0, X0, X0, st);
+  }
+  e.l("s_nop 1");
+  e.l("v_readlane_b32 %s, %s, 63", dst, X0);
+  e.l("s_nop 1");
+}
+
+// Lmerge (the group reached OTHER or the count limit: its pc is PCOFF) and Lsched
+std::string simt_sched() {
+  Em e;
+  e.l(".p2align 6");
+  e.l("Lmerge:");
+  e.l("v_lshrrev_b32_e64 %s, 5, s62", VPC);
+  flush(e);
+  e.l("Lsched:");
+  // every pick costs 16 of the budget as well: the core returns to the kernel (limits,
+  // interrupts) even if the lanes retired nothing
+  e.l("s_sub_u32 s64, s64, 16");
+  e.l("s_cselect_b32 s64, 0, s64");
+  e.l("s_mov_b64 exec, -1");
+  e.l("s_nop 4");
+  wave_min_vpc(e, "s[96:97]", "s68");                  // the lowest pc
+  e.l("v_cmp_eq_u32_e64 s[74:75], s68, %s", VPC);
+  e.l("s_and_b64 s[74:75], s[74:75], s[96:97]");       // the group: ALL at that pc
+  e.l("s_cmp_eq_u32 s95, -1");                         // were the banks converged?
+  e.l("s_cselect_b32 s69, 1, 0");
+  e.l("s_andn2_b64 vcc, s[96:97], s[74:75]");          // the lanes left waiting
+  e.l("s_cbranch_vccz Lsc_conv");
+  wave_min_vpc(e, "vcc", "s63");
+  e.l("s_lshl_b32 s63, s63, 5");
+  e.l("s_mov_b32 s95, s63");
+  e.l("s_cmp_eq_u32 s69, 0");
+  e.l("s_cbranch_scc1 Lsc_disp");
+  e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
+  e.l("s_addc_u32 s71, s71, 0");
+  e.l("s_branch Lsc_bankb");
+  e.l("Lsc_conv:");
+  e.l("s_mov_b32 s63, -1");
+  e.l("s_mov_b32 s95, -1");
+  e.l("s_cmp_eq_u32 s69, 1");
+  e.l("s_cbranch_scc1 Lsc_disp");
+  e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
+  e.l("s_subb_u32 s71, s71, 0");
+  e.l("Lsc_bankb:");
+  e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
+  e.l("s_addc_u32 s73, s71, 0");
+  e.l("Lsc_disp:");
+  e.l("s_mov_b64 exec, s[74:75]");
+  e.l("s_lshl_b32 s62, s68, 5");
+  e.l("s_cmp_eq_u32 s64, 0");                          // budget spent: to the kernel
+  e.l("s_cbranch_scc1 Lsc_out");
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+  e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("s_add_u32 s68, s70, s76");
+  e.l("s_addc_u32 s69, s71, 0");
+  e.l("s_setpc_b64 s[68:69]");
+  e.l("Lsc_out:");
+  e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+  e.l("s_addc_u32 s69, s71, 0");
+  e.l("s_setpc_b64 s[68:69]");
+  return e.o;
+}
+
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost) {
+                       const JitCost *cost, bool simt) {
+  if (cost) simt = false;
+  // which divergence events stay in the core (debug aid): 1 split branches, 2 split
+  // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
+  // SIMT)
+  const char *sxe = getenv("WB_SIMT_X");
+  const unsigned sx = simt ? (sxe ? unsigned(atoi(sxe)) : 7u) : 0u;
   const char *se = getenv("WB_JIT_SCHED");   // 0: keep program order (A/B measurement aid)
   const bool sched = !(se && se[0] == '0');
   // One asm statement holds every run (behind a jump) and a table of their offsets from
@@ -1162,6 +1305,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
           "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
           "s_setpc_b64 s[8:9]\n";
+  if (simt) body += simt_sched();
   // run index by start pc: a transfer to one jumps straight to its code
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
@@ -1223,6 +1367,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_or_b64 %s, %s, vcc", T2, T2);
       e.leave_if_t2();
     }
+    std::string extra;   // SIMT split code, placed after the run
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
     const size_t body_at = e.o.size();
@@ -1299,7 +1444,27 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       taken_checks();
       go(tgt, preload);
     } else if (lop == OP_RET) {
-      emit_ret(e, last);
+      const std::string rout = emit_ret(e, last, (sx & 2) ? "Lrs" + K : std::string());
+      if (sx & 2) {
+        // lanes returning to different places: each records its return pc and count
+        // (unless one leaves the entry function: the C++ step finishes those) and the
+        // scheduler picks who goes on
+        const uint32_t a = last.w1 & 0xFFFFu, nres = last.w1 >> 16, fb = e.fb;
+        Em x;
+        x.l("Lrs%s:", K.c_str());
+        x.l("v_and_b32_e32 %s, 0xfffff, %s", X0, Y1);
+        x.l("v_cmp_eq_u32_e32 vcc, 0xfffff, %s", X0);
+        x.l("s_and_b64 vcc, vcc, exec");
+        x.l("s_cbranch_vccnz %s", rout.c_str());
+        x.l("v_subrev_u32_e32 v102, 1, v102");
+        for (uint32_t q = 0; q < nres; q++)
+          if (a != fb) x.l("v_mov_b32 %s, %s", Em::V(fb + q).c_str(), Em::V(a + q).c_str());
+        x.l("v_mov_b32 %s, %s", VPC, X0);
+        x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+        flush(x);
+        long_jump(x, "Lsched", "Lrq" + K);
+        extra += x.o;
+      }
       e.gas_add(c_fall);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       taken_checks();
@@ -1328,9 +1493,27 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("s_and_b64 %s, vcc, exec", T2);
         e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
         e.l("s_cmp_eq_u64 %s, exec", T2);
-        const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
-        e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done, e.cdone});
-        e.l("s_cbranch_scc0 %s", lab_split.c_str());   // lanes disagree: the C++ step splits
+        if (sx & 1) {
+          // lanes disagree: each records where it goes on (vcc: taken) and its count,
+          // and the scheduler picks who goes first
+          e.l("s_cbranch_scc0 Lbs%s", K.c_str());
+          Em x;
+          x.l("Lbs%s:", K.c_str());
+          x.l("v_mov_b32 %s, 0x%x", X0, fall);
+          x.l("v_mov_b32 %s, 0x%x", X1, tgt);
+          x.l("v_cndmask_b32_e32 %s, %s, %s, vcc", VPC, X0, X1);
+          x.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));   // a taken branch's correction
+          x.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
+          x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+          x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+          flush(x);
+          long_jump(x, "Lsched", "Lbq" + K);
+          extra += x.o;
+        } else {
+          const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
+          e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done, e.cdone});
+          e.l("s_cbranch_scc0 %s", lab_split.c_str());   // lanes disagree: the C++ step splits
+        }
       }
       e.gas_add(uint64_t(int64_t(c_fall) + c_adj));
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
@@ -1346,9 +1529,14 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       fallthrough(r.cnt);
     }
     e.l("Lxs%s:", K.c_str());
-    e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
-    e.l("s_addc_u32 s69, s71, 0");
-    e.l("s_setpc_b64 s[68:69]");
+    if (sx & 4) {   // reached a waiting lane or the count limit: merge / reschedule
+      long_jump(e, "Lmerge", "Lmq" + K);
+    } else {
+      e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+      e.l("s_addc_u32 s69, s71, 0");
+      e.l("s_setpc_b64 s[68:69]");
+    }
+    e.o += extra;
     for (const auto &s : e.stubs) {   // leave before instruction s.pc
       e.l("%s:", s.lab.c_str());
       e.gas_add(s.cdone);
@@ -1464,10 +1652,11 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       *instrs = 0;
       for (const auto &r : runs) *instrs += r.len;
     }
-    if (!runs.empty()) {
+    // both flavours: plain runs and SIMT scheduling (KParams::simt)
+    for (int simt = 0; simt < 2 && e.empty() && !runs.empty(); simt++) {
       std::vector<char> obj;
-      const std::string src = wb::jit_source(P, runs, glog);
-      if (const char *dump = getenv("WB_JIT_DUMP"))
+      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0);
+      if (const char *dump = getenv(simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
         if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
       e = src.empty() ? "no source" : wb::jit_compile(src, &obj);
     }

@@ -49,8 +49,10 @@ struct JitCost {
 // The hiprtc source: one kernel, wbjit_addrs(uint64_t *out), that writes the address of
 // run k's code to out[k]; the runs' code sits inside it behind branches. glog: linear-
 // memory granule = 4 << glog bytes (batch_ctx.h lane_word). cost: metered contexts.
+// simt: lanes that part ways (a split branch or return, reaching a waiting lane) stay in
+// the core and are scheduled there (Lsched, KParams::simt); not with cost.
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost = nullptr);
+                       const JitCost *cost = nullptr, bool simt = false);
 
 // Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
 std::string jit_compile(const std::string &src, std::vector<char> *code);
