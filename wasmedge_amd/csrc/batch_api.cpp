@@ -150,7 +150,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const char *sme = getenv("WB_SIMT");
   const bool want_simt = !C->conf.CostLimit && (sme ? sme[0] == '1' : C->sched == 0);
   if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
-    const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv);
+    const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt);
     if (!runs.empty()) {
       std::vector<uint8_t> start(P.code.size() + 1, 0);
       for (const auto &r : runs) start[r.pc] = 1;

@@ -28,6 +28,7 @@ namespace {
 
 constexpr uint32_t kMinRun = 3;   // shorter runs gain less than the entry/exit costs
 constexpr uint32_t kMaxRun = 1500;   // keeps a run's branches to its exit stubs in range
+constexpr uint32_t kMaxBrTable = 32;   // br_table entries compiled as a compare chain
 
 const char *const PAGES = "v105", *const MEM = "v[106:107]", *const HWM = "v101";
 const char *const A0 = "v108", *const A1 = "v109", *const AP = "v[108:109]";
@@ -615,6 +616,15 @@ bool emit(Em &e, const DInstr &I) {
     case OP_BR_GT_U_I: case OP_BR_LE_S_I: case OP_BR_LE_U_I: case OP_BR_GE_S_I: case OP_BR_GE_U_I:
       // the last instruction of a run (emit_branch); as tc.cpp: a taken count >= 0
       return int32_t((I.w0 >> 16) & 0xFFu) + int32_t(int16_t(d)) >= 0 && imm < (1u << 26);
+    case OP_BR_TABLE: {   // the last instruction of a run (emit_br_table): small tables
+      if (!e.prog || b >= kMaxBrTable || (uint64_t(imm) + b + 1) * 2 > e.prog->brtab.size()) return false;
+      for (uint32_t k = 0; k <= b; k++) {
+        const uint32_t t = e.prog->brtab[2 * (imm + k)];
+        const int32_t tc = int32_t(e.prog->brtab[2 * (imm + k) + 1]);
+        if (t >= (1u << 26) || int32_t((I.w0 >> 16) & 0xFFu) + tc < 0) return false;
+      }
+      return true;
+    }
     case OP_RET:    // the last instruction of a run (emit_ret)
       return e.fb < TC_VF_CELLS && uint64_t(a) + b <= TC_VF_CELLS;
     case OP_ZERO_LOCALS:   // a = first cell, b = count
@@ -1100,6 +1110,24 @@ std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
   return out;
 }
 
+// BR_TABLE (controlInstr.cpp:53-70; dbc_step.inc): index = min(cell a, b) (b = the
+// default's index), entry brtab[imm + index] = (target pc, taken-count correction).
+// Per lane: Y0 = target, Y1 = correction (a compare chain over the entries).
+void emit_br_table(Em &e, const DInstr &I) {
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, imm = I.w3;
+  const std::vector<uint32_t> &bt = e.prog->brtab;
+  e.l("v_min_u32_e32 %s, 0x%x, %s", X0, b, e.v(a));
+  e.l("v_mov_b32 %s, 0x%x", Y0, bt[2 * (imm + b)]);
+  e.l("v_mov_b32 %s, 0x%x", Y1, bt[2 * (imm + b) + 1]);
+  for (uint32_t k = 0; k < b; k++) {
+    e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", k, X0);
+    e.l("v_mov_b32 %s, 0x%x", X1, bt[2 * (imm + k)]);
+    e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", Y0, Y0, X1);
+    e.l("v_mov_b32 %s, 0x%x", X1, bt[2 * (imm + k) + 1]);
+    e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", Y1, Y1, X1);
+  }
+}
+
 // can instruction I be compiled (dry run)
 bool jit_ok(const Program &P, const DInstr &I) {
   const uint16_t op = op_of(I);
@@ -1129,7 +1157,7 @@ bool is_xfer(uint16_t op) { return op == OP_CALL || op == OP_RET; }
 bool is_branch_op(uint16_t op) {
   return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
-bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op); }
+bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op) || op == OP_BR_TABLE; }
 
 // The compare of a branch into vcc (true = taken).
 void branch_cond(Em &e, const DInstr &I) {
@@ -1150,14 +1178,17 @@ void branch_cond(Em &e, const DInstr &I) {
 
 }  // namespace
 
-std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt) {
   std::vector<JitRun> runs;
   const size_t n = P.code.size();
   if (P.total_cells() > TC_VF_CELLS) return runs;
   const std::vector<uint8_t> target = jump_targets(P);
   std::vector<uint8_t> ok(n, 0);
   (void)tc;
-  for (size_t pc = 0; pc < n; pc++) ok[pc] = jit_ok(P, P.code[pc]);
+  // (br_table only with SIMT: its splits stay in the core, and SIMT contexts are never
+  // metered, whose compiled runs would have to price each table entry)
+  for (size_t pc = 0; pc < n; pc++)
+    ok[pc] = jit_ok(P, P.code[pc]) && (simt || op_of(P.code[pc]) != OP_BR_TABLE);
   for (size_t pc = 0; pc < n;) {
     if (!ok[pc]) { pc++; continue; }
     // a run ends after a call, return or branch (the run's code makes the transfer)
@@ -1170,9 +1201,10 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc) {
     bool calls = false;   // the call protocol's handlers are long: worth a run of any length
     for (size_t k = pc; k < end; k++) {
       const uint16_t o = op_of(P.code[k]);
-      calls |= is_xfer(o) || o == OP_POST_CALL;
+      calls |= is_xfer(o) || o == OP_POST_CALL || o == OP_BR_TABLE;
     }
-    if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = false;   // a lone branch
+    // a lone branch: only with SIMT, where its splits then stay in the core
+    if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = simt && op_of(P.code[pc]) != OP_JMP;
     if (end - pc >= kMinRun || calls) {
       uint32_t cnt = 0;
       for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
@@ -1341,7 +1373,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const uint32_t fall = r.pc + r.len;
     const uint32_t tgt = (lop == OP_CALL || is_branch_op(lop)) ? last.w3 : 0;
     const uint32_t pre = lop == OP_CALL ? tgt : fall;
-    const bool preload = lop != OP_RET && lop != OP_JMP && !start.count(pre);
+    const bool preload = lop != OP_RET && lop != OP_JMP && lop != OP_BR_TABLE && !start.count(pre);
     e.fb = P.global_cells;
     e.prog = &P;
     if (preload) {
@@ -1483,6 +1515,38 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("Lrt%s_%zu:", K.c_str(), q);
         go(sites[q], false);
       }
+    } else if (lop == OP_BR_TABLE) {
+      emit_br_table(e, last);
+      // every lane to the same entry: jump there (count + that entry's correction);
+      // else (SIMT) each lane records its target and count and the scheduler picks, or
+      // (no SIMT) the C++ step splits the wave
+      e.l("v_readfirstlane_b32 s68, %s", Y0);
+      e.l("v_readfirstlane_b32 s69, %s", Y1);
+      e.l("s_nop 1");
+      e.l("v_cmp_ne_u32_e64 %s, s68, %s", T2, Y0);
+      e.l("v_cmp_ne_u32_e32 vcc, s69, %s", Y1);
+      e.l("s_or_b64 %s, %s, vcc", T2, T2);
+      e.l("s_and_b64 %s, %s, exec", T2, T2);
+      if (sx & 1) {
+        e.l("s_cbranch_scc1 Lts%s", K.c_str());
+        Em x;
+        x.l("Lts%s:", K.c_str());
+        x.l("v_mov_b32 %s, %s", VPC, Y0);
+        x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, Y1);
+        x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+        flush(x);
+        long_jump(x, "Lsched", "Ltq" + K);
+        extra += x.o;
+      } else {
+        const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
+        e.stubs.push_back(Em::Stub{lab_split, e.pc, e.done, e.cdone});
+        e.l("s_cbranch_scc1 %s", lab_split.c_str());
+      }
+      e.l("s_lshl_b32 s62, s68, 5");
+      e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+      e.l("s_add_u32 s65, s65, s69");
+      taken_checks();
+      go(~0u, false);
     } else if (is_branch_op(lop)) {
       const uint32_t bcnt = (last.w0 >> 16) & 0xFFu;
       const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
@@ -1652,8 +1716,10 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       *instrs = 0;
       for (const auto &r : runs) *instrs += r.len;
     }
-    // both flavours: plain runs and SIMT scheduling (KParams::simt)
-    for (int simt = 0; simt < 2 && e.empty() && !runs.empty(); simt++) {
+    // both flavours: plain runs and SIMT scheduling (KParams::simt, its own run choice)
+    for (int simt = 0; simt < 2 && e.empty(); simt++) {
+      if (simt) runs = wb::jit_runs(P, tc, true);
+      if (runs.empty()) continue;
       std::vector<char> obj;
       const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0);
       if (const char *dump = getenv(simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))

@@ -31,7 +31,9 @@ struct JitRun {
 // Runs worth compiling: maximal straight-line stretches of compilable instructions with
 // no jump target past their first, at least kMinRun long. `tc`: build_threaded's array
 // (an instruction without a handler there is never compiled).
-std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc);
+// simt: (KParams::simt) lone conditional branches and br_table end runs too, so that
+// their splits stay in the core.
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt = false);
 
 // Gas prices of a metered context (batch_ctx.h cost_off_h / cost_pool_h): per DBC
 // instruction its cost list's prefix sums. A compiled run checks at entry that every lane
