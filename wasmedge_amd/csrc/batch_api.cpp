@@ -127,9 +127,10 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (C->frame_hbm) C->threaded = false;
   std::vector<TInstr> tcv;
   // V frames (frame cells in VGPRs while the core runs) when the frame fits in
-  // v128..v255 and the batch needs at most 2 waves per SIMD (the V kernel's 256 VGPRs
-  // allow no more; beyond that the LDS kernel's occupancy wins: C5 at 256K instances
-  // 7.2e11 vs 6.2e11). WB_VFRAME=0 / 1 forces LDS / V frames (A/B measurement aid).
+  // v128..v255: 2 waves per SIMD (256 VGPRs), against 4 for the LDS kernel, but the
+  // compiled runs and SIMT scheduling only exist for V frames (C5 at 256K instances =
+  // 4 waves per SIMD: 1.60e12 instr/s against 1.13e12). WB_VFRAME=0 / 1 forces LDS / V
+  // frames (A/B measurement aid).
   const char *vfe = getenv("WB_VFRAME");
   const char *sce = getenv("WB_SCHED");
   C->sched = sce ? (uint32_t)atoi(sce) : 1u;
@@ -137,18 +138,18 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (std::all_of(P.loops.begin(), P.loops.end(), [](uint32_t v) { return v == 0xFFFFFFFFu; }))
     C->sched = 0;
   const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
-  C->vframe = vf_fit && (vfe ? vfe[0] == '1' : C->nwaves <= 2 * 1024);
+  C->vframe = vf_fit && (vfe ? vfe[0] == '1' : true);
   if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);
   // compiled runs (jit.h) for the V-frame core; WB_JIT=0 interprets them instead. A
   // compile failure is not fatal (the core interprets) but is kept as the last error.
   const char *jte = getenv("WB_JIT");
   // Metered contexts run only the compiled runs in the core (they price themselves,
   // JitCost); every other instruction stays in the exact compiled / per-lane step.
-  // SIMT scheduling inside the compiled runs (KParams::simt): for modules the kernel
-  // schedules by plain min pc (the scan-loop policy lives in the kernel's scheduler), not
-  // for metered contexts; WB_SIMT=0 / 1 forces it off / on (A/B measurement aid)
+  // SIMT scheduling inside the compiled runs (KParams::simt), not for metered contexts;
+  // WB_SIMT=0 turns it off (A/B measurement aid). (C3 4K: 1.19e11 instr/s against 9.8e10
+  // with the kernel's scan-loop policy between core calls.)
   const char *sme = getenv("WB_SIMT");
-  const bool want_simt = !C->conf.CostLimit && (sme ? sme[0] == '1' : C->sched == 0);
+  const bool want_simt = !C->conf.CostLimit && !(sme && sme[0] == '0');
   if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
     const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt);
     if (!runs.empty()) {
@@ -200,7 +201,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // at the occupancy this batch reaches (nwaves over 256 CUs, at most 16 waves per CU)
   {
     const uint32_t tc = C->frame_hbm ? 0 : P.total_cells() ? P.total_cells() : 1;
-    const uint32_t per_cu = std::min<uint32_t>(16, std::max<uint32_t>(4, (C->nwaves + 255) / 256));
+    const uint32_t per_cu = std::min<uint32_t>(C->vframe ? 8 : 16, std::max<uint32_t>(4, (C->nwaves + 255) / 256));
     const uint32_t wave_cells = (160 * 1024 - 1024) / 256 / per_cu;   // 256 B per cell row
     uint32_t s = wave_cells > tc + 1 ? wave_cells - tc - 1 : 0;
     if (s > C->gs_depth) s = C->gs_depth;
