@@ -166,17 +166,64 @@ struct Em {
     dstp[1] = direct ? P(c + 2) : ZP;
     return out;
   }
-  // leave before this instruction when any active lane's result is a NaN: the handlers'
-  // rule (gen_tc.py nan_exit); the C++ step then produces the reference's payload.
-  // regs: result registers or pairs, w: 32 / 64
-  void nan_leave(std::initializer_list<const char *> regs, int w) {
+  // NaN results fixed in place (an out-of-line block, taken only when some active lane's
+  // result is a NaN) to what the reference's x86 build produces: the first NaN operand,
+  // quieted, else the default NaN with the sign bit set (dbc_ops.h nan_fix32/64). The
+  // sources must be intact (results in temporaries or cells that overlap no source).
+  // Items: result register (w 32) or lo/hi registers and the aligned pair (w 64), and the
+  // source cells a, b.
+  struct NanItem { std::string lo, hi, pair; uint32_t a, b; };
+  std::string tail;   // out-of-line code of the run (placed after it)
+  int nfix = 0;
+  void nan_fix(const std::vector<NanItem> &items, int w) {
+    const std::string id = std::to_string(run) + "_" + std::to_string(nfix++);
     bool first = true;
-    for (const char *r : regs) {
-      l("v_cmp_u_f%d_e64 %s, %s, %s", w, first ? T2 : "vcc", r, r);
+    for (const auto &it : items) {
+      const std::string &r = w == 64 ? it.pair : it.lo;
+      l("v_cmp_u_f%d_e64 %s, %s, %s", w, first ? T2 : "vcc", r.c_str(), r.c_str());
       if (!first) l("s_or_b64 %s, %s, vcc", T2, T2);
       first = false;
     }
-    leave_if_t2();
+    l("s_and_b64 %s, %s, exec", T2, T2);
+    l("s_cbranch_scc1 Lnf%s", id.c_str());
+    l("Lnr%s:", id.c_str());
+    std::string o2;
+    o.swap(o2);   // (emit the block into `tail`)
+    l("Lnf%s:", id.c_str());
+    for (const auto &it : items) {
+      if (w == 64) {
+        l("v_mov_b32 %s, %s", A0, v(it.a));
+        l("v_mov_b32 %s, %s", A1, v(it.a + 1));
+        l("v_mov_b32 %s, %s", B0, v(it.b));
+        l("v_mov_b32 %s, %s", B1, v(it.b + 1));
+        l("v_cmp_u_f64_e64 s[68:69], %s, %s", AP, AP);
+        l("v_cmp_u_f64_e64 vcc, %s, %s", BP, BP);
+        l("v_mov_b32 %s, 0", X0);
+        l("v_mov_b32 %s, 0xfff80000", X1);
+        l("v_or_b32_e32 %s, 0x80000, %s", Y1, B1);
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", X0, X0, B0);
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", X1, X1, Y1);
+        l("v_or_b32_e32 %s, 0x80000, %s", Y1, A1);
+        l("v_cndmask_b32_e64 %s, %s, %s, s[68:69]", X0, X0, A0);
+        l("v_cndmask_b32_e64 %s, %s, %s, s[68:69]", X1, X1, Y1);
+        l("v_cmp_u_f64_e64 vcc, %s, %s", it.pair.c_str(), it.pair.c_str());
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", it.lo.c_str(), it.lo.c_str(), X0);
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", it.hi.c_str(), it.hi.c_str(), X1);
+      } else {
+        l("v_cmp_u_f32_e64 s[68:69], %s, %s", v(it.a), v(it.a));
+        l("v_cmp_u_f32_e64 vcc, %s, %s", v(it.b), v(it.b));
+        l("v_mov_b32 %s, 0xffc00000", X0);
+        l("v_or_b32_e32 %s, 0x400000, %s", Y1, v(it.b));
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", X0, X0, Y1);
+        l("v_or_b32_e32 %s, 0x400000, %s", Y1, v(it.a));
+        l("v_cndmask_b32_e64 %s, %s, %s, s[68:69]", X0, X0, Y1);
+        l("v_cmp_u_f32_e64 vcc, %s, %s", it.lo.c_str(), it.lo.c_str());
+        l("v_cndmask_b32_e64 %s, %s, %s, vcc", it.lo.c_str(), it.lo.c_str(), X0);
+      }
+    }
+    l("s_branch Lnr%s", id.c_str());
+    o.swap(o2);
+    tail += o2;
   }
   // leave before instruction pc (the C++ step executes it) when any active lane's T2 bit
   // is set
@@ -386,7 +433,7 @@ bool emit(Em &e, const DInstr &I) {
       e.sync({a, b, c});
       const char *ins = op == OP_F32_MUL ? "v_mul_f32_e32" : op == OP_F32_SUB ? "v_sub_f32_e32" : "v_add_f32_e32";
       e.l("%s %s, %s, %s", ins, R0, e.v(a), e.v(b));
-      e.nan_leave({R0}, 32);
+      e.nan_fix({{R0, "", "", a, b}}, 32);
       e.l("v_mov_b32 %s, %s", e.v(c), R0);
       return true;
     }
@@ -395,7 +442,7 @@ bool emit(Em &e, const DInstr &I) {
       const char *x = e.src64(a, A0, A1, AP), *y = e.src64(b, B0, B1, BP);
       if (op == OP_F64_MUL) e.l("v_mul_f64 %s, %s, %s", RP, x, y);
       else e.l("v_add_f64 %s, %s, %s%s", RP, x, op == OP_F64_SUB ? "-" : "", y);
-      e.nan_leave({RP}, 64);
+      e.nan_fix({{R0, R1, RP, a, b}}, 64);
       e.put64(c);
       return true;
     }
@@ -510,7 +557,8 @@ bool emit(Em &e, const DInstr &I) {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
       const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
-      e.nan_leave({r[0], r[1], r[2], r[3]}, 32);
+      e.nan_fix({{r[0], "", "", a, b}, {r[1], "", "", a + 1, b + 1}, {r[2], "", "", a + 2, b + 2},
+                 {r[3], "", "", a + 3, b + 3}}, 32);
       e.put128(c, r);
       return true;
     }
@@ -523,7 +571,7 @@ bool emit(Em &e, const DInstr &I) {
         if (op == OP_V_F64X2_MUL) e.l("v_mul_f64 %s, %s, %s", res[k].c_str(), x, y);
         else e.l("v_add_f64 %s, %s, %s%s", res[k].c_str(), x, op == OP_V_F64X2_SUB ? "-" : "", y);
       }
-      e.nan_leave({res[0].c_str(), res[1].c_str()}, 64);
+      e.nan_fix({{r[0], r[1], res[0], a, b}, {r[2], r[3], res[1], a + 2, b + 2}}, 64);
       e.put128(c, r);
       return true;
     }
@@ -1601,6 +1649,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_setpc_b64 s[68:69]");
     }
     e.o += extra;
+    e.o += e.tail;
     for (const auto &s : e.stubs) {   // leave before instruction s.pc
       e.l("%s:", s.lab.c_str());
       e.gas_add(s.cdone);
