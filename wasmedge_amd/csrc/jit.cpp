@@ -1325,6 +1325,12 @@ std::string simt_sched() {
   e.l("s_mov_b64 exec, -1");
   e.l("s_nop 4");
   wave_min_vpc(e, "s[96:97]", "s68");                  // the lowest pc
+  e.l("s_lshl_b32 s62, s68, 5");
+  // the group's TInstr loads while the rest of the pick goes on (a prefetch still in
+  // flight must land first: SMEM returns out of order)
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+  e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
   e.l("v_cmp_eq_u32_e64 s[74:75], s68, %s", VPC);
   e.l("s_and_b64 s[74:75], s[74:75], s[96:97]");       // the group: ALL at that pc
   e.l("s_cmp_eq_u32 s95, -1");                         // were the banks converged?
@@ -1334,6 +1340,7 @@ std::string simt_sched() {
   wave_min_vpc(e, "vcc", "s63");
   e.l("s_lshl_b32 s63, s63, 5");
   e.l("s_mov_b32 s95, s63");
+  // (s69 = 1 when the banks were the converged ones)
   e.l("s_cmp_eq_u32 s69, 0");
   e.l("s_cbranch_scc1 Lsc_disp");
   e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
@@ -1349,14 +1356,12 @@ std::string simt_sched() {
   e.l("Lsc_bankb:");
   e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
   e.l("s_addc_u32 s73, s71, 0");
+  // (entered with the group in s[74:75], s62 = its pc, its TInstr loading, the banks of
+  // the right mode; split paths jump here directly)
   e.l("Lsc_disp:");
   e.l("s_mov_b64 exec, s[74:75]");
-  e.l("s_lshl_b32 s62, s68, 5");
   e.l("s_cmp_eq_u32 s64, 0");                          // budget spent: to the kernel
   e.l("s_cbranch_scc1 Lsc_out");
-  e.l("s_waitcnt lgkmcnt(0)");
-  e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
-  e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
   e.l("s_waitcnt lgkmcnt(0)");
   e.l("s_add_u32 s68, s70, s76");
   e.l("s_addc_u32 s69, s71, 0");
@@ -1619,7 +1624,35 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
           x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
           flush(x);
-          long_jump(x, "Lsched", "Lbq" + K);
+          if (fall != tgt) {
+            // No waiting lane at or below the nearer destination `lo`: the lanes going
+            // there are the next group, those going to `hi` wait, and the lowest waiting
+            // pc becomes min(LOW, hi) -- a pick without the wave reductions of Lsched
+            const uint32_t lo = std::min(fall, tgt), hi = std::max(fall, tgt);
+            x.l("s_cmp_le_u32 s95, 0x%x", lo * 32u);
+            x.l("s_cbranch_scc0 Lbf%s", K.c_str());
+            long_jump(x, "Lsched", "Lbq" + K);
+            x.l("Lbf%s:", K.c_str());
+            x.l("s_sub_u32 s64, s64, 16");
+            x.l("s_cselect_b32 s64, 0, s64");
+            x.l("s_cmp_eq_u32 s95, -1");                  // converged until now: D banks
+            x.l("s_cbranch_scc0 Lbm%s", K.c_str());
+            x.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);
+            x.l("s_addc_u32 s71, s71, 0");
+            x.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
+            x.l("s_addc_u32 s73, s71, 0");
+            x.l("Lbm%s:", K.c_str());
+            x.l("s_min_u32 s95, s95, 0x%x", hi * 32u);
+            x.l("s_mov_b32 s63, s95");
+            x.l(lo == tgt ? "s_and_b64 s[74:75], vcc, exec" : "s_andn2_b64 s[74:75], exec, vcc");
+            x.l("s_mov_b32 s62, 0x%x", lo * 32u);
+            x.l("s_waitcnt lgkmcnt(0)");
+            x.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+            x.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+            long_jump(x, "Lsc_disp", "Lbt" + K);   // (clobbers s[68:69])
+          } else {
+            long_jump(x, "Lsched", "Lbq" + K);
+          }
           extra += x.o;
         } else {
           const std::string lab_split = "Lx" + K + "_" + std::to_string(e.stubs.size());
