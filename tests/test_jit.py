@@ -121,6 +121,22 @@ def _stmt(r, calls=True):
         ins, n = r.choice(STORES64)
         ad, off = _addr(r, n)
         return "(%s offset=%d %s %s)" % (ins, off, ad, _g64(r))
+    if r.random() < 0.3:
+        # a load-scan loop (jit.cpp scan loops: 8 iterations per trip): up or down by a
+        # word from a per-lane start, on while the loaded word compares true; zero words
+        # stop the `gt_u` form at once, the `lt_u` form runs through them to the end of
+        # memory (the unrolled window fails its bounds check first, then the plain run
+        # traps with 0x88 at the exact instruction)
+        x, y = "$a%d" % r.randrange(N32), "$a%d" % r.randrange(N32)
+        if x == y:
+            y = "$a%d" % ((int(x[2:]) + 1) % N32)
+        cmp = r.choice(["gt_u", "lt_u"])
+        lim = "(local.get %s)" % y if cmp == "gt_u" else "(i32.and (local.get %s) (i32.const 7))" % y
+        lab = r.randrange(1 << 30)
+        return ("(local.set %s (i32.and (local.get %s) (i32.const 0xFFFC)))"
+                "(loop $s%d (local.set %s (i32.%s (local.get %s) (i32.const 4)))"
+                "(br_if $s%d (i32.%s (i32.load offset=%d (local.get %s)) %s)))"
+                % (x, x, lab, x, r.choice(["add", "sub"]), x, lab, cmp, r.choice([0, 4, 256]), x, lim))
     return "(local.set %s (i32.%s %s %s))" % (d32, r.choice(["add", "sub", "xor"]), _g32(r), _c32(r))
 
 
@@ -206,9 +222,13 @@ def test_runs_assemble(built, glog):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("jit", ["1", "0"])
+@pytest.mark.parametrize("jit", ["1", "0", "scan"])
 @pytest.mark.parametrize("granule", [4, 16, 128])
 def test_gpu_random_modules(built, monkeypatch, jit, granule):
+    """jit "scan": compiled runs with the opt-in unrolled scan loops (WB_SCAN=1)"""
+    if jit == "scan":
+        monkeypatch.setenv("WB_SCAN", "1")
+        jit = "1"
     monkeypatch.setenv("WB_JIT", jit)
     runs = 0
     for s in SEEDS:

@@ -458,7 +458,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
         if (status == WB_STATUS_RUNNING) {
           pc = so.vpc;
-          count += so.vcnt;
+          count += (uint64_t)(int64_t)(int32_t)so.vcnt;   // (a taken jump's count can be < 0)
         }
         if (why) {   // the core's budget is spent: nothing for the C++ step this round
           WB_STAT_ADD(ST_TC_SCHED, 1);
@@ -527,7 +527,9 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, cost,
                             p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why);
-          asc += ncnt;
+          // (sign-extended: a core call that only takes a jump whose count correction is
+          // negative -- a `br` out of blocks, cnt 1 + tcnt -2 -- retires -1 instructions)
+          asc += (uint64_t)(int64_t)(int32_t)ncnt;
           WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
           if (why) WB_STAT_ADD(ST_TC_SCHED, 1);
           if (why) { xpc = pcs; tcode = 0; xadj = 0; break; }   // = k_leave
@@ -610,7 +612,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_OP
 #undef SLOW_IF
 #undef HOST_YIELD
-      count += (uint64_t)sc + asc;
+      count += (uint64_t)(int64_t)(int32_t)sc + asc;
       cost += scost;
       if (tcode == 0) {
         pc = xpc;

@@ -1373,6 +1373,139 @@ std::string simt_sched() {
   return e.o;
 }
 
+// ---------------------------------------------------------------- SIMT scan loops
+// A run that IS a load-scan loop (Hoare partition's `while (a[i] < p) i++`): exactly
+//   x += d (I32_ADD_I / I32_SUB_I in place, d a multiple of 4, |d| <= 64)
+//   y = i32.load(x + off)
+//   br_<cmp> y, p (or p, y; p loop-invariant; an immediate form) back to the run's start
+// can run kScanUnroll iterations per trip (SIMT only, opt-in: WB_SCAN=1, see jit_source):
+// every lane's next kScanUnroll loads go
+// out together (one memory latency instead of one per iteration), then each lane's exit
+// iteration is found in order. A lane that leaves at iteration j gets x + d*j, the j-th
+// value and j iterations' count (j - 1 taken) and waits at the fall-through pc; the lanes
+// still looping go round again. Any lane whose kScanUnroll loads are not all in bounds and
+// aligned runs the plain run instead (which meets the failing access itself).
+constexpr uint32_t kScanUnroll = 8;
+struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
+
+bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
+  if (r.len != 3) return false;
+  const DInstr &i0 = P.code[r.pc], &i1 = P.code[r.pc + 1], &i2 = P.code[r.pc + 2];
+  const uint16_t o0 = op_of(i0), o1 = op_of(i1), o2 = op_of(i2);
+  if ((o0 != OP_I32_ADD_I && o0 != OP_I32_SUB_I) || (i0.w1 & 0xFFFFu) != (i0.w2 & 0xFFFFu)) return false;
+  if (i0.w3 == 0 || i0.w3 % 4 || i0.w3 > 64) return false;
+  const uint32_t x = i0.w1 & 0xFFFFu;
+  if (o1 != OP_LD32 || (i1.w1 & 0xFFFFu) != x || (i1.w2 & 0xFFFFu) == x) return false;
+  const uint32_t y = i1.w2 & 0xFFFFu;
+  if (!is_branch_op(o2) || o2 == OP_JMP || o2 == OP_BR_IF || o2 == OP_BR_UNLESS || i2.w3 != r.pc) return false;
+  const uint32_t a = i2.w1 & 0xFFFFu, b = i2.w1 >> 16;
+  bool y_first;
+  if (o2 >= OP_BR_EQ_I) {
+    if (a != y) return false;
+    y_first = true;
+  } else if (a == y && b != y && b != x) {
+    y_first = true;
+  } else if (b == y && a != y && a != x) {
+    y_first = false;
+  } else {
+    return false;
+  }
+  if (uint64_t(i1.w3) + 64u * kScanUnroll + 4 > 0xFFFFFFFFull) return false;
+  *sl = ScanLoop{x, y, i1.w3, o0 == OP_I32_ADD_I ? int32_t(i0.w3) : -int32_t(i0.w3), y_first};
+  return true;
+}
+
+// the scan loop's branch condition (true = go round) with the loaded value in `val`
+void scan_cond(Em &e, const DInstr &I, const ScanLoop &sl, const char *val) {
+  const uint16_t op = op_of(I);
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16;
+  if (op >= OP_BR_EQ_I) {
+    const uint16_t k = uint16_t(op - OP_BR_EQ_I);
+    e.l("v_cmp_%s32_e32 vcc, %d, %s", cmp_kind(cmp_swap(k)), int32_t(int16_t(b)), val);
+  } else {
+    const uint16_t k = uint16_t(op - OP_BR_EQ);
+    if (sl.y_first) e.l("v_cmp_%s32_e32 vcc, %s, %s", cmp_kind(cmp_swap(k)), e.v(b), val);   // p CMP' y
+    else e.l("v_cmp_%s32_e32 vcc, %s, %s", cmp_kind(k), e.v(a), val);                        // p CMP y
+  }
+}
+
+// the block at the run's start (label Lb<K>); the plain run follows at Lbo<K>
+void scan_loop_block(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl,
+                     const std::string &K) {
+  const uint32_t U = kScanUnroll, fall = r.pc + 3;
+  const DInstr &br = P.code[r.pc + 2];
+  const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
+  const uint32_t x = sl.x, y = sl.y;
+  static const char *const T[kScanUnroll] = {"v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115"};
+  e.l("Lb%s:", K.c_str());
+  flush(e);   // counts per lane from here
+  // the window: bytes (x + d*j) + off .. +3 for j = 1..U, in bounds and aligned, x + d*j
+// not wrapping (the loop's i32.add / i32.sub wraps; the 33-bit address sum does not)
+  const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
+  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(x));
+  e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
+  e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(x));
+  if (sl.d < 0) {   // x itself must not wrap below 0 (i32.sub), whatever the offset
+    e.l("v_cmp_gt_u32_e32 vcc, 0x%x, %s", uint32_t(-sl.d) * U, e.v(x));
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  }
+  e.l("v_and_b32_e32 %s, 3, %s", Y1, Y0);
+  e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y1);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  e.l("s_and_b64 %s, %s, exec", T2, T2);
+  e.l("s_cbranch_scc1 Lbo%s", K.c_str());
+  for (uint32_t j = 1; j <= U; j++) {
+    e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(x));
+    if (e.g == 0) {
+      e.l("v_mov_b32 %s, %s", W0, Y0);
+      e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+    } else {
+      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
+      e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+      e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+    }
+    e.l("global_load_dword %s, %s, off", T[j - 1], XP);
+  }
+  e.l("s_waitcnt vmcnt(0)");
+  // exits in iteration order; s[74:75] = the lanes still looping
+  e.l("s_mov_b64 s[74:75], exec");
+  for (uint32_t j = 1; j <= U; j++) {
+    const std::string nx = "Lsn" + K + "_" + std::to_string(j);
+    scan_cond(e, br, sl, T[j - 1]);
+    e.l("s_andn2_b64 s[68:69], s[74:75], vcc");   // leave in this iteration
+    e.l("s_and_b64 s[74:75], s[74:75], vcc");
+    e.l("s_cmp_eq_u64 s[68:69], 0");
+    e.l("s_cbranch_scc1 %s", nx.c_str());
+    e.l("s_mov_b64 exec, s[68:69]");
+    e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(j)), e.v(x));
+    e.l("v_mov_b32 %s, %s", e.v(y), T[j - 1]);
+    e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(int32_t(j * r.cnt) + int32_t(j - 1) * tcnt), VCNT);
+    e.l("v_mov_b32 %s, 0x%x", VPC, fall);
+    e.l("s_mov_b64 exec, s[74:75]");
+    e.l("%s:", nx.c_str());
+  }
+  // the lanes still looping: U iterations done, go round
+  e.l("s_mov_b64 exec, s[74:75]");
+  e.l("s_cbranch_execz Lsd%s", K.c_str());
+  const uint32_t per = U * uint32_t(int32_t(r.cnt) + tcnt);
+  e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(U)), e.v(x));
+  e.l("v_mov_b32 %s, %s", e.v(y), T[U - 1]);
+  e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, per, VCNT);
+  e.l("s_sub_u32 s64, s64, 0x%x", per);
+  e.l("s_cselect_b32 s64, 0, s64");
+  e.l("s_cmp_eq_u32 s64, 0");
+  e.l("s_cbranch_scc0 Lb%s", K.c_str());
+  e.l("v_mov_b32 %s, 0x%x", VPC, r.pc);   // budget spent: to the kernel through Lsched
+  e.l("Lsd%s:", K.c_str());
+  long_jump(e, "Lsched", "Lsq" + K);
+  e.l("Lbo%s:", K.c_str());
+}
+
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost, bool simt) {
   if (cost) simt = false;
@@ -1416,7 +1549,23 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.run = uint32_t(k);
     const std::string K = std::to_string(k);
     e.l(".p2align 6");
-    e.l("Lb%s:", K.c_str());
+    ScanLoop sl;
+    // Scan blocks are opt-in (WB_SCAN=1; WB_SCAN=p+1: only the loop at pc p): measured on
+    // C3 they do not pay (4K elements: 1.23e11 instr/s with, 1.26e11 without) -- Hoare
+    // scans over random data stop after ~2 iterations, so the 8 speculative loads and the
+    // exit search cost more than the latency they hide.
+    const char *sce = getenv("WB_SCAN");
+    const bool scan = simt && !cost && sce && atoi(sce) >= 1 &&
+                      (atoi(sce) == 1 || uint32_t(atoi(sce)) == r.pc + 1) && scan_loop_of(P, r, &sl);
+    if (scan) {
+      e.g = glog;
+      e.fb = P.global_cells;
+      e.prog = &P;
+      e.run = uint32_t(k);
+      scan_loop_block(e, P, r, sl, K);   // its own label Lb<K>; the plain run at Lbo<K>
+    } else {
+      e.l("Lb%s:", K.c_str());
+    }
     const DInstr &last = P.code[r.pc + r.len - 1];
     const uint16_t lop = op_of(last);
     // Where the run goes on: the instruction after it (fall-through, untaken branch), a
