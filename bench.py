@@ -305,7 +305,7 @@ def main():
     t0 = time.perf_counter()
     ksum = 0.0
     for k in range(args.steps):
-        ctx.reset()
+        ctx.reset(timed=False)   # (no host round trip: the run orders after it)
         ksum += ctx.run()        # HIP-event time of the interpreter kernel (its stream)
         if elapsed_hint(args):
             progress("step %d/%d done" % (k + 1, args.steps))

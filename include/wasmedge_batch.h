@@ -168,7 +168,9 @@ WASMEDGE_BATCH_API void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *Cxt);
  *   SetArgs  -> resolve FuncName, check types (FuncSigMismatch), upload params
  *   Reset    -> fresh instances: memory image, globals, then the start function
  *               (lib/executor/instantiate/module.cpp:16-172); a lane whose start
- *               function traps reports that trap from every later Run
+ *               function traps reports that trap from every later Run.
+ *               *KernelSeconds = the reset kernels' time; NULL: Reset does not wait
+ *               for them (without a start function), the next Run orders after them
  *   Run      -> launch the interpreter; *KernelSeconds = HIP-event time on the
  *               library's stream (may be NULL)
  *   Results  -> copy returns / statuses / counts back. */

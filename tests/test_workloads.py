@@ -1,6 +1,8 @@
 """Parity of the config workloads (BASELINE.json configs 2-5): device (or the host
 emulator of the kernel's step code) vs the oracle -- return bits, trap codes, reference
 instruction counts and final-memory hashes, per instance."""
+import os
+
 import numpy as np
 import pytest
 
@@ -104,16 +106,26 @@ def test_gpu_blake3_64k(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", ["0", "1", "4"])
+@pytest.mark.parametrize("sched", ["0", "1", "4", "nosimt", "scan"])
 def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
-    """The wave scheduler only decides which lanes run together: min-pc (0) and the
-    loop-aware largest-group policy (1, 4) must give identical per-lane results on the
-    divergent workloads (quicksort with per-lane data, Collatz with traps)."""
-    monkeypatch.setenv("WB_SCHED", sched)
+    """The wave scheduler only decides which lanes run together: the kernel's min-pc (0)
+    and loop-aware largest-group policies (1, 4) between core calls, SIMT scheduling inside
+    the compiled runs (default) or not (nosimt: WB_SIMT=0), with or without the unrolled
+    scan loops (scan: WB_SCAN=1), must give identical per-lane results on the divergent
+    workloads (recursion with per-lane depth, quicksort with per-lane data, Collatz's
+    br_table state machine with traps, Mandelbrot's per-lane escape)."""
+    if sched == "nosimt":
+        monkeypatch.setenv("WB_SIMT", "0")
+    elif sched == "scan":
+        monkeypatch.setenv("WB_SCAN", "1")
+    else:
+        monkeypatch.setenv("WB_SCHED", sched)
     cases = _cases()
     wasm, func, pt, rt, _ = cases["qsort"]
     cases["qsort"] = (wasm, func, pt, rt, [[i, (i * 37) % 700] for i in range(192)])
-    for name in ("qsort", "collatz"):
+    fib = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fibonacci.wasm"), "rb").read()
+    cases["fib"] = (fib, "fib", [I32], [I32], [[(i * 7) % 19] for i in range(192)])
+    for name in ("fib", "qsort", "collatz", "mandel"):
         wasm, func, pt, rt, rows = cases[name]
         ref = oracle_run(O.Module(wasm), func, rows)
         rets, st, cnt, h = gpu_run(wasm, func, rows, pt, rt)

@@ -272,9 +272,11 @@ class BatchContext:
         self.func = func
         self._keep = values
 
-    def reset(self):
+    def reset(self, timed=True):
+        """Re-instantiate every instance; returns the reset kernels' time (timed=False: no
+        host synchronisation, returns 0 -- the next run orders after it on the stream)."""
         t = ctypes.c_double(0)
-        self._check(lib().WasmEdge_BatchReset(self._h, ctypes.byref(t)))
+        self._check(lib().WasmEdge_BatchReset(self._h, ctypes.byref(t) if timed else None))
         return t.value
 
     def run(self):

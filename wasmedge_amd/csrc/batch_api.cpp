@@ -449,10 +449,15 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
                                       C->init_cost, C->stream), "state init"))
     return R(kRuntimeError);
   (void)hipEventRecord(C->ev1, C->stream);
-  if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
-  float ms = 0;
-  (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
-  double secs = ms * 1e-3;
+  // without a start function and without a request for the time, the next launch on the
+  // stream orders after this one: no host round trip (errors surface at the next sync)
+  double secs = 0;
+  if (KernelSeconds || P.start_func >= 0) {
+    if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
+    secs = ms * 1e-3;
+  }
   // module.cpp:160-170: the start function runs as the last step of instantiation; a
   // lane whose start function traps keeps that ErrCode as its instance status
   if (P.start_func >= 0) {

@@ -783,6 +783,29 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
                    const uint32_t *ls, uint32_t ls_slots, uint32_t full, uint32_t g) {
   const uint32_t chunks = (init_words + 1023u) / 1024u;
   __shared__ uint32_t smax;
+  if (!full && ls) {
+    // a Reset after a run: one block per wave reads the wave's write mark once and
+    // rewrites the rows below it (usually a few; the mark is per lane, the rows per wave)
+    for (size_t wave = blockIdx.x; wave < nwaves; wave += gridDim.x) {
+      if (threadIdx.x == 0) smax = 0;
+      __syncthreads();
+      if (threadIdx.x < 64) atomicMax(&smax, ls[((size_t)wave * ls_slots + LS_HWM) * 64u + threadIdx.x]);
+      __syncthreads();
+      const uint64_t hw = ((uint64_t)smax + 3u) / 4u;
+      uint32_t rows = (uint32_t)(hw < init_words ? hw : init_words);
+      if (rows < image_words && image_words <= init_words) rows = image_words;
+      const uint32_t gm = (1u << g) - 1u;
+      rows = (rows + gm) & ~gm;
+      if (rows > init_words) rows = init_words;
+      __syncthreads();   // smax is reused by the next wave
+      uint32_t *wm = mem + wave * mem_words * 64u;
+      for (size_t i = threadIdx.x; i < (size_t)rows * 64u; i += blockDim.x) {
+        const uint32_t word = (uint32_t)(((i >> (6 + g)) << g) | (i & ((1u << g) - 1u)));
+        wm[i] = word < image_words ? image[word] : 0u;
+      }
+    }
+    return;
+  }
   for (size_t b = blockIdx.x; b < (size_t)nwaves * chunks; b += gridDim.x) {
     const size_t wave = b / chunks;
     const uint32_t r0 = (uint32_t)(b - wave * chunks) * 1024u;
@@ -882,7 +905,9 @@ extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t g, hipStream_t s) {
   const size_t total = (size_t)nwaves * ((init_words + 1023u) / 1024u);
   if (total == 0) return hipSuccess;
-  const size_t blocks = total < 262144 ? total : 262144;
+  // full (re)initialisation: a block per 1024 rows of a wave; after a run: a block per
+  // wave (the kernel's write-mark path)
+  const size_t blocks = (!full && ls) ? nwaves : (total < 262144 ? total : 262144);
   hipLaunchKernelGGL(wb_mem_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, mem, image,
                      image_words, init_words, mem_words, nwaves, ls, ls_slots, full, g);
   return hipGetLastError();
