@@ -87,9 +87,13 @@ struct Em {
     o += buf;
     o += '\n';
   }
-  static std::string V(uint32_t c) { return "v" + std::to_string(128 + c); }
-  static std::string P(uint32_t c) {
-    return "v[" + std::to_string(128 + c) + ":" + std::to_string(129 + c) + "]";
+  // Inlined calls (jit_source): the callee's cells from the frame base on live `shift`
+  // cells higher, above the caller's live cells (globals stay).
+  uint32_t shift = 0;
+  uint32_t sc(uint32_t c) const { return (shift && c >= fb) ? c + shift : c; }
+  std::string V(uint32_t c) const { return "v" + std::to_string(128 + sc(c)); }
+  std::string P(uint32_t c) const {
+    return "v[" + std::to_string(128 + sc(c)) + ":" + std::to_string(129 + sc(c)) + "]";
   }
   const char *v(uint32_t c) {   // (short-lived: valid until the next call)
     static thread_local std::string s[8];
@@ -1614,6 +1618,8 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
       if (cost) e.cdone += cost->full(P, r.pc + i);
+      // an inlined call goes on here, after the POST_CALL it makes unnecessary
+      if (i == 0 && op_of(I) == OP_POST_CALL) e.l("Lpa%s:", K.c_str());
     }
     e.drain();
     if (sched) e.o = e.o.substr(0, body_at) + schedule(e.o.substr(body_at));
@@ -1668,7 +1674,112 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_cbranch_scc1 %s", xs.c_str());
       go(fall, preload);
     };
-    if (lop == OP_CALL) {
+    // Inlined call: a leaf callee that is one compiled run ending in its return runs in
+    // this run's code, its cells `off` = L - fb higher (above the caller's live cells,
+    // which therefore need no spill), its arguments already in place at L.., its result
+    // moved to L.., and the caller goes on after its POST_CALL (no call-stack traffic, no
+    // return-record check). A leave inside the callee first makes the call real (spill,
+    // return record, callee cells down to fb) so the C++ step meets the reference layout.
+    const bool inl_env = !(getenv("WB_INLINE") && getenv("WB_INLINE")[0] == '0');
+    int64_t inl_f = -1, inl_post = -1;
+    if (lop == OP_CALL && !cost && inl_env && start.count(tgt)) {
+      const JitRun &rf = runs[start[tgt]];
+      const uint32_t L = last.w1 & 0xFFFFu, fb = P.global_cells;
+      const uint32_t off = L - fb;
+      auto nx = fentry.upper_bound(tgt);
+      const uint32_t fend = nx == fentry.end() ? uint32_t(P.code.size()) : nx->first;
+      // (a call enters past its callee's ZERO_LOCALS: the call zeroes the locals itself)
+      bool ok = op_of(P.code[rf.pc + rf.len - 1]) == OP_RET && rf.pc + rf.len == fend &&
+                func_of(tgt) >= 0 && L >= fb && off % 2 == 0 && off < 255 &&
+                uint64_t(P.total_cells()) + off <= TC_VF_CELLS;
+      for (uint32_t i = 0; ok && i + 1 < rf.len; i++) {
+        const uint16_t o = op_of(P.code[rf.pc + i]);
+        ok = !ends_run(o) && o != OP_POST_CALL;
+      }
+      auto pm = start.find(e.pc + 1);
+      ok = ok && pm != start.end() && op_of(P.code[e.pc + 1]) == OP_POST_CALL &&
+           (P.code[e.pc + 1].w1 & 0xFFFFu) == L;
+      if (ok) { inl_f = int64_t(start[tgt]); inl_post = int64_t(pm->second); }
+    }
+    if (inl_f >= 0) {
+      const JitRun &rf = runs[size_t(inl_f)];
+      const uint32_t L = last.w1 & 0xFFFFu, nargs = last.w1 >> 16, nloc = last.w2 & 0xFFFFu;
+      const uint32_t fb = P.global_cells, off = L - fb, n = L - fb, callpc = e.pc;
+      const std::string IK = "i" + K;
+      // the real call's LDS check first: a call that would pass the LDS part of the call
+      // stack leaves before the CALL (the C++ step makes it), as without inlining
+      e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
+      e.l("v_cmp_lt_u32_e64 %s, s93, %s", T2, X0);
+      e.leave_if_t2();
+      const std::vector<uint8_t> dead = dead_zeros(P, rf);
+      Em ei;
+      ei.g = glog;
+      ei.run = uint32_t(runs.size() + k);   // (labels apart from every real run's)
+      ei.fb = fb;
+      ei.prog = &P;
+      ei.shift = off;
+      ei.done = r.cnt;                      // counted before the callee: the caller's run
+      for (uint32_t q = 0; q < nloc; q++)
+        if (dead.empty() || !dead[fb + nargs + q]) ei.l("v_mov_b32 %s, 0", ei.v(fb + nargs + q));
+      std::vector<int> lead2;
+      const std::vector<MemGroup> groups2 = jit_groups(P, rf, &lead2);
+      const size_t body2 = ei.o.size();
+      for (uint32_t i = 0; i + 1 < rf.len; i++) {
+        const DInstr &I = P.code[rf.pc + i];
+        ei.pc = rf.pc + i;
+        ei.group = lead2[i] >= 0 ? &groups2[size_t(lead2[i])] : nullptr;
+        if (!emit(ei, I)) return "";
+        ei.done += (I.w0 >> 16) & 0xFFu;
+      }
+      ei.drain();
+      ei.group = nullptr;
+      if (sched) ei.o = ei.o.substr(0, body2) + schedule(ei.o.substr(body2));
+      // the return: results (shifted cells a..) to L.., every instruction counted, on after
+      // the caller's POST_CALL (its run's banks as that run would have loaded them)
+      const DInstr &rt = P.code[rf.pc + rf.len - 1];
+      const uint32_t ra = rt.w1 & 0xFFFFu, nres = rt.w1 >> 16;
+      for (uint32_t q = 0; q < nres; q++)
+        ei.l("v_mov_b32 v%u, %s", 128 + L + q, ei.v(ra + q));
+      ei.l("s_add_u32 s65, s65, 0x%x", r.cnt + rf.cnt);
+      {
+        const JitRun &rp = runs[size_t(inl_post)];
+        const DInstr &pl = P.code[rp.pc + rp.len - 1];
+        const uint16_t plo = op_of(pl);
+        const uint32_t ptgt = (plo == OP_CALL || is_branch_op(plo)) ? pl.w3 : 0;
+        const uint32_t ppre = plo == OP_CALL ? ptgt : rp.pc + rp.len;
+        if (plo != OP_RET && plo != OP_JMP && plo != OP_BR_TABLE && !start.count(ppre)) {
+          ei.l("s_waitcnt lgkmcnt(0)");
+          ei.l("s_mov_b32 s68, 0x%x", ppre * 32u);
+          ei.l("s_load_dwordx8 s[76:83], s[60:61], s68");
+          ei.l("s_load_dwordx8 s[84:91], s[60:61], s68 offset:0x20");
+        }
+      }
+      ei.l("s_mov_b32 s62, 0x%x", (callpc + 1) * 32u);
+      long_jump(ei, "Lpa" + std::to_string(inl_post), "Lpq" + IK);
+      // leaves inside the callee: make the call real first
+      std::string deopt;
+      {
+        Em d;
+        d.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+        for (uint32_t q = 0; q < n; q++) d.l("ds_write_b32 %s, v%u offset:%u", X1, 128 + fb + q, q * 256u);
+        d.l("v_mov_b32 %s, 0x%x", Y1, ((callpc + 1) & 0xFFFFFu) | (L << 20));
+        d.l("ds_write_b32 %s, %s offset:%u", X1, Y1, n * 256u);
+        d.l("v_add_u32_e32 v102, %u, v102", n + 1);
+        for (uint32_t c = fb; c < P.total_cells(); c++) d.l("v_mov_b32 v%u, v%u", 128 + c, 128 + c + off);
+        deopt = d.o;
+      }
+      ei.o += ei.tail;
+      for (const auto &st : ei.stubs) {
+        ei.o += st.lab + ":\n" + deopt;
+        ei.l("s_mov_b32 s62, 0x%x", st.pc * 32u);
+        ei.l("s_add_u32 s65, s65, 0x%x", st.done);
+        ei.l("s_setpc_b64 s[70:71]");
+      }
+      extra += ei.o;
+      e.l("s_add_u32 s65, s65, 0");   // (the callee's block counts the caller's run)
+      long_jump(e, "Li" + IK, "Liq" + IK);
+      extra = "Li" + IK + ":\n" + extra;
+    } else if (lop == OP_CALL) {
       std::vector<uint8_t> dead;
       if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
       emit_call(e, last, e.pc, dead.empty() ? nullptr : &dead);
@@ -1692,7 +1803,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         x.l("s_cbranch_vccnz %s", rout.c_str());
         x.l("v_subrev_u32_e32 v102, 1, v102");
         for (uint32_t q = 0; q < nres; q++)
-          if (a != fb) x.l("v_mov_b32 %s, %s", Em::V(fb + q).c_str(), Em::V(a + q).c_str());
+          if (a != fb) x.l("v_mov_b32 %s, %s", x.V(fb + q).c_str(), x.V(a + q).c_str());
         x.l("v_mov_b32 %s, %s", VPC, X0);
         x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
         flush(x);
