@@ -1,0 +1,91 @@
+"""Loop-carried memory forwarding in the compiled runs (jit.cpp "Loop-carried memory
+forwarding", DESIGN.md "Compiled runs").
+
+A loop whose body calls an inlined leaf that reads and writes constant addresses gets a
+second copy of its run in which the callee's loads are register moves (the words the
+previous trip stored or loaded). These modules vary what the addresses do -- disjoint
+words, a word one access stores and another loads (same address through different
+cells), misaligned words (no forwarding: every trip leaves to the C++ step), words past
+the one page of memory (every lane traps in the first trip) -- with per-lane trip counts
+so that lanes leave the loop at different trips (the copies' split paths), and check
+every lane against the oracle bit for bit with forwarding on and off."""
+import ctypes
+import os
+
+import pytest
+
+import oracle_py as O
+from helpers import compare, gpu_run
+from wasmedge_amd.wat import assemble
+
+I32 = 0x7F
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROWS = [[(i * 2654435761 + 12345) & 0xFFFFFFFF] for i in range(160)]
+CASES = [(64, 96), (64, 68), (64, 66), (65528, 96)]
+
+
+def loop_module(a, b):
+    return assemble(r"""
+(module
+  (memory 1)
+  (func $leaf (param $a i32) (param $b i32) (param $x i32) (result i32)
+    (local $t i32) (local $u i32)
+    (local.set $t (i32.load offset=0 (local.get $a)))
+    (local.set $u (i32.load offset=4 (local.get $b)))
+    (i32.store offset=0 (local.get $b) (i32.add (local.get $t) (local.get $x)))
+    (i32.store offset=8 (local.get $a) (i32.xor (i32.rotl (local.get $u) (i32.const 5)) (local.get $t)))
+    (i32.add (i32.load offset=8 (local.get $a)) (local.get $u)))
+  (func (export "run") (param $s i32) (result i32)
+    (local $i i32) (local $acc i32) (local $n i32) (local $pad i32)
+    (i32.store (i32.const 64) (local.get $s))
+    (i32.store (i32.const 100) (i32.mul (local.get $s) (i32.const 7)))
+    (local.set $n (i32.add (i32.const 3) (i32.rem_u (local.get $s) (i32.const 29))))
+    (loop $l
+      (local.set $acc (i32.add (local.get $acc)
+        (call $leaf (i32.const %d) (i32.const %d) (local.get $i))))
+      (local.set $i (i32.add (local.get $i) (i32.const 1)))
+      (br_if $l (i32.lt_u (local.get $i) (local.get $n))))
+    (i32.add (local.get $acc) (i32.load (i32.const 96)))))
+""" % (a, b))
+
+
+def _copies(wasm):
+    """forwarding copies of the compiled SIMT code (wb_jit_check's dump: labels Lb<k>c)"""
+    L = ctypes.CDLL(os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch.so"))
+    L.wb_jit_check.restype = ctypes.c_int
+    L.wb_jit_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p, ctypes.c_uint32]
+    path = "/tmp/wb_fwd_%d.s" % os.getpid()
+    os.environ["WB_JIT_DUMP_SIMT"] = path
+    try:
+        err = ctypes.create_string_buffer(4096)
+        assert L.wb_jit_check(wasm, len(wasm), 0, None, err, 4096) >= 0, err.value
+        src = open(path).read()
+        return sum(1 for ln in src.splitlines() if ln.strip().startswith('"Lb') and 'c:' in ln)
+    finally:
+        os.environ.pop("WB_JIT_DUMP_SIMT", None)
+
+
+def test_forwarding_copies(built):
+    """aligned disjoint or coinciding words forward; misaligned ones do not"""
+    got = [_copies(loop_module(a, b)) for a, b in CASES]
+    assert got[0] == 1 and got[1] == 1 and got[2] == 0, got
+
+
+def test_loop_modules_trap_and_succeed():
+    codes = set()
+    for a, b in CASES:
+        m = O.Module(loop_module(a, b))
+        codes |= {m.run("run", r)[0] for r in ROWS[:8]}
+    assert 0 in codes and 0x88 in codes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fwd", ["1", "0"])
+def test_gpu_forwarding_bit_exact(built, monkeypatch, fwd):
+    monkeypatch.setenv("WB_FWD", fwd)
+    for a, b in CASES:
+        wasm = loop_module(a, b)
+        ref = [O.Module(wasm).run("run", r) for r in ROWS]
+        rets, st, cnt, h = gpu_run(wasm, "run", ROWS, [I32], [I32])
+        assert compare(ref, rets, st, cnt, h, [I32], exact=True) == [], (a, b)

@@ -72,6 +72,14 @@ struct Em {
   bool metered = false;
   bool pend[256] = {};   // cells with a global load in flight
   bool any = false;
+  // Counted waits: vector-memory operations complete in issue order (loads and stores
+  // alike: MI355X_MICROARCH.md "vmcnt"), so waiting for the load into cell c leaves the
+  // operations issued after it in flight: vmcnt(nvm - 1 - seq[c]). nvm counts the
+  // operations this code issued since its last vmcnt(0) (code that issues others waits
+  // for them itself, which only makes these counts stricter).
+  uint32_t seq[256] = {};
+  uint32_t nvm = 0;
+  uint32_t basev = 122;   // the current access group's base pair (BASE or v[124:125])
   struct Stub { std::string lab; uint32_t pc, done; uint64_t cdone; };
   std::vector<Stub> stubs;
   const struct MemGroup *group = nullptr;   // set on a group's first access (group_check)
@@ -112,14 +120,33 @@ struct Em {
   // wait for loads in flight into any of these cells (read after load, write after load)
   void sync(std::initializer_list<uint32_t> cells) {
     if (!any) return;
+    int64_t last = -1;
     for (uint32_t c : cells)
-      if (c < 256 && pend[c]) { drain(); return; }
+      if (c < 256 && pend[c]) last = std::max<int64_t>(last, seq[c]);
+    if (last < 0) return;
+    const int64_t younger = int64_t(nvm) - 1 - last;
+    if (younger <= 0) { drain(); return; }
+    l("s_waitcnt vmcnt(%d)", int(std::min<int64_t>(younger, 63)));
+    any = false;
+    for (uint32_t c = 0; c < 256; c++) {
+      if (pend[c] && seq[c] <= uint64_t(last)) pend[c] = false;
+      any = any || pend[c];
+    }
   }
   void drain() {
     if (!any) return;
     l("s_waitcnt vmcnt(0)");
     for (bool &b : pend) b = false;
     any = false;
+    nvm = 0;
+  }
+  void loaded(uint32_t c) {   // a global load into cell c was just issued
+    pend[c] = any = true;
+    seq[c] = nvm++;
+  }
+  std::string base(int half = -1) const {   // the group's base pair, or one half of it
+    if (half < 0) return "v[" + std::to_string(basev) + ":" + std::to_string(basev + 1) + "]";
+    return "v" + std::to_string(basev + uint32_t(half));
   }
   // the lanes' gas total (v[96:97]) += c
   void gas_add(uint64_t c) {
@@ -251,7 +278,7 @@ struct Em {
 // past the group's highest stored byte. In the word interleave (g = 0) an aligned word
 // access is at MEM + ea * 64: the group computes MEM + a * 64 once (BASE) and each access
 // adds offset * 64 in its instruction's offset field.
-const char *const BASE = "v[122:123]", *const BASE0 = "v122", *const BASE1 = "v123";
+// (BASE = v[122:123]; a load batch's second group uses v[124:125]: Em::basev)
 
 struct MemGroup {
   uint32_t base = 0;                // address cell
@@ -283,9 +310,10 @@ void group_check(Em &e, const MemGroup &G) {
     e.l("v_max_u32_e32 %s, %s, %s", HWM, HWM, Y1);
   }
   if (e.g == 0) {
+    const std::string bp = e.base();
     e.l("v_mov_b32 %s, %s", W0, e.v(a));
-    e.l("v_lshlrev_b64 %s, 6, %s", BASE, WP);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", BASE, BASE, MEM);
+    e.l("v_lshlrev_b64 %s, 6, %s", bp.c_str(), WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", bp.c_str(), bp.c_str(), MEM);
   }
 }
 
@@ -295,11 +323,11 @@ void mem_ea(Em &e, uint32_t a, uint32_t imm, uint32_t n, std::string *w1, std::s
   if (e.g == 0 && n >= 4) {
     const uint64_t k = uint64_t(imm) * 64u;
     if (k + (n == 8 ? 256 : 0) <= 4095) {
-      *w1 = std::string(BASE) + ", off offset:" + std::to_string(k);
-      *w2 = std::string(BASE) + ", off offset:" + std::to_string(k + 256);
+      *w1 = e.base() + ", off offset:" + std::to_string(k);
+      *w2 = e.base() + ", off offset:" + std::to_string(k + 256);
     } else {
-      e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(k), BASE0);
-      e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(k >> 32), BASE1);
+      e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(k), e.base(0).c_str());
+      e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(k >> 32), e.base(1).c_str());
       *w1 = std::string(XP) + ", off";
       *w2 = std::string(XP) + ", off offset:256";
     }
@@ -337,14 +365,14 @@ bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
   std::string w1, w2;
   mem_ea(e, a, imm, n, &w1, &w2);
   e.l("%s %s, %s", ins, e.v(c), w1.c_str());
-  e.pend[c] = e.any = true;
+  e.loaded(c);
   if (op == OP_LD64) {
     e.l("global_load_dword %s, %s", e.v(c + 1), w2.c_str());
-    e.pend[c + 1] = true;
+    e.loaded(c + 1);
   } else if (op == OP_LD8U64 || op == OP_LD16U64 || op == OP_LD32U64) {
     e.l("v_mov_b32 %s, 0", e.v(c + 1));
   } else if (wide) {   // sign extension needs the loaded word
-    e.drain();
+    e.sync({c});
     e.l("v_ashrrev_i32_e32 %s, 31, %s", e.v(c + 1), e.v(c));
   }
   return true;
@@ -359,7 +387,11 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm) {
   const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
   const size_t k1 = w1.find(", off"), k2 = w2.find(", off");
   e.l("%s %s, %s%s", ins, w1.substr(0, k1).c_str(), e.v(b), w1.substr(k1).c_str());
-  if (n == 8) e.l("global_store_dword %s, %s%s", w2.substr(0, k2).c_str(), e.v(b + 1), w2.substr(k2).c_str());
+  e.nvm++;
+  if (n == 8) {
+    e.l("global_store_dword %s, %s%s", w2.substr(0, k2).c_str(), e.v(b + 1), w2.substr(k2).c_str());
+    e.nvm++;
+  }
   return true;
 }
 
@@ -891,6 +923,8 @@ bool emit(Em &e, const DInstr &I) {
 struct SIns {
   std::string text;
   std::vector<int> defs, uses;
+  bool wait = false;   // a counted vmcnt wait: defs = the registers of the loads it retires
+  int est = 0;         // (wait) estimated cycle its loads are in
 };
 
 void regs_of(const std::string &tok, std::vector<int> *out) {
@@ -955,12 +989,16 @@ std::string schedule(const std::string &body) {
       std::vector<std::vector<std::pair<int, int>>> pred(n), succ(n);
       std::map<int, int> last_def;
       std::map<int, std::vector<int>> readers;
+      int last_wait = -1;
       for (size_t i = 0; i < n; i++) {
         std::map<int, int> dep;   // pred -> latency
         for (int r : seg[i].uses) {
           auto it = last_def.find(r);
-          if (it != last_def.end()) dep[it->second] = std::max(dep[it->second], kLat);
+          if (it != last_def.end())
+            dep[it->second] = std::max(dep[it->second], seg[size_t(it->second)].wait ? 0 : kLat);
         }
+        if (seg[i].wait && last_wait >= 0) dep[last_wait] = std::max(dep[last_wait], 0);
+        if (seg[i].wait) last_wait = int(i);
         for (int r : seg[i].defs) {
           auto it = last_def.find(r);
           if (it != last_def.end()) dep[it->second] = std::max(dep[it->second], 1);
@@ -978,7 +1016,10 @@ std::string schedule(const std::string &body) {
       for (size_t i = n; i-- > 0;)
         for (auto &s : succ[i]) height[i] = std::max(height[i], height[size_t(s.first)] + s.second);
       std::vector<int> npred(n), at(n, 0);
-      for (size_t i = 0; i < n; i++) npred[i] = int(pred[i].size());
+      for (size_t i = 0; i < n; i++) {
+        npred[i] = int(pred[i].size());
+        if (seg[i].wait) at[i] = seg[i].est;
+      }
       std::vector<int> ready;
       for (size_t i = 0; i < n; i++)
         if (!npred[i]) ready.push_back(int(i));
@@ -995,7 +1036,7 @@ std::string schedule(const std::string &body) {
         const int i = ready[best];
         ready.erase(ready.begin() + long(best));
         const int t = std::max(at[size_t(i)], clock);
-        clock = t + kIssue;
+        clock = seg[size_t(i)].wait ? t : t + kIssue;
         out += seg[size_t(i)].text;
         out += '\n';
         for (auto &s : succ[size_t(i)]) {
@@ -1009,14 +1050,55 @@ std::string schedule(const std::string &body) {
     }
     seg.clear();
   };
+  // Counted waits float: the vector-memory operations issued so far (oldest first, the
+  // registers each load writes) tell which loads an "s_waitcnt vmcnt(N)" retires; the
+  // wait becomes an instruction of the segment that defines those registers, so their
+  // readers stay behind it and independent VALU work moves above it. A label whose
+  // arrivals may differ (anything but an inlined call's Lpa / a NaN fix's Lnr return)
+  // makes the state unknown until the next full wait, and waits then stay barriers.
+  constexpr int kLoadLat = 100, kLoadStep = 22;   // cycles: first L2-hit load, each further
+  std::vector<std::vector<int>> vq;   // operations in flight, oldest first
+  bool known = true;
+  int retired = 0;                    // loads retired by this segment's waits so far
   for (const auto &ln : lines) {
     SIns ins;
     if (parse_valu(ln, &ins)) {
       seg.push_back(std::move(ins));
-    } else {
-      flush();
-      out += ln;
-      out += '\n';
+      continue;
+    }
+    int nwait = -1;
+    if (ln.compare(0, 16, "s_waitcnt vmcnt(") == 0 && ln.find("lgkmcnt") == std::string::npos)
+      nwait = atoi(ln.c_str() + 16);
+    if (nwait >= 0 && known) {
+      SIns w;
+      w.text = ln;
+      w.wait = true;
+      while (vq.size() > size_t(nwait)) {
+        for (int r : vq.front()) w.defs.push_back(r);
+        vq.erase(vq.begin());
+        retired++;
+      }
+      w.est = kLoadLat + kLoadStep * retired;
+      seg.push_back(std::move(w));
+      continue;
+    }
+    flush();
+    retired = 0;
+    out += ln;
+    out += '\n';
+    if (ln.compare(0, 11, "global_load") == 0) {
+      std::vector<int> d;
+      const size_t sp = ln.find(' '), cm = ln.find(',');
+      if (sp != std::string::npos && cm != std::string::npos) regs_of(ln.substr(sp + 1, cm - sp - 1), &d);
+      vq.push_back(d);
+    } else if (ln.compare(0, 7, "global_") == 0 || ln.compare(0, 7, "buffer_") == 0) {
+      vq.push_back({});
+    } else if (ln.find("vmcnt(0)") != std::string::npos) {
+      vq.clear();
+      known = true;
+    } else if (!ln.empty() && ln.back() == ':' && ln.compare(0, 3, "Lpa") != 0 &&
+               ln.compare(0, 3, "Lnr") != 0) {
+      known = false;
     }
   }
   flush();
@@ -1072,6 +1154,113 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
     if (open >= 0 && std::find(wr.begin(), wr.end(), G[size_t(open)].base) != wr.end()) open = -1;
   }
   return G;
+}
+
+// Load batches: a run's consecutive loads (BLAKE3's 16 message and 8 chaining words) are
+// issued in the order the rest of the run first needs them, so that counted waits
+// (Em::sync) let the first uses start while later words still stream in (one wave per
+// SIMD: each further L2-hit load waited for costs ~22 cycles, MI355X_MICROARCH.md).
+// Every group of the batch is checked first; a failing check leaves before the batch's
+// first load (nothing of the batch has happened yet, and the C++ step or the handlers
+// then meet the failing access in program order). A batch is at most two groups (base
+// pairs v[122:123], v[124:125]) and no load of it writes a cell another one reads or
+// writes.
+struct LoadBatch {
+  uint32_t i0 = 0, i1 = 0;       // run body indices [i0, i1)
+  std::vector<uint32_t> order;   // issue order (body indices)
+};
+
+bool is_store_op(uint16_t op) { return op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64; }
+
+bool load_wide(uint16_t op) {
+  return op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
+         op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
+}
+
+// an operand field naming the cell (or the cell below it: a 64-bit operand's high word);
+// only the batch's issue order depends on it
+bool mentions(const DInstr &I, uint32_t cell) {
+  const uint32_t f[5] = {I.w1 & 0xFFFFu, I.w1 >> 16, I.w2 & 0xFFFFu, I.w2 >> 16,
+                         op_of(I) == OP_I32_ADD3_XROTR_I ? (I.w3 & 0xFFFFu) : 0xFFFFu};
+  for (uint32_t x : f)
+    if (x != 0xFFFFu && (cell == x || cell == x + 1)) return true;
+  return false;
+}
+
+std::vector<LoadBatch> load_batches(const Program &P, const JitRun &r, uint32_t nbody,
+                                    const std::vector<int> &lead) {
+  std::vector<LoadBatch> out;
+  auto is_load = [&](uint32_t i) {
+    const uint16_t op = op_of(P.code[r.pc + i]);
+    return mem_bytes(op) && !is_store_op(op);
+  };
+  for (uint32_t i = 0; i < nbody;) {
+    if (!is_load(i) || lead[i] < 0) { i++; continue; }
+    std::vector<uint32_t> addr, dest;
+    uint32_t j = i, leads = 0;
+    for (; j < nbody && is_load(j); j++) {
+      const DInstr &I = P.code[r.pc + j];
+      const uint32_t a = I.w1 & 0xFFFFu, c = I.w2 & 0xFFFFu, nc = load_wide(op_of(I)) ? 2 : 1;
+      if (lead[j] >= 0 && ++leads > 2) break;
+      bool clash = std::find(dest.begin(), dest.end(), a) != dest.end();
+      for (uint32_t q = 0; q < nc; q++)
+        clash = clash || std::find(dest.begin(), dest.end(), c + q) != dest.end() ||
+                std::find(addr.begin(), addr.end(), c + q) != addr.end();
+      if (clash) break;
+      addr.push_back(a);
+      for (uint32_t q = 0; q < nc; q++) dest.push_back(c + q);
+    }
+    if (j - i >= 2) {
+      LoadBatch b;
+      b.i0 = i;
+      b.i1 = j;
+      std::vector<std::pair<uint32_t, uint32_t>> key;   // (first use, index)
+      for (uint32_t k = i; k < j; k++) {
+        const DInstr &I = P.code[r.pc + k];
+        const uint32_t c = I.w2 & 0xFFFFu, nc = load_wide(op_of(I)) ? 2 : 1;
+        uint32_t t = j;
+        for (; t < r.len; t++) {
+          bool m = false;
+          for (uint32_t q = 0; q < nc; q++) m = m || mentions(P.code[r.pc + t], c + q);
+          if (m) break;
+        }
+        key.push_back({t, k});
+      }
+      std::stable_sort(key.begin(), key.end(),
+                       [](const std::pair<uint32_t, uint32_t> &x, const std::pair<uint32_t, uint32_t> &y) {
+                         return x.first < y.first;
+                       });
+      for (auto &kv : key) b.order.push_back(kv.second);
+      out.push_back(std::move(b));
+    }
+    i = j;
+  }
+  return out;
+}
+
+bool emit(Em &e, const DInstr &I);
+
+// the batch's checks (leaving before its first load), then its loads in issue order
+void emit_batch(Em &e, const Program &P, uint32_t rpc, const LoadBatch &b,
+                const std::vector<MemGroup> &G, const std::vector<int> &lead) {
+  std::vector<uint32_t> bv(b.i1 - b.i0, 122);
+  uint32_t groups = 0;
+  e.pc = rpc + b.i0;
+  for (uint32_t k = b.i0; k < b.i1; k++) {
+    if (lead[k] >= 0) {
+      e.basev = groups++ ? 124 : 122;
+      group_check(e, G[size_t(lead[k])]);
+    }
+    bv[k - b.i0] = e.basev;
+  }
+  e.group = nullptr;
+  for (uint32_t k : b.order) {
+    e.pc = rpc + k;
+    e.basev = bv[k - b.i0];
+    emit(e, P.code[rpc + k]);
+  }
+  e.basev = bv.back();   // (the group still open after the batch)
+  e.pc = rpc + b.i1 - 1;
 }
 
 // CALL (gen_tc.py call_body_v): spill [fb, L) and the return record to the LDS call
@@ -1510,6 +1699,124 @@ void scan_loop_block(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
   e.l("Lbo%s:", K.c_str());
 }
 
+// the cells an instruction writes, exactly for the 32-bit results (written() counts c + 1
+// too), else as written()
+void written_exact(const DInstr &I, std::vector<uint32_t> *out) {
+  const uint32_t c = I.w2 & 0xFFFFu;
+  switch (op_of(I)) {
+    case OP_I32_ADD: case OP_I32_ADD3: case OP_I32_ADD_I: case OP_I32_AND: case OP_I32_AND_I:
+    case OP_I32_CLZ: case OP_I32_CTZ: case OP_I32_EQ: case OP_I32_EQZ: case OP_I32_EQ_I:
+    case OP_I32_EXT16S: case OP_I32_EXT8S: case OP_I32_GE_S: case OP_I32_GE_S_I:
+    case OP_I32_GE_U: case OP_I32_GE_U_I: case OP_I32_GT_S: case OP_I32_GT_S_I:
+    case OP_I32_GT_U: case OP_I32_GT_U_I: case OP_I32_LE_S: case OP_I32_LE_S_I:
+    case OP_I32_LE_U: case OP_I32_LE_U_I: case OP_I32_LT_S: case OP_I32_LT_S_I:
+    case OP_I32_LT_U: case OP_I32_LT_U_I: case OP_I32_MUL: case OP_I32_MUL_I: case OP_I32_NE:
+    case OP_I32_NE_I: case OP_I32_OR: case OP_I32_OR_I: case OP_I32_POPCNT: case OP_I32_ROTL:
+    case OP_I32_ROTL_I: case OP_I32_ROTR: case OP_I32_ROTR_I: case OP_I32_SHL:
+    case OP_I32_SHL_I: case OP_I32_SHR_S: case OP_I32_SHR_S_I: case OP_I32_SHR_U:
+    case OP_I32_SHR_U_I: case OP_I32_SUB: case OP_I32_SUB_I: case OP_I32_XOR:
+    case OP_I32_XOR_I: case OP_I32_XOR_ROTL_I: case OP_I32_XOR_ROTR_I: case OP_CONST32:
+    case OP_MOV32: case OP_LD32: case OP_LD8S32: case OP_LD8U32: case OP_LD16S32:
+    case OP_LD16U32:
+      out->assign(1, c);
+      return;
+    case OP_I32_ADD_XROTR_I: *out = {c, I.w2 >> 16}; return;
+    case OP_I32_ADD3_XROTR_I: *out = {c, I.w3 & 0xFFFFu}; return;
+    default: written(I, out);
+  }
+}
+
+// Loop-carried memory forwarding. A loop whose body is a run R ending in an inlined leaf
+// call and the post-call run Pp branching back to R's start (C2: the chain loop around
+// BLAKE3's compression) reads the words its previous trip stored or loaded: the callee's
+// 32-bit accesses all go to constant addresses (i32.const arguments, params never
+// written) and nothing else on the loop touches memory. Every access then also keeps its
+// word in a VGPR above every cell (F); the inlined call's end goes on in a copy of Pp
+// (suffix p) whose taken branch enters a copy of R (suffix c) where the callee's loads
+// are moves from F: no loads, hence no waits behind the previous trip's stores (vmcnt
+// retires in issue order). Stores stay real (memory is always current) and a copy's
+// lanes are the group that ran the trip before (the fast path keeps exec), so every
+// lane's F words are its own memory's. The c copy skips the load-only groups' checks:
+// the first trip, in R, checked the same constant addresses and memory never shrinks.
+struct FwdPlan {
+  size_t post = 0;                                       // Pp (run index)
+  std::vector<int64_t> addr;                             // callee body index -> address
+  std::map<uint32_t, uint32_t> freg;                     // address -> VGPR
+  std::vector<std::pair<uint32_t, uint32_t>> end_copy;   // (VGPR, physical cell)
+  std::vector<uint8_t> copy_now;   // body index: a load whose cell changes later (copy at once)
+};
+
+bool fwd_plan(const Program &P, const std::vector<JitRun> &runs, size_t k, size_t f, size_t post,
+              FwdPlan *out) {
+  const JitRun &R = runs[k], &F = runs[f], &Q = runs[post];
+  const DInstr &call = P.code[R.pc + R.len - 1], &br = P.code[Q.pc + Q.len - 1];
+  if (!is_branch_op(op_of(br)) || br.w3 != R.pc) return false;
+  const uint32_t fb = P.global_cells, L = call.w1 & 0xFFFFu, off = L - fb;
+  for (uint32_t i = 0; i < Q.len; i++)
+    if (mem_bytes(op_of(P.code[Q.pc + i]))) return false;
+  std::map<uint32_t, uint32_t> cst;   // physical cell -> constant
+  std::vector<uint32_t> wr;
+  auto step = [&](const DInstr &I, uint32_t sh) {
+    const uint16_t op = op_of(I);
+    const uint32_t a = I.w1 & 0xFFFFu, c = I.w2 & 0xFFFFu;
+    auto ph = [&](uint32_t x) { return x >= fb ? x + sh : x; };
+    if (op == OP_CONST32) { cst[ph(c)] = I.w3; return; }
+    if (op == OP_MOV32 && cst.count(ph(a))) { cst[ph(c)] = cst[ph(a)]; return; }
+    written_exact(I, &wr);
+    for (uint32_t x : wr) cst.erase(ph(x));
+  };
+  for (uint32_t i = 0; i + 1 < R.len; i++) {
+    if (mem_bytes(op_of(P.code[R.pc + i]))) return false;
+    step(P.code[R.pc + i], 0);
+  }
+  const uint32_t nloc = call.w2 & 0xFFFFu, nargs = call.w1 >> 16;
+  for (uint32_t q = 0; q < nloc; q++) cst.erase(L + nargs + q);   // (the callee's zeroed locals)
+  out->post = post;
+  out->addr.assign(F.len, -1);
+  out->copy_now.assign(F.len, 0);
+  std::map<uint32_t, std::pair<bool, uint32_t>> lastacc;   // address -> (load, body index)
+  for (uint32_t i = 0; i + 1 < F.len; i++) {
+    const DInstr &I = P.code[F.pc + i];
+    const uint16_t op = op_of(I);
+    if (mem_bytes(op)) {
+      const uint32_t a = I.w1 & 0xFFFFu, pa = a >= fb ? a + off : a;
+      if ((op != OP_LD32 && op != OP_ST32) || !cst.count(pa)) return false;
+      const uint64_t A = uint64_t(cst[pa]) + I.w3;
+      if ((A & 3) || A + 4 > 0xFFFFFFFFull) return false;
+      out->addr[i] = int64_t(A);
+      lastacc[uint32_t(A)] = {op == OP_LD32, i};
+    }
+    step(I, off);
+  }
+  uint32_t prev = 0;
+  bool first = true;
+  for (auto &kv : lastacc) {   // (ordered) distinct words must not overlap
+    if (!first && kv.first - prev < 4) return false;
+    prev = kv.first;
+    first = false;
+  }
+  const uint32_t base = uint32_t(P.total_cells()) + off;
+  if (lastacc.empty() || lastacc.size() > 64 || base + lastacc.size() > TC_VF_CELLS) return false;
+  uint32_t n = 0;
+  for (auto &kv : lastacc) {
+    const uint32_t v = 128 + base + n++;
+    out->freg[kv.first] = v;
+    if (!kv.second.first) continue;
+    // a word last loaded: copied at the callee's end if its cell still holds it then,
+    // else right after the load
+    const DInstr &ld = P.code[F.pc + kv.second.second];
+    const uint32_t c = ld.w2 & 0xFFFFu;
+    bool kept = true;
+    for (uint32_t i = kv.second.second + 1; kept && i + 1 < F.len; i++) {
+      written_exact(P.code[F.pc + i], &wr);
+      kept = std::find(wr.begin(), wr.end(), c) == wr.end();
+    }
+    if (kept) out->end_copy.push_back({v, c >= fb ? c + off : c});
+    else out->copy_now[kv.second.second] = 1;
+  }
+  return true;
+}
+
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost, bool simt) {
   if (cost) simt = false;
@@ -1520,6 +1827,8 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   const unsigned sx = simt ? (sxe ? unsigned(atoi(sxe)) : 7u) : 0u;
   const char *se = getenv("WB_JIT_SCHED");   // 0: keep program order (A/B measurement aid)
   const bool sched = !(se && se[0] == '0');
+  const char *lbe = getenv("WB_LOAD_BATCH");   // 0: loads in program order (A/B aid)
+  const bool batching = !(lbe && lbe[0] == '0');
   // One asm statement holds every run (behind a jump) and a table of their offsets from
   // the table itself; the kernel reads the table and writes the absolute addresses.
   std::string body;
@@ -1546,12 +1855,65 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const int64_t f = func_of(P.code[pc].w3);
       if (f >= 0) ret_sites[uint32_t(f)].push_back(pc + 1);
     }
-  for (size_t k = 0; k < runs.size(); k++) {
+  // Inlined call: a leaf callee that is one compiled run ending in its return runs in
+  // the calling run's code, its cells `off` = L - fb higher (above the caller's live
+  // cells, which therefore need no spill), its arguments already in place at L.., its
+  // result moved to L.., and the caller goes on after its POST_CALL (no call-stack
+  // traffic, no return-record check). A leave inside the callee first makes the call real
+  // (spill, return record, callee cells down to fb) so the C++ step meets the reference
+  // layout. inline_of: the callee's run and the post-call run, or -1.
+  const bool inl_env = !(getenv("WB_INLINE") && getenv("WB_INLINE")[0] == '0');
+  auto inline_of = [&](size_t k, int64_t *inl_f, int64_t *inl_post) {
+    *inl_f = *inl_post = -1;
+    const JitRun &r = runs[k];
+    const DInstr &last = P.code[r.pc + r.len - 1];
+    const uint32_t tgt = last.w3, cpc = r.pc + r.len - 1;
+    if (op_of(last) != OP_CALL || cost || !inl_env || !start.count(tgt)) return;
+    const JitRun &rf = runs[start[tgt]];
+    const uint32_t L = last.w1 & 0xFFFFu, fb = P.global_cells;
+    const uint32_t off = L - fb;
+    auto nx = fentry.upper_bound(tgt);
+    const uint32_t fend = nx == fentry.end() ? uint32_t(P.code.size()) : nx->first;
+    // (a call enters past its callee's ZERO_LOCALS: the call zeroes the locals itself)
+    bool ok = op_of(P.code[rf.pc + rf.len - 1]) == OP_RET && rf.pc + rf.len == fend &&
+              func_of(tgt) >= 0 && L >= fb && off % 2 == 0 && off < 255 &&
+              uint64_t(P.total_cells()) + off <= TC_VF_CELLS;
+    for (uint32_t i = 0; ok && i + 1 < rf.len; i++) {
+      const uint16_t o = op_of(P.code[rf.pc + i]);
+      ok = !ends_run(o) && o != OP_POST_CALL;
+    }
+    auto pm = start.find(cpc + 1);
+    ok = ok && pm != start.end() && op_of(P.code[cpc + 1]) == OP_POST_CALL &&
+         (P.code[cpc + 1].w1 & 0xFFFFu) == L;
+    if (ok) { *inl_f = int64_t(start[tgt]); *inl_post = int64_t(pm->second); }
+  };
+  // runs compiled twice more for loop-carried forwarding (FwdPlan): (k, 0) every run,
+  // (R, 1) the copy entered with F valid, (Pp, 2) the post-call copy that enters it
+  const char *fwe = getenv("WB_FWD");   // 0: no forwarding copies (A/B aid)
+  std::map<size_t, FwdPlan> plans;      // R -> plan
+  std::map<size_t, size_t> loop_of;     // Pp -> R
+  std::vector<std::pair<size_t, int>> jobs;
+  for (size_t k = 0; k < runs.size(); k++) jobs.push_back({k, 0});
+  for (size_t k = 0; k < runs.size() && !(fwe && fwe[0] == '0'); k++) {
+    int64_t f, post;
+    inline_of(k, &f, &post);
+    FwdPlan pl;
+    if (f < 0 || loop_of.count(size_t(post)) || size_t(post) == k ||
+        !fwd_plan(P, runs, k, size_t(f), size_t(post), &pl))
+      continue;
+    plans[k] = pl;
+    loop_of[size_t(post)] = k;
+    jobs.push_back({k, 1});
+    jobs.push_back({size_t(post), 2});
+  }
+  for (size_t jb = 0; jb < jobs.size(); jb++) {
+    const size_t k = jobs[jb].first;
+    const int var = jobs[jb].second;
     const JitRun &r = runs[k];
     Em e;
     e.g = glog;
-    e.run = uint32_t(k);
-    const std::string K = std::to_string(k);
+    e.run = uint32_t(k + size_t(var) * 2 * runs.size());   // (stub labels apart)
+    const std::string K = std::to_string(k) + (var == 1 ? "c" : var == 2 ? "p" : "");
     e.l(".p2align 6");
     ScanLoop sl;
     // Scan blocks are opt-in (WB_SCAN=1; WB_SCAN=p+1: only the loop at pc p): measured on
@@ -1559,7 +1921,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     // scans over random data stop after ~2 iterations, so the 8 speculative loads and the
     // exit search cost more than the latency they hide.
     const char *sce = getenv("WB_SCAN");
-    const bool scan = simt && !cost && sce && atoi(sce) >= 1 &&
+    const bool scan = var == 0 && simt && !cost && sce && atoi(sce) >= 1 &&
                       (atoi(sce) == 1 || uint32_t(atoi(sce)) == r.pc + 1) && scan_loop_of(P, r, &sl);
     if (scan) {
       e.g = glog;
@@ -1611,7 +1973,20 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const size_t body_at = e.o.size();
     const std::string xs = "Lxs" + K;
     const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
+    const std::vector<LoadBatch> batches = batching ? load_batches(P, r, nbody, lead)
+                                                    : std::vector<LoadBatch>();
+    size_t nb = 0;
     for (uint32_t i = 0; i < nbody; i++) {
+      if (nb < batches.size() && batches[nb].i0 == i) {
+        const LoadBatch &b = batches[nb++];
+        emit_batch(e, P, r.pc, b, groups, lead);
+        for (uint32_t k = b.i0; k < b.i1; k++) {
+          e.done += (P.code[r.pc + k].w0 >> 16) & 0xFFu;
+          if (cost) e.cdone += cost->full(P, r.pc + k);
+        }
+        i = b.i1 - 1;
+        continue;
+      }
       const DInstr &I = P.code[r.pc + i];
       e.pc = r.pc + i;
       e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
@@ -1636,12 +2011,15 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("s_add_u32 s68, s62, 0x%x", (runs[it->second].len - 1) * 32u);
         e.l("s_cmp_ge_u32 s68, s63");
         e.l("s_cbranch_scc1 %s", disp.c_str());
-        // (a long jump: the code object can outgrow s_branch's +-128 KiB)
+        // (a long jump: the code object can outgrow s_branch's +-128 KiB); a forwarding
+        // loop's post-call copy enters its run's forwarding copy
         const std::string q = "Lq" + K + "_" + std::to_string(lab);
+        const std::string tl = "Lb" + std::to_string(it->second) +
+                               (var == 2 && loop_of.count(k) && loop_of[k] == it->second ? "c" : "");
         e.l("s_getpc_b64 s[68:69]");
         e.l("%s:", q.c_str());
-        e.l("s_add_u32 s68, s68, Lb%zu - %s", it->second, q.c_str());
-        e.l("s_addc_u32 s69, s69, (Lb%zu - %s) >> 32", it->second, q.c_str());
+        e.l("s_add_u32 s68, s68, %s - %s", tl.c_str(), q.c_str());
+        e.l("s_addc_u32 s69, s69, (%s - %s) >> 32", tl.c_str(), q.c_str());
         e.l("s_setpc_b64 s[68:69]");
         e.l("%s:", disp.c_str());
         banks = false;
@@ -1674,33 +2052,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_cbranch_scc1 %s", xs.c_str());
       go(fall, preload);
     };
-    // Inlined call: a leaf callee that is one compiled run ending in its return runs in
-    // this run's code, its cells `off` = L - fb higher (above the caller's live cells,
-    // which therefore need no spill), its arguments already in place at L.., its result
-    // moved to L.., and the caller goes on after its POST_CALL (no call-stack traffic, no
-    // return-record check). A leave inside the callee first makes the call real (spill,
-    // return record, callee cells down to fb) so the C++ step meets the reference layout.
-    const bool inl_env = !(getenv("WB_INLINE") && getenv("WB_INLINE")[0] == '0');
     int64_t inl_f = -1, inl_post = -1;
-    if (lop == OP_CALL && !cost && inl_env && start.count(tgt)) {
-      const JitRun &rf = runs[start[tgt]];
-      const uint32_t L = last.w1 & 0xFFFFu, fb = P.global_cells;
-      const uint32_t off = L - fb;
-      auto nx = fentry.upper_bound(tgt);
-      const uint32_t fend = nx == fentry.end() ? uint32_t(P.code.size()) : nx->first;
-      // (a call enters past its callee's ZERO_LOCALS: the call zeroes the locals itself)
-      bool ok = op_of(P.code[rf.pc + rf.len - 1]) == OP_RET && rf.pc + rf.len == fend &&
-                func_of(tgt) >= 0 && L >= fb && off % 2 == 0 && off < 255 &&
-                uint64_t(P.total_cells()) + off <= TC_VF_CELLS;
-      for (uint32_t i = 0; ok && i + 1 < rf.len; i++) {
-        const uint16_t o = op_of(P.code[rf.pc + i]);
-        ok = !ends_run(o) && o != OP_POST_CALL;
-      }
-      auto pm = start.find(e.pc + 1);
-      ok = ok && pm != start.end() && op_of(P.code[e.pc + 1]) == OP_POST_CALL &&
-           (P.code[e.pc + 1].w1 & 0xFFFFu) == L;
-      if (ok) { inl_f = int64_t(start[tgt]); inl_post = int64_t(pm->second); }
-    }
+    inline_of(k, &inl_f, &inl_post);
+    const FwdPlan *fwd = plans.count(k) ? &plans[k] : nullptr;
     if (inl_f >= 0) {
       const JitRun &rf = runs[size_t(inl_f)];
       const uint32_t L = last.w1 & 0xFFFFu, nargs = last.w1 >> 16, nloc = last.w2 & 0xFFFFu;
@@ -1714,7 +2068,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const std::vector<uint8_t> dead = dead_zeros(P, rf);
       Em ei;
       ei.g = glog;
-      ei.run = uint32_t(runs.size() + k);   // (labels apart from every real run's)
+      ei.run = e.run + uint32_t(runs.size());   // (labels apart from every real run's)
       ei.fb = fb;
       ei.prog = &P;
       ei.shift = off;
@@ -1724,14 +2078,51 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       std::vector<int> lead2;
       const std::vector<MemGroup> groups2 = jit_groups(P, rf, &lead2);
       const size_t body2 = ei.o.size();
+      const bool fc = fwd && var == 1;   // the forwarding copy: the callee's loads from F
+      const std::vector<LoadBatch> batches2 = batching && !fc ? load_batches(P, rf, rf.len - 1, lead2)
+                                                              : std::vector<LoadBatch>();
+      size_t nb2 = 0;
       for (uint32_t i = 0; i + 1 < rf.len; i++) {
+        if (nb2 < batches2.size() && batches2[nb2].i0 == i) {
+          const LoadBatch &b = batches2[nb2++];
+          emit_batch(ei, P, rf.pc, b, groups2, lead2);
+          for (uint32_t k = b.i0; k < b.i1; k++) {
+            ei.done += (P.code[rf.pc + k].w0 >> 16) & 0xFFu;
+            if (fwd && fwd->copy_now[k]) {
+              const uint32_t c = P.code[rf.pc + k].w2 & 0xFFFFu;
+              ei.sync({c});
+              ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fwd->addr[k])), ei.v(c));
+            }
+          }
+          i = b.i1 - 1;
+          continue;
+        }
         const DInstr &I = P.code[rf.pc + i];
         ei.pc = rf.pc + i;
         ei.group = lead2[i] >= 0 ? &groups2[size_t(lead2[i])] : nullptr;
+        const int64_t fa = fwd ? fwd->addr[i] : -1;
+        if (fa >= 0 && fc && op_of(I) == OP_LD32) {
+          // (a group that also stores still computes its base: its stores use it)
+          if (ei.group && ei.group->store_end) group_check(ei, *ei.group);
+          ei.group = nullptr;
+          const uint32_t c = I.w2 & 0xFFFFu;
+          ei.sync({c});
+          ei.l("v_mov_b32 %s, v%u", ei.v(c), fwd->freg.at(uint32_t(fa)));
+          ei.done += (I.w0 >> 16) & 0xFFu;
+          continue;
+        }
         if (!emit(ei, I)) return "";
+        if (fa >= 0 && op_of(I) == OP_ST32)
+          ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w1 >> 16));
+        if (fa >= 0 && fwd->copy_now[i]) {
+          ei.sync({I.w2 & 0xFFFFu});
+          ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w2 & 0xFFFFu));
+        }
         ei.done += (I.w0 >> 16) & 0xFFu;
       }
       ei.drain();
+      if (fwd && !fc)
+        for (const auto &fc2 : fwd->end_copy) ei.l("v_mov_b32 v%u, v%u", fc2.first, 128 + fc2.second);
       ei.group = nullptr;
       if (sched) ei.o = ei.o.substr(0, body2) + schedule(ei.o.substr(body2));
       // the return: results (shifted cells a..) to L.., every instruction counted, on after
@@ -1755,11 +2146,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         }
       }
       ei.l("s_mov_b32 s62, 0x%x", (callpc + 1) * 32u);
-      long_jump(ei, "Lpa" + std::to_string(inl_post), "Lpq" + IK);
+      long_jump(ei, "Lpa" + std::to_string(inl_post) + (fwd ? "p" : ""), "Lpq" + IK);
       // leaves inside the callee: make the call real first
       std::string deopt;
       {
         Em d;
+        d.l("s_waitcnt vmcnt(0)");   // (the callee's loads in flight land before the moves)
         d.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
         for (uint32_t q = 0; q < n; q++) d.l("ds_write_b32 %s, v%u offset:%u", X1, 128 + fb + q, q * 256u);
         d.l("v_mov_b32 %s, 0x%x", Y1, ((callpc + 1) & 0xFFFFFu) | (L << 20));
