@@ -1478,13 +1478,53 @@ void flush(Em &e) {
   e.l("s_mov_b32 s65, 0");
 }
 
-// jump to label `to` from anywhere in the code object
+// jump to label `to` from anywhere in the code object: a placeholder that resolve_jumps
+// turns into s_branch when the target is surely within its +-128 KiB, else into a
+// pc-relative s_setpc through s[68:69]
 void long_jump(Em &e, const std::string &to, const std::string &tag) {
-  e.l("s_getpc_b64 s[68:69]");
-  e.l("%s:", tag.c_str());
-  e.l("s_add_u32 s68, s68, %s - %s", to.c_str(), tag.c_str());
-  e.l("s_addc_u32 s69, s69, (%s - %s) >> 32", to.c_str(), tag.c_str());
-  e.l("s_setpc_b64 s[68:69]");
+  e.l("LJMP %s %s", to.c_str(), tag.c_str());
+}
+
+std::string resolve_jumps(const std::string &body) {
+  std::vector<std::string> lines;
+  for (size_t at = 0; at < body.size();) {
+    size_t nl = body.find('\n', at);
+    if (nl == std::string::npos) nl = body.size();
+    lines.push_back(body.substr(at, nl - at));
+    at = nl + 1;
+  }
+  // an upper bound on the bytes before each line: 12 per instruction (8 + a literal),
+  // 64 per alignment
+  std::vector<uint64_t> pos(lines.size() + 1, 0);
+  std::map<std::string, size_t> lab;
+  for (size_t i = 0; i < lines.size(); i++) {
+    const std::string &ln = lines[i];
+    uint64_t b = 12;
+    if (ln.empty() || ln[0] == '.') b = ln.compare(0, 8, ".p2align") == 0 ? 64 : 0;
+    if (!ln.empty() && ln.back() == ':') { lab[ln.substr(0, ln.size() - 1)] = i; b = 0; }
+    pos[i + 1] = pos[i] + b;
+  }
+  std::string out;
+  out.reserve(body.size() + body.size() / 4);
+  for (size_t i = 0; i < lines.size(); i++) {
+    const std::string &ln = lines[i];
+    if (ln.compare(0, 5, "LJMP ") != 0) { out += ln; out += '\n'; continue; }
+    const size_t sp = ln.find(' ', 5);
+    const std::string to = ln.substr(5, sp - 5), tag = ln.substr(sp + 1);
+    auto it = lab.find(to);
+    const uint64_t d = it == lab.end() ? ~0ull
+                                       : (pos[it->second] > pos[i] ? pos[it->second] - pos[i]
+                                                                    : pos[i] - pos[it->second]);
+    if (d < 100000) {
+      out += "s_branch " + to + "\n";
+    } else {
+      out += "s_getpc_b64 s[68:69]\n" + tag + ":\n";
+      out += "s_add_u32 s68, s68, " + to + " - " + tag + "\n";
+      out += "s_addc_u32 s69, s69, (" + to + " - " + tag + ") >> 32\n";
+      out += "s_setpc_b64 s[68:69]\n";
+    }
+  }
+  return out;
 }
 
 // min over the lanes of `mask` (an SGPR pair) of VPC into SGPR `dst` (~0 when none);
@@ -2016,11 +2056,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         const std::string q = "Lq" + K + "_" + std::to_string(lab);
         const std::string tl = "Lb" + std::to_string(it->second) +
                                (var == 2 && loop_of.count(k) && loop_of[k] == it->second ? "c" : "");
-        e.l("s_getpc_b64 s[68:69]");
-        e.l("%s:", q.c_str());
-        e.l("s_add_u32 s68, s68, %s - %s", tl.c_str(), q.c_str());
-        e.l("s_addc_u32 s69, s69, (%s - %s) >> 32", tl.c_str(), q.c_str());
-        e.l("s_setpc_b64 s[68:69]");
+        long_jump(e, tl, q);
         e.l("%s:", disp.c_str());
         banks = false;
       }
@@ -2167,10 +2203,10 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         ei.l("s_add_u32 s65, s65, 0x%x", st.done);
         ei.l("s_setpc_b64 s[70:71]");
       }
-      extra += ei.o;
-      e.l("s_add_u32 s65, s65, 0");   // (the callee's block counts the caller's run)
-      long_jump(e, "Li" + IK, "Liq" + IK);
-      extra = "Li" + IK + ":\n" + extra;
+      // the callee's code follows the caller's (falls through into it; its block counts
+      // the caller's run)
+      e.l("Li%s:", IK.c_str());
+      e.o += ei.o;
     } else if (lop == OP_CALL) {
       std::vector<uint8_t> dead;
       if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
@@ -2344,6 +2380,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     }
     body += e.o;
   }
+  body = resolve_jumps(body);
   body += ".p2align 3\nLtab:\n";
   for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
   body += "Lend:\n";
