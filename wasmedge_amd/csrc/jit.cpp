@@ -378,7 +378,8 @@ bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
   return true;
 }
 
-bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm) {
+// (data: the register to store from instead of cell b's -- a forwarded word's own VGPR)
+bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const char *data = nullptr) {
   const uint32_t n = mem_bytes(op);
   e.drain();   // a store never overtakes a load of this run (same-address ordering)
   if (e.group) group_check(e, *e.group);
@@ -386,7 +387,7 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm) {
   mem_ea(e, a, imm, n, &w1, &w2);
   const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
   const size_t k1 = w1.find(", off"), k2 = w2.find(", off");
-  e.l("%s %s, %s%s", ins, w1.substr(0, k1).c_str(), e.v(b), w1.substr(k1).c_str());
+  e.l("%s %s, %s%s", ins, w1.substr(0, k1).c_str(), data ? data : e.v(b), w1.substr(k1).c_str());
   e.nvm++;
   if (n == 8) {
     e.l("global_store_dword %s, %s%s", w2.substr(0, k2).c_str(), e.v(b + 1), w2.substr(k2).c_str());
@@ -2147,9 +2148,17 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
         }
+        if (fa >= 0 && op_of(I) == OP_ST32) {
+          // the word goes to its VGPR first and is stored from there: the stack cell that
+          // held it is free at once for the next value (no wait for the store's data read)
+          const std::string fr = "v" + std::to_string(fwd->freg.at(uint32_t(fa)));
+          ei.sync({I.w1 >> 16});
+          ei.l("v_mov_b32 %s, %s", fr.c_str(), ei.v(I.w1 >> 16));
+          emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
+          ei.done += (I.w0 >> 16) & 0xFFu;
+          continue;
+        }
         if (!emit(ei, I)) return "";
-        if (fa >= 0 && op_of(I) == OP_ST32)
-          ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w1 >> 16));
         if (fa >= 0 && fwd->copy_now[i]) {
           ei.sync({I.w2 & 0xFFFFu});
           ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w2 & 0xFFFFu));
