@@ -36,7 +36,13 @@ for u in (2, 4):   # the chain loop's body compresses u times per trip (iters % 
     variants["unroll%d" % u] = base.replace(loop_call, loop_call * u)
 n, iters = 65536, 1000
 only = sys.argv[1:] or list(variants)
-for name in only:
+# NAME@VAR=VAL: the variant with an environment knob set while its context compiles
+for spec in only:
+    name, _, env = spec.partition("@")
+    saved = dict(os.environ)
+    if env:
+        k, _, v = env.partition("=")
+        os.environ[k] = v
     wasm = assemble(variants[name])
     ctx = batch.BatchContext(wasm, n)
     ctx.set_args("run", batch.make_values([[i, iters] for i in range(n)], [0x7F, 0x7F]))
@@ -46,6 +52,8 @@ for name in only:
         ctx.reset(timed=False)
         ks.append(ctx.run())
     _, st, cnt = ctx.results(1)
-    print("%-6s kernel %.3f ms  instr/lane %d  traps %d" % (name, 1e3 * min(ks), int(cnt[0]),
+    print("%-6s kernel %.3f ms  instr/lane %d  traps %d" % (spec, 1e3 * min(ks), int(cnt[0]),
                                                          int((st != 0).sum())), flush=True)
     ctx.close()
+    os.environ.clear()
+    os.environ.update(saved)

@@ -99,7 +99,14 @@ struct Em {
   // cells higher, above the caller's live cells (globals stay).
   uint32_t shift = 0;
   uint32_t sc(uint32_t c) const { return (shift && c >= fb) ? c + shift : c; }
-  std::string V(uint32_t c) const { return "v" + std::to_string(128 + sc(c)); }
+  // (one cell may be renamed to another VGPR for one instruction: a forwarded store's
+  // value computed straight into its word's VGPR)
+  int64_t alias_cell = -1;
+  uint32_t alias_reg = 0;
+  std::string V(uint32_t c) const {
+    if (int64_t(c) == alias_cell) return "v" + std::to_string(alias_reg);
+    return "v" + std::to_string(128 + sc(c));
+  }
   std::string P(uint32_t c) const {
     return "v[" + std::to_string(128 + sc(c)) + ":" + std::to_string(129 + sc(c)) + "]";
   }
@@ -287,6 +294,15 @@ struct MemGroup {
   std::vector<std::pair<uint32_t, uint32_t>> aligns;   // distinct (offset & m, m)
 };
 
+// the group's base pair (word interleave): MEM + a * 64
+void group_base(Em &e, const MemGroup &G) {
+  if (e.g != 0) return;
+  const std::string bp = e.base();
+  e.l("v_mov_b32 %s, %s", W0, e.v(G.base));
+  e.l("v_lshlrev_b64 %s, 6, %s", bp.c_str(), WP);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", bp.c_str(), bp.c_str(), MEM);
+}
+
 void group_check(Em &e, const MemGroup &G) {
   const uint32_t a = G.base;
   e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, G.maxlast, e.v(a));
@@ -309,12 +325,7 @@ void group_check(Em &e, const MemGroup &G) {
     e.l("v_add_u32_e64 %s, %s, s69 clamp", Y1, e.v(a));
     e.l("v_max_u32_e32 %s, %s, %s", HWM, HWM, Y1);
   }
-  if (e.g == 0) {
-    const std::string bp = e.base();
-    e.l("v_mov_b32 %s, %s", W0, e.v(a));
-    e.l("v_lshlrev_b64 %s, 6, %s", bp.c_str(), WP);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", bp.c_str(), bp.c_str(), MEM);
-  }
+  group_base(e, G);
 }
 
 // Address operand(s) of the access at offset imm (n bytes) of the current group: the
@@ -926,6 +937,7 @@ struct SIns {
   std::vector<int> defs, uses;
   bool wait = false;   // a counted vmcnt wait: defs = the registers of the loads it retires
   int est = 0;         // (wait) estimated cycle its loads are in
+  bool store = false;  // a global store: uses its address and data registers
 };
 
 void regs_of(const std::string &tok, std::vector<int> *out) {
@@ -998,8 +1010,9 @@ std::string schedule(const std::string &body) {
           if (it != last_def.end())
             dep[it->second] = std::max(dep[it->second], seg[size_t(it->second)].wait ? 0 : kLat);
         }
-        if (seg[i].wait && last_wait >= 0) dep[last_wait] = std::max(dep[last_wait], 0);
-        if (seg[i].wait) last_wait = int(i);
+        // waits and stores keep their order (the counts are issue-order counts)
+        if ((seg[i].wait || seg[i].store) && last_wait >= 0) dep[last_wait] = std::max(dep[last_wait], 0);
+        if (seg[i].wait || seg[i].store) last_wait = int(i);
         for (int r : seg[i].defs) {
           auto it = last_def.find(r);
           if (it != last_def.end()) dep[it->second] = std::max(dep[it->second], 1);
@@ -1058,6 +1071,8 @@ std::string schedule(const std::string &body) {
   // arrivals may differ (anything but an inlined call's Lpa / a NaN fix's Lnr return)
   // makes the state unknown until the next full wait, and waits then stay barriers.
   constexpr int kLoadLat = 100, kLoadStep = 22;   // cycles: first L2-hit load, each further
+  const char *fse = getenv("WB_SCHED_STORES");   // 0: stores stay barriers (A/B aid)
+  const bool float_stores = !(fse && fse[0] == '0');
   std::vector<std::vector<int>> vq;   // operations in flight, oldest first
   bool known = true;
   int retired = 0;                    // loads retired by this segment's waits so far
@@ -1081,6 +1096,18 @@ std::string schedule(const std::string &body) {
       }
       w.est = kLoadLat + kLoadStep * retired;
       seg.push_back(std::move(w));
+      continue;
+    }
+    if (ln.compare(0, 12, "global_store") == 0 && known && float_stores) {
+      // a store only reads registers: VALU work moves across it (its data and address
+      // registers' writers stay before it, later writers after it)
+      SIns st;
+      st.text = ln;
+      st.store = true;
+      const size_t sp = ln.find(' ');
+      if (sp != std::string::npos) regs_of(ln.substr(sp + 1), &st.uses);
+      seg.push_back(std::move(st));
+      vq.push_back({});
       continue;
     }
     flush();
@@ -1931,6 +1958,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // runs compiled twice more for loop-carried forwarding (FwdPlan): (k, 0) every run,
   // (R, 1) the copy entered with F valid, (Pp, 2) the post-call copy that enters it
   const char *fwe = getenv("WB_FWD");   // 0: no forwarding copies (A/B aid)
+  const bool fwd_store = !(getenv("WB_FWD_STORE") && getenv("WB_FWD_STORE")[0] == '0');
   std::map<size_t, FwdPlan> plans;      // R -> plan
   std::map<size_t, size_t> loop_of;     // Pp -> R
   std::vector<std::pair<size_t, int>> jobs;
@@ -2116,6 +2144,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const std::vector<MemGroup> groups2 = jit_groups(P, rf, &lead2);
       const size_t body2 = ei.o.size();
       const bool fc = fwd && var == 1;   // the forwarding copy: the callee's loads from F
+      int64_t renamed = -1;              // the stack cell computed into a word's VGPR
       const std::vector<LoadBatch> batches2 = batching && !fc ? load_batches(P, rf, rf.len - 1, lead2)
                                                               : std::vector<LoadBatch>();
       size_t nb2 = 0;
@@ -2140,7 +2169,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         const int64_t fa = fwd ? fwd->addr[i] : -1;
         if (fa >= 0 && fc && op_of(I) == OP_LD32) {
           // (a group that also stores still computes its base: its stores use it)
-          if (ei.group && ei.group->store_end) group_check(ei, *ei.group);
+          if (ei.group && ei.group->store_end) group_base(ei, *ei.group);
           ei.group = nullptr;
           const uint32_t c = I.w2 & 0xFFFFu;
           ei.sync({c});
@@ -2148,17 +2177,46 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
         }
-        if (fa >= 0 && op_of(I) == OP_ST32) {
+        if (fa >= 0 && op_of(I) == OP_ST32 && fwd_store) {
           // the word goes to its VGPR first and is stored from there: the stack cell that
           // held it is free at once for the next value (no wait for the store's data read)
           const std::string fr = "v" + std::to_string(fwd->freg.at(uint32_t(fa)));
-          ei.sync({I.w1 >> 16});
-          ei.l("v_mov_b32 %s, %s", fr.c_str(), ei.v(I.w1 >> 16));
+          if (renamed != int64_t(I.w1 >> 16)) {
+            ei.sync({I.w1 >> 16});
+            ei.l("v_mov_b32 %s, %s", fr.c_str(), ei.v(I.w1 >> 16));
+          }
+          renamed = -1;
+          if (fc) {   // (the first trip checked these constant addresses, raised the mark)
+            if (ei.group) group_base(ei, *ei.group);
+            ei.group = nullptr;
+          }
           emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
         }
+        // a stack cell computed only to be stored as a forwarded word (it is dead after
+        // the store pops it): computed straight into the word's VGPR
+        renamed = -1;
+        // (only in the copy: there the store cannot leave, which would need the cell)
+        if (fc && fwd_store && i + 2 < rf.len && fwd->addr[i + 1] >= 0 &&
+            op_of(P.code[rf.pc + i + 1]) == OP_ST32) {
+          const uint32_t y = P.code[rf.pc + i + 1].w1 >> 16;
+          std::vector<uint32_t> w;
+          written_exact(I, &w);
+          const bool srcs = (I.w1 & 0xFFFFu) != y && (I.w1 >> 16) != y && (I.w2 >> 16) != y &&
+                            (op_of(I) != OP_I32_ADD3_XROTR_I || (I.w3 & 0xFFFFu) != y);
+          if (y >= fb + nargs + nloc && w.size() == 1 && w[0] == y && srcs &&
+              op_of(I) != OP_LD32 && !mem_bytes(op_of(I))) {
+            ei.sync({y});
+            ei.alias_cell = y;
+            ei.alias_reg = fwd->freg.at(uint32_t(fwd->addr[i + 1]));
+            renamed = y;
+          }
+        }
         if (!emit(ei, I)) return "";
+        ei.alias_cell = -1;
+        if (fa >= 0 && op_of(I) == OP_ST32)   // (WB_FWD_STORE=0: copied after the store)
+          ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w1 >> 16));
         if (fa >= 0 && fwd->copy_now[i]) {
           ei.sync({I.w2 & 0xFFFFu});
           ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w2 & 0xFFFFu));
