@@ -103,9 +103,28 @@ struct Em {
   // value computed straight into its word's VGPR)
   int64_t alias_cell = -1;
   uint32_t alias_reg = 0;
+  // (and cells whose value is a forwarded word read straight from its VGPR until they
+  // are written: amap cell -> VGPR)
+  std::map<uint32_t, uint32_t> amap;
   std::string V(uint32_t c) const {
     if (int64_t(c) == alias_cell) return "v" + std::to_string(alias_reg);
+    if (!amap.empty()) {
+      auto it = amap.find(c);
+      if (it != amap.end()) return "v" + std::to_string(it->second);
+    }
     return "v" + std::to_string(128 + sc(c));
+  }
+  void materialize(uint32_t c) {   // the cell's own register gets its aliased value
+    auto it = amap.find(c);
+    if (it == amap.end()) return;
+    l("v_mov_b32 v%u, v%u", 128 + sc(c), it->second);
+    amap.erase(it);
+  }
+  void before_write(uint32_t reg) {   // VGPR reg changes: cells aliased to it get it first
+    std::vector<uint32_t> cells;
+    for (const auto &kv : amap)
+      if (kv.second == reg) cells.push_back(kv.first);
+    for (uint32_t c : cells) materialize(c);
   }
   std::string P(uint32_t c) const {
     return "v[" + std::to_string(128 + sc(c)) + ":" + std::to_string(129 + sc(c)) + "]";
@@ -1768,8 +1787,8 @@ void scan_loop_block(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
 }
 
 // the cells an instruction writes, exactly for the 32-bit results (written() counts c + 1
-// too), else as written()
-void written_exact(const DInstr &I, std::vector<uint32_t> *out) {
+// too; true), else as written() (false)
+bool written_exact(const DInstr &I, std::vector<uint32_t> *out) {
   const uint32_t c = I.w2 & 0xFFFFu;
   switch (op_of(I)) {
     case OP_I32_ADD: case OP_I32_ADD3: case OP_I32_ADD_I: case OP_I32_AND: case OP_I32_AND_I:
@@ -1787,10 +1806,10 @@ void written_exact(const DInstr &I, std::vector<uint32_t> *out) {
     case OP_MOV32: case OP_LD32: case OP_LD8S32: case OP_LD8U32: case OP_LD16S32:
     case OP_LD16U32:
       out->assign(1, c);
-      return;
-    case OP_I32_ADD_XROTR_I: *out = {c, I.w2 >> 16}; return;
-    case OP_I32_ADD3_XROTR_I: *out = {c, I.w3 & 0xFFFFu}; return;
-    default: written(I, out);
+      return true;
+    case OP_I32_ADD_XROTR_I: *out = {c, I.w2 >> 16}; return true;
+    case OP_I32_ADD3_XROTR_I: *out = {c, I.w3 & 0xFFFFu}; return true;
+    default: written(I, out); return false;
   }
 }
 
@@ -1959,6 +1978,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // (R, 1) the copy entered with F valid, (Pp, 2) the post-call copy that enters it
   const char *fwe = getenv("WB_FWD");   // 0: no forwarding copies (A/B aid)
   const bool fwd_store = !(getenv("WB_FWD_STORE") && getenv("WB_FWD_STORE")[0] == '0');
+  const bool fwd_alias = !(getenv("WB_FWD_ALIAS") && getenv("WB_FWD_ALIAS")[0] == '0');
   std::map<size_t, FwdPlan> plans;      // R -> plan
   std::map<size_t, size_t> loop_of;     // Pp -> R
   std::vector<std::pair<size_t, int>> jobs;
@@ -2173,14 +2193,32 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           ei.group = nullptr;
           const uint32_t c = I.w2 & 0xFFFFu;
           ei.sync({c});
-          ei.l("v_mov_b32 %s, v%u", ei.v(c), fwd->freg.at(uint32_t(fa)));
+          if (fwd_alias) ei.amap[c] = fwd->freg.at(uint32_t(fa));
+          else ei.l("v_mov_b32 %s, v%u", ei.v(c), fwd->freg.at(uint32_t(fa)));
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
+        }
+        if (!ei.amap.empty() && !(fa >= 0 && op_of(I) == OP_ST32 && fwd_store)) {
+          // an aliased cell this instruction writes gets its own register back first if
+          // the instruction also reads it (else the alias just ends); anything but a plain
+          // 32-bit op (which might leave, or names register pairs) gets every cell back
+          std::vector<uint32_t> w;
+          const bool ex = written_exact(I, &w);
+          std::vector<uint32_t> cells;
+          for (const auto &kv : ei.amap) cells.push_back(kv.first);
+          for (uint32_t x : cells) {
+            const bool wr = std::find(w.begin(), w.end(), x) != w.end();
+            const bool rd = (I.w1 & 0xFFFFu) == x || (I.w1 >> 16) == x || (I.w2 >> 16) == x ||
+                            (op_of(I) == OP_I32_ADD3_XROTR_I && (I.w3 & 0xFFFFu) == x);
+            if (!ex || (wr && rd)) ei.materialize(x);
+            else if (wr) ei.amap.erase(x);
+          }
         }
         if (fa >= 0 && op_of(I) == OP_ST32 && fwd_store) {
           // the word goes to its VGPR first and is stored from there: the stack cell that
           // held it is free at once for the next value (no wait for the store's data read)
           const std::string fr = "v" + std::to_string(fwd->freg.at(uint32_t(fa)));
+          ei.before_write(fwd->freg.at(uint32_t(fa)));
           if (renamed != int64_t(I.w1 >> 16)) {
             ei.sync({I.w1 >> 16});
             ei.l("v_mov_b32 %s, %s", fr.c_str(), ei.v(I.w1 >> 16));
@@ -2208,6 +2246,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           if (y >= fb + nargs + nloc && w.size() == 1 && w[0] == y && srcs &&
               op_of(I) != OP_LD32 && !mem_bytes(op_of(I))) {
             ei.sync({y});
+            ei.before_write(fwd->freg.at(uint32_t(fwd->addr[i + 1])));
             ei.alias_cell = y;
             ei.alias_reg = fwd->freg.at(uint32_t(fwd->addr[i + 1]));
             renamed = y;
@@ -2215,8 +2254,10 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         }
         if (!emit(ei, I)) return "";
         ei.alias_cell = -1;
-        if (fa >= 0 && op_of(I) == OP_ST32)   // (WB_FWD_STORE=0: copied after the store)
+        if (fa >= 0 && op_of(I) == OP_ST32) {   // (WB_FWD_STORE=0: copied after the store)
+          ei.before_write(fwd->freg.at(uint32_t(fa)));
           ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w1 >> 16));
+        }
         if (fa >= 0 && fwd->copy_now[i]) {
           ei.sync({I.w2 & 0xFFFFu});
           ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w2 & 0xFFFFu));
@@ -2234,6 +2275,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const uint32_t ra = rt.w1 & 0xFFFFu, nres = rt.w1 >> 16;
       for (uint32_t q = 0; q < nres; q++)
         ei.l("v_mov_b32 v%u, %s", 128 + L + q, ei.v(ra + q));
+      ei.amap.clear();   // (the callee's cells are dead once its results are out)
       ei.l("s_add_u32 s65, s65, 0x%x", r.cnt + rf.cnt);
       {
         const JitRun &rp = runs[size_t(inl_post)];
