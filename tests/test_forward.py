@@ -86,9 +86,9 @@ def test_loop_modules_trap_and_succeed():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fwd", ["1", "0"])
-def test_gpu_forwarding_bit_exact(built, monkeypatch, fwd):
-    monkeypatch.setenv("WB_FWD", fwd)
+@pytest.mark.parametrize("knob", ["WB_FWD=1", "WB_FWD=0", "WB_SIMT=0", "WB_FWD_ALIAS=0"])
+def test_gpu_forwarding_bit_exact(built, monkeypatch, knob):
+    monkeypatch.setenv(*knob.split("="))
     for a, b, div in [(a, b, False) for a, b in CASES] + [(64, 68, True), (64, 96, True)]:
         wasm = loop_module(a, b, div)
         ref = [O.Module(wasm).run("run", r) for r in ROWS]
