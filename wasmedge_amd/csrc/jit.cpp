@@ -2165,6 +2165,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const size_t body2 = ei.o.size();
       const bool fc = fwd && var == 1;   // the forwarding copy: the callee's loads from F
       int64_t renamed = -1;              // the stack cell computed into a word's VGPR
+      std::vector<std::pair<uint32_t, uint32_t>> deferred;   // (cell, VGPR) read, then written
       const std::vector<LoadBatch> batches2 = batching && !fc ? load_batches(P, rf, rf.len - 1, lead2)
                                                               : std::vector<LoadBatch>();
       size_t nb2 = 0;
@@ -2210,7 +2211,10 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
             const bool wr = std::find(w.begin(), w.end(), x) != w.end();
             const bool rd = (I.w1 & 0xFFFFu) == x || (I.w1 >> 16) == x || (I.w2 >> 16) == x ||
                             (op_of(I) == OP_I32_ADD3_XROTR_I && (I.w3 & 0xFFFFu) == x);
-            if (!ex || (wr && rd)) ei.materialize(x);
+            size_t shared = 0;
+            for (const auto &kv : ei.amap) shared += kv.second == ei.amap[x];
+            if (ex && wr && rd && shared == 1) deferred.push_back({x, ei.amap[x]});
+            else if (!ex || (wr && rd)) ei.materialize(x);
             else if (wr) ei.amap.erase(x);
           }
         }
@@ -2252,8 +2256,47 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
             renamed = y;
           }
         }
+        const size_t mark = ei.o.size();
         if (!emit(ei, I)) return "";
         ei.alias_cell = -1;
+        // A cell read through its alias and written by this instruction: the instruction
+        // read the word's VGPR; its first line that writes the VGPR writes the cell's own
+        // register instead, and later lines read that (else: the cell back first, again)
+        for (const auto &dx : deferred) {
+          const std::string fv = "v" + std::to_string(dx.second);
+          const std::string rv = "v" + std::to_string(128 + ei.sc(dx.first));
+          std::string out;
+          bool written = false;
+          for (size_t at = mark; at < ei.o.size();) {
+            size_t nl = ei.o.find('\n', at);
+            std::string ln = ei.o.substr(at, nl - at);
+            at = nl + 1;
+            const size_t sp = ln.find(' ');
+            if (!written && ln.compare(0, 2, "v_") == 0 && sp != std::string::npos &&
+                ln.compare(sp + 1, fv.size(), fv) == 0 &&
+                (sp + 1 + fv.size() == ln.size() || ln[sp + 1 + fv.size()] == ',')) {
+              ln = ln.substr(0, sp + 1) + rv + ln.substr(sp + 1 + fv.size());
+              written = true;
+            } else if (written) {
+              for (size_t q = ln.find(fv); q != std::string::npos; q = ln.find(fv, q + rv.size())) {
+                const size_t e2 = q + fv.size();
+                if ((q == 0 || !isalnum((unsigned char)ln[q - 1])) &&
+                    (e2 == ln.size() || !isdigit((unsigned char)ln[e2])))
+                  ln = ln.substr(0, q) + rv + ln.substr(e2);
+              }
+            }
+            out += ln + "\n";
+          }
+          if (written) {
+            ei.o = ei.o.substr(0, mark) + out;
+            ei.amap.erase(dx.first);
+          } else {   // (not expected: every exact write names the cell's register)
+            ei.o.resize(mark);
+            ei.materialize(dx.first);
+            if (!emit(ei, I)) return "";
+          }
+        }
+        deferred.clear();
         if (fa >= 0 && op_of(I) == OP_ST32) {   // (WB_FWD_STORE=0: copied after the store)
           ei.before_write(fwd->freg.at(uint32_t(fa)));
           ei.l("v_mov_b32 v%u, %s", fwd->freg.at(uint32_t(fa)), ei.v(I.w1 >> 16));
