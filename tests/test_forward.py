@@ -53,6 +53,48 @@ def loop_module(a, b, div=False):
 """ % (tail, a, b))
 
 
+def random_loop_module(seed):
+    """loop_module's shape with a random leaf: loads, stores and 32-bit ops over four
+    locals, addresses a + k*4 / b + k*4 with constant a, b (coinciding words included)"""
+    import random
+    rnd = random.Random(seed)
+    a, b = rnd.choice([(64, 96), (64, 72), (80, 64), (65520, 64)])
+    ops = ["i32.add", "i32.sub", "i32.xor", "i32.or", "i32.and", "i32.mul", "i32.rotl", "i32.shl"]
+    body = []
+    for _ in range(rnd.randint(6, 14)):
+        k = rnd.random()
+        p, o = rnd.choice(["$a", "$b"]), 4 * rnd.randint(0, 3)
+        t, u, v = ("$t%d" % rnd.randint(0, 3) for _ in range(3))
+        if k < 0.35:
+            body.append("(local.set %s (i32.load offset=%d (local.get %s)))" % (t, o, p))
+        elif k < 0.6:
+            body.append("(i32.store offset=%d (local.get %s) (%s (local.get %s) (local.get %s)))"
+                        % (o, p, rnd.choice(ops), u, v))
+        else:
+            body.append("(local.set %s (%s (local.get %s) (local.get %s)))" % (t, rnd.choice(ops), u, v))
+    return assemble(r"""
+(module
+  (memory 1)
+  (func $leaf (param $a i32) (param $b i32) (param $x i32) (result i32)
+    (local $t0 i32) (local $t1 i32) (local $t2 i32) (local $t3 i32)
+    (local.set $t0 (local.get $x))
+    %s
+    (i32.xor (i32.xor (local.get $t0) (local.get $t1)) (i32.xor (local.get $t2) (local.get $t3))))
+  (func (export "run") (param $s i32) (result i32)
+    (local $i i32) (local $acc i32) (local $n i32) (local $pad i32)
+    (i32.store (i32.const 64) (local.get $s))
+    (i32.store (i32.const 76) (i32.mul (local.get $s) (i32.const 7)))
+    (i32.store (i32.const 100) (i32.xor (local.get $s) (i32.const 0x5A5A)))
+    (local.set $n (i32.add (i32.const 2) (i32.rem_u (local.get $s) (i32.const 17))))
+    (loop $l
+      (local.set $acc (i32.add (local.get $acc)
+        (call $leaf (i32.const %d) (i32.const %d) (local.get $i))))
+      (local.set $i (i32.add (local.get $i) (i32.const 1)))
+      (br_if $l (i32.lt_u (local.get $i) (local.get $n))))
+    (i32.add (local.get $acc) (i32.xor (i32.load (i32.const 64)) (i32.load (i32.const 100))))))
+""" % ("\n    ".join(body), a, b))
+
+
 def _copies(wasm):
     """forwarding copies of the compiled SIMT code (wb_jit_check's dump: labels Lb<k>c)"""
     L = ctypes.CDLL(os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch.so"))
@@ -77,6 +119,10 @@ def test_forwarding_copies(built):
     assert _copies(loop_module(64, 68, True)) == 1
 
 
+def test_random_loop_modules_forward(built):
+    assert sum(_copies(random_loop_module(seed)) for seed in range(12)) >= 6
+
+
 def test_loop_modules_trap_and_succeed():
     codes = set()
     for a, b in CASES:
@@ -94,3 +140,12 @@ def test_gpu_forwarding_bit_exact(built, monkeypatch, knob):
         ref = [O.Module(wasm).run("run", r) for r in ROWS]
         rets, st, cnt, h = gpu_run(wasm, "run", ROWS, [I32], [I32])
         assert compare(ref, rets, st, cnt, h, [I32], exact=True) == [], (a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_random_forwarding_bit_exact(built):
+    for seed in range(12):
+        wasm = random_loop_module(seed)
+        ref = [O.Module(wasm).run("run", r) for r in ROWS]
+        rets, st, cnt, h = gpu_run(wasm, "run", ROWS, [I32], [I32])
+        assert compare(ref, rets, st, cnt, h, [I32], exact=True) == [], seed
