@@ -63,7 +63,10 @@ def test_gpu_interrupt(built):
     from wasmedge_amd.wat import assemble
     spin = assemble("(module (func (export \"spin\") (param i32) (result i32)"
                     " (loop $l (local.set 0 (i32.add (local.get 0) (i32.const 1))) (br $l))"
-                    " (local.get 0)))")
+                    " (local.get 0))"
+                    " (func (export \"count\") (param i32) (result i32) (local i32)"
+                    " (loop $l (local.set 1 (i32.add (local.get 1) (i32.const 1)))"
+                    " (br_if $l (i32.lt_u (local.get 1) (local.get 0)))) (local.get 1)))")
     ctx = batch.BatchContext(spin, 65536, device=0, time_limit=60.0)
     try:
         t = threading.Timer(1.0, ctx.interrupt)
@@ -73,6 +76,11 @@ def test_gpu_interrupt(built):
         t.join()
         assert time.time() - t0 < 30
         assert all(int(s) == 0x07 for s in st)
+        # the interrupt ends that run only: the next one runs to completion
+        ctx.reset()
+        rets, st, cnt = ctx.execute("count", batch.make_values([[2000]] * 65536, [I32]), 1)
+        assert all(int(s) == 0 for s in st) and len(set(int(c) for c in cnt)) == 1
+        assert int(cnt[0]) > 2000
     finally:
         ctx.close()
 

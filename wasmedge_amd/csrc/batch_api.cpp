@@ -321,7 +321,9 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
 uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
                     double *KernelSeconds) {
   if (KernelSeconds) *KernelSeconds = 0;
-  if (!C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
+  // (the flag is cleared only after an Interrupt: one stream operation less per run)
+  if (C->stop_dirty.exchange(false) &&
+      !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
   if (e || !C->prog.n_imported) return e;
   for (;;) {
@@ -765,6 +767,7 @@ void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *C) {
   static const uint32_t one = 1;
   (void)hipMemcpyAsync(C->stop, &one, 4, hipMemcpyHostToDevice, C->ctl_stream);
   (void)hipStreamSynchronize(C->ctl_stream);
+  C->stop_dirty.store(true);   // (after the write landed: the next run clears it)
 }
 
 void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
