@@ -251,8 +251,9 @@ def main():
                     help="weak: --instances per GPU; strong: --instances for the whole job")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: shards, barrier and reductions, no GPU")
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 20 for C2, whose step is ~1.6 ms; 3 otherwise)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2 / 1)")
     ap.add_argument("--iters", type=int, default=ITERS)
     ap.add_argument("--instances", type=int, default=INSTANCES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -263,6 +264,10 @@ def main():
                     help="meter gas with the unit cost table up to this limit (measures the "
                          "cost of exact metering; not the headline configuration)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 20 if args.workload == "c2" else 3
+    if args.warmup is None:
+        args.warmup = 2 if args.workload == "c2" else 1
 
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
