@@ -31,6 +31,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip-level parameters
 VALU_PEAK = 256 * 4 * 32 * 2.4e9   # VALU lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 INSTANCES = 65536
 ITERS = 1000                   # chained compressions per instance
+# C3 linear-memory bytes per wasm instruction, counted by the oracle over CPU-baseline
+# samples of 262,144-element sorts (r02/r03 bench lines: 0.410); used when the baseline leg
+# is skipped (profiling runs)
+C3_BYTES_PER_INSTR = 0.4100
 
 
 def c2_mem_bytes(iters):
@@ -221,21 +225,19 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     return rec, state["mbytes"] / state["instrs"]
 
 
-def load_profile():
-    """The committed rocprofv3 PMC summary of this bench command (profiles/traffic_c2.json,
-    tools/prof_summary.py): HBM bytes and VALU instructions per interpreter launch, when
-    it matches the configuration (see DESIGN.md 'Measurement')."""
-    p = os.path.join(ROOT, "profiles", "traffic_c2.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            d = json.load(f)
-        if d.get("iters") == ITERS and d.get("instances") == INSTANCES:
-            return d
-    return {}
-
-
-def load_profile_traffic():
-    return load_profile().get("hbm_bytes_per_launch")
+def load_profile(workload, config):
+    """The committed rocprofv3 summary of this bench configuration
+    (profiles/prof_<workload>.json, written by tools/prof_summary.py from a
+    tools/prof_bench.sh run of the same command): HBM bytes, VALU instructions, active
+    lanes per VALU instruction, resident waves per SIMD, VMEM latency per interpreter
+    launch -- only when its configuration equals this run's (DESIGN.md 'Measurement')."""
+    p = os.path.join(ROOT, "profiles", "prof_%s.json" % workload)
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        d = json.load(f)
+    key = {k: config.get(k) for k in ("workload", "instances_per_gpu", "elements", "iters")}
+    return d if d.get("config") == key else {}
 
 
 def elapsed_hint(args):
@@ -279,32 +281,54 @@ def main():
         return dry_run(args, dist)
     from wasmedge_amd import batch
     wasm, func, build_rows, ptypes, desc, extra = workload(args.workload, args)
-    n = args.instances
+    # this rank's shard first: the context holds exactly its instances (strong scaling
+    # splits --instances over the ranks, weak gives every rank --instances of its own)
+    ids = shard_ids(dist.rank, args.instances, dist.world, args.scaling)
+    n = len(ids)
     kw = {"max_memory_page": 17} if args.workload == "c3" else {}
     if args.cost_limit:
         kw["cost_limit"] = args.cost_limit
-    ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
-    ids = shard_ids(dist.rank, n, dist.world, args.scaling)
-    n = len(ids)
     rows = build_rows(ids)
-    ctx.set_args(func, batch.make_values(rows, ptypes))
+    values = batch.make_values(rows, ptypes)
     nret = 1
-    dist.init()
+    t_start = time.perf_counter()
 
     def progress(msg):
         if dist.rank == 0:
             print("[bench] %s %.1fs" % (msg, time.perf_counter() - t_start), file=sys.stderr, flush=True)
 
-    t_start = time.perf_counter()
-    for w in range(args.warmup):
+    def outcome():
+        _, st, cnt = ctx.results(nret)
+        traps = int((st != 0).sum())
+        if traps and args.workload != "c4":
+            raise SystemExit("%s instances trapped: %s" % (args.workload, np.unique(st)))
+        return float(cnt.sum()), traps
+
+    # End-to-end passes (SURVEY.md 8(d) variant ii), the warmup steps themselves:
+    #  cold = BatchCreate (decode, validate, lower, hiprtc compile of the compiled runs,
+    #         device allocation, instantiation) + SetArgs (params H2D) + Run + Results
+    #         (returns, statuses, counts D2H);
+    #  warm = the same on the live context: SetArgs + Reset + Run + Results.
+    t = time.perf_counter()
+    ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
+    t_create = time.perf_counter() - t
+    ctx.set_args(func, values)
+    e2e_s = {}
+    if args.warmup:
+        ctx.run()
+        instrs_per_step, traps = outcome()
+        e2e_s["cold"] = time.perf_counter() - t
+        progress("warmup 1/%d done (end-to-end cold)" % args.warmup)
+    for w in range(1, args.warmup):
+        t = time.perf_counter()
+        ctx.set_args(func, values)
         ctx.reset()
         ctx.run()
+        outcome()
+        if w == 1:
+            e2e_s["warm"] = time.perf_counter() - t
         progress("warmup %d/%d done" % (w + 1, args.warmup))
-    _, st, cnt = ctx.results(nret)
-    traps = int((st != 0).sum())
-    if traps and args.workload != "c4":
-        raise SystemExit("%s instances trapped: %s" % (args.workload, np.unique(st)))
-    instrs_per_step = float(cnt.sum())
+    dist.init()
 
     dist.barrier()
     t0 = time.perf_counter()
@@ -317,9 +341,11 @@ def main():
     elapsed = time.perf_counter() - t0   # BatchRun synchronises its stream
     dist.barrier()
     elapsed = dist.max(elapsed)
-    total_instrs = dist.sum(instrs_per_step) * args.steps
+    if not args.warmup:
+        instrs_per_step, traps = outcome()
     rets, st, cnt = ctx.results(nret)
     assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == traps
+    total_instrs = dist.sum(instrs_per_step) * args.steps
     # checksum of checksums over every instance's final linear memory (hash kernel, after
     # the timed region)
     hashes = ctx.memory_hash()
@@ -327,6 +353,11 @@ def main():
     gpu = {"counts": cnt, "hashes": hashes, "status": st, "ret": rets["lo"][:, 0],
            "ret32": args.workload != "c5"}
     kernel_avg = ksum / args.steps
+    e2e = {"create_s": dist.max(t_create)}
+    for k in ("cold", "warm"):
+        if k in e2e_s:
+            e2e["e2e_%s_s" % k] = dist.max(e2e_s[k])
+            e2e["e2e_%s_instr_per_s" % k] = dist.sum(instrs_per_step) / e2e["e2e_%s_s" % k]
     out = {
         "metric": METRIC,
         "value": total_instrs / elapsed,
@@ -352,51 +383,70 @@ def main():
         out["config"]["trapped_instances"] = traps
     if args.cost_limit:
         out["config"]["cost_limit"] = args.cost_limit
-    if args.workload == "c2":
-        bytes_launch = float(c2_mem_bytes(args.iters)) * n
-        achieved = bytes_launch / kernel_avg / 1e9
-        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                           "traffic": load_profile_traffic(),
-                           "note": "algorithmic = linear-memory bytes the wasm program moves; "
-                                   "the path is dispatch-issue bound, see issue_roofline"}
-
-    else:
-        out["data"] = "synthetic: per-instance inputs derived from the instance id"
-    # the bound that matters for the interpreter: vector issue at one wave per SIMD. The
-    # achieved rate is the VALU lane-ops the kernel issues (SQ_INSTS_VALU x 64 from the
-    # committed PMC pass of this same command) over this run's measured kernel time
-    per_gpu = total_instrs / elapsed / dist.world
-    prof = load_profile() if (args.workload == "c2" and args.iters == ITERS and n == INSTANCES) else {}
-    if prof.get("valu_insts_per_launch"):
-        valu = prof["valu_insts_per_launch"] * 64.0 / kernel_avg
-        out["issue_roofline"] = {
-            "bound": "valu", "achieved": valu, "peak": VALU_PEAK, "unit": "VALU lane-op/s",
-            "frac": valu / VALU_PEAK,
-            "wasm_instr_per_valu_lane_op": (total_instrs / args.steps / dist.world) /
-                                           (prof["valu_insts_per_launch"] * 64.0),
-            "source": "SQ_INSTS_VALU per launch, profiles/%s_counters.md" % prof.get("source"),
-            "basis": "DESIGN.md 'Roofline': 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
-                     "(MI355X_MICROARCH.md)"}
-    else:
-        out["issue_roofline"] = {
-            "bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "VALU lane-op/s",
-            "frac": None, "wasm_instr_per_s_per_gpu": per_gpu,
-            "note": "no PMC summary for this configuration (tools/prof_bench.sh)"}
+    c3_bytes_per_instr, c3_bpi_src = C3_BYTES_PER_INSTR, ", committed oracle figure"
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads = host_cores()
         out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
                                                 threads, gpu, args.workload.upper())
         if args.workload == "c3":
-            # algorithmic bytes: the linear-memory bytes the wasm program moves, counted
-            # per instance by the oracle on the sample, per instruction x this launch's
-            # instructions (qsort's bytes per instruction is stable across instances)
-            bytes_launch = bpi * instrs_per_step
-            achieved = bytes_launch / kernel_avg / 1e9
-            out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                               "note": "algorithmic = linear-memory bytes of the wasm loads and "
-                                       "stores (%.3f B per wasm instr on the oracle sample)" % bpi}
+            # qsort's bytes per instruction is stable across instances
+            c3_bytes_per_instr, c3_bpi_src = bpi, " on the oracle sample"
+    if args.workload != "c2":
+        out["data"] = "synthetic: per-instance inputs derived from the instance id"
+    out["workload_key"] = args.workload
+    out.update(e2e)
+    prof = load_profile(args.workload, out["config"])
+    kernel_max = dist.max(kernel_avg)
+    # The interpreter's bound is vector issue (VALU), not HBM, for every config but C3:
+    # SQ_INSTS_VALU per launch (committed PMC pass of this same command) x 64 lanes over
+    # this run's live kernel time (HIP events on the library's stream), against 256 CU x
+    # 4 SIMD-32 x 32 lanes x 2.4 GHz. One wave alone issues a VALU instruction every 4
+    # cycles at best, so at one wave per SIMD (64K instances) 0.5 of that peak is the
+    # ceiling (2 waves per SIMD: 1.0).
+    issue = {"bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "VALU lane-op/s",
+             "frac": None,
+             "basis": "256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md); one "
+                      "wave issues VALU at most every 4 cycles"}
+    if prof.get("valu_insts_per_launch"):
+        valu = prof["valu_insts_per_launch"] * 64.0 / kernel_max
+        wps = prof.get("waves_per_simd")
+        issue.update({
+            "achieved": valu, "frac": valu / VALU_PEAK,
+            "single_wave_ceiling": min(1.0, 0.5 * wps) if wps else None,
+            "waves_per_simd": wps,
+            "lanes_per_valu": prof.get("lanes_per_valu"),
+            "wasm_instr_per_valu_lane_op": instrs_per_step / (prof["valu_insts_per_launch"] * 64.0),
+            "source": "profiles/%s_counters.md (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, "
+                      "SQ_WAVE_CYCLES per launch)" % prof.get("source")})
+    else:
+        issue["note"] = "no PMC summary for this configuration (tools/prof_bench.sh)"
+    traffic = prof.get("hbm_bytes_per_launch")
+    if args.workload == "c3":
+        # HBM-bound config: algorithmic bytes = the linear-memory bytes of the wasm loads and
+        # stores, per wasm instruction as the oracle counts them on the CPU-baseline sample
+        # (or the committed figure when the baseline leg is skipped) x this launch's count
+        bpi = c3_bytes_per_instr
+        bytes_launch = bpi * instrs_per_step
+        achieved = bytes_launch / kernel_max / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                           "traffic": traffic,
+                           "note": "algorithmic = linear-memory bytes of the wasm loads and "
+                                   "stores (%.4f B per wasm instr%s); traffic = HBM bytes per "
+                                   "launch from FETCH_SIZE + WRITE_SIZE" % (bpi, c3_bpi_src)}
+        out["issue_roofline"] = issue
+    else:
+        out["roofline"] = dict(issue)
+        hbm = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
+               "achieved": traffic / kernel_max / 1e9 if traffic else None}
+        if hbm["achieved"] is not None:
+            hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
+        if args.workload == "c2":
+            hbm["wasm_level_bytes"] = float(c2_mem_bytes(args.iters)) * n
+            hbm["note"] = ("the wasm program names %.4g B of linear memory per launch, but the "
+                           "compiled loop forwards its loads in registers: the counters see the "
+                           "stores only" % hbm["wasm_level_bytes"])
+        out["hbm_roofline"] = hbm
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

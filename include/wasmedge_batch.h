@@ -56,7 +56,7 @@ typedef struct WasmEdge_Result {
 #define WASMEDGE_BATCH_OK 0x00u
 #define WASMEDGE_BATCH_INTERRUPTED 0x07u      /* ErrCode::Interrupted: step/time limit */
 #define WASMEDGE_BATCH_STACK_EXHAUSTED 0xB0u  /* device call stack full */
-#define WASMEDGE_BATCH_HOST_CALL 0xB1u        /* reached a host import (yield: not yet) */
+#define WASMEDGE_BATCH_HOST_CALL 0xB1u        /* reached a host import no host function is bound to */
 
 typedef struct WasmEdge_BatchConfigure {
   /* Page budget per instance; plays RuntimeConfigure::MaxMemPage
@@ -82,10 +82,13 @@ typedef struct WasmEdge_BatchConfigure {
    * CostLimitExceeded (0x03), counted but not executed (engine.cpp:1616-1630). The total
    * starts at instantiation, whose constant expressions and start function spend gas too,
    * and runs on across Execute/Run calls until BatchReset, like the reference VM's
-   * Statistics::CostSum. Metered runs use the compiled step only (no threaded core). */
+   * Statistics::CostSum. Metered contexts run the compiled runs, which price themselves
+   * exactly, and the per-lane step (no SIMT scheduling). */
   uint64_t CostLimit;
-  /* Host threads serving lanes parked at host imports (0 = min(16, cores)). Waves are
-   * spread over the threads, so host functions must be reentrant. */
+  /* Host threads serving lanes parked at host imports. 0 or 1: one thread, host
+   * functions are called one at a time. More: waves are spread over that many threads
+   * (a wave's lanes stay on one), so host functions must then be reentrant, as the
+   * reference's are under concurrent VM::execute. */
   uint32_t HostThreads;
   /* Cost per instruction, indexed by the reference's OpCode (include/common/enum.inc:
    * one-byte opcodes, 0xFCxx, 0xFDxx): CostTableLen entries, the rest 0 -- the batched

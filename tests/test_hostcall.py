@@ -105,3 +105,45 @@ def test_gpu_unregistered_import_status(built):
         assert all(int(s) == 0xB1 for s in st)
     finally:
         ctx.close()
+
+
+SERIAL = assemble(r"""
+(module
+  (import "env" "tick" (func $tick (param i32) (result i32)))
+  (func (export "run") (param $iid i32) (result i32)
+    (call $tick (local.get $iid))))
+""")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [0, 1])
+def test_gpu_default_host_threads_are_serial(built, threads):
+    """HostThreads 0 (the default) and 1 call host functions one at a time from one
+    thread, so a host function with shared mutable state (a plain counter, no lock) is
+    safe there; only HostThreads > 1 asks for reentrant host functions."""
+    import threading
+    import time
+    from wasmedge_amd import batch
+    n = 640   # 10 waves
+    state = {"inside": 0, "overlap": 0, "count": 0, "tids": set()}
+
+    def tick(mem, a):
+        state["inside"] += 1
+        if state["inside"] > 1:
+            state["overlap"] += 1
+        state["tids"].add(threading.get_ident())
+        c = state["count"]
+        time.sleep(0)        # would let a second service thread in
+        state["count"] = c + 1
+        state["inside"] -= 1
+        return 0, [(a[0] * 3 + 1) & 0xFFFFFFFF]
+
+    ctx = batch.BatchContext(SERIAL, n, device=0, host_threads=threads)
+    try:
+        ctx.add_host_function("env", "tick", tick, 1, 1)
+        rets, st, cnt = ctx.execute("run", batch.make_values([[i] for i in range(n)], [I32]), 1)
+        assert all(int(s) == 0 for s in st)
+        assert [int(v[0]) for v in batch.ret_ints(rets)] == [(3 * i + 1) & 0xFFFFFFFF for i in range(n)]
+        assert state["count"] == n and state["overlap"] == 0 and len(state["tids"]) == 1
+    finally:
+        ctx.close()

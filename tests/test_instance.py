@@ -195,3 +195,42 @@ def test_gpu_reset_memory_over_4096_pages(built):
             ctx.reset()
     finally:
         ctx.close()
+
+
+PEEK = assemble(r"""
+(module
+  (memory 64)
+  (global $g (export "g") (mut i32) (i32.const 5))
+  (data (i32.const 1048576) "\01\00\00\00")
+  (func (export "peek") (param $a i32) (result i32)
+    (i32.add (global.get $g) (i32.add (i32.load (local.get $a)) (i32.load (i32.const 1048576))))))
+""")
+
+
+@pytest.mark.gpu
+def test_gpu_host_writes_after_untimed_reset(built):
+    """a Reset that does not wait for its init kernels (KernelSeconds
+    NULL, no start function) leaves them queued on the context's non-blocking stream;
+    host SetMemory / GlobalSetValue right after it must land after them, not be
+    overwritten by them (4 MiB of image per lane, so the init kernels take a while)."""
+    from wasmedge_amd import batch
+    n = 4096
+    rows = [[(i * 64) % 4000000 & ~3] for i in range(n)]
+    vals = batch.make_values(rows, [I32])
+    ctx = batch.BatchContext(PEEK, n, device=0)
+    try:
+        for rnd in range(3):
+            ctx.execute("peek", vals, 1)                 # dirty rows below every write mark
+            ctx.reset(timed=False)
+            ctx.global_set("g", batch.ALL_INSTANCES, 100 + rnd, I32)
+            for i in range(0, n, 97):
+                ctx.set_memory(i, rows[i][0], (1000 + i).to_bytes(4, "little"))
+            assert ctx.memory_pages(7) == 64
+            rets, st, _ = ctx.execute("peek", vals, 1)
+            assert (st == 0).all()
+            got = batch.ret_ints(rets)[:, 0]
+            for i in range(n):
+                want = 100 + rnd + 1 + ((1000 + i) if i % 97 == 0 else 0)
+                assert int(got[i]) == want, (rnd, i)
+    finally:
+        ctx.close()

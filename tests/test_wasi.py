@@ -156,10 +156,10 @@ def _gpu(wasm, rows, func, ptypes, host_threads=0, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads,granule", [(1, 4), (0, 4), (0, 16)])
+@pytest.mark.parametrize("threads,granule", [(0, 4), (16, 4), (16, 16)])
 def test_gpu_wasi_matches_oracle(built, threads, granule):
-    """One service thread and the default pool (waves served concurrently); word and
-    16-byte memory interleave under the host's memory view."""
+    """The default single service thread and a 16-thread pool (waves served
+    concurrently); word and 16-byte memory interleave under the host's memory view."""
     rows = [[x] for x in range(640)]
     ref = _oracle(WASI, rows)
     got, side = _gpu(WASI, rows, "run", [I32], host_threads=threads, memory_granule=granule)

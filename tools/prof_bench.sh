@@ -1,16 +1,36 @@
 #!/bin/bash
 # usage: tools/prof_bench.sh <outdir> [bench args...]
-# rocprofv3 evidence for bench.py, each collection in its own run (gpurun forbids mixing
-# --pmc with tracing): kernel trace + stats of the bench command itself, then FETCH_SIZE,
-# WRITE_SIZE (separate passes: TCC slots) and SQ issue counters of the same command.
+# rocprofv3 evidence for one bench.py configuration, each collection in its own run (gpurun
+# forbids mixing --pmc with tracing; one pass per counter group, MI355X_MICROARCH.md):
+#   trace  kernel trace + stats of the bench command itself (kernel durations)
+#   fetch  FETCH_SIZE        write  WRITE_SIZE          (HBM bytes, separate TCC passes)
+#   sq1    issue counts: waves, wave cycles, VALU / SALU / SMEM / LDS / branch instructions
+#   sq2    where wave cycles go: active / waiting, VMEM instructions, GRBM_GUI_ACTIVE
+#   util   SQ_THREAD_CYCLES_VALU (active lanes per VALU instruction = exec-mask efficiency),
+#          L2 hits / misses
+#   lat    VmemLatency (mean cycles a vector-memory instruction is in flight)
+# PROF_PASSES="trace fetch ..." runs a subset. Summarise with tools/prof_summary.py.
 OUT=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/$OUT
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --no-cpu-baseline $*"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $B > $R/$OUT/trace.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$OUT/fetch -o run -- python3 $B > $R/$OUT/fetch.log 2>&1 || exit 2
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$OUT/write -o run -- python3 $B > $R/$OUT/write.log 2>&1 || exit 3
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH --output-format csv -d $R/$OUT/sq1 -o run -- python3 $B > $R/$OUT/sq1.log 2>&1 || exit 4
-timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d $R/$OUT/sq2 -o run -- python3 $B > $R/$OUT/sq2.log 2>&1 || exit 5
+T=${PROF_TIMEOUT:-300}
+PASSES=${PROF_PASSES:-"trace fetch write sq1 sq2 util lat"}
+k=0
+for p in $PASSES; do
+  k=$((k + 1))
+  case $p in
+    trace) A="--kernel-trace --stats" ;;
+    fetch) A="--pmc FETCH_SIZE" ;;
+    write) A="--pmc WRITE_SIZE" ;;
+    sq1) A="--pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH" ;;
+    sq2) A="--pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" ;;
+    util) A="--pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU TCC_HIT_sum TCC_MISS_sum" ;;
+    lat) A="--pmc VmemLatency" ;;
+    *) echo "unknown pass $p"; exit 9 ;;
+  esac
+  echo "[prof] pass $p" >&2
+  timeout -k 10 $T rocprofv3 $A --output-format csv -d $R/$OUT/$p -o run -- python3 $B > $R/$OUT/$p.log 2>&1 || { echo "pass $p failed"; tail -5 $R/$OUT/$p.log; exit $k; }
+done
 echo done

@@ -1,17 +1,27 @@
 """Summarise a tools/prof_bench.sh output directory into profiles/.
 
-usage: python tools/prof_summary.py <prof dir> <tag> [iters] [instances] [pages] [label]
-(pages: linear-memory pages per instance, what wb_mem_hash_kernel reads; label: the
-bench workload, default C2)
-Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim),
-profiles/<tag>_counters.md (per-kernel PMC means) and profiles/traffic_c2.json
-(HBM bytes per interpreter launch, read by bench.py for roofline.traffic).
+usage: python tools/prof_summary.py <prof dir> <tag> <pages>
+  pages: linear-memory pages per instance at the end of the run (what wb_mem_hash_kernel
+  reads; 0 for a module without memory)
+
+Reads the bench line the trace pass printed (its configuration identifies the profile)
+and writes:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats of the trace pass, verbatim
+  profiles/<tag>_counters.md        per-kernel PMC means + the derived figures
+  profiles/prof_<workload>.json     what bench.py reads for that configuration: HBM bytes,
+                                    VALU instructions, active lanes per VALU instruction,
+                                    occupancy, VMEM latency, wait fraction per launch
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE (KiB) come from
-separate passes; gfx950 FETCH_SIZE reports half the bytes of coalesced reads, and we
-calibrate that factor on our own access pattern with wb_mem_hash_kernel, which reads a
-known byte count (every instance's pages, 4 B/lane lane-interleaved, the interpreter's
-layout) -- so the correction is measured, not assumed.
+separate passes; gfx950 FETCH_SIZE reports half the bytes of coalesced reads, and the
+factor is calibrated on our own access pattern with wb_mem_hash_kernel, which reads a
+known byte count (every instance's pages in the interpreter's interleaved layout); a
+module without memory takes the guide's x2.
+
+Exec-mask efficiency: SQ_THREAD_CYCLES_VALU counts, per VALU instruction, its cycles
+times its active lanes; divided by SQ_ACTIVE_INST_VALU (cycles of VALU instructions) it
+is the mean number of active lanes per VALU instruction (64 = no divergence; the
+rocprofv3 derived metric VALUUtilization is this over 64).
 """
 import collections
 import csv
@@ -21,43 +31,82 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+XCDS = 8
+SIMDS = 256 * 4
 
 
 def counters(path):
     agg = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return {}
     for r in csv.DictReader(open(path)):
         agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def bench_line(path):
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    raise SystemExit("no bench line in " + path)
+
+
+def profile_key(cfg):
+    """The configuration fields a profile is valid for (bench.py compares them)."""
+    return {k: cfg.get(k) for k in ("workload", "instances_per_gpu", "elements", "iters")}
+
+
 def main():
-    d, tag = sys.argv[1], sys.argv[2]
-    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
-    inst = int(sys.argv[4]) if len(sys.argv) > 4 else 65536
-    pages = int(sys.argv[5]) if len(sys.argv) > 5 else 1
-    label = sys.argv[6] if len(sys.argv) > 6 else None
+    d, tag, pages = sys.argv[1], sys.argv[2], int(sys.argv[3])
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
+    line = bench_line(os.path.join(d, "trace.log"))
+    cfg = line["config"]
+    inst = cfg["instances_per_gpu"]
+    wl = line.get("workload_key") or cfg["workload"].split()[0].lower()
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, tag + "_kernel_stats.csv"))
     C = {}
-    for p in ["fetch", "write", "sq1", "sq2"]:
+    for p in ["fetch", "write", "sq1", "sq2", "util", "lat"]:
         C.update(counters(os.path.join(d, p, "run_counter_collection.csv")))
-    stats0 = {r["Name"] for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv")))}
-    # the interpreter kernel: the V-frame variant when the batch used it
-    K = "wb_exec_vf_kernel" if "wb_exec_vf_kernel" in stats0 else "wb_exec_kernel"
-    H = "wb_mem_hash_kernel"
-    hash_bytes = 65536.0 * pages * inst      # every instance's pages (C2: 1 page each)
-    fetch_factor = hash_bytes / (C[(H, "FETCH_SIZE")] * 1024.0)
-    fetch = C[(K, "FETCH_SIZE")] * 1024.0 * fetch_factor
-    write = C[(K, "WRITE_SIZE")] * 1024.0
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(d, "trace",
                                                                     "run_kernel_stats.csv")))}
+    K = next(k for k in ("wb_exec_vf_kernel", "wb_exec_kernel", "wb_exec_hbm_kernel") if k in stats)
+    H = "wb_mem_hash_kernel"
+    g = lambda c, k=K: C.get((k, c))
+    hash_bytes = 65536.0 * pages * inst
+    fetch_factor = hash_bytes / (g("FETCH_SIZE", H) * 1024.0) if pages and g("FETCH_SIZE", H) else 2.0
+    fetch = g("FETCH_SIZE") * 1024.0 * fetch_factor
+    write = g("WRITE_SIZE") * 1024.0
     avg_ns = float(stats[K]["AverageNs"])
-    waves = C[(K, "SQ_WAVES")]
-    smem = C[(K, "SQ_INSTS_SMEM")]
-    head = label or ("C2, %d instances x %d compressions" % (inst, iters))
-    lines = ["# %s: rocprofv3 counters, `bench.py` (%s)" % (tag, head), "",
+    waves = g("SQ_WAVES")
+    wc = g("SQ_WAVE_CYCLES")                 # quad-cycles, summed over waves
+    gui = g("GRBM_GUI_ACTIVE")               # cycles, summed over the XCDs
+    valu = g("SQ_INSTS_VALU")
+    out = {"config": profile_key(cfg), "source": tag, "kernel": K, "kernel_avg_ns": avg_ns,
+           "waves": waves, "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch,
+           "write_bytes": write, "fetch_factor": fetch_factor,
+           "valu_insts_per_launch": valu, "salu_insts_per_launch": g("SQ_INSTS_SALU"),
+           "vmem_insts_per_launch": g("SQ_INSTS_VMEM"), "lds_insts_per_launch": g("SQ_INSTS_LDS"),
+           "branch_insts_per_launch": g("SQ_INSTS_BRANCH"),
+           "wave_quad_cycles_per_launch": wc,
+           "wait_any_frac": g("SQ_WAIT_ANY") / wc, "active_any_frac": g("SQ_ACTIVE_INST_ANY") / wc,
+           "active_valu_frac": g("SQ_ACTIVE_INST_VALU") / wc,
+           "bench_ms_per_step": line["ms_per_step"]}
+    # mean resident waves per SIMD over the kernel: wave cycles / (kernel cycles x SIMDs)
+    if gui:
+        out["waves_per_simd"] = 4.0 * wc / (gui / XCDS) / SIMDS
+    tc = g("SQ_THREAD_CYCLES_VALU")
+    if tc is not None and g("SQ_ACTIVE_INST_VALU"):
+        out["lanes_per_valu"] = tc / g("SQ_ACTIVE_INST_VALU")
+        out["valu_utilization"] = out["lanes_per_valu"] / 64.0
+    if g("TCC_HIT_sum") is not None:
+        h, m = g("TCC_HIT_sum"), g("TCC_MISS_sum")
+        out["l2_hit_rate"] = h / max(h + m, 1.0)
+    if g("VmemLatency") is not None:
+        out["vmem_latency_cycles"] = g("VmemLatency")
+    lines = ["# %s: rocprofv3 counters, `bench.py` %s" % (tag, json.dumps(out["config"])), "",
              "Per-kernel means over launches (counter passes run separately, see "
              "tools/prof_bench.sh).", "",
              "| kernel | counter | mean per launch |", "|---|---|---|"]
@@ -65,32 +114,22 @@ def main():
         if k.startswith("wb_"):
             lines.append("| %s | %s | %.6g |" % (k, c, v))
     lines += ["", "## Derived (interpreter kernel `%s`)" % K, "",
-              "* average duration (kernel trace): %.3f ms" % (avg_ns / 1e6),
-              "* FETCH_SIZE calibration on wb_mem_hash_kernel: x%.4f (known %d B read)"
-              % (fetch_factor, hash_bytes),
+              "* average duration (kernel trace): %.3f ms; bench ms per step in the trace "
+              "pass %.3f" % (avg_ns / 1e6, line["ms_per_step"]),
+              "* FETCH_SIZE calibration: x%.4f (%s)" % (
+                  fetch_factor, "wb_mem_hash_kernel reads a known %d B" % hash_bytes if pages
+                  else "no memory: the guide's x2"),
               "* HBM bytes per launch: fetch %.4g (corrected) + write %.4g = %.4g"
               % (fetch, write, fetch + write),
-              "* waves %d; dispatches per wave ~ SQ_INSTS_SMEM/waves = %.0f" % (waves, smem / waves)]
-    per = lambda c: C[(K, c)] / smem
-    for c in ["SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
-              "SQ_INSTS_VMEM"]:
-        lines.append("* %s per dispatch: %.2f" % (c, per(c)))
-    wc = C[(K, "SQ_WAVE_CYCLES")]
-    lines += ["* SQ_WAIT_ANY / SQ_WAVE_CYCLES = %.3f (parked on s_waitcnt)"
-              % (C[(K, "SQ_WAIT_ANY")] / wc),
-              "* SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES = %.3f" % (C[(K, "SQ_ACTIVE_INST_ANY")] / wc),
-              "* SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES = %.3f" % (C[(K, "SQ_WAIT_INST_ANY")] / wc),
-              "* shader cycles per dispatch (4 x wave quad-cycles / dispatches) = %.0f"
-              % (4 * wc / smem)]
+              "* waves %d; resident waves per SIMD %.2f" % (waves, out.get("waves_per_simd", 0)),
+              "* VALU instructions per launch %.4g; issue rate %.4g lane-op/s (x64 / duration)"
+              % (valu, valu * 64 / (avg_ns * 1e-9))]
+    for k in ("lanes_per_valu", "l2_hit_rate", "vmem_latency_cycles", "wait_any_frac",
+              "active_any_frac", "active_valu_frac"):
+        if k in out:
+            lines.append("* %s = %.4g" % (k, out[k]))
     open(os.path.join(prof, tag + "_counters.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"iters": iters, "instances": inst, "hbm_bytes_per_launch": fetch + write,
-               "fetch_bytes": fetch, "write_bytes": write, "fetch_factor": fetch_factor,
-               "kernel_avg_ns": avg_ns, "source": tag,
-               "valu_insts_per_launch": C[(K, "SQ_INSTS_VALU")],
-               "salu_insts_per_launch": C[(K, "SQ_INSTS_SALU")],
-               "wave_quad_cycles_per_launch": wc, "waves": waves},
-              open(os.path.join(prof, "traffic_c2.json" if label is None else
-                                "traffic_%s.json" % tag), "w"), indent=1)
+    json.dump(out, open(os.path.join(prof, "prof_%s.json" % wl), "w"), indent=1)
     print("\n".join(lines))
 
 

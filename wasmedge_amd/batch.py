@@ -265,7 +265,11 @@ class BatchContext:
 
     def set_args(self, func, values):
         values = np.ascontiguousarray(values, VALUE_DTYPE)
-        nparams = values.shape[1] if values.ndim == 2 else 0
+        # WasmEdge_BatchSetArgs reads NumInstances rows: a shorter array would be read past
+        if values.ndim != 2 or values.shape[0] != self.n:
+            raise ValueError("values must be [%d instances][params], got shape %s"
+                             % (self.n, values.shape))
+        nparams = values.shape[1]
         self._check(lib().WasmEdge_BatchSetArgs(self._h, self._name(func),
                                                 values.ctypes.data if values.size else None,
                                                 nparams))

@@ -307,6 +307,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     return kRuntimeError;
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;
+  C->reset_pending = false;   // (the stream is drained)
   if (KernelSeconds) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
@@ -454,7 +455,9 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   // without a start function and without a request for the time, the next launch on the
   // stream orders after this one: no host round trip (errors surface at the next sync)
   double secs = 0;
+  C->reset_pending = true;   // host accessors settle() before touching instance state
   if (KernelSeconds || P.start_func >= 0) {
+    C->reset_pending = false;
     if (!C->hip_ok(hipStreamSynchronize(C->stream), "mem init")) return R(kRuntimeError);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
@@ -554,6 +557,7 @@ uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) { return 
 
 WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *Costs) {
   if (!C || !Costs) return R(kWrongVMWorkflow);
+  if (!C->settle()) return R(kRuntimeError);
   const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
   std::vector<uint32_t> lo(size_t(C->nwaves) * 64), hi(lo.size());
   if (!C->hip_ok(hipMemcpy2D(lo.data(), row, C->lstate.ptr + LS_COST * 64, pitch, row, C->nwaves,
@@ -566,7 +570,7 @@ WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *
 }
 
 uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
-  if (!C || Inst >= C->n || !C->prog.has_mem) return 0;
+  if (!C || Inst >= C->n || !C->prog.has_mem || !C->settle()) return 0;
   uint32_t p = 0;
   const size_t at = (size_t(Inst / 64) * C->ls_slots + LS_PAGES) * 64 + Inst % 64;
   (void)hipMemcpy(&p, C->lstate.ptr + at, 4, hipMemcpyDeviceToHost);
@@ -602,10 +606,12 @@ size_t lane_at(uint32_t Inst, size_t stride, size_t slot) {
 }
 bool get_lane(WasmEdge_BatchContext *C, const uint32_t *buf, size_t stride, size_t slot,
               uint32_t Inst, uint32_t *v) {
+  if (!C->settle()) return false;
   return C->hip_ok(hipMemcpy(v, buf + lane_at(Inst, stride, slot), 4, hipMemcpyDeviceToHost), "read");
 }
 bool put_lane(WasmEdge_BatchContext *C, uint32_t *buf, size_t stride, size_t slot,
               uint32_t Inst, uint32_t v) {
+  if (!C->settle()) return false;
   if (Inst != WASMEDGE_BATCH_ALL_INSTANCES)
     return C->hip_ok(hipMemcpy(buf + lane_at(Inst, stride, slot), &v, 4, hipMemcpyHostToDevice), "write");
   std::vector<uint32_t> row(size_t(C->nwaves) * 64, v);   // one 64-lane row per wave
@@ -655,6 +661,7 @@ WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmE
   if (Inst == WASMEDGE_BATCH_ALL_INSTANCES) {
     // every lane: bounds against each lane's own size (all lanes checked first)
     std::vector<uint32_t> sizes(size_t(C->nwaves) * 64);
+    if (!C->settle()) return R(kRuntimeError);
     const size_t slot = LS_GLOBALS + P.global_cells + t;
     if (!C->hip_ok(hipMemcpy2D(sizes.data(), 256, C->lstate.ptr + slot * 64, size_t(C->ls_slots) * 256,
                                256, C->nwaves, hipMemcpyDeviceToHost), "read"))

@@ -124,6 +124,10 @@ struct WasmEdge_BatchContext {
   std::vector<uint8_t> result_types;
   bool ran = false;         // a Run completed since the last Reset (results are valid)
   bool mem_fresh = true;    // memory never initialised: the next Reset writes every page
+  // A Reset that skipped its host sync left init kernels queued on `stream` (non-blocking,
+  // so NOT ordered before the host accessors' synchronous null-stream copies): every host
+  // accessor settles first.
+  bool reset_pending = false;
 
   uint8_t fail(uint8_t code, const std::string &m) {
     last_error = m;
@@ -133,6 +137,12 @@ struct WasmEdge_BatchContext {
     if (e == hipSuccess) return true;
     last_error = std::string(what) + ": " + hipGetErrorString(e);
     return false;
+  }
+  // wait for queued Reset kernels before a host copy touches instance state
+  bool settle() {
+    if (!reset_pending) return true;
+    reset_pending = false;
+    return hip_ok(hipStreamSynchronize(stream), "reset kernels");
   }
 };
 

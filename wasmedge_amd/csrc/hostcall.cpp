@@ -151,6 +151,7 @@ uint64_t mem_size(const WasmEdge_BatchMemoryContext *M) {
 uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
                uint8_t *Dst, const uint8_t *Src) {
   if (Inst >= C->n) return C->fail(kRuntimeError, "instance index out of range");
+  if (!C->settle()) return kRuntimeError;
   const uint32_t lane = Inst % 64;
   uint32_t pages[64] = {0}, hwm[64] = {0};
   pages[lane] = WasmEdge_BatchGetMemoryPages(C, Inst);
@@ -261,8 +262,10 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
     }
     resumed.fetch_add(mine);
   };
-  uint32_t threads = C->host_threads ? C->host_threads
-                                     : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  // HostThreads 0 (the default) = one thread: host functions are called serially, as
+  // before pools existed; a caller whose host functions are reentrant opts in with
+  // HostThreads > 1 (a wave's lanes always stay on one thread)
+  uint32_t threads = C->host_threads ? C->host_threads : 1u;
   threads = std::min<uint32_t>(threads, uint32_t(waves.size() - 1));
   if (threads <= 1) {
     worker();
