@@ -285,11 +285,43 @@ struct Em {
   // leave before instruction pc (the C++ step executes it) when any active lane's T2 bit
   // is set
   std::string leave_if_t2() {
+    if (trip) return trip_leave();
     const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(stubs.size());
     l("s_and_b64 %s, %s, exec", T2, T2);
     l("s_cbranch_scc1 %s", lab.c_str());
     stubs.push_back(Stub{lab, pc, done, cdone});
     return lab;
+  }
+  // Trip mode (jit_source): the lanes of T2 leave alone, before instruction pc -- each
+  // records it as its pc (VPC v92) with the instructions the run retired before it (VCNT
+  // v93), no longer runs in this trip (TPC v98 = -1) and waits outside the trips as an
+  // escape (OUTSIDE s[76:77], ESC s[78:79]: the C++ step executes that instruction);
+  // the other lanes go on (past the stage's end when none is left). Out of line.
+  bool trip = false;
+  std::string stage_end;   // label: the end of the run's current stage (EXEC = its lanes)
+  int nleave = 0;
+  std::string trip_leave() {
+    const std::string id = std::to_string(run) + "_" + std::to_string(nleave++);
+    l("s_and_b64 %s, %s, exec", T2, T2);
+    l("s_cbranch_scc1 Llv%s", id.c_str());
+    l("Llr%s:", id.c_str());
+    std::string o2;
+    o.swap(o2);
+    l("Llv%s:", id.c_str());
+    l("s_andn2_b64 exec, exec, %s", T2);
+    l("s_or_b64 s[76:77], s[76:77], %s", T2);
+    l("s_or_b64 s[78:79], s[78:79], %s", T2);
+    l("s_mov_b64 s[68:69], exec");
+    l("s_mov_b64 exec, %s", T2);
+    l("v_mov_b32 v92, 0x%x", pc);
+    if (done) l("v_add_u32_e32 v93, 0x%x, v93", done);
+    l("v_mov_b32 v98, -1");
+    l("s_mov_b64 exec, s[68:69]");
+    l("s_cbranch_execz %s", stage_end.c_str());
+    l("s_branch Llr%s", id.c_str());
+    o.swap(o2);
+    tail += o2;
+    return "Llv" + id;
   }
 };
 
@@ -1466,7 +1498,7 @@ void branch_cond(Em &e, const DInstr &I) {
 
 }  // namespace
 
-std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt) {
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt, bool trip) {
   std::vector<JitRun> runs;
   const size_t n = P.code.size();
   if (P.total_cells() > TC_VF_CELLS) return runs;
@@ -1493,7 +1525,8 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bo
     }
     // a lone branch: only with SIMT, where its splits then stay in the core
     if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = simt && op_of(P.code[pc]) != OP_JMP;
-    if (end - pc >= kMinRun || calls) {
+    // (trip mode: every compilable stretch, or its lanes would wait outside the trips)
+    if (end - pc >= kMinRun || calls || (trip && simt)) {
       uint32_t cnt = 0;
       for (size_t k = pc; k < end; k++) cnt += (P.code[k].w0 >> 16) & 0xFFu;
       runs.push_back(JitRun{uint32_t(pc), uint32_t(end - pc), cnt});
@@ -2635,6 +2668,29 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
     code.push_back(DInstr{0, 0, 0, 0});
     const std::vector<TInstr> tc = wb::build_threaded(P, code, true);
     runs = wb::jit_runs(P, tc);
+    // debug listing: every DBC instruction (op, fields) with the SIMT run it belongs to
+    if (const char *lst = getenv("WB_JIT_LIST"))
+      if (FILE *f = fopen(lst, "w")) {
+        static const char *const names[] = {
+#define WB_NAME(x) #x,
+            DBC_OPS(WB_NAME)
+#undef WB_NAME
+        };
+        const std::vector<wb::JitRun> sr = wb::jit_runs(P, tc, true);
+        std::vector<int> at(P.code.size(), -1);
+        for (size_t k = 0; k < sr.size(); k++)
+          for (uint32_t i = 0; i < sr[k].len; i++) at[sr[k].pc + i] = int(k);
+        for (size_t pc = 0; pc < P.code.size(); pc++) {
+          const DInstr &I = P.code[pc];
+          const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
+          fprintf(f, "%4zu %s%-4s %-22s a=%u b=%u c=%u d=%d imm=0x%x cnt=%u\n", pc,
+                  at[pc] >= 0 && sr[at[pc]].pc == pc ? "R" : " ",
+                  at[pc] >= 0 ? std::to_string(at[pc]).c_str() : "-",
+                  op < OP_DBC_NUM_OPS ? names[op] : "?", I.w1 & 0xFFFFu, I.w1 >> 16, I.w2 & 0xFFFFu,
+                  int(int16_t(I.w2 >> 16)), I.w3, (I.w0 >> 16) & 0xFFu);
+        }
+        fclose(f);
+      }
     if (instrs) {
       *instrs = 0;
       for (const auto &r : runs) *instrs += r.len;
