@@ -56,9 +56,14 @@ def test_gpu_cost_limit(built, name):
 
 
 @pytest.mark.gpu
-def test_gpu_interrupt(built):
+@pytest.mark.parametrize("trip", ["0", "1"])
+def test_gpu_interrupt(built, monkeypatch, trip):
     """An endless loop on 64K lanes stops with Interrupted (0x07) when another thread
-    calls WasmEdge_BatchInterrupt."""
+    calls WasmEdge_BatchInterrupt, within 100 ms of the call (the kernel polls the flag
+    every scheduler round and a core call returns at least every 2^20 instructions; the
+    reference checks its StopToken on every branch: helper.cpp:184-187), with SIMT
+    scheduling and in trip mode."""
+    monkeypatch.setenv("WB_TRIP", trip)
     from wasmedge_amd import batch
     from wasmedge_amd.wat import assemble
     spin = assemble("(module (func (export \"spin\") (param i32) (result i32)"
@@ -69,13 +74,18 @@ def test_gpu_interrupt(built):
                     " (br_if $l (i32.lt_u (local.get 1) (local.get 0)))) (local.get 1)))")
     ctx = batch.BatchContext(spin, 65536, device=0, time_limit=60.0)
     try:
-        t = threading.Timer(1.0, ctx.interrupt)
+        asked = []
+
+        def stop():
+            asked.append(time.perf_counter())
+            ctx.interrupt()
+        t = threading.Timer(1.0, stop)
         t.start()
-        t0 = time.time()
         rets, st, cnt = ctx.execute("spin", batch.make_values([[i] for i in range(65536)], [I32]), 1)
+        latency = time.perf_counter() - asked[0]
         t.join()
-        assert time.time() - t0 < 30
         assert all(int(s) == 0x07 for s in st)
+        assert latency < 0.1, latency
         # the interrupt ends that run only: the next one runs to completion
         ctx.reset()
         rets, st, cnt = ctx.execute("count", batch.make_values([[2000]] * 65536, [I32]), 1)
@@ -83,6 +93,30 @@ def test_gpu_interrupt(built):
         assert int(cnt[0]) > 2000
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("trip", ["0", "1"])
+def test_gpu_max_steps_is_tight(built, monkeypatch, trip):
+    """MaxSteps: a lane stops (Interrupted) once its count reaches the budget, past it by
+    less than one compiled run (the core's budget per call is the smallest remaining budget
+    of the running lanes), whatever each lane had retired before."""
+    monkeypatch.setenv("WB_TRIP", trip)
+    from wasmedge_amd import batch
+    from wasmedge_amd.wat import assemble
+    spin = assemble("(module (func (export \"spin\") (param i32) (result i32)"
+                    " (loop $l (br_if $l (i32.and (i32.const 1) (i32.gt_u (local.get 0) (i32.const 7))))"
+                    "   (local.set 0 (i32.add (local.get 0) (i32.const 1))) (br $l))"
+                    " (local.get 0)))")
+    for budget in (1000, 123457):
+        ctx = batch.BatchContext(spin, 4096, device=0, max_steps=budget)
+        try:
+            rets, st, cnt = ctx.execute("spin", batch.make_values([[i % 13] for i in range(4096)], [I32]), 1)
+            assert all(int(s) == 0x07 for s in st)
+            over = [int(c) - budget for c in cnt]
+            assert min(over) >= 0 and max(over) < 16, (budget, min(over), max(over))
+        finally:
+            ctx.close()
 
 
 @pytest.mark.gpu

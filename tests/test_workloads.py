@@ -106,15 +106,19 @@ def test_gpu_blake3_64k(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", ["0", "1", "4", "nosimt", "scan"])
+@pytest.mark.parametrize("sched", ["0", "1", "4", "nosimt", "scan", "trip", "notrip"])
 def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
     """The wave scheduler only decides which lanes run together: the kernel's min-pc (0)
     and loop-aware largest-group policies (1, 4) between core calls, SIMT scheduling inside
     the compiled runs (default) or not (nosimt: WB_SIMT=0), with or without the unrolled
-    scan loops (scan: WB_SCAN=1), must give identical per-lane results on the divergent
-    workloads (recursion with per-lane depth, quicksort with per-lane data, Collatz's
-    br_table state machine with traps, Mandelbrot's per-lane escape)."""
-    if sched == "nosimt":
+    scan loops (scan: WB_SCAN=1), trip mode forced on or off (WB_TRIP, jit.cpp "Trip
+    mode": every lane runs its own compiled run in each trip), must give identical per-lane
+    results on the divergent workloads (recursion with per-lane depth, quicksort with
+    per-lane data, Collatz's br_table state machine with traps, Mandelbrot's per-lane
+    escape)."""
+    if sched in ("trip", "notrip"):
+        monkeypatch.setenv("WB_TRIP", "1" if sched == "trip" else "0")
+    elif sched == "nosimt":
         monkeypatch.setenv("WB_SIMT", "0")
     elif sched == "scan":
         monkeypatch.setenv("WB_SCAN", "1")
@@ -229,3 +233,40 @@ def test_gpu_memory_granules_bit_exact(built, granule):
         ref = oracle_run(O.Module(wasm), func, rows)
         got = gpu_run(wasm, func, rows, pt, rt, memory_granule=granule)
         assert compare(ref, *got, rt, exact=True) == [], name
+
+
+# Partial waves: a batch whose last wave is not full (8 lanes: one
+# partial wave; 65: a full wave and a 1-lane wave) through every engine. The lanes past
+# NumInstances are never running (batch_kernel.hip: status OK from the start), so no engine
+# may read their params, frames or memory or write their results. (Round 2's only GPU fault,
+# gpurun_out/g3, hit an 8-lane batch while the SIMT core was being built: see DESIGN.md
+# "Partial waves".)
+ENGINES = {
+    "simt": {},                                   # V frames, compiled runs, SIMT scheduling
+    "trip": {"WB_TRIP": "1"},                     # V frames, trip mode
+    "nosimt": {"WB_SIMT": "0"},                   # V frames, compiled runs without SIMT
+    "nojit": {"WB_JIT": "0"},                     # V frames, threaded core handlers only
+    "lds": {"WB_VFRAME": "0"},                    # LDS frames, threaded core
+    "step": {"WB_THREADED": "0"},                 # the compiled C++ step only
+    "hbm": {"WB_HBMFRAME": "1"},                  # frames in HBM (compiled step)
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", sorted(ENGINES))
+@pytest.mark.parametrize("n", [8, 65])
+def test_gpu_partial_waves_every_engine(built, monkeypatch, engine, n):
+    for k, v in ENGINES[engine].items():
+        monkeypatch.setenv(k, v)
+    fib = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fibonacci.wasm"), "rb").read()
+    cases = {
+        "fib": (fib, "fib", [I32], [I32], [[(i * 7) % 19] for i in range(n)]),
+        "qsort": (W.qsort_wasm(), "sort", [I32, I32], [I32], [[i, (i * 37) % 300] for i in range(n)]),
+        "collatz": (W.collatz_wasm(), "collatz", [I32, I32], [I32],
+                    [[i * 89 if i % 5 == 0 else i, 10000] for i in range(n)]),
+        "mandel": (W.mandel_wasm(), "tile", [I32, I32, I32], [I64], [[i * 5, 128, 50] for i in range(n)]),
+    }
+    for name, (wasm, func, pt, rt, rows) in cases.items():
+        ref = oracle_run(O.Module(wasm), func, rows)
+        rets, st, cnt, h = gpu_run(wasm, func, rows, pt, rt)
+        assert compare(ref, rets, st, cnt, h, rt) == [], (engine, name)

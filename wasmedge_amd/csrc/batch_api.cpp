@@ -150,15 +150,25 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // with the kernel's scan-loop policy between core calls.)
   const char *sme = getenv("WB_SIMT");
   const bool want_simt = !C->conf.CostLimit && !(sme && sme[0] == '0');
+  // Trip mode (jit.h) for modules whose load/store addresses depend on per-instance data
+  // (Program::divergent_mem: lanes part ways on loaded data); WB_TRIP=0 / 1 forces it off /
+  // on (A/B measurement aid). SIMT contexts only.
+  const char *tre = getenv("WB_TRIP");
+  bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem);
   if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
-    const std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt);
+    std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt, want_trip);
+    if (want_trip && runs.size() > wb::kTripMaxRuns) {   // (too many runs to visit per trip)
+      want_trip = false;
+      runs = wb::jit_runs(P, tcv, want_simt, false);
+    }
     if (!runs.empty()) {
       std::vector<uint8_t> start(P.code.size() + 1, 0);
       for (const auto &r : runs) start[r.pc] = 1;
       std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
       std::vector<uint64_t> addr;
       const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
-      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt);
+      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
+                                             want_trip);
       const std::string err = src.empty() ? std::string("compiled runs: no source")
                                           : wb::jit_load(src, runs.size(), C->device, &addr);
       if (err.empty()) {
@@ -172,6 +182,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
         tcv.swap(tcj);
         C->jit_runs = uint32_t(runs.size());
         C->simt = want_simt;
+        C->trip = want_trip;
       } else {
         C->last_error = err;
       }

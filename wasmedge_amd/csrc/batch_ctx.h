@@ -83,6 +83,7 @@ struct WasmEdge_BatchContext {
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
   uint32_t jit_runs = 0;          // compiled straight-line runs (jit.h)
   bool simt = false;              // KParams::simt: the compiled runs schedule diverged lanes
+  bool trip = false;              // ... in trip mode (jit.h)
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
   DevBuf<uint32_t> hframe;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
@@ -106,7 +107,7 @@ struct WasmEdge_BatchContext {
   uint32_t hb_cells = 0;
   struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; };
   std::vector<HostFn> hosts;      // per function index (imports only)
-  uint32_t host_threads = 0;      // service-round worker threads (0 = min(16, cores))
+  uint32_t host_threads = 0;      // service-round worker threads (0 or 1: one, serial)
   // built-in WASI subset (wasi.cpp): args/envs shared by every instance, captured
   // stdout/stderr and the proc_exit code per instance
   struct WasiSlot { WasmEdge_BatchContext *ctx; int fn; };

@@ -172,7 +172,7 @@ struct HbmFrame {
       "v_mov_b32 %[hwm], v101" \
       : [npc] "=s"(npc), [cnt] "=s"(cnt), [why] "=s"(why), [gsp] "+v"(gsp), [hwm] "+v"(hwm), \
         [glo] "+v"(glo), [ghi] "+v"(ghi) \
-      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
+      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(lim), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
@@ -244,14 +244,14 @@ struct HbmFrame {
       : [npc] "=&s"(npc), [cnt] "=&s"(cnt), [why] "=&s"(why), [noth] "=&s"(noth), [nlow] "=&s"(nlow), \
         [ngrp] "=&s"(ngrp), [gsp] "+v"(gsp), [hwm] "+v"(hwm), [glo] "+v"(glo), [ghi] "+v"(ghi), \
         [vpc] "+v"(vpc), [vcnt] "=&v"(vcnt) \
-      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(1u << 24), [fr] "v"(fr), \
+      : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(lim), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi), \
         [all] "s"(all), [grp] "s"(grp), [ex] "s"(ex) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", \
-        "v92", "v93", "v94", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+        "v92", "v93", "v94", "v98", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
 #define TC_VREGS "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", \
@@ -276,8 +276,9 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
                                            uint32_t fr, uint32_t pages, const uint32_t *mem, uint32_t g,
                                            uint32_t &gsp, uint32_t &hwm, uint32_t stk, uint32_t slds,
                                            uint32_t vsync, uint64_t &gas, uint64_t gas_limit,
-                                           uint32_t *ncnt, uint32_t *reason, SimtOut *so = nullptr,
-                                           uint64_t all = 0, uint64_t grp = 0, uint32_t vpc = 0) {
+                                           uint32_t *ncnt, uint32_t *reason, uint32_t lim,
+                                           SimtOut *so = nullptr, uint64_t all = 0, uint64_t grp = 0,
+                                           uint32_t vpc = 0) {
   uint32_t npc, cnt, why;
   // metered contexts: the lane's gas total in v[96:97] and the limit in v[94:95] for the
   // compiled runs (jit.cpp), which price themselves; handlers never touch them
@@ -387,7 +388,6 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t rounds = 0;
 #ifdef WB_STATS
   uint64_t *const stw = p.stats ? p.stats + (size_t)(inst >> 6) * ST_N : nullptr;
 #endif
@@ -440,6 +440,16 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         other = moved ? wave_min_u32(status == WB_STATUS_RUNNING && pc > pcs ? pc : 0xFFFFFFFFu) : low;
       }
     }
+    // The core's budget per call (instructions of the groups it runs; trip mode: 256 per
+    // trip): it returns to this loop, which checks the limits and the interrupt flag, at
+    // least every 2^20 instructions -- and, under MaxSteps, before any running lane could
+    // pass its budget by more than the run it is in
+    uint32_t core_lim = 1u << 20;
+    if (p.max_steps < (1ull << 62)) {
+      const uint64_t rem = count < p.max_steps ? p.max_steps - count : 1;
+      const uint32_t r32 = (uint32_t)min(rem, (uint64_t)core_lim);
+      core_lim = max(1u, wave_min_u32(status == WB_STATUS_RUNNING ? r32 : 0xFFFFFFFFu));
+    }
     bool slow = false;   // the run stopped at an instruction that needs the slow step
     bool first = false;  // SIMT: the core left the group before a HOT instruction
     if constexpr (VF) {
@@ -454,7 +464,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         uint32_t ncnt, why;
         const uint32_t gpc = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm,
                                         stk_lds, S_lds, (TC_VF_CELLS - p.total_cells) * 8u, cost, ~0ull,
-                                        &ncnt, &why, &so, runmask, act, pc);
+                                        &ncnt, &why, core_lim, &so, runmask, act, pc);
         WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
         if (status == WB_STATUS_RUNNING) {
           pc = so.vpc;
@@ -526,7 +536,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           scost = 0;
           pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, cost,
-                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why);
+                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why, core_lim);
           // (sign-extended: a core call that only takes a jump whose count correction is
           // negative -- a `br` out of blocks, cnt 1 + tcnt -2 -- retires -1 instructions)
           asc += (uint64_t)(int64_t)(int32_t)ncnt;
@@ -586,7 +596,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         // every 1024 taken jumps (and before the SGPR count could overflow) the run
         // returns to the scheduler, which flushes counts and checks the limits
         if (pcs <= low) other = low;   // jumped back below every waiting lane
-        if (--tick == 0 || (int32_t)sc < 0 || pcs >= other) goto k_leave;
+        if (--tick == 0 || (int32_t)sc < 0 || sc >= core_lim || pcs >= other) goto k_leave;
         I = code[pcs];
         continue;
       k_exit:
@@ -686,10 +696,11 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef HOST_YIELD
     }
     WB_STAT_ADD(ST_CYC_SLOW, WB_NOW() - ts2);
-    // budget, wall clock, and (every 64th round) the host's interrupt request, read
-    // from uncached device memory at system scope
-    const bool stop = (++rounds & 63u) == 0 &&
-                      __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // budget, wall clock, and the host's interrupt request (every round: a core call
+    // returns at least every 2^20 instructions), read from uncached device memory at
+    // system scope -- the reference's StopToken, checked on every branch, call and return
+    // (helper.cpp:24-27,184-187, controlInstr.cpp:75-78)
+    const bool stop = __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (status == WB_STATUS_RUNNING &&
         (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks || stop))
       status = WB_ERR_INTERRUPTED;

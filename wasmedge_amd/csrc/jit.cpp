@@ -1623,6 +1623,71 @@ void wave_min_vpc(Em &e, const char *mask, const char *dst) {
   e.l("s_nop 1");
 }
 
+// The scheduler's pick: the lanes of `mask` (ALL, or another SGPR pair: trip mode's
+// lanes outside the trips) at their lowest pc are the group, OTHER/LOW = the lowest pc of
+// the other lanes in ALL, the handler banks of the matching mode, and the group's TInstr
+// is dispatched. `p`: label prefix (Lsc for Lsched).
+void sched_block(Em &e, const std::string &p, const char *mask) {
+  // every pick costs 16 of the budget as well: the core returns to the kernel (limits,
+  // interrupts) even if the lanes retired nothing
+  e.l("s_sub_u32 s64, s64, 16");
+  e.l("s_cselect_b32 s64, 0, s64");
+  e.l("s_mov_b64 exec, -1");
+  if (mask) e.l("s_mov_b64 s[74:75], %s", mask);   // (the TInstr load below overwrites s[76:91])
+  e.l("s_nop 4");
+  wave_min_vpc(e, mask ? "s[74:75]" : "s[96:97]", "s68");   // the lowest pc
+  e.l("s_lshl_b32 s62, s68, 5");
+  // the group's TInstr loads while the rest of the pick goes on (a prefetch still in
+  // flight must land first: SMEM returns out of order)
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+  e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+  if (mask) {
+    e.l("v_cmp_eq_u32_e64 vcc, s68, %s", VPC);
+    e.l("s_and_b64 s[74:75], vcc, s[74:75]");          // the group: the mask's lanes at that pc
+  } else {
+    e.l("v_cmp_eq_u32_e64 s[74:75], s68, %s", VPC);
+    e.l("s_and_b64 s[74:75], s[74:75], s[96:97]");     // the group: ALL at that pc
+  }
+  e.l("s_cmp_eq_u32 s95, -1");                         // were the banks converged?
+  e.l("s_cselect_b32 s69, 1, 0");
+  e.l("s_andn2_b64 vcc, s[96:97], s[74:75]");          // the lanes left waiting
+  e.l("s_cbranch_vccz %s_conv", p.c_str());
+  wave_min_vpc(e, "vcc", "s63");
+  e.l("s_lshl_b32 s63, s63, 5");
+  e.l("s_mov_b32 s95, s63");
+  // (s69 = 1 when the banks were the converged ones)
+  e.l("s_cmp_eq_u32 s69, 0");
+  e.l("s_cbranch_scc1 %s_disp", p.c_str());
+  e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
+  e.l("s_addc_u32 s71, s71, 0");
+  e.l("s_branch %s_bankb", p.c_str());
+  e.l("%s_conv:", p.c_str());
+  e.l("s_mov_b32 s63, -1");
+  e.l("s_mov_b32 s95, -1");
+  e.l("s_cmp_eq_u32 s69, 1");
+  e.l("s_cbranch_scc1 %s_disp", p.c_str());
+  e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
+  e.l("s_subb_u32 s71, s71, 0");
+  e.l("%s_bankb:", p.c_str());
+  e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
+  e.l("s_addc_u32 s73, s71, 0");
+  // (entered with the group in s[74:75], s62 = its pc, its TInstr loading, the banks of
+  // the right mode; split paths jump here directly)
+  e.l("%s_disp:", p.c_str());
+  e.l("s_mov_b64 exec, s[74:75]");
+  e.l("s_cmp_eq_u32 s64, 0");                          // budget spent: to the kernel
+  e.l("s_cbranch_scc1 %s_out", p.c_str());
+  e.l("s_waitcnt lgkmcnt(0)");
+  e.l("s_add_u32 s68, s70, s76");
+  e.l("s_addc_u32 s69, s71, 0");
+  e.l("s_setpc_b64 s[68:69]");
+  e.l("%s_out:", p.c_str());
+  e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+  e.l("s_addc_u32 s69, s71, 0");
+  e.l("s_setpc_b64 s[68:69]");
+}
+
 // Lmerge (the group reached OTHER or the count limit: its pc is PCOFF) and Lsched
 std::string simt_sched() {
   Em e;
@@ -1631,58 +1696,7 @@ std::string simt_sched() {
   e.l("v_lshrrev_b32_e64 %s, 5, s62", VPC);
   flush(e);
   e.l("Lsched:");
-  // every pick costs 16 of the budget as well: the core returns to the kernel (limits,
-  // interrupts) even if the lanes retired nothing
-  e.l("s_sub_u32 s64, s64, 16");
-  e.l("s_cselect_b32 s64, 0, s64");
-  e.l("s_mov_b64 exec, -1");
-  e.l("s_nop 4");
-  wave_min_vpc(e, "s[96:97]", "s68");                  // the lowest pc
-  e.l("s_lshl_b32 s62, s68, 5");
-  // the group's TInstr loads while the rest of the pick goes on (a prefetch still in
-  // flight must land first: SMEM returns out of order)
-  e.l("s_waitcnt lgkmcnt(0)");
-  e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
-  e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
-  e.l("v_cmp_eq_u32_e64 s[74:75], s68, %s", VPC);
-  e.l("s_and_b64 s[74:75], s[74:75], s[96:97]");       // the group: ALL at that pc
-  e.l("s_cmp_eq_u32 s95, -1");                         // were the banks converged?
-  e.l("s_cselect_b32 s69, 1, 0");
-  e.l("s_andn2_b64 vcc, s[96:97], s[74:75]");          // the lanes left waiting
-  e.l("s_cbranch_vccz Lsc_conv");
-  wave_min_vpc(e, "vcc", "s63");
-  e.l("s_lshl_b32 s63, s63, 5");
-  e.l("s_mov_b32 s95, s63");
-  // (s69 = 1 when the banks were the converged ones)
-  e.l("s_cmp_eq_u32 s69, 0");
-  e.l("s_cbranch_scc1 Lsc_disp");
-  e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
-  e.l("s_addc_u32 s71, s71, 0");
-  e.l("s_branch Lsc_bankb");
-  e.l("Lsc_conv:");
-  e.l("s_mov_b32 s63, -1");
-  e.l("s_mov_b32 s95, -1");
-  e.l("s_cmp_eq_u32 s69, 1");
-  e.l("s_cbranch_scc1 Lsc_disp");
-  e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
-  e.l("s_subb_u32 s71, s71, 0");
-  e.l("Lsc_bankb:");
-  e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
-  e.l("s_addc_u32 s73, s71, 0");
-  // (entered with the group in s[74:75], s62 = its pc, its TInstr loading, the banks of
-  // the right mode; split paths jump here directly)
-  e.l("Lsc_disp:");
-  e.l("s_mov_b64 exec, s[74:75]");
-  e.l("s_cmp_eq_u32 s64, 0");                          // budget spent: to the kernel
-  e.l("s_cbranch_scc1 Lsc_out");
-  e.l("s_waitcnt lgkmcnt(0)");
-  e.l("s_add_u32 s68, s70, s76");
-  e.l("s_addc_u32 s69, s71, 0");
-  e.l("s_setpc_b64 s[68:69]");
-  e.l("Lsc_out:");
-  e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
-  e.l("s_addc_u32 s69, s71, 0");
-  e.l("s_setpc_b64 s[68:69]");
+  sched_block(e, "Lsc", nullptr);
   return e.o;
 }
 
@@ -1937,9 +1951,343 @@ bool fwd_plan(const Program &P, const std::vector<JitRun> &runs, size_t k, size_
   return true;
 }
 
+// ---------------------------------------------------------------- trip mode
+// SIMT scheduling runs one group of lanes at a time -- the lanes at the lowest pc -- and a
+// group waits out the latency of each load it makes. Where lanes part ways on loaded data
+// (C3's Hoare scans: every lane leaves its `while (a[i] < p) i++` after its own number of
+// steps) the groups are small (4.0 active lanes per VALU instruction, 62% of wave cycles
+// waiting on memory: profiles/r03b_c3_counters.md), so the wave pays one memory latency
+// per few lane-steps. Trip mode runs every lane instead: in one trip each lane of the wave
+// that waits at the start of a compiled run executes that whole run, whichever it is,
+// and all the runs' loads are in flight together:
+//   stage A  for each run with lanes: EXEC = its lanes, its instructions up to its loads
+//            and the loads themselves (nothing here reads a loaded cell: trip_split);
+//   one s_waitcnt vmcnt(0) for every load of the trip;
+//   stage B  for each run with lanes: the rest of the run and its transfer, per lane
+//            (VPC = the lane's next pc, VCNT += what it retired, the taken count
+//            corrections per lane; calls, returns and br_table per lane too).
+// The lanes' register state is their own (VGPRs under disjoint EXEC masks), so a run's
+// temporaries survive from its stage A to its stage B. TPC (v98) = the pc a lane started
+// the trip at: a lane moved to another run in stage B runs that one in the next trip.
+// Lanes at a pc where no run starts wait outside the trips (OUTSIDE s[76:77]), and so do
+// lanes that must leave before an instruction (a failed bounds/alignment check, a call
+// stack past its LDS part, a return from the entry function: ESC s[78:79], Em::trip_leave).
+// Trips go on while more lanes are in the runs than outside them; then escapes go to the
+// C++ step (xh) and the other outside lanes to the scheduler's pick among them (their
+// handlers, Ltq), and they come back through a run's entry. Every trip costs 256 of the
+// core's budget (or the longest run's count, if more): the core returns to the kernel
+// (limits, interrupts) every 4K trips, and no lane retires more than the budget plus one run.
+namespace {
+const char *const TPC = "v98";
+
+// does I name a cell of `set` in any operand field (one cell per field for the 32-bit
+// ops of written_exact, else conservatively 4)
+bool names_any(const DInstr &I, const std::vector<uint8_t> &set) {
+  const uint32_t f[5] = {I.w1 & 0xFFFFu, I.w1 >> 16, I.w2 & 0xFFFFu, I.w2 >> 16,
+                         op_of(I) == OP_I32_ADD3_XROTR_I ? (I.w3 & 0xFFFFu) : 0xFFFFu};
+  std::vector<uint32_t> w;
+  const uint32_t width = written_exact(I, &w) ? 1u : 4u;
+  for (uint32_t x : f)
+    for (uint32_t k = 0; k < width; k++)
+      if (x + k < set.size() && set[x + k]) return true;
+  return false;
+}
+
+// stage A of a run = its instructions before trip_split: up to its first store or
+// POST_CALL past the first, or the first instruction that names a cell loaded before it;
+// 0 when that prefix loads nothing (all in stage B)
+uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
+  std::vector<uint8_t> loaded(TC_VF_CELLS + 8, 0);
+  uint32_t s = 0;
+  bool any = false;
+  for (uint32_t i = 0; i < nbody; i++) {
+    const DInstr &I = P.code[r.pc + i];
+    const uint16_t op = op_of(I);
+    if (names_any(I, loaded) || (op == OP_POST_CALL && i) || is_store_op(op)) break;
+    if (mem_bytes(op)) {
+      const uint32_t c = I.w2 & 0xFFFFu;
+      for (uint32_t k = 0; k < (load_wide(op) ? 2u : 1u); k++) loaded[c + k] = 1;
+      any = true;
+    }
+    s = i + 1;
+  }
+  return any ? s : 0;
+}
+}  // namespace
+
+std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog) {
+  std::map<uint32_t, size_t> start;
+  for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
+  auto in_region = [&](uint32_t pc) { return start.count(pc) != 0; };
+  // the pcs a return of function f can land on: after each direct call of f and after
+  // every call_indirect
+  std::map<uint32_t, uint32_t> fentry;
+  for (uint32_t f = 0; f < P.funcs.size(); f++)
+    if (!P.funcs[f].imported) fentry[P.funcs[f].entry_pc] = f;
+  auto func_of = [&](uint32_t pc) -> int64_t {
+    auto it = fentry.upper_bound(pc);
+    return it == fentry.begin() ? -1 : int64_t(std::prev(it)->second);
+  };
+  std::map<int64_t, std::vector<uint32_t>> ret_out;   // function -> return pcs outside the runs
+  std::vector<uint32_t> ind_out;
+  for (uint32_t pc = 0; pc + 1 < P.code.size(); pc++) {
+    const uint16_t o = op_of(P.code[pc]);
+    if (o == OP_CALL && !in_region(pc + 1)) ret_out[func_of(P.code[pc].w3)].push_back(pc + 1);
+    if (o == OP_CALL_INDIRECT && !in_region(pc + 1)) ind_out.push_back(pc + 1);
+  }
+  std::string body;
+  body += "s_getpc_b64 s[6:7]\nLpt:\ns_add_u32 s6, s6, Ltab - Lpt\ns_addc_u32 s7, s7, 0\n"
+          "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
+          "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
+          "s_setpc_b64 s[8:9]\n";
+  Em h;   // entry stubs, the trip loop and its exits
+  // a run's entry (its TInstr): the group's lanes record their pc and count; then every
+  // lane's place is sorted out (OUTSIDE: not at a run start) and the trips begin
+  for (size_t k = 0; k < runs.size(); k++) {
+    h.l(".p2align 6");   // (jit_load expects 64-byte aligned run addresses)
+    h.l("Lb%zu:", k);
+    h.l("v_lshrrev_b32_e64 %s, 5, s62", VPC);
+    flush(h);
+    long_jump(h, "Ltin", "Ltiq" + std::to_string(k));
+  }
+  h.l(".p2align 6");
+  h.l("Ltin:");
+  h.l("s_mov_b64 exec, s[96:97]");
+  h.l("s_mov_b64 s[76:77], s[96:97]");
+  h.l("s_mov_b64 s[78:79], 0");
+  for (const auto &r : runs) {
+    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", r.pc, VPC);
+    h.l("s_andn2_b64 s[76:77], s[76:77], vcc");
+  }
+  // TPC for the next trip: the pc of every lane in the runs, -1 outside
+  h.l("Ltp:");
+  h.l("s_mov_b64 exec, s[96:97]");
+  h.l("v_mov_b32 %s, %s", TPC, VPC);
+  h.l("s_mov_b64 exec, s[76:77]");
+  h.l("v_mov_b32 %s, -1", TPC);
+  h.l("s_mov_b64 exec, s[96:97]");
+  // ---- the trip (EXEC = ALL between the runs)
+  std::string ooa, oob;   // the runs' stage code, out of line
+  std::vector<uint32_t> split(runs.size());
+  const uint32_t nr = uint32_t(runs.size());
+  for (uint32_t k = 0; k < nr; k++) {
+    const JitRun &r = runs[k];
+    const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
+    split[k] = trip_split(P, r, ends_run(lop) ? r.len - 1 : r.len);
+  }
+  h.l("Ltrip:");
+  for (uint32_t k = 0; k < nr; k++) {
+    if (!split[k]) continue;
+    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
+    h.l("s_and_b64 s[74:75], vcc, exec");
+    h.l("s_cbranch_scc1 LtA%u", k);
+    h.l("LtAr%u:", k);
+  }
+  h.l("s_waitcnt vmcnt(0)");
+  for (uint32_t k = 0; k < nr; k++) {
+    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
+    h.l("s_and_b64 s[74:75], vcc, exec");
+    h.l("s_cbranch_scc1 LtB%u", k);
+    h.l("LtBr%u:", k);
+  }
+  // ---- after the trip: go on while more lanes are in the runs than outside them
+  h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
+  h.l("s_cmp_eq_u64 s[80:81], 0");
+  h.l("s_cbranch_scc1 Ltx");
+  h.l("s_cmp_eq_u64 s[76:77], 0");
+  h.l("s_cbranch_scc1 Ltbud");
+  h.l("s_bcnt1_i32_b64 s68, s[80:81]");
+  h.l("s_bcnt1_i32_b64 s69, s[76:77]");
+  h.l("s_cmp_gt_u32 s69, s68");
+  h.l("s_cbranch_scc1 Ltx");
+  h.l("Ltbud:");
+  uint32_t trip_cost = 256;   // (>= any run's count: a lane never retires more than a trip costs)
+  for (const auto &r : runs) trip_cost = std::max(trip_cost, r.cnt);
+  h.l("s_sub_u32 s64, s64, 0x%x", trip_cost);
+  h.l("s_cselect_b32 s64, 0, s64");
+  h.l("s_cmp_eq_u32 s64, 0");
+  h.l("s_cbranch_scc0 Ltp");
+  // budget spent: back to the kernel with no group (reason 1)
+  h.l("s_mov_b64 exec, 0");
+  h.l("s_mov_b32 s65, 0");
+  h.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+  h.l("s_addc_u32 s69, s71, 0");
+  h.l("s_setpc_b64 s[68:69]");
+  // ---- leaving the trips: escapes first (the C++ step executes their instruction: xh),
+  // then the other lanes outside (their handlers, through the scheduler's pick)
+  h.l("Ltx:");
+  h.l("s_cmp_eq_u64 s[78:79], 0");
+  h.l("s_cbranch_scc1 Ltq");
+  h.l("s_mov_b64 exec, -1");
+  h.l("s_mov_b64 s[74:75], s[78:79]");
+  h.l("s_nop 4");
+  wave_min_vpc(h, "s[74:75]", "s68");
+  h.l("s_lshl_b32 s62, s68, 5");
+  h.l("v_cmp_eq_u32_e64 vcc, s68, %s", VPC);
+  h.l("s_and_b64 s[74:75], vcc, s[74:75]");
+  h.l("s_andn2_b64 vcc, s[96:97], s[74:75]");
+  h.l("s_mov_b32 s63, -1");
+  h.l("s_cbranch_vccz Ltxg");
+  wave_min_vpc(h, "vcc", "s63");
+  h.l("s_lshl_b32 s63, s63, 5");
+  h.l("Ltxg:");
+  h.l("s_mov_b32 s95, s63");
+  h.l("s_mov_b32 s65, 0");
+  h.l("s_mov_b64 exec, s[74:75]");
+  h.l("s_setpc_b64 s[70:71]");
+  h.l("Ltq:");
+  sched_block(h, "Ltq", "s[76:77]");
+  // ---- the runs' stages
+  for (uint32_t k = 0; k < nr; k++) {
+    const JitRun &r = runs[k];
+    const DInstr &last = P.code[r.pc + r.len - 1];
+    const uint16_t lop = op_of(last);
+    const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
+    std::vector<int> lead;
+    const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
+    uint32_t done = 0;
+    for (int st = 0; st < 2; st++) {
+      if (st == 0 && !split[k]) continue;
+      Em e;
+      e.trip = true;
+      e.g = glog;
+      e.fb = P.global_cells;
+      e.prog = &P;
+      e.run = k + uint32_t(st) * nr;
+      e.done = done;
+      const std::string L = (st ? "LtB" : "LtA") + std::to_string(k);
+      e.stage_end = L + "e";
+      e.l(".p2align 2");
+      e.l("%s:", L.c_str());
+      e.l("s_mov_b64 exec, s[74:75]");
+      const size_t at = e.o.size();
+      for (uint32_t i = st ? split[k] : 0; i < (st ? nbody : split[k]); i++) {
+        const DInstr &I = P.code[r.pc + i];
+        e.pc = r.pc + i;
+        e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
+        if (!emit(e, I)) return "";
+        e.done += (I.w0 >> 16) & 0xFFu;
+      }
+      done = e.done;
+      if (st == 1) {
+        // the transfer, per lane: VPC = where each lane goes on, VCNT += what the run
+        // retired (with a taken branch's count correction)
+        const uint32_t fall = r.pc + r.len;
+        const uint32_t tgt = (lop == OP_CALL || is_branch_op(lop)) ? last.w3 : 0;
+        e.pc = r.pc + r.len - 1;
+        e.group = nullptr;
+        auto out_if = [&](const char *m) { e.l("s_or_b64 s[76:77], s[76:77], %s", m); };
+        auto add_cnt = [&](int64_t c) { if (c) e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(c), VCNT); };
+        if (is_branch_op(lop) && lop != OP_JMP) {
+          const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
+          branch_cond(e, last);   // vcc = taken
+          e.l("v_mov_b32 %s, 0x%x", X0, fall);
+          e.l("v_mov_b32 %s, 0x%x", X1, tgt);
+          e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", VPC, X0, X1);
+          if (tcnt) {
+            e.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));
+            e.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
+            e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+          }
+          add_cnt(r.cnt);
+          if (!in_region(tgt)) { e.l("s_and_b64 s[68:69], vcc, exec"); out_if("s[68:69]"); }
+          if (!in_region(fall)) { e.l("s_andn2_b64 s[68:69], exec, vcc"); out_if("s[68:69]"); }
+        } else if (lop == OP_JMP) {
+          e.l("v_mov_b32 %s, 0x%x", VPC, tgt);
+          add_cnt(int64_t(r.cnt) + int16_t(last.w2 >> 16));
+          if (!in_region(tgt)) out_if("exec");
+        } else if (lop == OP_BR_TABLE) {
+          emit_br_table(e, last);   // Y0 = target, Y1 = correction
+          e.l("v_mov_b32 %s, %s", VPC, Y0);
+          e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, Y1);
+          add_cnt(r.cnt);
+          std::vector<uint32_t> seen;
+          for (uint32_t q = 0; q <= (last.w1 >> 16); q++) {
+            const uint32_t t = P.brtab[2 * (last.w3 + q)];
+            if (in_region(t) || std::find(seen.begin(), seen.end(), t) != seen.end()) continue;
+            seen.push_back(t);
+            e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", t, Y0);
+            e.l("s_and_b64 s[68:69], vcc, exec");
+            out_if("s[68:69]");
+          }
+        } else if (lop == OP_CALL) {
+          std::vector<uint8_t> dead;
+          if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
+          emit_call(e, last, e.pc, dead.empty() ? nullptr : &dead);
+          e.l("v_mov_b32 %s, 0x%x", VPC, tgt);
+          add_cnt(r.cnt);
+          if (!in_region(tgt)) out_if("exec");
+        } else if (lop == OP_RET) {
+          // per lane: the call stack past its LDS part and the entry function's return
+          // leave (the C++ step); the others pop their own return record
+          const uint32_t a = last.w1 & 0xFFFFu, nres = last.w1 >> 16, fb = e.fb;
+          e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
+          e.leave_if_t2();
+          e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+          e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
+          e.l("ds_read_b32 %s, %s", Y1, X1);
+          e.l("s_waitcnt lgkmcnt(0)");
+          e.l("v_and_b32_e32 %s, 0xfffff, %s", X0, Y1);
+          e.l("v_cmp_eq_u32_e32 vcc, 0xfffff, %s", X0);
+          e.l("s_mov_b64 %s, vcc", T2);
+          e.leave_if_t2();
+          e.l("v_subrev_u32_e32 v102, 1, v102");
+          for (uint32_t q = 0; q < nres; q++)
+            if (a != fb) e.l("v_mov_b32 %s, %s", e.v(fb + q), e.v(a + q));
+          e.l("v_mov_b32 %s, %s", VPC, X0);
+          add_cnt(r.cnt);
+          std::vector<uint32_t> outs = ind_out;
+          const auto it = ret_out.find(func_of(e.pc));
+          if (it != ret_out.end()) outs.insert(outs.end(), it->second.begin(), it->second.end());
+          std::sort(outs.begin(), outs.end());
+          outs.erase(std::unique(outs.begin(), outs.end()), outs.end());
+          for (uint32_t t : outs) {
+            e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", t, X0);
+            e.l("s_and_b64 s[68:69], vcc, exec");
+            out_if("s[68:69]");
+          }
+        } else {   // falls through into the instruction after the run
+          e.l("v_mov_b32 %s, 0x%x", VPC, fall);
+          add_cnt(r.cnt);
+          if (!in_region(fall)) out_if("exec");
+        }
+        e.drain();
+      }
+      std::string code = e.o.substr(0, at) + schedule(e.o.substr(at));
+      code += e.stage_end + ":\n";
+      code += "s_mov_b64 exec, s[96:97]\n";
+      code += "s_branch " + std::string(st ? "LtBr" : "LtAr") + std::to_string(k) + "\n";
+      code += e.tail;
+      (st ? oob : ooa) += code;
+    }
+  }
+  body += h.o + ooa + oob;
+  body = resolve_jumps(body);
+  body += ".p2align 3\nLtab:\n";
+  for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
+  body += "Lend:\n";
+  std::string src =
+      "// generated by jit.cpp: compiled runs of the V-frame threaded core (trip mode)\n"
+      "extern \"C\" __global__ void wbjit_addrs(unsigned long long *out, unsigned n) {\n"
+      "  unsigned lo, hi;\n"
+      "  asm volatile(\n";
+  for (size_t at = 0; at < body.size();) {
+    const size_t nl = body.find('\n', at);
+    src += "      \"" + body.substr(at, nl - at) + "\\n\"\n";
+    at = nl + 1;
+  }
+  src += "      : \"=s\"(lo), \"=s\"(hi) : : \"s6\", \"s7\", \"s8\", \"s9\", \"scc\", \"memory\");\n"
+         "  const long long *tab = (const long long *)(((unsigned long long)hi << 32) | lo);\n"
+         "  for (unsigned k = threadIdx.x; k < n; k += blockDim.x)\n"
+         "    out[k] = (unsigned long long)tab + (unsigned long long)tab[k];\n"
+         "}\n";
+  return src;
+}
+
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost, bool simt) {
+                       const JitCost *cost, bool simt, bool trip) {
   if (cost) simt = false;
+  if (trip && simt && runs.size() <= kTripMaxRuns) return trip_source(P, runs, glog);
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
@@ -2695,13 +3043,14 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       *instrs = 0;
       for (const auto &r : runs) *instrs += r.len;
     }
-    // both flavours: plain runs and SIMT scheduling (KParams::simt, its own run choice)
-    for (int simt = 0; simt < 2 && e.empty(); simt++) {
-      if (simt) runs = wb::jit_runs(P, tc, true);
+    // every flavour: plain runs, SIMT scheduling (KParams::simt, its own run choice) and
+    // trip mode (its own run choice too)
+    for (int simt = 0; simt < 3 && e.empty(); simt++) {
+      if (simt) runs = wb::jit_runs(P, tc, true, simt == 2);
       if (runs.empty()) continue;
       std::vector<char> obj;
-      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0);
-      if (const char *dump = getenv(simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
+      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2);
+      if (const char *dump = getenv(simt == 2 ? "WB_JIT_DUMP_TRIP" : simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
         if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
       e = src.empty() ? "no source" : wb::jit_compile(src, &obj);
     }

@@ -32,8 +32,10 @@ struct JitRun {
 // no jump target past their first, at least kMinRun long. `tc`: build_threaded's array
 // (an instruction without a handler there is never compiled).
 // simt: (KParams::simt) lone conditional branches and br_table end runs too, so that
-// their splits stay in the core.
-std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt = false);
+// their splits stay in the core. trip: runs for trip mode (below): any length, lone jumps
+// too (a lane at a pc outside every run waits outside the trips).
+std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bool simt = false,
+                             bool trip = false);
 
 // Gas prices of a metered context (batch_ctx.h cost_off_h / cost_pool_h): per DBC
 // instruction its cost list's prefix sums. A compiled run checks at entry that every lane
@@ -53,8 +55,13 @@ struct JitCost {
 // memory granule = 4 << glog bytes (batch_ctx.h lane_word). cost: metered contexts.
 // simt: lanes that part ways (a split branch or return, reaching a waiting lane) stay in
 // the core and are scheduled there (Lsched, KParams::simt); not with cost.
+// Trip mode visits every run twice per trip: modules with more runs keep SIMT scheduling.
+constexpr size_t kTripMaxRuns = 96;
+// trip: (with simt, not with cost) trip mode instead of per-group runs: every lane of the
+// wave at a run start runs that run in each trip, all of them together (jit.cpp "Trip
+// mode"); for modules whose lanes part ways on loaded data.
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost = nullptr, bool simt = false);
+                       const JitCost *cost = nullptr, bool simt = false, bool trip = false);
 
 // Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
 std::string jit_compile(const std::string &src, std::vector<char> *code);
