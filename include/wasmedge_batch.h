@@ -57,6 +57,7 @@ typedef struct WasmEdge_Result {
 #define WASMEDGE_BATCH_INTERRUPTED 0x07u      /* ErrCode::Interrupted: step/time limit */
 #define WASMEDGE_BATCH_STACK_EXHAUSTED 0xB0u  /* device call stack full */
 #define WASMEDGE_BATCH_HOST_CALL 0xB1u        /* reached a host import no host function is bound to */
+#define WASMEDGE_BATCH_TAIL_CALL_HOST 0xB2u   /* return_call_indirect reached a host import */
 
 typedef struct WasmEdge_BatchConfigure {
   /* Page budget per instance; plays RuntimeConfigure::MaxMemPage
@@ -102,6 +103,13 @@ typedef struct WasmEdge_BatchConfigure {
    * are the same in every instance, 128 when they depend on per-instance data). Layout
    * only: results never depend on it. */
   uint32_t MemoryGranule;
+  /* The TailCall proposal (return_call, return_call_indirect; WasmEdge_ConfigureAddProposal
+   * (Conf, WasmEdge_Proposal_TailCall), include/common/configure.h:176-182 leaves it off):
+   * 0 = off, the opcodes fail BatchCreate with IllegalOpCode (0x37) as in the reference's
+   * loader. On: a tail call reuses the caller's frame, so tail recursion never exhausts the
+   * device call stack. A return_call to a host import fails BatchCreate (0x02), and a
+   * return_call_indirect that reaches one ends the instance with 0xB2. */
+  uint32_t TailCall;
 } WasmEdge_BatchConfigure;
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;

@@ -238,6 +238,11 @@ static int load_immediates(OMod *m, Rd *r, uint32_t ii) {
   return r->err;
 }
 
+/* The TailCall proposal (configure.h:176-182: off by default); TEST INFRASTRUCTURE knob
+ * mirroring WasmEdge_BatchConfigure::TailCall for modules loaded from now on. */
+static int g_tail_call;
+void om_set_tail_call(int on) { g_tail_call = on != 0; }
+
 /* lib/loader/ast/instruction.cpp:35-116 -- decode one expression with block stack. */
 static int load_instr_seq(OMod *m, Rd *r, uint32_t *start, uint32_t *len) {
   uint32_t bstack[1024], bsp = 0;
@@ -250,6 +255,8 @@ static int load_instr_seq(OMod *m, Rd *r, uint32_t *start, uint32_t *len) {
       op = (uint16_t)(op << 8 | sub);
     }
     if (r->err) return r->err;
+    /* instruction.cpp:903-907: return_call(_indirect) need the TailCall proposal */
+    if ((op == 0x12 || op == 0x13) && !g_tail_call) return E_ILLEGAL_OPCODE;
     uint32_t ii = push_instr(m);
     m->code[ii].op = op;
     int reach_end = 0;
@@ -534,6 +541,8 @@ static int check_func(OMod *m, uint32_t fi) {
     case 0x10: case 0x12: {
       if (in->idx >= m->nfuncs) { c.err = E_TYPECHECK; break; }
       FType *t = &m->types[m->funcs[in->idx].type];
+      /* formchecker.cpp:526-530: a tail call's callee returns what the caller returns */
+      if (op == 0x12 && (t->nr != c.nret || memcmp(t->r, c.returns, t->nr))) { c.err = E_TYPECHECK; break; }
       ck_pops(&c, t->p, t->np);
       if (op == 0x12) { ck_unreachable(&c); break; }
       ck_pushs(&c, t->r, t->nr);
@@ -543,6 +552,7 @@ static int check_func(OMod *m, uint32_t fi) {
       if (in->idx >= m->ntypes || in->idx2 >= m->ntables) { c.err = E_TYPECHECK; break; }
       ck_pop_t(&c, T_I32);
       FType *t = &m->types[in->idx];
+      if (op == 0x13 && (t->nr != c.nret || memcmp(t->r, c.returns, t->nr))) { c.err = E_TYPECHECK; break; }
       ck_pops(&c, t->p, t->np);
       if (op == 0x13) { ck_unreachable(&c); break; }
       ck_pushs(&c, t->r, t->nr);
@@ -833,9 +843,11 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
       uint32_t n = rd_u32(&s);
       if (n != nfunc_decl) { *err = E_MALFORMED; break; }
       m->funcs = realloc(m->funcs, sizeof(Func) * (m->nfuncs + n + 1));
+      /* (all of them: a body that fails to load leaves the rest unvisited, and om_free
+       * frees every function's ltypes) */
+      memset(&m->funcs[m->nfuncs], 0, sizeof(Func) * (n + 1));
       for (uint32_t k = 0; k < n && !*err; k++) {
         Func *F = &m->funcs[m->nfuncs + k];
-        memset(F, 0, sizeof *F);
         F->type = func_types[k];
         if (F->type >= m->ntypes) { *err = E_TYPECHECK; break; }
         uint32_t blen = rd_u32(&s);

@@ -58,7 +58,8 @@ class _Conf(ctypes.Structure):
                 ("MaxSteps", ctypes.c_uint64), ("TimeLimitSeconds", ctypes.c_double),
                 ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64),
                 ("HostThreads", ctypes.c_uint32), ("CostTable", ctypes.c_void_p),
-                ("CostTableLen", ctypes.c_uint32), ("MemoryGranule", ctypes.c_uint32)]
+                ("CostTableLen", ctypes.c_uint32), ("MemoryGranule", ctypes.c_uint32),
+                ("TailCall", ctypes.c_uint32)]
 
 
 class _String(ctypes.Structure):
@@ -217,7 +218,7 @@ class BatchContext:
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
-                 memory_granule=0, imports=None):
+                 memory_granule=0, imports=None, tail_call=False):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
         metering is on when cost_limit > 0."""
         L = lib()
@@ -226,7 +227,7 @@ class BatchContext:
             tab = np.ascontiguousarray(cost_table, np.uint64)
         conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit,
                      host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
-                     len(tab) if tab is not None else 0, memory_granule)
+                     len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0)
         res = _Result(0)
         imps = imports or []
         arr = (_Import * max(1, len(imps)))()

@@ -16,6 +16,7 @@
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s);
+extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, uint32_t threads, size_t lds_bytes);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
@@ -36,7 +37,8 @@ namespace {
 
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
-  std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports);
+  std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports,
+                                     C->conf.TailCall != 0);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
   // gas tables (statistics.h:32: unit costs unless the caller set a table)
@@ -312,9 +314,25 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   uint32_t wpb = 4;
   while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
   uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
+  // persistent waves when the batch has more waves than the device holds at once (C5: 4,096
+  // waves, 2 per SIMD): as many blocks as fit, each wave taking the next batch wave when
+  // its own ends (batch_kernel.hip next_wave); WB_PERSIST=0 launches a wave per batch wave
+  const bool vf = C->vframe && k.tcode;
+  if (C->cap_threads != wpb * 64 || C->cap_lds != wave_lds * wpb + 256) {
+    C->cap_threads = wpb * 64;
+    C->cap_lds = wave_lds * wpb + 256;
+    C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, C->cap_threads, C->cap_lds);
+  }
+  const char *pe = getenv("WB_PERSIST");
+  if (C->cap_blocks && blocks > C->cap_blocks && !(pe && pe[0] == '0')) {
+    if (!C->wave_ctr.ptr && !C->wave_ctr.alloc(1)) return C->fail(kRuntimeError, "device allocation failed");
+    if (!C->hip_ok(hipMemsetAsync(C->wave_ctr.ptr, 0, 4, C->stream), "wave counter")) return kRuntimeError;
+    k.wave_ctr = C->wave_ctr.ptr;
+    blocks = C->cap_blocks;
+  }
   (void)hipEventRecord(C->ev0, C->stream);
   // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
-  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, C->vframe && k.tcode, C->stream), "launch"))
+  if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, vf, C->stream), "launch"))
     return kRuntimeError;
   (void)hipEventRecord(C->ev1, C->stream);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;

@@ -86,6 +86,11 @@ struct WasmEdge_BatchContext {
   bool trip = false;              // ... in trip mode (jit.h)
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
   DevBuf<uint32_t> hframe;
+  // persistent waves (KParams::wave_ctr): the exec kernel's resident blocks for the last
+  // launch geometry, and the counter of batch waves taken
+  uint32_t cap_threads = 0, cap_blocks = 0;
+  size_t cap_lds = 0;
+  DevBuf<uint32_t> wave_ctr;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
   DevBuf<uint32_t> loops;         // Program::loops (scheduler)
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;

@@ -744,19 +744,36 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 
 // General kernel: frames of any size in LDS (4 waves per block when they fit). VF: the
 // threaded core keeps the frame in VGPRs (frames up to TC_VF_CELLS cells; 256 VGPRs).
+// The wave of the batch a launch wave runs next: its own (blockIdx) when the launch has a
+// wave per batch wave, else (persistent waves: more batch waves than the chip holds at
+// once, C5's 4,096 at 2 per SIMD) the next one not yet taken -- a wave whose lanes finish
+// early takes more work instead of leaving its SIMD idle until the slowest wave of its
+// block ends. Every instance-state buffer is indexed by the batch wave, so which launch
+// wave runs it does not matter. ~0: none left.
+__device__ __forceinline__ uint32_t next_wave(const KParams &p, uint32_t &turn) {
+  const uint32_t nwaves = (p.n + 63u) >> 6;
+  if (!p.wave_ctr) return turn++ ? 0xFFFFFFFFu : (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  uint32_t w = 0;
+  if ((threadIdx.x & 63u) == 0) w = __hip_atomic_fetch_add(p.wave_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  w = __builtin_amdgcn_readfirstlane(w);
+  return w < nwaves ? w : 0xFFFFFFFFu;
+}
+
 template <bool VF>
 __device__ __forceinline__ void exec_body(const KParams &p) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t inst = wave * 64u + lane;
   LdsFrame F{(lds_u32 *)(lds + ((wib * p.total_cells) << 6) + lane)};
   // LDS call-stack slots of this wave follow the frames of all the block's waves
   lds_u32 *const stk = (lds_u32 *)(lds + ((((blockDim.x >> 6) * p.total_cells) + wib * p.gs_lds) << 6) + lane);
-  interp<VF>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
-         GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
-         p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
-         p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+  uint32_t turn = 0;
+  for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
+    const uint32_t inst = wave * 64u + lane;
+    interp<VF>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+               GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
+               p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
+               p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4) wb_exec_kernel(const KParams p) {
@@ -766,14 +783,16 @@ extern "C" __global__ void __launch_bounds__(256, 4) wb_exec_kernel(const KParam
 extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KParams p) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t inst = wave * 64u + lane;
-  HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
   lds_u32 *const stk = (lds_u32 *)(lds + ((wib * p.gs_lds) << 6) + lane);
-  interp<false>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
-                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
-                p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
-                p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+  uint32_t turn = 0;
+  for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
+    const uint32_t inst = wave * 64u + lane;
+    HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
+    interp<false>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+                  GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
+                  p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
+                  p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+  }
 }
 extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_kernel(const KParams p) {
   exec_body<true>(p);
@@ -908,6 +927,19 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
   else
     hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
   return hipGetLastError();
+}
+// Blocks of the exec kernel the whole device holds at once (persistent waves, KParams::
+// wave_ctr): resident blocks per CU at this block size and LDS share x CUs; 0 on failure.
+extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, uint32_t threads, size_t lds_bytes) {
+  int per_cu = 0, cus = 0, dev = 0;
+  const void *k = hbm ? reinterpret_cast<const void *>(&wb_exec_hbm_kernel)
+                : vframe ? reinterpret_cast<const void *>(&wb_exec_vf_kernel)
+                         : reinterpret_cast<const void *>(&wb_exec_kernel);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, int(threads), lds_bytes) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return uint32_t(per_cu > 0 ? per_cu : 0) * uint32_t(cus > 0 ? cus : 0);
 }
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,

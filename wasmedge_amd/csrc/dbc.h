@@ -49,6 +49,8 @@ struct DInstr {
   X(UNREACHABLE)                                                                       \
   X(HOST_CALL)    /* a = first arg cell (results land there), b = arg cells,         */ \
                   /* c = result cells, imm = function index of the import            */ \
+  X(TAIL_CALL)    /* return_call: a = L, b = arg cells, c = local cells, imm = target */ \
+  X(TAIL_CALL_INDIRECT) /* return_call_indirect: fields as CALL_INDIRECT             */ \
   /* data movement: a -> c ; d = cond cell for select                                 */ \
   X(MOV32) X(MOV64) X(MOV128) X(CONST32) X(CONST64) X(CONST128)                       \
   X(SELECT32) X(SELECT64) X(SELECT128)                                                 \
@@ -165,6 +167,8 @@ struct DFunc {
 #define WB_STATUS_OK 0x00u
 #define WB_ERR_INTERRUPTED 0x07u        // ErrCode::Interrupted (fuel / time limit)
 #define WB_ERR_STACK_EXHAUSTED 0xB0u    // device call stack full (no reference code)
+#define WB_ERR_TAIL_HOST 0xB2u          // return_call_indirect reached a host import (not
+                                        // supported: see DESIGN.md "Tail calls")
 #define WB_ERR_HOST_CALL 0xB1u          // lane yielded at a host import; BatchRun's host loop
                                         // services it and resumes the lane. It stays the
                                         // final status only when no host function is

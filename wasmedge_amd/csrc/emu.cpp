@@ -28,6 +28,7 @@ typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
                              uint32_t *rets, uint8_t *mem, uint64_t mem_bytes);
 static wb_emu_host_t g_host = nullptr;
 static uint64_t g_cost_limit = ~0ull;   // gas limit (0 = none)
+static bool g_tail_call = false;      // TailCall proposal (wb_emu_set_tail_call)
 static std::vector<uint64_t> g_cost_tab;   // cost per OpCode (empty: the unit table)
 static std::vector<uint64_t> g_costs;      // per instance: its gas total after the last run
 static std::vector<wb::HostImport> g_imports;   // provided tables / memories / globals
@@ -66,6 +67,8 @@ __attribute__((visibility("default"))) void wb_emu_set_pc_trace(uint32_t *buf, u
 }
 __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC_NUM_OPS; }
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
+// the TailCall proposal for modules loaded from now on (WasmEdge_BatchConfigure::TailCall)
+__attribute__((visibility("default"))) void wb_emu_set_tail_call(int on) { g_tail_call = on != 0; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
 // WasmEdge_StatisticsSetCostTable (statistics.h:59-66): `len` entries, the rest 0;
 // tab = NULL and len = 0: back to the default unit table
@@ -115,7 +118,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     uint32_t max_pages, uint32_t gs_depth, uint64_t max_steps) {
   wb::Program P;
   uint8_t ec = 0;
-  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull, &g_imports);
+  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull, &g_imports, g_tail_call);
   if (!g_err.empty()) return ec ? ec : 2;
   int f = wb::find_export(P, func);
   if (f < 0) { g_err = "function not found"; return 0x05; }
@@ -304,7 +307,7 @@ __attribute__((visibility("default"))) int wb_emu_disasm(const uint8_t *wasm, ui
                                                          char *out, uint32_t outlen) {
   wb::Program P;
   uint8_t ec = 0;
-  g_err = wb::load_program(wasm, len, P, &ec);
+  g_err = wb::load_program(wasm, len, P, &ec, false, nullptr, g_tail_call);
   if (!g_err.empty()) return ec ? ec : 2;
   std::string s;
   char buf[160];

@@ -318,7 +318,7 @@ class Lowerer {
     switch (op) {
       case OP_JMP: case OP_BR_IF: case OP_BR_UNLESS: case OP_BR_IF_MOV1: case OP_BR_IF_MOV2:
       case OP_BR_TABLE: case OP_CALL: case OP_CALL_INDIRECT: case OP_RET: case OP_UNREACHABLE:
-      case OP_HOST_CALL:
+      case OP_HOST_CALL: case OP_TAIL_CALL: case OP_TAIL_CALL_INDIRECT:
       case OP_I32_DIV_S: case OP_I32_DIV_U: case OP_I32_REM_S: case OP_I32_REM_U:
       case OP_I32_DIV_S_I: case OP_I32_DIV_U_I: case OP_I32_REM_S_I: case OP_I32_REM_U_I:
       case OP_I64_DIV_S: case OP_I64_DIV_U: case OP_I64_REM_S: case OP_I64_REM_U:
@@ -1039,6 +1039,55 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         for (uint8_t rt : t.results) push_cell(rt);
         break;
       }
+      case 0x12: case 0x13: {  // return_call / return_call_indirect (TailCall proposal;
+                               // formchecker.cpp:515-560, controlInstr.cpp:83-158)
+        if (!P.tail_call) fail(E_ILLEGAL_OPCODE, "return_call needs the TailCall proposal");
+        const bool ind = op == 0x13;
+        uint32_t callee = 0, ti = 0, tab = 0;
+        if (ind) {
+          ti = r.u32();
+          tab = r.u32();
+          if (tab >= P.ntables || P.tables[tab].type != FUNCREF) fail(E_TYPECHECK, "unknown table");
+          if (ti >= P.types.size()) fail(E_TYPECHECK, "unknown type");
+        } else {
+          callee = r.u32();
+          if (callee >= P.funcs.size()) fail(E_TYPECHECK, "unknown function");
+          ti = P.funcs[callee].type;
+        }
+        const FuncType &t = P.types[ti];
+        if (t.results != ft->results) fail(E_TYPECHECK, "type mismatch");   // the caller's results
+        Entry idx{};
+        if (ind) idx = pop_t(I32);
+        std::vector<Entry> args(t.params.size());
+        for (size_t k = args.size(); k > 0; k--) args[k - 1] = pop_t(t.params[k - 1]);
+        if (!ind && !P.funcs[callee].imported)
+          for (size_t k = 0; k < args.size(); k++)
+            if (args[k].var) set_var_local(callee, uint32_t(k));
+        if (live()) {
+          if (!ind && P.funcs[callee].imported)
+            fail(E_UNSUPPORTED, "return_call to a host import is not supported by the batched path");
+          for (auto &e : args) st.push_back(e);
+          materialize_top(args.size());
+          uint32_t argcells = 0;
+          for (auto &e : args) argcells += cells_of(e.type);
+          const uint32_t L = top_cell() - argcells;
+          uint32_t ic = 0;
+          if (ind) {
+            ic = src(idx);
+            if (ic + 1 > max_cell) max_cell = ic + 1;
+          }
+          st.resize(st.size() - args.size());
+          if (ind) {
+            emit(OP_TAIL_CALL_INDIRECT, L, argcells, ic, tab, P.type_canon[ti]);
+          } else {
+            emit(OP_TAIL_CALL, L, argcells, P.funcs[callee].local_cells, 0, 0);
+            callfix->push_back(CallFix{uint32_t(last_emit), callee});
+          }
+          if (L + argcells > max_cell) max_cell = L + argcells;
+        }
+        set_unreachable();
+        break;
+      }
       case 0x1A: pop_any(); break;  // drop
       case 0x1B: case 0x1C: {       // select (engine.cpp:152-166)
         uint8_t want = UNKNOWN;
@@ -1481,7 +1530,7 @@ void fuse_arx(Program &P) {
   for (size_t pc = 0; pc < n; pc++) {
     const DInstr &I = P.code[pc];
     const uint16_t op = I.w0 & 0x7FFF;
-    if ((is_pc_branch(op) || op == OP_CALL) && I.w3 < n) target[I.w3] = 1;
+    if ((is_pc_branch(op) || op == OP_CALL || op == OP_TAIL_CALL) && I.w3 < n) target[I.w3] = 1;
     if (op == OP_CALL || op == OP_CALL_INDIRECT) target[pc + 1] = 1;   // return pc
   }
   for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
@@ -1527,7 +1576,7 @@ void fuse_arx(Program &P) {
   remap[n] = uint32_t(out.size());
   for (DInstr &I : out) {
     const uint16_t op = I.w0 & 0x7FFF;
-    if ((is_pc_branch(op) || op == OP_CALL) && I.w3 <= n) I.w3 = remap[I.w3];
+    if ((is_pc_branch(op) || op == OP_CALL || op == OP_TAIL_CALL) && I.w3 <= n) I.w3 = remap[I.w3];
   }
   for (size_t k = 0; k + 1 < P.brtab.size(); k += 2)
     if (P.brtab[k] <= n) P.brtab[k] = remap[P.brtab[k]];
@@ -1850,7 +1899,13 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
       Lowerer L(P, wasm, vi);
       std::vector<CallFix> callfix;
       for (uint32_t f = P.n_imported; f < P.funcs.size(); f++) L.lower_function(f, callfix);
-      for (auto &c : callfix) P.code[c.instr].w3 = P.funcs[c.callee].body_pc;
+      // a call to a function lowered after its caller learns the callee's body pc and
+      // local cells (the locals the call zeroes: helper.cpp:155-161) only now
+      for (auto &c : callfix) {
+        DInstr &I = P.code[c.instr];
+        I.w3 = P.funcs[c.callee].body_pc;
+        I.w2 = (I.w2 & 0xFFFF0000u) | P.funcs[c.callee].local_cells;
+      }
       if (!vi.changed || round >= 16) {
         if (vi.changed) P.divergent_mem = true;   // not settled: assume divergence
         break;
@@ -1922,10 +1977,11 @@ uint64_t build_cost_pool(const Program &P, const uint64_t *tab, uint64_t limit,
 }
 
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
-                         bool exact_globals, const std::vector<HostImport> *imports) {
+                         bool exact_globals, const std::vector<HostImport> *imports, bool tail_call) {
   try {
     out = Program();
     out.exact_globals = exact_globals;
+    out.tail_call = tail_call;
     parse_and_lower(wasm, len, out, imports);
     *errcode = 0;
     return "";

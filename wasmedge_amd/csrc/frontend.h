@@ -114,6 +114,9 @@ struct Program {
   // metered lowering: global.set never retargets its producer, so a cost-limit trap
   // between a value and its global.set leaves the global unwritten as in the reference
   bool exact_globals = false;
+  // the TailCall proposal (return_call / return_call_indirect) is enabled; off, they fail
+  // to load with IllegalOpCode like the reference's default (loader/ast/instruction.cpp:903-907)
+  bool tail_call = false;
   // some load/store address depends on per-instance data (a parameter, a loaded value, a
   // global): the batch then interleaves memory in 128-byte granules (batch_api.cpp)
   bool divergent_mem = false;
@@ -138,7 +141,7 @@ struct HostImport {
 // IncompatibleImportType 0x61).
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
                          bool exact_globals = false,
-                         const std::vector<HostImport> *imports = nullptr);
+                         const std::vector<HostImport> *imports = nullptr, bool tail_call = false);
 
 int find_export(const Program &p, const std::string &name);
 

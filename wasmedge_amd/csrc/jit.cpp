@@ -2070,7 +2070,11 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   std::string ooa, oob;   // the runs' stage code, out of line
   std::vector<uint32_t> split(runs.size());
   const uint32_t nr = uint32_t(runs.size());
-  for (uint32_t k = 0; k < nr; k++) {
+  // (A/B and debugging aids: WB_TRIP_SPLIT=0 runs every run whole in stage B;
+  // WB_JIT_SCHED=0 keeps program order)
+  const bool split_on = !(getenv("WB_TRIP_SPLIT") && getenv("WB_TRIP_SPLIT")[0] == '0');
+  const bool sched_on = !(getenv("WB_JIT_SCHED") && getenv("WB_JIT_SCHED")[0] == '0');
+  for (uint32_t k = 0; k < nr && split_on; k++) {
     const JitRun &r = runs[k];
     const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
     split[k] = trip_split(P, r, ends_run(lop) ? r.len - 1 : r.len);
@@ -2253,7 +2257,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         }
         e.drain();
       }
-      std::string code = e.o.substr(0, at) + schedule(e.o.substr(at));
+      std::string code = sched_on ? e.o.substr(0, at) + schedule(e.o.substr(at)) : e.o;
       code += e.stage_end + ":\n";
       code += "s_mov_b64 exec, s[96:97]\n";
       code += "s_branch " + std::string(st ? "LtBr" : "LtAr") + std::to_string(k) + "\n";

@@ -70,6 +70,8 @@ struct KParams {
                                 // group outside their innermost loop if it has >= sched x
                                 // as many (0: min pc only)
   const uint32_t *loops;        // per pc: innermost loop (head, end), ~0 = none
+  uint32_t *wave_ctr;           // persistent waves: the next wave to run (NULL: one launch
+                                // wave per wave of the batch, the block's own)
   uint32_t simt;                // V frames + compiled runs: every running lane enters the
                                 // core, whose compiled runs schedule the lanes among
                                 // themselves (jit.cpp Lsched); the C++ loop only serves

@@ -28,7 +28,8 @@ std::vector<uint8_t> jump_targets(const Program &P) {
   for (size_t pc = 0; pc < n; pc++) {
     const DInstr &I = P.code[pc];
     const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
-    if ((is_branch(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2 || op == OP_CALL) && I.w3 < n)
+    if ((is_branch(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2 || op == OP_CALL || op == OP_TAIL_CALL) &&
+        I.w3 < n)
       target[I.w3] = 1;
     if (op == OP_CALL || op == OP_CALL_INDIRECT || op == OP_HOST_CALL) target[pc + 1] = 1;
   }
