@@ -71,6 +71,17 @@ def workload(name, args):
                 lambda ids: np.stack([ids, np.full_like(ids, 4096), np.full_like(ids, 50)], 1),
                 [I32, I32, I32], "C5 f64x2 Mandelbrot 8x8 tiles of 4096^2, 50 iters (configs[4])",
                 {})
+    if name == "mt":
+        # not a BASELINE config: a second real module through the compiled runs (VERDICT r2
+        # item 8) -- the reference's own mt19937 test module (i64 + SIMD128 + memory),
+        # every instance drawing `mt_n` numbers from its own seed
+        mt = open(os.path.join(ROOT, "tests", "golden", "mt19937.wasm"), "rb").read()
+        n = args.mt_n
+        return (mt, "mt19937",
+                lambda ids: np.stack([np.zeros_like(ids), 5489 + ids, np.full_like(ids, n)], 1),
+                [batch.I32, batch.I64, batch.I64],
+                "mt19937 of test/thread/ThreadTest.cpp:31-163, %d draws from a per-instance seed" % n,
+                {"draws": n})
     raise SystemExit("unknown workload " + name)
 
 
@@ -236,8 +247,8 @@ def load_profile(workload, config):
         return {}
     with open(p) as f:
         d = json.load(f)
-    key = {k: config.get(k) for k in ("workload", "instances_per_gpu", "elements", "iters")}
-    return d if d.get("config") == key else {}
+    key = {k: config[k] for k in ("workload", "instances_per_gpu", "elements", "iters", "draws") if k in config}
+    return d if {k: v for k, v in d.get("config", {}).items() if v is not None} == key else {}
 
 
 def elapsed_hint(args):
@@ -260,7 +271,8 @@ def main():
     ap.add_argument("--instances", type=int, default=INSTANCES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "mt"])
+    ap.add_argument("--mt-n", type=int, default=100000, help="mt19937 draws per instance")
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     ap.add_argument("--cost-limit", type=int, default=0,
                     help="meter gas with the unit cost table up to this limit (measures the "
@@ -351,7 +363,7 @@ def main():
     hashes = ctx.memory_hash()
     checksum = int(hashes.sum(dtype=np.uint64))
     gpu = {"counts": cnt, "hashes": hashes, "status": st, "ret": rets["lo"][:, 0],
-           "ret32": args.workload != "c5"}
+           "ret32": args.workload not in ("c5", "mt")}
     kernel_avg = ksum / args.steps
     e2e = {"create_s": dist.max(t_create)}
     for k in ("cold", "warm"):
@@ -369,7 +381,7 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "i32" if args.workload != "c5" else "f64",
+        "dtype": {"c5": "f64", "mt": "i64"}.get(args.workload, "i32"),
         "data": "synthetic: per-instance inputs derived from the instance id inside the "
                 "wasm module",
         "config": dict({"workload": desc, "instances_per_gpu": n,

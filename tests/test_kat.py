@@ -84,3 +84,21 @@ def test_gpu_fib_64k_divergent(built):
         k = 20 + (i % 11)
         assert rets[i] == ref[k][1] and int(cnt[i]) == ref[k][2], i
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", ["1", "0"])
+def test_gpu_mt19937_per_instance_seeds(built, monkeypatch, jit):
+    """bench.py's `mt` workload (a second real module through the
+    compiled runs, whose v128 loads/stores, bitselect and i64x2 shifts now compile): 4,096
+    instances each drawing 3,000 numbers from its own seed, against the oracle on a sample,
+    with the compiled runs on and off."""
+    monkeypatch.setenv("WB_JIT", jit)
+    wasm = golden("mt19937.wasm")
+    n = 4096
+    rows = [[0, 5489 + i, 3000] for i in range(n)]
+    rets, st, cnt, h = gpu_run(wasm, "mt19937", rows, [I32, I64, I64], [I64])
+    idx = list(range(0, n, 37)) + [n - 1]
+    ref = oracle_run(O.Module(wasm), "mt19937", [rows[i] for i in idx])
+    assert compare(ref, [rets[i] for i in idx], [st[i] for i in idx], [cnt[i] for i in idx],
+                   [h[i] for i in idx], [I64]) == []

@@ -54,7 +54,7 @@ def bench_line(path):
 
 def profile_key(cfg):
     """The configuration fields a profile is valid for (bench.py compares them)."""
-    return {k: cfg.get(k) for k in ("workload", "instances_per_gpu", "elements", "iters")}
+    return {k: cfg[k] for k in ("workload", "instances_per_gpu", "elements", "iters", "draws") if k in cfg}
 
 
 def main():

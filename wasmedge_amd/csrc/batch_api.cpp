@@ -163,6 +163,24 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       want_trip = false;
       runs = wb::jit_runs(P, tcv, want_simt, false);
     }
+    // debugging aids (tools/trip_debug.py): WB_TRIP_LIST=<file> writes the runs' start pcs,
+    // WB_TRIP_EXCL=<pc>,<pc>,... leaves the runs starting there to the handlers
+    if (const char *tl = getenv("WB_TRIP_LIST"))
+      if (FILE *f = fopen(tl, "w")) {
+        for (const auto &r : runs) fprintf(f, "%u %u\n", r.pc, r.len);
+        fclose(f);
+      }
+    if (const char *tx = getenv("WB_TRIP_EXCL")) {
+      std::vector<uint32_t> ex;
+      for (const char *q = tx; *q;) {
+        ex.push_back(uint32_t(strtoul(q, const_cast<char **>(&q), 10)));
+        if (*q == ',') q++;
+        else break;
+      }
+      runs.erase(std::remove_if(runs.begin(), runs.end(),
+                                [&](const wb::JitRun &r) { return std::find(ex.begin(), ex.end(), r.pc) != ex.end(); }),
+                 runs.end());
+    }
     if (!runs.empty()) {
       std::vector<uint8_t> start(P.code.size() + 1, 0);
       for (const auto &r : runs) start[r.pc] = 1;

@@ -42,12 +42,17 @@ const char *const T2 = "s[74:75]";
 
 uint16_t op_of(const DInstr &I) { return uint16_t(I.w0 & 0x7FFFu); }
 
+bool is_store_op(uint16_t op) {
+  return op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64 || op == OP_ST128;
+}
+
 uint32_t mem_bytes(uint16_t op) {
   switch (op) {
     case OP_LD8S32: case OP_LD8U32: case OP_LD8S64: case OP_LD8U64: case OP_ST8: return 1;
     case OP_LD16S32: case OP_LD16U32: case OP_LD16S64: case OP_LD16U64: case OP_ST16: return 2;
     case OP_LD32: case OP_LD32S64: case OP_LD32U64: case OP_ST32: return 4;
     case OP_LD64: case OP_ST64: return 8;
+    case OP_LD128: case OP_ST128: return 16;
     default: return 0;
   }
 }
@@ -415,8 +420,49 @@ void mem_ea(Em &e, uint32_t a, uint32_t imm, uint32_t n, std::string *w1, std::s
   }
 }
 
+// v128 (16 bytes, 4-byte aligned: group_check): the address operand of each of its 4
+// words -- in the word interleave offsets from the group's base (or from one computed
+// base), else each word's granule address in its own register pair
+const char *const WPAIR[4] = {"v[118:119]", "v[126:127]", "v[108:109]", "v[110:111]"};
+void mem_ea16(Em &e, uint32_t a, uint32_t imm, std::string w[4]) {
+  if (e.g == 0) {
+    uint64_t k = uint64_t(imm) * 64u;
+    std::string base = e.base();
+    if (k + 768 > 4095) {
+      e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(k), e.base(0).c_str());
+      e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(k >> 32), e.base(1).c_str());
+      base = XP;
+      k = 0;
+    }
+    for (int q = 0; q < 4; q++) w[q] = base + ", off offset:" + std::to_string(k + 256u * q);
+    return;
+  }
+  for (int q = 0; q < 4; q++) {
+    const std::string pr = WPAIR[q];
+    const std::string lo = "v" + pr.substr(2, pr.find(':') - 2);
+    e.l("v_add_u32_e32 %s, 0x%x, %s", Y1, imm + 4u * q, e.v(a));
+    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y1);
+    e.l("v_lshlrev_b64 %s, %u, %s", pr.c_str(), 8 + e.g, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", pr.c_str(), pr.c_str(), MEM);
+    e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y1, 2 + e.g);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", pr.c_str(), WP, pr.c_str());
+    w[q] = pr + ", off";
+  }
+}
+
 bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
   const uint32_t n = mem_bytes(op);
+  if (n == 16) {   // LD128 (memory.ipp loadValue of a uint128): 4 words into c..c+3
+    e.sync({a, c, c + 1, c + 2, c + 3});
+    if (e.group) group_check(e, *e.group);
+    std::string w[4];
+    mem_ea16(e, a, imm, w);
+    for (int q = 0; q < 4; q++) {
+      e.l("global_load_dword %s, %s", e.v(c + q), w[q].c_str());
+      e.loaded(c + q);
+    }
+    return true;
+  }
   const char *ins = n == 1 ? (op == OP_LD8S32 || op == OP_LD8S64 ? "global_load_sbyte" : "global_load_ubyte")
                     : n == 2 ? (op == OP_LD16S32 || op == OP_LD16S64 ? "global_load_sshort" : "global_load_ushort")
                              : "global_load_dword";
@@ -445,6 +491,16 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const 
   const uint32_t n = mem_bytes(op);
   e.drain();   // a store never overtakes a load of this run (same-address ordering)
   if (e.group) group_check(e, *e.group);
+  if (n == 16) {   // ST128: 4 words from b..b+3
+    std::string w[4];
+    mem_ea16(e, a, imm, w);
+    for (int q = 0; q < 4; q++) {
+      const size_t k = w[q].find(", off");
+      e.l("global_store_dword %s, %s%s", w[q].substr(0, k).c_str(), e.v(b + q), w[q].substr(k).c_str());
+      e.nvm++;
+    }
+    return true;
+  }
   std::string w1, w2;
   mem_ea(e, a, imm, n, &w1, &w2);
   const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
@@ -696,6 +752,38 @@ bool emit(Em &e, const DInstr &I) {
         e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
         e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[2 * q]);
         e.l("v_mov_b32 %s, %s", r[2 * q + 1], r[2 * q]);
+      }
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_BITSELECT: {   // (a & d) | (b & ~d) per bit: v_bfi_b32(d, a, b)
+      e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, d, d + 1, d + 2, d + 3, c, c + 1, c + 2, c + 3});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}, {d, 4}});
+      for (int k = 0; k < 4; k++) e.l("v_bfi_b32 %s, %s, %s, %s", r[k], e.v(d + k), e.v(a + k), e.v(b + k));
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_I32X4_SHL: case OP_V_I32X4_SHR_S: case OP_V_I32X4_SHR_U: {   // count mod 32
+      e.sync({a, a + 1, a + 2, a + 3, b, c, c + 1, c + 2, c + 3});
+      const char *ins = op == OP_V_I32X4_SHL ? "v_lshlrev_b32_e32" : op == OP_V_I32X4_SHR_U ? "v_lshrrev_b32_e32"
+                                                                                         : "v_ashrrev_i32_e32";
+      e.l("v_and_b32_e32 %s, 31, %s", Y0, e.v(b));
+      const char *const *r = e.res128(c, {{a, 4}});
+      for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], Y0, e.v(a + k));
+      e.put128(c, r);
+      return true;
+    }
+    case OP_V_I64X2_SHL: case OP_V_I64X2_SHR_S: case OP_V_I64X2_SHR_U: {   // count mod 64
+      e.sync({a, a + 1, a + 2, a + 3, b, c, c + 1, c + 2, c + 3});
+      const char *ins = op == OP_V_I64X2_SHL ? "v_lshlrev_b64" : op == OP_V_I64X2_SHR_U ? "v_lshrrev_b64"
+                                                                                     : "v_ashrrev_i64";
+      e.l("v_and_b32_e32 %s, 63, %s", Y0, e.v(b));
+      const char *const *r = e.res128(c, {{a, 4}}, true);
+      (void)r;
+      const std::string res[2] = {e.dstp[0], e.dstp[1]};
+      for (int k = 0; k < 2; k++) {
+        const char *x = e.src64(a + 2 * k, A0, A1, AP);
+        e.l("%s %s, %s, %s", ins, res[k].c_str(), Y0, x);
       }
       e.put128(c, r);
       return true;
@@ -969,7 +1057,7 @@ bool emit(Em &e, const DInstr &I) {
       break;
   }
   if (mem_bytes(op)) {
-    if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64) return emit_store(e, op, a, b, imm);
+    if (is_store_op(op)) return emit_store(e, op, a, b, imm);
     return emit_load(e, op, a, c, imm);
   }
   return false;
@@ -1190,13 +1278,12 @@ void written(const DInstr &I, std::vector<uint32_t> *out) {
   const uint16_t op = op_of(I);
   const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
   out->clear();
-  if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64 || op == OP_NOP_CNT) return;
+  if (is_store_op(op) || op == OP_NOP_CNT) return;
   if (op == OP_ZERO_LOCALS) {
     for (uint32_t k = 0; k < b; k++) out->push_back(a + k);
     return;
   }
-  out->push_back(c);
-  out->push_back(c + 1);   // (over-approximates 32-bit results)
+  for (uint32_t k = 0; k < 4; k++) out->push_back(c + k);   // (over-approximates narrower results)
   if (op == OP_I32_ADD_XROTR_I) out->push_back(d);
   if (op == OP_I32_ADD3_XROTR_I) out->push_back(I.w3 & 0xFFFFu);
 }
@@ -1221,7 +1308,7 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
       }
       MemGroup &g = G[size_t(open)];
       g.maxlast = std::max(g.maxlast, imm + n - 1);
-      if (op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64)
+      if (is_store_op(op))
         g.store_end = std::max<uint64_t>(g.store_end, uint64_t(imm) + n);
       const uint32_t m = n >= 4 ? 3 : n - 1;
       if (m) {
@@ -1249,12 +1336,11 @@ struct LoadBatch {
   std::vector<uint32_t> order;   // issue order (body indices)
 };
 
-bool is_store_op(uint16_t op) { return op == OP_ST8 || op == OP_ST16 || op == OP_ST32 || op == OP_ST64; }
-
 bool load_wide(uint16_t op) {
   return op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
          op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
 }
+uint32_t load_cells(uint16_t op) { return op == OP_LD128 ? 4u : load_wide(op) ? 2u : 1u; }
 
 // an operand field naming the cell (or the cell below it: a 64-bit operand's high word);
 // only the batch's issue order depends on it
@@ -1279,7 +1365,7 @@ std::vector<LoadBatch> load_batches(const Program &P, const JitRun &r, uint32_t 
     uint32_t j = i, leads = 0;
     for (; j < nbody && is_load(j); j++) {
       const DInstr &I = P.code[r.pc + j];
-      const uint32_t a = I.w1 & 0xFFFFu, c = I.w2 & 0xFFFFu, nc = load_wide(op_of(I)) ? 2 : 1;
+      const uint32_t a = I.w1 & 0xFFFFu, c = I.w2 & 0xFFFFu, nc = load_cells(op_of(I));
       if (lead[j] >= 0 && ++leads > 2) break;
       bool clash = std::find(dest.begin(), dest.end(), a) != dest.end();
       for (uint32_t q = 0; q < nc; q++)
@@ -1296,7 +1382,7 @@ std::vector<LoadBatch> load_batches(const Program &P, const JitRun &r, uint32_t 
       std::vector<std::pair<uint32_t, uint32_t>> key;   // (first use, index)
       for (uint32_t k = i; k < j; k++) {
         const DInstr &I = P.code[r.pc + k];
-        const uint32_t c = I.w2 & 0xFFFFu, nc = load_wide(op_of(I)) ? 2 : 1;
+        const uint32_t c = I.w2 & 0xFFFFu, nc = load_cells(op_of(I));
         uint32_t t = j;
         for (; t < r.len; t++) {
           bool m = false;
@@ -2006,7 +2092,7 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
     if (names_any(I, loaded) || (op == OP_POST_CALL && i) || is_store_op(op)) break;
     if (mem_bytes(op)) {
       const uint32_t c = I.w2 & 0xFFFFu;
-      for (uint32_t k = 0; k < (load_wide(op) ? 2u : 1u); k++) loaded[c + k] = 1;
+      for (uint32_t k = 0; k < load_cells(op); k++) loaded[c + k] = 1;
       any = true;
     }
     s = i + 1;
@@ -2174,6 +2260,9 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       }
       done = e.done;
       if (st == 1) {
+        // (loads in flight land first: the transfer reads cells -- a branch's operands, a
+        // call's spill, a return's results)
+        e.drain();
         // the transfer, per lane: VPC = where each lane goes on, VCNT += what the run
         // retired (with a taken branch's count correction)
         const uint32_t fall = r.pc + r.len;
