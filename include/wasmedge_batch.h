@@ -69,7 +69,8 @@ typedef struct WasmEdge_BatchConfigure {
   /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
   uint32_t CallStackCells;
   /* Instruction budget per instance (0 = unlimited; counted in the reference's
-   * Statistics units, enforced at 1024-dispatch granularity) and wall-clock limit per
+   * Statistics units; checked every scheduler round, and a device-side core call never
+   * runs a lane more than one compiled run past its remaining budget) and wall-clock limit per
    * launch in seconds (0 = 600); exceeding either marks the instance Interrupted (0x07),
    * mirroring the reference's cost limit / StopToken (statistics.h:69-91,
    * helper.cpp:24-27). */
@@ -169,7 +170,8 @@ WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName
                       uint8_t *PerInstance, uint64_t *InstrCounts);
 
 /* Ask a running BatchExecute/BatchRun on this context to stop (any thread): every
- * instance still running ends with Interrupted (0x07) within ~1024 dispatches, like the
+ * instance still running ends with Interrupted (0x07) at the next scheduler round (the
+ * flag is read every round; a core call runs at most 2^20 instructions), like the
  * reference's StopToken / async cancel (helper.cpp:24-27, include/common/async.h:73-77).
  * The request is cleared when the next Run starts. */
 WASMEDGE_BATCH_API void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *Cxt);
