@@ -346,12 +346,7 @@ class Lowerer {
                uint32_t imm = 0) {
     if (a > 0xFFFF || b > 0xFFFF || c > 0xFFFF)
       fail(E_UNSUPPORTED, "cell index out of range for the DBC encoding");
-    while (pending > 255) {                  // cnt is 8 bits: spill into NOP_CNT
-      P.code.push_back(DInstr{uint32_t(OP_NOP_CNT) | (255u << 16), 0, 0, 0});
-      P.dops.emplace_back(pend_ops.begin(), pend_ops.begin() + 255);
-      pend_ops.erase(pend_ops.begin(), pend_ops.begin() + 255);
-      pending -= 255;
-    }
+    spill_pending();                         // cnt is 8 bits
     DInstr I;
     I.w0 = uint32_t(op) | (pending << 16) | (is_ctl(op) ? DBC_CTL : 0u);
     I.w1 = (a & 0xFFFF) | (b << 16);
@@ -367,7 +362,22 @@ class Lowerer {
     return P.code.back();
   }
 
-  void place_label() { can_retarget = false; }
+  // pending counts above 255 go into NOP_CNT carriers (255 each). Before a label too: a
+  // branch to it skips the carriers (or, to a loop, does not re-run them), so its count
+  // correction stays within [-255, 0] however many folded instructions precede the label
+  // (40,000 nops before a loop once gave a correction that did not fit the 16-bit field).
+  void spill_pending() {
+    while (pending > 255) {
+      P.code.push_back(DInstr{uint32_t(OP_NOP_CNT) | (255u << 16), 0, 0, 0});
+      P.dops.emplace_back(pend_ops.begin(), pend_ops.begin() + 255);
+      pend_ops.erase(pend_ops.begin(), pend_ops.begin() + 255);
+      pending -= 255;
+    }
+  }
+  void place_label() {
+    can_retarget = false;
+    spill_pending();
+  }
 
   // ---------------- stack
   Entry &push_cell(uint8_t t, int64_t producer = -1) {
