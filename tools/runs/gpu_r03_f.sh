@@ -14,4 +14,10 @@ for n in 65536 131072; do
   step c3_4k_$n 200 python bench.py --workload c3 --elements 4096 --instances $n --steps 2 --warmup 1 --no-cpu-baseline
   step c3_4k_notrip_$n 200 env WB_TRIP=0 python bench.py --workload c3 --elements 4096 --instances $n --steps 2 --warmup 1 --no-cpu-baseline
 done
+# half waves: the 64K batch as 2048 launch waves of 32 lanes
+step c1_half 200 env WB_HALF=1 python bench.py --workload c1 --steps 2 --warmup 1 --cpu-seconds 3
+step c4_half 200 env WB_HALF=1 python bench.py --workload c4 --steps 3 --warmup 1 --cpu-seconds 3
+step c3_4k_half 200 env WB_HALF=1 python bench.py --workload c3 --elements 4096 --steps 2 --warmup 1 --cpu-seconds 3
+step c3_4k_half_notrip 200 env WB_HALF=1 WB_TRIP=0 python bench.py --workload c3 --elements 4096 --steps 2 --warmup 1 --cpu-seconds 3
+step c2_half 200 env WB_HALF=1 python bench.py --cpu-seconds 3 --steps 5
 for f in $O/c*.log; do echo $f $(grep -h '"metric"' $f | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('%.3g'%d['value'], '%.3f'%d['ms_per_step'])" 2>/dev/null); done
