@@ -203,6 +203,24 @@ def test_gpu_c3_full_size_sample(built):
 
 
 @pytest.mark.gpu
+def test_gpu_c3_64k_x_1mib(built):
+    """C3 exactly as configs[2] / bench.py --workload c3: 64K instances x 262,144 i32
+    (64 GiB of linear memory on the device). Every lane must finish without a trap; 48
+    instances spread over the batch (both halves of several waves) are bit-exact against
+    the oracle (status, checksum, count, memory hash of the whole 17-page memory)."""
+    wasm = W.qsort_wasm()
+    n = 65536
+    rows = [[i, 262144] for i in range(n)]
+    rets, st, cnt, h = gpu_run(wasm, "sort", rows, [I32, I32], [I32], max_memory_page=17)
+    assert all(int(s) == 0 for s in st)
+    assert min(int(c) for c in cnt) > 262144 * 10
+    idx = sorted(set([0, 1, 31, 32, 63, 64, n - 1] + list(range(97, n, 1601))))[:48]
+    ref = _oracle_batch(wasm, "sort", [rows[i] for i in idx], page_limit=17)
+    sub = lambda a: [a[i] for i in idx]
+    assert compare(ref, _mask32(sub(rets)), sub(st), sub(cnt), sub(h), [I32]) == []
+
+
+@pytest.mark.gpu
 def test_gpu_c5_full_size(built):
     """C5 at its configs[4] size: 256K 8x8 tiles of a 4096^2 image, 50 iterations. This
     batch (4096 waves) selects the LDS-frame threaded core. Every 7th tile against the
