@@ -11,3 +11,7 @@ step c3test 400 python -u -m pytest tests/test_workloads.py -m gpu -v --timeout 
 step c3 600 python bench.py --workload c3 --steps 3 --warmup 1
 export PROF_TIMEOUT=240
 step prof 1500 bash tools/prof_bench.sh gpurun_out/r03g/prof --workload c3 --steps 1 --warmup 0
+# mt19937 (not a config): SIMT + word interleave against the default (trip mode, 128-byte
+# granules: its addresses depend on loaded data, so the static analysis calls it divergent)
+step mt_t0_g4 200 env WB_TRIP=0 WB_GRANULE=4 python bench.py --workload mt --steps 3 --warmup 1 --no-cpu-baseline
+step mt_t0 200 env WB_TRIP=0 python bench.py --workload mt --steps 3 --warmup 1 --no-cpu-baseline
