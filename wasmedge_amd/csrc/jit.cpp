@@ -1774,14 +1774,28 @@ void sched_block(Em &e, const std::string &p, const char *mask) {
   e.l("s_setpc_b64 s[68:69]");
 }
 
-// Lmerge (the group reached OTHER or the count limit: its pc is PCOFF) and Lsched
-std::string simt_sched() {
+// Lmerge (the group reached OTHER or the count limit: its pc is PCOFF) and Lsched.
+// hybrid (trip mode beside SIMT scheduling, jit_source): a wave whose lanes are not all at
+// one pc goes to the trips (Ltin) instead of picking a group; the trips come back here
+// once every lane is at one pc again.
+std::string simt_sched(bool hybrid) {
   Em e;
   e.l(".p2align 6");
   e.l("Lmerge:");
   e.l("v_lshrrev_b32_e64 %s, 5, s62", VPC);
   flush(e);
   e.l("Lsched:");
+  if (hybrid) {
+    e.l("s_mov_b64 exec, s[96:97]");
+    e.l("s_nop 4");
+    e.l("v_readfirstlane_b32 s68, %s", VPC);
+    e.l("s_nop 1");
+    e.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
+    e.l("s_cbranch_vccz Lsc_one");
+    e.l("s_waitcnt lgkmcnt(0)");   // (a TInstr prefetch must land: the trips use s[76:81])
+    long_jump(e, "Ltin", "Lsc_tq");
+    e.l("Lsc_one:");
+  }
   sched_block(e, "Lsc", nullptr);
   return e.o;
 }
@@ -2101,7 +2115,12 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
 }
 }  // namespace
 
-std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog) {
+// hybrid: only the trips' code (Ltin, the trip loop, the runs' stages, the exits), for
+// jit_source's SIMT code object, whose Lsched sends diverged waves to Ltin; a trip after
+// which every lane is at one pc goes back to Lsched (SIMT scheduling, direct run-to-run
+// jumps) -- converged phases (C3's fill and checksum loops; modules like mt19937 whose
+// addresses merely look divergent to the static analysis) run without trips.
+std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog, bool hybrid) {
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
   auto in_region = [&](uint32_t pc) { return start.count(pc) != 0; };
@@ -2122,14 +2141,16 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     if (o == OP_CALL_INDIRECT && !in_region(pc + 1)) ind_out.push_back(pc + 1);
   }
   std::string body;
-  body += "s_getpc_b64 s[6:7]\nLpt:\ns_add_u32 s6, s6, Ltab - Lpt\ns_addc_u32 s7, s7, 0\n"
-          "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
-          "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
-          "s_setpc_b64 s[8:9]\n";
+  if (!hybrid)
+    body += "s_getpc_b64 s[6:7]\nLpt:\ns_add_u32 s6, s6, Ltab - Lpt\ns_addc_u32 s7, s7, 0\n"
+            "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
+            "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
+            "s_setpc_b64 s[8:9]\n";
   Em h;   // entry stubs, the trip loop and its exits
   // a run's entry (its TInstr): the group's lanes record their pc and count; then every
   // lane's place is sorted out (OUTSIDE: not at a run start) and the trips begin
-  for (size_t k = 0; k < runs.size(); k++) {
+  // (hybrid: the runs' TInstrs enter their SIMT code; Lsched enters the trips)
+  for (size_t k = 0; k < runs.size() && !hybrid; k++) {
     h.l(".p2align 6");   // (jit_load expects 64-byte aligned run addresses)
     h.l("Lb%zu:", k);
     h.l("v_lshrrev_b32_e64 %s, 5, s62", VPC);
@@ -2179,6 +2200,17 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     h.l("s_and_b64 s[74:75], vcc, exec");
     h.l("s_cbranch_scc1 LtB%u", k);
     h.l("LtBr%u:", k);
+  }
+  if (hybrid) {
+    // ---- every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL)
+    h.l("s_cmp_eq_u64 s[76:77], 0");
+    h.l("s_cbranch_scc0 Ltnc");
+    h.l("v_readfirstlane_b32 s68, %s", VPC);
+    h.l("s_nop 1");
+    h.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
+    h.l("s_cbranch_vccnz Ltnc");
+    long_jump(h, "Lsched", "Ltcq");
+    h.l("Ltnc:");
   }
   // ---- after the trip: go on while more lanes are in the runs than outside them
   h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
@@ -2243,7 +2275,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       e.g = glog;
       e.fb = P.global_cells;
       e.prog = &P;
-      e.run = k + uint32_t(st) * nr;
+      e.run = (hybrid ? 8 * nr : 0) + k + uint32_t(st) * nr;   // (labels apart from the SIMT runs')
       e.done = done;
       const std::string L = (st ? "LtB" : "LtA") + std::to_string(k);
       e.stage_end = L + "e";
@@ -2355,6 +2387,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     }
   }
   body += h.o + ooa + oob;
+  if (hybrid) return body;
   body = resolve_jumps(body);
   body += ".p2align 3\nLtab:\n";
   for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
@@ -2380,7 +2413,10 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost, bool simt, bool trip) {
   if (cost) simt = false;
-  if (trip && simt && runs.size() <= kTripMaxRuns) return trip_source(P, runs, glog);
+  // trip mode beside SIMT scheduling (hybrid, the default) or alone (WB_HYBRID=0)
+  const bool trips = trip && simt && runs.size() <= kTripMaxRuns;
+  const bool hybrid = trips && !(getenv("WB_HYBRID") && getenv("WB_HYBRID")[0] == '0');
+  if (trips && !hybrid) return trip_source(P, runs, glog, false);
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
@@ -2397,7 +2433,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
           "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
           "s_setpc_b64 s[8:9]\n";
-  if (simt) body += simt_sched();
+  if (simt) body += simt_sched(hybrid);
   // run index by start pc: a transfer to one jumps straight to its code
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
@@ -2938,7 +2974,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
           x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
           flush(x);
-          if (fall != tgt) {
+          if (fall != tgt && !hybrid) {   // (hybrid: every split goes to Lsched, hence the trips)
             // No waiting lane at or below the nearer destination `lo`: the lanes going
             // there are the next group, those going to `hi` wait, and the lowest waiting
             // pc becomes min(LOW, hi) -- a pick without the wave reductions of Lsched
@@ -3006,6 +3042,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     }
     body += e.o;
   }
+  if (hybrid) body += trip_source(P, runs, glog, true);
   body = resolve_jumps(body);
   body += ".p2align 3\nLtab:\n";
   for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
