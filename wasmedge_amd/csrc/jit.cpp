@@ -237,7 +237,9 @@ struct Em {
   struct NanItem { std::string lo, hi, pair; uint32_t a, b; };
   std::string tail;   // out-of-line code of the run (placed after it)
   int nfix = 0;
+  const std::vector<uint8_t> *nanobs = nullptr;   // nan_observable(), per pc
   void nan_fix(const std::vector<NanItem> &items, int w) {
+    if (nanobs && pc < nanobs->size() && !(*nanobs)[pc]) return;   // payload never observed
     const std::string id = std::to_string(run) + "_" + std::to_string(nfix++);
     bool first = true;
     for (const auto &it : items) {
@@ -1565,6 +1567,7 @@ bool is_branch_op(uint16_t op) {
 }
 bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op) || op == OP_BR_TABLE; }
 
+
 // The compare of a branch into vcc (true = taken).
 void branch_cond(Em &e, const DInstr &I) {
   const uint16_t op = op_of(I);
@@ -1960,6 +1963,215 @@ bool written_exact(const DInstr &I, std::vector<uint32_t> *out) {
   }
 }
 
+// ---------------------------------------------------------------- NaN payload liveness
+// The compiled runs give every NaN result of an f32/f64 add/sub/mul the payload the
+// reference's x86 build produces (Em::nan_fix: a compare and a branch per result). That
+// only matters where the payload can be observed: stored, returned, kept in a global,
+// passed to a call, or read as bits by an op whose result can be. A float compare sees
+// every NaN alike. nan_observable() is a backward dataflow over the program's cells:
+// obs(pc) = the cells whose bits may still reach such a sink after instruction pc; an
+// add/sub/mul whose result is in no obs(pc) needs no fix (C5: the Mandelbrot iteration's
+// z values only ever reach a compare). Unmodelled instructions make everything they name
+// observable and kill nothing; calls, host calls and tail calls make every cell
+// observable; globals always are (the host reads them after a trap or an interrupt).
+// Returns per pc: 1 = the instruction's result may be observed.
+std::vector<uint8_t> nan_observable(const Program &P) {
+  const size_t n = P.code.size();
+  const uint32_t nc = P.total_cells() + 8;   // (+8: 4-wide over-approximations stay in range)
+  const size_t W = (nc + 63) / 64;
+  typedef std::vector<uint64_t> Set;
+  std::vector<Set> before(n + 1, Set(W, 0));
+  auto put = [&](Set &s, uint32_t c, uint32_t k) {
+    for (uint32_t q = 0; q < k; q++)
+      if (c + q < nc) s[(c + q) >> 6] |= 1ull << ((c + q) & 63);
+  };
+  auto kill = [&](Set &s, uint32_t c, uint32_t k) {
+    for (uint32_t q = 0; q < k; q++)
+      if (c + q < nc) s[(c + q) >> 6] &= ~(1ull << ((c + q) & 63));
+  };
+  auto any = [&](const Set &s, uint32_t c, uint32_t k) {
+    for (uint32_t q = 0; q < k; q++)
+      if (c + q < nc && (s[(c + q) >> 6] >> ((c + q) & 63) & 1)) return true;
+    return false;
+  };
+  Set all(W, ~0ull), globals(W, 0);
+  put(globals, 0, P.global_cells);
+  std::vector<uint8_t> res(n, 1);
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (size_t pc = n; pc-- > 0;) {
+      const DInstr &I = P.code[pc];
+      const uint16_t op = op_of(I);
+      const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
+      Set after = globals, s;
+      auto succ = [&](size_t t) {
+        if (t <= n) for (size_t w = 0; w < W; w++) after[w] |= before[t][w];
+      };
+      // what the instruction does with cells: prop = its results carry its sources' bits
+      // (sources observable when a result is), hide = a float compare, sink = every cell it
+      // names is observable
+      uint32_t src[3][2] = {{0, 0}, {0, 0}, {0, 0}}, dst[2] = {0, 0};   // (cell, count)
+      enum { PROP, HIDE, SINK, ALL, EXIT } kind = SINK;
+      auto bin = [&](uint32_t w, uint32_t rw) { src[0][0] = a; src[0][1] = w; src[1][0] = b; src[1][1] = w; dst[0] = c; dst[1] = rw; };
+      auto un = [&](uint32_t w, uint32_t rw) { src[0][0] = a; src[0][1] = w; dst[0] = c; dst[1] = rw; };
+      std::vector<uint32_t> wx;
+      switch (op) {
+        case OP_F32_ADD: case OP_F32_SUB: case OP_F32_MUL: case OP_F32_DIV: case OP_F32_MIN:
+        case OP_F32_MAX: case OP_F32_COPYSIGN: kind = PROP; bin(1, 1); break;
+        case OP_F64_ADD: case OP_F64_SUB: case OP_F64_MUL: case OP_F64_DIV: case OP_F64_MIN:
+        case OP_F64_MAX: case OP_F64_COPYSIGN: kind = PROP; bin(2, 2); break;
+        case OP_F32_ABS: case OP_F32_NEG: case OP_F32_CEIL: case OP_F32_FLOOR: case OP_F32_TRUNC:
+        case OP_F32_NEAREST: case OP_F32_SQRT: case OP_MOV32: kind = PROP; un(1, 1); break;
+        case OP_F64_ABS: case OP_F64_NEG: case OP_F64_CEIL: case OP_F64_FLOOR: case OP_F64_TRUNC:
+        case OP_F64_NEAREST: case OP_F64_SQRT: case OP_MOV64: kind = PROP; un(2, 2); break;
+        case OP_F32_DEMOTE_F64: kind = PROP; un(2, 1); break;
+        case OP_F64_PROMOTE_F32: kind = PROP; un(1, 2); break;
+        case OP_MOV128: case OP_V_NOT: case OP_V_F32X4_ABS: case OP_V_F32X4_NEG: case OP_V_F32X4_SQRT:
+        case OP_V_F64X2_ABS: case OP_V_F64X2_NEG: case OP_V_F64X2_SQRT: kind = PROP; un(4, 4); break;
+        case OP_CONST32: kind = PROP; dst[0] = c; dst[1] = 1; break;
+        case OP_CONST64: kind = PROP; dst[0] = c; dst[1] = 2; break;
+        case OP_CONST128: kind = PROP; dst[0] = c; dst[1] = 4; break;
+        case OP_V_I32X4_SPLAT: case OP_V_F32X4_SPLAT: kind = PROP; un(1, 4); break;
+        case OP_V_I64X2_SPLAT: case OP_V_F64X2_SPLAT: kind = PROP; un(2, 4); break;
+        case OP_V_AND: case OP_V_OR: case OP_V_XOR: case OP_V_ANDNOT: case OP_V_I32X4_ADD:
+        case OP_V_I32X4_SUB: case OP_V_I32X4_MUL: case OP_V_I64X2_ADD: case OP_V_I64X2_SUB:
+        case OP_V_F32X4_ADD: case OP_V_F32X4_SUB: case OP_V_F32X4_MUL: case OP_V_F32X4_DIV:
+        case OP_V_F32X4_MIN: case OP_V_F32X4_MAX: case OP_V_F32X4_PMIN: case OP_V_F32X4_PMAX:
+        case OP_V_F64X2_ADD: case OP_V_F64X2_SUB: case OP_V_F64X2_MUL: case OP_V_F64X2_DIV:
+        case OP_V_F64X2_MIN: case OP_V_F64X2_MAX: case OP_V_F64X2_PMIN: case OP_V_F64X2_PMAX:
+          kind = PROP; bin(4, 4); break;
+        case OP_V_EXTRACT32: kind = PROP; un(4, 1); break;
+        case OP_V_EXTRACT64: kind = PROP; un(4, 2); break;
+        case OP_V_REPLACE32: kind = PROP; bin(4, 4); src[1][1] = 1; break;
+        case OP_V_REPLACE64: kind = PROP; bin(4, 4); src[1][1] = 2; break;
+        case OP_V_ANY_TRUE: kind = PROP; un(4, 1); break;
+        case OP_F32_EQ: case OP_F32_NE: case OP_F32_LT: case OP_F32_GT: case OP_F32_LE: case OP_F32_GE:
+          kind = HIDE; dst[0] = c; dst[1] = 1; break;
+        case OP_F64_EQ: case OP_F64_NE: case OP_F64_LT: case OP_F64_GT: case OP_F64_LE: case OP_F64_GE:
+          kind = HIDE; dst[0] = c; dst[1] = 1; break;
+        case OP_V_F32X4_EQ: case OP_V_F32X4_NE: case OP_V_F32X4_LT: case OP_V_F32X4_GT:
+        case OP_V_F32X4_LE: case OP_V_F32X4_GE: case OP_V_F64X2_EQ: case OP_V_F64X2_NE:
+        case OP_V_F64X2_LT: case OP_V_F64X2_GT: case OP_V_F64X2_LE: case OP_V_F64X2_GE:
+          kind = HIDE; dst[0] = c; dst[1] = 4; break;
+        case OP_I64_ADD: case OP_I64_SUB: case OP_I64_MUL: case OP_I64_AND: case OP_I64_OR:
+        case OP_I64_XOR: case OP_I64_SHL: case OP_I64_SHR_S: case OP_I64_SHR_U: case OP_I64_ROTL:
+        case OP_I64_ROTR: kind = PROP; bin(2, 2); break;
+        case OP_I64_EQ: case OP_I64_NE: case OP_I64_LT_S: case OP_I64_LT_U: case OP_I64_GT_S:
+        case OP_I64_GT_U: case OP_I64_LE_S: case OP_I64_LE_U: case OP_I64_GE_S: case OP_I64_GE_U:
+          kind = PROP; bin(2, 1); break;
+        case OP_I64_ADD_I: case OP_I64_SUB_I: case OP_I64_MUL_I: case OP_I64_AND_I: case OP_I64_OR_I:
+        case OP_I64_XOR_I: case OP_I64_SHL_I: case OP_I64_SHR_S_I: case OP_I64_SHR_U_I:
+        case OP_I64_ROTL_I: case OP_I64_ROTR_I: case OP_I64_CLZ: case OP_I64_CTZ: case OP_I64_POPCNT:
+        case OP_I64_EXT8S: case OP_I64_EXT16S: case OP_I64_EXT32S: kind = PROP; un(2, 2); break;
+        case OP_I64_EQ_I: case OP_I64_NE_I: case OP_I64_LT_S_I: case OP_I64_LT_U_I: case OP_I64_GT_S_I:
+        case OP_I64_GT_U_I: case OP_I64_LE_S_I: case OP_I64_LE_U_I: case OP_I64_GE_S_I:
+        case OP_I64_GE_U_I: case OP_I64_EQZ: kind = PROP; un(2, 1); break;
+        case OP_I64_EXTEND_I32_S: case OP_I64_EXTEND_I32_U: case OP_F64_CONVERT_I32_S:
+        case OP_F64_CONVERT_I32_U: kind = PROP; un(1, 2); break;
+        case OP_F32_CONVERT_I32_S: case OP_F32_CONVERT_I32_U: kind = PROP; un(1, 1); break;
+        case OP_F32_CONVERT_I64_S: case OP_F32_CONVERT_I64_U: kind = PROP; un(2, 1); break;
+        case OP_F64_CONVERT_I64_S: case OP_F64_CONVERT_I64_U: kind = PROP; un(2, 2); break;
+        case OP_SELECT32: case OP_SELECT64: case OP_SELECT128: {
+          const uint32_t w = op == OP_SELECT32 ? 1 : op == OP_SELECT64 ? 2 : 4;
+          kind = PROP; bin(w, w); src[2][0] = d; src[2][1] = 1; break;
+        }
+        case OP_V_I8X16_EQ: case OP_V_I8X16_NE: case OP_V_I16X8_EQ: case OP_V_I16X8_NE:
+        case OP_V_I32X4_EQ: case OP_V_I32X4_NE: case OP_V_I32X4_LT_S: case OP_V_I32X4_LT_U:
+        case OP_V_I32X4_GT_S: case OP_V_I32X4_GT_U: case OP_V_I32X4_LE_S: case OP_V_I32X4_LE_U:
+        case OP_V_I32X4_GE_S: case OP_V_I32X4_GE_U: case OP_V_I64X2_EQ: case OP_V_I64X2_NE:
+        case OP_V_I64X2_LT_S: case OP_V_I64X2_GT_S: case OP_V_I64X2_LE_S: case OP_V_I64X2_GE_S:
+        case OP_V_I64X2_MUL: case OP_V_I8X16_ADD: case OP_V_I8X16_SUB: case OP_V_I16X8_ADD:
+        case OP_V_I16X8_SUB: case OP_V_I16X8_MUL: kind = PROP; bin(4, 4); break;
+        case OP_V_I8X16_BITMASK: case OP_V_I16X8_BITMASK: case OP_V_I32X4_BITMASK:
+        case OP_V_I64X2_BITMASK: case OP_V_I8X16_ALL_TRUE: case OP_V_I16X8_ALL_TRUE:
+        case OP_V_I32X4_ALL_TRUE: case OP_V_I64X2_ALL_TRUE: kind = PROP; un(4, 1); break;
+        // float -> int: a NaN traps or saturates whatever its payload
+        case OP_I32_TRUNC_F32_S: case OP_I32_TRUNC_F32_U: case OP_I32_TRUNC_F64_S:
+        case OP_I32_TRUNC_F64_U: case OP_I32_TRUNC_SAT_F32_S: case OP_I32_TRUNC_SAT_F32_U:
+        case OP_I32_TRUNC_SAT_F64_S: case OP_I32_TRUNC_SAT_F64_U:
+          kind = HIDE; dst[0] = c; dst[1] = 1; break;
+        case OP_I64_TRUNC_F32_S: case OP_I64_TRUNC_F32_U: case OP_I64_TRUNC_F64_S:
+        case OP_I64_TRUNC_F64_U: case OP_I64_TRUNC_SAT_F32_S: case OP_I64_TRUNC_SAT_F32_U:
+        case OP_I64_TRUNC_SAT_F64_S: case OP_I64_TRUNC_SAT_F64_U:
+          kind = HIDE; dst[0] = c; dst[1] = 2; break;
+        case OP_NOP_CNT: kind = PROP; break;
+        case OP_ZERO_LOCALS: kind = PROP; dst[0] = a; dst[1] = b; break;
+        case OP_RET: case OP_UNREACHABLE: kind = EXIT; break;
+        case OP_CALL: case OP_CALL_INDIRECT: case OP_HOST_CALL: case OP_TAIL_CALL:
+        case OP_TAIL_CALL_INDIRECT: kind = ALL; break;
+        default:
+          // exact single-result 32-bit integer ops (not the loads: their address can trap)
+          if (!mem_bytes(op) && written_exact(I, &wx) && wx.size() == 1 && wx[0] == c) {
+            kind = PROP;
+            src[0][0] = a; src[0][1] = 1; src[1][0] = b; src[1][1] = 1; dst[0] = c; dst[1] = 1;
+            src[2][0] = d; src[2][1] = 1;   // (I32_ADD3's third operand)
+          }
+          // (the other DBC_CTL ops may trap -- an exit, after which only globals and
+          // memory remain -- or leave the core; their successor is still pc + 1)
+          break;
+      }
+      // successors
+      if (kind == ALL) {
+        s = all;
+      } else if (kind == EXIT) {
+        s = globals;
+        if (op == OP_RET) put(s, a, b);
+      } else {
+        if (op == OP_BR_TABLE) {
+          for (uint32_t k = 0; k <= b; k++)
+            if (2 * (size_t(I.w3) + k) < P.brtab.size()) succ(P.brtab[2 * (size_t(I.w3) + k)]);
+        } else {
+          if (op != OP_JMP) succ(pc + 1);
+          if (is_branch_op(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2) succ(I.w3);
+        }
+        s = after;
+        if (kind == PROP || kind == HIDE) {
+          const bool used = any(after, dst[0], dst[1]);
+          if (dst[1]) res[pc] = used ? 1 : 0;
+          kill(s, dst[0], dst[1]);
+          if (kind == PROP && used)
+            for (auto &x : src) put(s, x[0], x[1]);
+        } else if (is_store_op(op)) {   // the address and the stored bits
+          put(s, a, 1);
+          put(s, b, std::max(1u, mem_bytes(op) / 4));
+        } else if (mem_bytes(op)) {     // a load: its address; its result is memory's
+          const bool w64 = op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 ||
+                           op == OP_LD16U64 || op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
+          kill(s, c, op == OP_LD128 ? 4 : w64 ? 2 : 1);
+          put(s, a, 1);
+        } else if (is_branch_op(op) || op == OP_BR_TABLE) {   // i32 operands
+          if (op != OP_JMP) put(s, a, 1);
+          if (op >= OP_BR_EQ && op <= OP_BR_GE_U) put(s, b, 1);
+        } else if (op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2) {   // a: condition, b -> c
+          put(s, a, 1);
+          put(s, b, op == OP_BR_IF_MOV1 ? 1 : 2);
+        } else {   // sink: every field it names, 4 wide, is observable
+          put(s, a, 4); put(s, b, 4); put(s, c, 4); put(s, d, 4);
+          if (op == OP_I32_ADD3_XROTR_I) put(s, I.w3 & 0xFFFFu, 1);
+        }
+        for (size_t w = 0; w < W; w++) s[w] |= globals[w];
+      }
+      if (s != before[pc]) {
+        before[pc] = s;
+        changed = true;
+      }
+    }
+  }
+  // (debugging aid: WB_NANOBS_LIST=<file> writes per pc the flag and the cells observable
+  // before it)
+  if (const char *lst = getenv("WB_NANOBS_LIST"))
+    if (FILE *f = fopen(lst, "w")) {
+      for (size_t pc = 0; pc < n; pc++) {
+        fprintf(f, "%4zu %d", pc, int(res[pc]));
+        for (uint32_t x = 0; x < nc; x++)
+          if (before[pc][x >> 6] >> (x & 63) & 1) fprintf(f, " %u", x);
+        fprintf(f, "\n");
+      }
+      fclose(f);
+    }
+  return res;
+}
+
 // Loop-carried memory forwarding. A loop whose body is a run R ending in an inlined leaf
 // call and the post-call run Pp branching back to R's start (C2: the chain loop around
 // BLAKE3's compression) reads the words its previous trip stored or loaded: the callee's
@@ -2181,6 +2393,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // WB_JIT_SCHED=0 keeps program order)
   const bool split_on = !(getenv("WB_TRIP_SPLIT") && getenv("WB_TRIP_SPLIT")[0] == '0');
   const bool sched_on = !(getenv("WB_JIT_SCHED") && getenv("WB_JIT_SCHED")[0] == '0');
+  const bool nob_on = !(getenv("WB_NANOBS") && getenv("WB_NANOBS")[0] == '0');
+  const std::vector<uint8_t> nob = nob_on ? nan_observable(P) : std::vector<uint8_t>();
   for (uint32_t k = 0; k < nr && split_on; k++) {
     const JitRun &r = runs[k];
     const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
@@ -2272,6 +2486,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       if (st == 0 && !split[k]) continue;
       Em e;
       e.trip = true;
+      if (!nob.empty()) e.nanobs = &nob;
       e.g = glog;
       e.fb = P.global_cells;
       e.prog = &P;
@@ -2417,6 +2632,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   const bool trips = trip && simt && runs.size() <= kTripMaxRuns;
   const bool hybrid = trips && !(getenv("WB_HYBRID") && getenv("WB_HYBRID")[0] == '0');
   if (trips && !hybrid) return trip_source(P, runs, glog, false);
+  // NaN fixes only where the payload can be observed (WB_NANOBS=0: everywhere)
+  const bool nob_on = !(getenv("WB_NANOBS") && getenv("WB_NANOBS")[0] == '0');
+  const std::vector<uint8_t> nob = nob_on ? nan_observable(P) : std::vector<uint8_t>();
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
@@ -2513,6 +2731,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     e.g = glog;
     e.run = uint32_t(k + size_t(var) * 2 * runs.size());   // (stub labels apart)
     const std::string K = std::to_string(k) + (var == 1 ? "c" : var == 2 ? "p" : "");
+    if (!nob.empty()) e.nanobs = &nob;
     e.l(".p2align 6");
     ScanLoop sl;
     // Scan blocks are opt-in (WB_SCAN=1; WB_SCAN=p+1: only the loop at pc p): measured on
@@ -2667,6 +2886,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       ei.fb = fb;
       ei.prog = &P;
       ei.shift = off;
+      ei.nanobs = e.nanobs;
       ei.done = r.cnt;                      // counted before the callee: the caller's run
       for (uint32_t q = 0; q < nloc; q++)
         if (dead.empty() || !dead[fb + nargs + q]) ei.l("v_mov_b32 %s, 0", ei.v(fb + nargs + q));
