@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "frontend.h"
 #include "tc_slots.h"
@@ -3285,11 +3286,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   return src;
 }
 
-std::string jit_compile(const std::string &src, std::vector<char> *code) {
+std::string jit_compile(const std::string &src, std::vector<char> *code, const std::string &arch) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "wbjit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     return "hiprtcCreateProgram failed";
-  const char *opts[] = {"--offload-arch=gfx950", "-O1"};
+  const std::string target = "--offload-arch=" + arch;
+  const char *opts[] = {target.c_str(), "-O1"};
   if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -3307,15 +3309,29 @@ std::string jit_compile(const std::string &src, std::vector<char> *code) {
 }
 
 std::string jit_load(const std::string &src, size_t nruns, int device, std::vector<uint64_t> *addr) {
-  // one code object per (device, source) for the life of the process: contexts of the
-  // same module share it
+  // one code object per (HIP context, device, source) while that context lives: contexts
+  // of the same module share it (a new primary context after hipDeviceReset gets its own)
   static std::mutex mu;
-  static std::map<std::pair<int, std::string>, std::vector<uint64_t>> cache;
+  static std::map<std::tuple<uintptr_t, int, std::string>, std::vector<uint64_t>> cache;
   std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find({device, src});
+  hipCtx_t hctx = nullptr;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wdeprecated-declarations"
+  (void)hipCtxGetCurrent(&hctx);
+#pragma clang diagnostic pop
+  const auto key = std::make_tuple(uintptr_t(hctx), device, src);
+  auto it = cache.find(key);
   if (it != cache.end()) { *addr = it->second; return ""; }
+  // the device's own target (gfx950 on MI355X), not a hard-coded one
+  std::string arch = "gfx950";
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.gcnArchName[0]) {
+    arch = prop.gcnArchName;
+    const size_t colon = arch.find(':');   // (feature suffixes such as :sramecc+:xnack-)
+    if (colon != std::string::npos) arch.resize(colon);
+  }
   std::vector<char> code;
-  std::string err = jit_compile(src, &code);
+  std::string err = jit_compile(src, &code, arch);
   if (!err.empty()) return err;
   hipModule_t mod;
   if (hipModuleLoadData(&mod, code.data()) != hipSuccess) return "hipModuleLoadData failed";
@@ -3326,14 +3342,18 @@ std::string jit_load(const std::string &src, size_t nruns, int device, std::vect
   unsigned nr = unsigned(nruns);
   void *args[] = {&dout, &nr};
   std::vector<uint64_t> a(nruns, 0);
-  const bool ok = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, nullptr, args, nullptr) == hipSuccess &&
-                  hipDeviceSynchronize() == hipSuccess &&
-                  hipMemcpy(a.data(), dout, nruns * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  // (a private stream: BatchCreate must not wait for other contexts' kernels)
+  hipStream_t qs = nullptr;
+  const bool ok = hipStreamCreateWithFlags(&qs, hipStreamNonBlocking) == hipSuccess &&
+                  hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, qs, args, nullptr) == hipSuccess &&
+                  hipMemcpyAsync(a.data(), dout, nruns * 8, hipMemcpyDeviceToHost, qs) == hipSuccess &&
+                  hipStreamSynchronize(qs) == hipSuccess;
+  if (qs) (void)hipStreamDestroy(qs);
   (void)hipFree(dout);
   if (!ok) return "compiled-run address query failed";
   for (uint64_t x : a)
     if (x == 0 || (x & 63)) return "compiled-run address query returned a bad address";
-  cache[{device, src}] = a;   // the module stays loaded: its code is jumped to
+  cache[key] = a;   // the module stays loaded: its code is jumped to
   *addr = a;
   return "";
 }

@@ -64,7 +64,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
                        const JitCost *cost = nullptr, bool simt = false, bool trip = false);
 
 // Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
-std::string jit_compile(const std::string &src, std::vector<char> *code);
+std::string jit_compile(const std::string &src, std::vector<char> *code, const std::string &arch = "gfx950");
 
 // Compile (cached per device and source), load on the current device and read back the
 // runs' code addresses. Returns "" or an error.
