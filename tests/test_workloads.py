@@ -264,6 +264,7 @@ ENGINES = {
     "trip": {"WB_TRIP": "1"},                     # V frames, trip mode
     "half": {"WB_HALF": "1"},                     # half waves (32 lanes per launch wave)
     "halftrip": {"WB_HALF": "1", "WB_TRIP": "1"},
+    "lsched": {"WB_LSCHED": "1"},                 # the pick by distinct-pc enumeration
     "nosimt": {"WB_SIMT": "0"},                   # V frames, compiled runs without SIMT
     "nojit": {"WB_JIT": "0"},                     # V frames, threaded core handlers only
     "lds": {"WB_VFRAME": "0"},                    # LDS frames, threaded core

@@ -1722,6 +1722,77 @@ void sched_block(Em &e, const std::string &p, const char *mask) {
   // interrupts) even if the lanes retired nothing
   e.l("s_sub_u32 s64, s64, 16");
   e.l("s_cselect_b32 s64, 0, s64");
+  const char *lse = getenv("WB_LSCHED");
+  if (!mask && lse && lse[0] == '1') {
+    // (A/B variant) the pick by enumerating the distinct pcs of ALL: each round takes the
+    // first remaining lane's pc and the lanes at it, keeping the lowest two pcs -- no wave
+    // reductions; a round per distinct pc
+    e.l("s_mov_b64 exec, s[96:97]");
+    e.l("s_waitcnt lgkmcnt(0)");            // (a TInstr prefetch into s[76:91] must land)
+    e.l("s_mov_b64 s[76:77], s[96:97]");    // lanes not yet visited
+    e.l("s_mov_b32 s82, -1");               // lowest pc
+    e.l("s_mov_b32 s83, -1");               // the next lowest
+    e.l("%s_lp:", p.c_str());
+    e.l("s_ff1_i32_b64 s78, s[76:77]");
+    e.l("s_nop 0");
+    e.l("v_readlane_b32 s79, %s, s78", VPC);
+    e.l("s_nop 1");
+    e.l("v_cmp_eq_u32_e64 s[80:81], s79, %s", VPC);
+    e.l("s_and_b64 s[80:81], s[80:81], s[76:77]");
+    e.l("s_andn2_b64 s[76:77], s[76:77], s[80:81]");
+    e.l("s_cmp_lt_u32 s79, s82");
+    e.l("s_cbranch_scc0 %s_nm", p.c_str());
+    e.l("s_mov_b32 s83, s82");
+    e.l("s_mov_b32 s82, s79");
+    e.l("s_mov_b64 s[74:75], s[80:81]");    // the group: the lanes at the lowest pc
+    e.l("s_branch %s_nx", p.c_str());
+    e.l("%s_nm:", p.c_str());
+    e.l("s_min_u32 s83, s83, s79");
+    e.l("%s_nx:", p.c_str());
+    e.l("s_cmp_lg_u64 s[76:77], 0");
+    e.l("s_cbranch_scc1 %s_lp", p.c_str());
+    e.l("s_lshl_b32 s62, s82, 5");
+    e.l("s_cmp_eq_u32 s95, -1");            // were the banks converged?
+    e.l("s_cselect_b32 s69, 1, 0");
+    e.l("s_cmp_eq_u32 s83, -1");
+    e.l("s_mov_b32 s63, -1");
+    e.l("s_cbranch_scc1 %s_lc", p.c_str());
+    e.l("s_lshl_b32 s63, s83, 5");
+    e.l("%s_lc:", p.c_str());
+    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+    e.l("s_cmp_eq_u32 s63, -1");
+    e.l("s_cbranch_scc1 %s_conv", p.c_str());
+    e.l("s_mov_b32 s95, s63");
+    e.l("s_cmp_eq_u32 s69, 0");
+    e.l("s_cbranch_scc1 %s_disp", p.c_str());
+    e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
+    e.l("s_addc_u32 s71, s71, 0");
+    e.l("s_branch %s_bankb", p.c_str());
+    e.l("%s_conv:", p.c_str());
+    e.l("s_mov_b32 s63, -1");
+    e.l("s_mov_b32 s95, -1");
+    e.l("s_cmp_eq_u32 s69, 1");
+    e.l("s_cbranch_scc1 %s_disp", p.c_str());
+    e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
+    e.l("s_subb_u32 s71, s71, 0");
+    e.l("%s_bankb:", p.c_str());
+    e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
+    e.l("s_addc_u32 s73, s71, 0");
+    e.l("%s_disp:", p.c_str());
+    e.l("s_mov_b64 exec, s[74:75]");
+    e.l("s_cmp_eq_u32 s64, 0");
+    e.l("s_cbranch_scc1 %s_out", p.c_str());
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_add_u32 s68, s70, s76");
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    e.l("%s_out:", p.c_str());
+    e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    return;
+  }
   e.l("s_mov_b64 exec, -1");
   if (mask) e.l("s_mov_b64 s[74:75], %s", mask);   // (the TInstr load below overwrites s[76:91])
   e.l("s_nop 4");
