@@ -1888,6 +1888,7 @@ std::string simt_sched(bool hybrid) {
 // still looping go round again. Any lane whose kScanUnroll loads are not all in bounds and
 // aligned runs the plain run instead (which meets the failing access itself).
 constexpr uint32_t kScanUnroll = 8;
+constexpr uint32_t kTripScan = 4;   // trip mode: scan iterations per trip (trip_scan_stage)
 struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
 
 bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
@@ -2399,6 +2400,92 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
 }
 }  // namespace
 
+// Trip-mode scan loops (trip_source): the lanes of a scan run whose window of U
+// addresses is in bounds and aligned (flag v112 = 1) load all U words in stage A
+// (v108..v108+U-1) and find their exit in stage B; the others (v112 = 0) run the plain
+// stage code that follows (exec = them; the stage ends at once when there are none).
+// Entered with EXEC = the run's lanes in this trip. Temporaries survive from stage A to
+// stage B per lane (other runs execute under disjoint EXEC masks).
+void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl, uint32_t U,
+                     int st, bool fall_in, const std::string &L) {
+  static const char *const T[kTripScan] = {"v108", "v109", "v110", "v111"};
+  const uint32_t x = sl.x, y = sl.y, fall = r.pc + 3;
+  const DInstr &br = P.code[r.pc + 2];
+  const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
+  if (st == 0) {
+    // the window: bytes (x + d*j) + off .. +3 for j = 1..U in bounds and aligned, and x +
+    // d*j not wrapping (as the SIMT scan block)
+    const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
+    e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(x));
+    e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
+    e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+    e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(x));
+    if (sl.d < 0) {
+      e.l("v_cmp_gt_u32_e32 vcc, 0x%x, %s", uint32_t(-sl.d) * U, e.v(x));
+      e.l("s_or_b64 %s, %s, vcc", T2, T2);
+    }
+    e.l("v_and_b32_e32 %s, 3, %s", Y1, Y0);
+    e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y1);
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+    e.l("s_and_b64 s[84:85], exec, %s", T2);     // plain lanes
+    e.l("s_andn2_b64 exec, exec, %s", T2);       // window lanes
+    e.l("s_cbranch_execz %s_sp", L.c_str());
+    e.l("v_mov_b32 v112, 1");
+    for (uint32_t j = 1; j <= U; j++) {
+      e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(x));
+      if (e.g == 0) {
+        e.l("v_mov_b32 %s, %s", W0, Y0);
+        e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+      } else {
+        e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
+        e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
+        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+        e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
+        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+      }
+      e.l("global_load_dword %s, %s, off", T[j - 1], XP);
+    }
+    e.l("%s_sp:", L.c_str());
+    e.l("s_mov_b64 exec, s[84:85]");
+    e.l("s_cbranch_execz %s", e.stage_end.c_str());
+    e.l("v_mov_b32 v112, 0");
+    return;
+  }
+  // stage B: the window lanes' exits in iteration order (s[82:83] = still looping)
+  e.l("v_cmp_ne_u32_e32 vcc, 0, v112");
+  e.l("s_andn2_b64 s[84:85], exec, vcc");        // plain lanes
+  e.l("s_and_b64 exec, exec, vcc");
+  e.l("s_cbranch_execz %s_sb", L.c_str());
+  e.l("s_mov_b64 s[82:83], exec");
+  for (uint32_t j = 1; j <= U; j++) {
+    const std::string nx = L + "_n" + std::to_string(j);
+    scan_cond(e, br, sl, T[j - 1]);
+    e.l("s_andn2_b64 s[68:69], s[82:83], vcc");   // leave in iteration j
+    e.l("s_and_b64 s[82:83], s[82:83], vcc");
+    e.l("s_cmp_eq_u64 s[68:69], 0");
+    e.l("s_cbranch_scc1 %s", nx.c_str());
+    e.l("s_mov_b64 exec, s[68:69]");
+    e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(j)), e.v(x));
+    e.l("v_mov_b32 %s, %s", e.v(y), T[j - 1]);
+    e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(int32_t(j * r.cnt) + int32_t(j - 1) * tcnt), VCNT);
+    e.l("v_mov_b32 %s, 0x%x", VPC, fall);
+    if (!fall_in) e.l("s_or_b64 s[76:77], s[76:77], exec");   // (waits outside the trips)
+    e.l("s_mov_b64 exec, s[82:83]");
+    e.l("%s:", nx.c_str());
+  }
+  // still looping after U iterations: round again in the next trip
+  e.l("s_mov_b64 exec, s[82:83]");
+  e.l("s_cbranch_execz %s_sb", L.c_str());
+  e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(U)), e.v(x));
+  e.l("v_mov_b32 %s, %s", e.v(y), T[U - 1]);
+  e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(int32_t(U) * (int32_t(r.cnt) + tcnt)), VCNT);
+  e.l("%s_sb:", L.c_str());
+  e.l("s_mov_b64 exec, s[84:85]");
+  e.l("s_cbranch_execz %s", e.stage_end.c_str());
+}
+
 // hybrid: only the trips' code (Ltin, the trip loop, the runs' stages, the exits), for
 // jit_source's SIMT code object, whose Lsched sends diverged waves to Ltin; a trip after
 // which every lane is at one pc goes back to Lsched (SIMT scheduling, direct run-to-run
@@ -2472,6 +2559,17 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
     split[k] = trip_split(P, r, ends_run(lop) ? r.len - 1 : r.len);
   }
+  // Scan loops (scan_loop_of: `x += d; y = load(x + off); br y CMP p` back to the run's
+  // start) run kTripScan iterations per trip: stage A checks the whole window of kTripScan
+  // addresses once per lane and loads them all; stage B finds each lane's exit iteration
+  // in order. A lane whose window fails the check (near its memory's end) takes the plain
+  // one-iteration path, which meets a failing access exactly. WB_TRIP_SCAN=0 turns it off.
+  const char *tse = getenv("WB_TRIP_SCAN");
+  const uint32_t scan_k = tse ? std::min<uint32_t>(uint32_t(atoi(tse)), kTripScan) : kTripScan;
+  std::vector<ScanLoop> scans(nr);
+  std::vector<uint8_t> is_scan(nr, 0);
+  for (uint32_t k = 0; k < nr && scan_k >= 2; k++)
+    is_scan[k] = split[k] == 2 && scan_loop_of(P, runs[k], &scans[k]);
   h.l("Ltrip:");
   for (uint32_t k = 0; k < nr; k++) {
     if (!split[k]) continue;
@@ -2510,7 +2608,13 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_cbranch_scc1 Ltx");
   h.l("Ltbud:");
   uint32_t trip_cost = 256;   // (>= any run's count: a lane never retires more than a trip costs)
-  for (const auto &r : runs) trip_cost = std::max(trip_cost, r.cnt);
+  for (uint32_t k = 0; k < nr; k++) {
+    const JitRun &r = runs[k];
+    trip_cost = std::max(trip_cost, r.cnt);
+    if (is_scan[k])
+      trip_cost = std::max<uint32_t>(trip_cost, scan_k * uint32_t(std::max<int32_t>(
+                                                    0, int32_t(r.cnt) + int16_t(P.code[r.pc + 2].w2 >> 16))) + r.cnt);
+  }
   h.l("s_sub_u32 s64, s64, 0x%x", trip_cost);
   h.l("s_cselect_b32 s64, 0, s64");
   h.l("s_cmp_eq_u32 s64, 0");
@@ -2569,6 +2673,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       e.l(".p2align 2");
       e.l("%s:", L.c_str());
       e.l("s_mov_b64 exec, s[74:75]");
+      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, st, in_region(r.pc + 3), L);
       const size_t at = e.o.size();
       for (uint32_t i = st ? split[k] : 0; i < (st ? nbody : split[k]); i++) {
         const DInstr &I = P.code[r.pc + i];
