@@ -2579,9 +2579,19 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     h.l("LtAr%u:", k);
   }
   h.l("s_waitcnt vmcnt(0)");
+  // Forward chaining (WB_TRIP_CHAIN=0 turns it off): a run without a stage A takes every
+  // lane now at its start -- the lanes that began the trip there and those an earlier
+  // run of this trip moved there -- except the lanes waiting outside the trips (escapes
+  // included). A run with a stage A takes only the lanes that began the trip there.
+  const bool chain = !(getenv("WB_TRIP_CHAIN") && getenv("WB_TRIP_CHAIN")[0] == '0');
   for (uint32_t k = 0; k < nr; k++) {
-    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
-    h.l("s_and_b64 s[74:75], vcc, exec");
+    if (chain && !split[k]) {
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, VPC);
+      h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
+    } else {
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
+      h.l("s_and_b64 s[74:75], vcc, exec");
+    }
     h.l("s_cbranch_scc1 LtB%u", k);
     h.l("LtBr%u:", k);
   }
@@ -2607,14 +2617,17 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_cmp_gt_u32 s69, s68");
   h.l("s_cbranch_scc1 Ltx");
   h.l("Ltbud:");
-  uint32_t trip_cost = 256;   // (>= any run's count: a lane never retires more than a trip costs)
+  // (>= what one lane can retire in a trip: one run, or with chaining every run once)
+  uint32_t trip_cost = 256, chained = 0;
   for (uint32_t k = 0; k < nr; k++) {
     const JitRun &r = runs[k];
     trip_cost = std::max(trip_cost, r.cnt);
+    chained += r.cnt + 64;   // (+ a taken branch's correction)
     if (is_scan[k])
       trip_cost = std::max<uint32_t>(trip_cost, scan_k * uint32_t(std::max<int32_t>(
                                                     0, int32_t(r.cnt) + int16_t(P.code[r.pc + 2].w2 >> 16))) + r.cnt);
   }
+  if (chain) trip_cost = std::max(trip_cost, chained + (uint32_t)kTripScan * 64u);
   h.l("s_sub_u32 s64, s64, 0x%x", trip_cost);
   h.l("s_cselect_b32 s64, 0, s64");
   h.l("s_cmp_eq_u32 s64, 0");
