@@ -279,3 +279,17 @@ def test_large_module_assembles(built):
     from conftest import golden
     n, ins = _jit_check(golden("rust_add.wasm"), 0)
     assert n > 1000 and ins > 5000
+
+
+def test_trip_mode_choice(built):
+    """Which modules run trip mode (jit.h trips_pay, Program::divergent_mem): C3 (addresses
+    from loaded data) and C4 (a br_table state machine, no calls) do; C1 (recursion), C2
+    (converged, with calls), C5 (an escape loop whose lanes leave one by one) do not."""
+    L = _check_lib()
+    L.wb_trip_choice.restype = ctypes.c_int
+    L.wb_trip_choice.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    fib = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fibonacci.wasm"), "rb").read()
+    want = {"c1": (fib, 0), "c2": (W.blake3_wasm(), 0), "c3": (W.qsort_wasm(), 1),
+            "c4": (W.collatz_wasm(), 1), "c5": (W.mandel_wasm(), 0)}
+    got = {k: L.wb_trip_choice(w, len(w)) for k, (w, _) in want.items()}
+    assert got == {k: v for k, (_, v) in want.items()}

@@ -153,10 +153,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   const char *sme = getenv("WB_SIMT");
   const bool want_simt = !C->conf.CostLimit && !(sme && sme[0] == '0');
   // Trip mode (jit.h) for modules whose load/store addresses depend on per-instance data
-  // (Program::divergent_mem: lanes part ways on loaded data); WB_TRIP=0 / 1 forces it off /
+  // (Program::divergent_mem: lanes part ways on loaded data) and for call-free modules
+  // whose lanes part ways inside their loops (wb::trips_pay); WB_TRIP=0 / 1 forces it off /
   // on (A/B measurement aid). SIMT contexts only.
   const char *tre = getenv("WB_TRIP");
-  bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem);
+  bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem || wb::trips_pay(P));
   if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
     std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt, want_trip);
     if (want_trip && runs.size() > wb::kTripMaxRuns) {   // (too many runs to visit per trip)

@@ -3475,6 +3475,50 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   return src;
 }
 
+bool trips_pay(const Program &P) {
+  const size_t n = P.code.size();
+  std::vector<std::pair<uint32_t, uint32_t>> spans;   // loops: (head, back-edge pc)
+  auto targets = [&](size_t pc, std::vector<uint32_t> *t) {
+    const DInstr &I = P.code[pc];
+    const uint16_t op = op_of(I);
+    t->clear();
+    if (op == OP_BR_TABLE) {
+      for (uint32_t k = 0; k <= (I.w1 >> 16); k++)
+        if (2 * (size_t(I.w3) + k) < P.brtab.size()) t->push_back(P.brtab[2 * (size_t(I.w3) + k)]);
+    } else if (is_branch_op(op) || op == OP_BR_IF_MOV1 || op == OP_BR_IF_MOV2) {
+      t->push_back(I.w3);
+      if (op != OP_JMP) t->push_back(uint32_t(pc + 1));
+    }
+  };
+  std::vector<uint32_t> t;
+  for (size_t pc = 0; pc < n; pc++) {
+    const uint16_t op = op_of(P.code[pc]);
+    if (op == OP_CALL || op == OP_CALL_INDIRECT || op == OP_TAIL_CALL || op == OP_TAIL_CALL_INDIRECT)
+      return false;
+    targets(pc, &t);
+    for (uint32_t x : t)
+      if (x <= pc) spans.push_back({x, uint32_t(pc)});
+  }
+  for (size_t pc = 0; pc < n; pc++) {
+    targets(pc, &t);
+    if (t.size() < 2) continue;
+    // the innermost loop around pc
+    uint32_t h = 0, e = 0, best = 0xFFFFFFFFu;
+    for (const auto &sp : spans)
+      if (sp.first <= pc && pc <= sp.second && sp.second - sp.first < best) {
+        best = sp.second - sp.first;
+        h = sp.first;
+        e = sp.second;
+      }
+    if (best == 0xFFFFFFFFu) continue;
+    std::vector<uint32_t> in;
+    for (uint32_t x : t)
+      if (x >= h && x <= e && std::find(in.begin(), in.end(), x) == in.end()) in.push_back(x);
+    if (in.size() >= 2) return true;
+  }
+  return false;
+}
+
 std::string jit_compile(const std::string &src, std::vector<char> *code, const std::string &arch) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "wbjit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
@@ -3619,4 +3663,13 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
     return -1;
   }
   return int(runs.size());
+}
+
+// TEST hook (tests/test_jit.py, CPU): whether a SIMT context of this module runs trip mode
+// (Program::divergent_mem or wb::trips_pay; WB_TRIP unset). 1 / 0, or -1 when it fails to load.
+extern "C" __attribute__((visibility("default"))) int wb_trip_choice(const uint8_t *wasm, uint32_t len) {
+  wb::Program P;
+  uint8_t ec = 0;
+  if (!wb::load_program(wasm, len, P, &ec).empty()) return -1;
+  return P.divergent_mem || wb::trips_pay(P) ? 1 : 0;
 }

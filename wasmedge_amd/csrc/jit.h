@@ -63,6 +63,15 @@ constexpr size_t kTripMaxRuns = 96;
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost = nullptr, bool simt = false, bool trip = false);
 
+// Whether trip mode pays for a module whose memory addresses do not depend on per-instance
+// data (Program::divergent_mem picks it for those): lanes part ways inside a loop on every
+// trip round it -- a conditional branch whose two successors, or a br_table with two
+// entries, stay in the innermost loop around it (C4's br_table state machine: 7.7e11
+// against 6.1e11 instr/s on SIMT) -- and the module makes no calls (recursion's
+// call/return transitions are cheaper under SIMT scheduling: C1 0.82x with trips).
+// Loops whose lanes leave one by one (C5's escape loop: 0.59x with trips) do not qualify.
+bool trips_pay(const Program &P);
+
 // Compile `src` for gfx950 (hiprtc). Returns "" and the code object, or an error.
 std::string jit_compile(const std::string &src, std::vector<char> *code, const std::string &arch = "gfx950");
 
