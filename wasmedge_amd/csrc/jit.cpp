@@ -214,13 +214,17 @@ struct Em {
   // re-executes it from intact sources), else the temporaries R0 R1 Z0 Z1 (put128 copies
   // them). pair64: the two 64-bit halves as aligned pairs (c even) for f64 / u64 ops.
   std::string dst[4], dstp[2];
+  // lanewise: result word (pair) k depends only on word (pair) k of each source and is
+  // written after it is read, so a source that IS the result (c..c+3 exactly) may be
+  // overwritten in place
   const char *const *res128(uint32_t c, std::initializer_list<std::pair<uint32_t, uint32_t>> src,
-                            bool pair64 = false) {
+                            bool pair64 = false, bool lanewise = false) {
     static const char *const tmp[4] = {R0, R1, Z0, Z1};
     static thread_local const char *out[4];
     bool direct = !(pair64 && (c & 1));
     for (const auto &r : src)
-      if (r.first < c + 4 && c < r.first + r.second) direct = false;
+      if (r.first < c + 4 && c < r.first + r.second && !(lanewise && r.first == c && r.second == 4))
+        direct = false;
     for (int k = 0; k < 4; k++) {
       dst[k] = direct ? V(c + k) : "";
       out[k] = direct ? dst[k].c_str() : tmp[k];
@@ -239,6 +243,7 @@ struct Em {
   std::string tail;   // out-of-line code of the run (placed after it)
   int nfix = 0;
   const std::vector<uint8_t> *nanobs = nullptr;   // nan_observable(), per pc
+  bool nan_needed() const { return !(nanobs && pc < nanobs->size() && !(*nanobs)[pc]); }
   void nan_fix(const std::vector<NanItem> &items, int w) {
     if (nanobs && pc < nanobs->size() && !(*nanobs)[pc]) return;   // payload never observed
     const std::string id = std::to_string(run) + "_" + std::to_string(nfix++);
@@ -684,14 +689,14 @@ bool emit(Em &e, const DInstr &I) {
                         : op == OP_V_XOR ? "v_xor_b32_e32" : op == OP_V_I32X4_ADD ? "v_add_u32_e32"
                         : op == OP_V_I32X4_SUB ? "v_sub_u32_e32" : "v_mul_lo_u32";
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, true);
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
       e.put128(c, r);
       return true;
     }
     case OP_V_I64X2_ADD: case OP_V_I64X2_SUB: case OP_V_I64X2_EQ: {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, true);
       for (int k = 0; k < 2; k++) {
         const uint32_t x = a + 2 * k, y = b + 2 * k;
         if (op == OP_V_I64X2_SUB) {
@@ -713,7 +718,7 @@ bool emit(Em &e, const DInstr &I) {
     case OP_V_F32X4_ADD: case OP_V_F32X4_SUB: case OP_V_F32X4_MUL: {
       const char *ins = op == OP_V_F32X4_MUL ? "v_mul_f32_e32" : op == OP_V_F32X4_SUB ? "v_sub_f32_e32" : "v_add_f32_e32";
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, !e.nan_needed());
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], e.v(a + k), e.v(b + k));
       e.nan_fix({{r[0], "", "", a, b}, {r[1], "", "", a + 1, b + 1}, {r[2], "", "", a + 2, b + 2},
                  {r[3], "", "", a + 3, b + 3}}, 32);
@@ -722,7 +727,7 @@ bool emit(Em &e, const DInstr &I) {
     }
     case OP_V_F64X2_ADD: case OP_V_F64X2_SUB: case OP_V_F64X2_MUL: {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, true);
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, true, !e.nan_needed());
       const std::string res[2] = {e.dstp[0], e.dstp[1]};
       for (int k = 0; k < 2; k++) {
         const char *x = e.src64(a + 2 * k, A0, A1, AP), *y = e.src64(b + 2 * k, B0, B1, BP);
@@ -737,7 +742,7 @@ bool emit(Em &e, const DInstr &I) {
     case OP_V_F32X4_LE: case OP_V_F32X4_GE: {
       static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, true);
       for (int q = 0; q < 4; q++) {
         e.l("v_cmp_%s_f32_e32 vcc, %s, %s", k[op - OP_V_F32X4_EQ], e.v(a + q), e.v(b + q));
         e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[q]);
@@ -749,7 +754,7 @@ bool emit(Em &e, const DInstr &I) {
     case OP_V_F64X2_LE: case OP_V_F64X2_GE: {
       static const char *const k[] = {"eq", "neq", "lt", "gt", "le", "ge"};
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, true);
       for (int q = 0; q < 2; q++) {
         const char *x = e.src64(a + 2 * q, A0, A1, AP), *y = e.src64(b + 2 * q, B0, B1, BP);
         e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
@@ -761,7 +766,7 @@ bool emit(Em &e, const DInstr &I) {
     }
     case OP_V_BITSELECT: {   // (a & d) | (b & ~d) per bit: v_bfi_b32(d, a, b)
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, d, d + 1, d + 2, d + 3, c, c + 1, c + 2, c + 3});
-      const char *const *r = e.res128(c, {{a, 4}, {b, 4}, {d, 4}});
+      const char *const *r = e.res128(c, {{a, 4}, {b, 4}, {d, 4}}, false, true);
       for (int k = 0; k < 4; k++) e.l("v_bfi_b32 %s, %s, %s, %s", r[k], e.v(d + k), e.v(a + k), e.v(b + k));
       e.put128(c, r);
       return true;
@@ -771,7 +776,7 @@ bool emit(Em &e, const DInstr &I) {
       const char *ins = op == OP_V_I32X4_SHL ? "v_lshlrev_b32_e32" : op == OP_V_I32X4_SHR_U ? "v_lshrrev_b32_e32"
                                                                                          : "v_ashrrev_i32_e32";
       e.l("v_and_b32_e32 %s, 31, %s", Y0, e.v(b));
-      const char *const *r = e.res128(c, {{a, 4}});
+      const char *const *r = e.res128(c, {{a, 4}}, false, true);
       for (int k = 0; k < 4; k++) e.l("%s %s, %s, %s", ins, r[k], Y0, e.v(a + k));
       e.put128(c, r);
       return true;
@@ -781,7 +786,7 @@ bool emit(Em &e, const DInstr &I) {
       const char *ins = op == OP_V_I64X2_SHL ? "v_lshlrev_b64" : op == OP_V_I64X2_SHR_U ? "v_lshrrev_b64"
                                                                                      : "v_ashrrev_i64";
       e.l("v_and_b32_e32 %s, 63, %s", Y0, e.v(b));
-      const char *const *r = e.res128(c, {{a, 4}}, true);
+      const char *const *r = e.res128(c, {{a, 4}}, true, true);
       (void)r;
       const std::string res[2] = {e.dstp[0], e.dstp[1]};
       for (int k = 0; k < 2; k++) {
