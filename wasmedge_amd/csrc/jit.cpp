@@ -242,6 +242,10 @@ struct Em {
   struct NanItem { std::string lo, hi, pair; uint32_t a, b; };
   std::string tail;   // out-of-line code of the run (placed after it)
   int nfix = 0;
+  // A run that starts with a POST_CALL (restoring cells) and ends with a RET reads the
+  // RET's return record together with the restored cells (one LDS wait instead of two):
+  // ret_pf asks POST_CALL to issue it into v113, ret_pf_done tells RET it is there
+  bool ret_pf = false, ret_pf_done = false;
   const std::vector<uint8_t> *nanobs = nullptr;   // nan_observable(), per pc
   bool nan_needed() const { return !(nanobs && pc < nanobs->size() && !(*nanobs)[pc]); }
   void nan_fix(const std::vector<NanItem> &items, int w) {
@@ -843,6 +847,11 @@ bool emit(Em &e, const DInstr &I) {
         e.l("v_subrev_u32_e32 v102, %u, v102", L - fb);
         e.l("v_lshl_add_u32 %s, v102, 8, v103", X0);
         for (uint32_t k = 0; k < L - fb; k++) e.l("ds_read_b32 %s, %s offset:%u", e.v(fb + k), X0, k * 256u);
+        if (e.ret_pf) {   // the run's RET record, one slot below the restored cells
+          e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X0);
+          e.l("ds_read_b32 v113, %s", X1);
+          e.ret_pf_done = true;
+        }
         e.l("s_waitcnt lgkmcnt(0)");
       }
       return true;
@@ -1505,10 +1514,14 @@ std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
   const uint32_t a = I.w1 & 0xFFFFu, nres = I.w1 >> 16, fb = e.fb;
   e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
   const std::string out = e.leave_if_t2();
-  e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
-  e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
-  e.l("ds_read_b32 %s, %s", Y1, X1);
-  e.l("s_waitcnt lgkmcnt(0)");
+  if (e.ret_pf_done) {
+    e.l("v_mov_b32 %s, v113", Y1);
+  } else {
+    e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+    e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
+    e.l("ds_read_b32 %s, %s", Y1, X1);
+    e.l("s_waitcnt lgkmcnt(0)");
+  }
   e.l("v_readfirstlane_b32 s68, %s", Y1);
   e.l("s_nop 1");
   e.l("v_cmp_ne_u32_e64 %s, s68, %s", T2, Y1);
@@ -2491,6 +2504,14 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
   e.l("s_cbranch_execz %s", e.stage_end.c_str());
 }
 
+// a run whose RET record POST_CALL may read along (Em::ret_pf): first a POST_CALL that
+// restores cells, last a RET (nothing in between moves the call stack)
+bool ret_prefetch_run(const Program &P, const JitRun &r) {
+  if (r.len < 2) return false;
+  const DInstr &f = P.code[r.pc], &l = P.code[r.pc + r.len - 1];
+  return op_of(f) == OP_POST_CALL && (f.w1 & 0xFFFFu) > P.global_cells && op_of(l) == OP_RET;
+}
+
 // hybrid: only the trips' code (Ltin, the trip loop, the runs' stages, the exits), for
 // jit_source's SIMT code object, whose Lsched sends diverged waves to Ltin; a trip after
 // which every lane is at one pc goes back to Lsched (SIMT scheduling, direct run-to-run
@@ -2559,6 +2580,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   const bool sched_on = !(getenv("WB_JIT_SCHED") && getenv("WB_JIT_SCHED")[0] == '0');
   const bool nob_on = !(getenv("WB_NANOBS") && getenv("WB_NANOBS")[0] == '0');
   const std::vector<uint8_t> nob = nob_on ? nan_observable(P) : std::vector<uint8_t>();
+  const bool ret_pf_on = !(getenv("WB_RET_PF") && getenv("WB_RET_PF")[0] == '0');
   for (uint32_t k = 0; k < nr && split_on; k++) {
     const JitRun &r = runs[k];
     const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
@@ -2681,6 +2703,10 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       Em e;
       e.trip = true;
       if (!nob.empty()) e.nanobs = &nob;
+      if (ret_pf_on && ret_prefetch_run(P, r)) {   // (POST_CALL in stage A: RET reads v113 in B)
+        e.ret_pf = true;
+        e.ret_pf_done = st == 1 && split[k] > 0;
+      }
       e.g = glog;
       e.fb = P.global_cells;
       e.prog = &P;
@@ -2758,10 +2784,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           const uint32_t a = last.w1 & 0xFFFFu, nres = last.w1 >> 16, fb = e.fb;
           e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
           e.leave_if_t2();
-          e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
-          e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
-          e.l("ds_read_b32 %s, %s", Y1, X1);
-          e.l("s_waitcnt lgkmcnt(0)");
+          if (e.ret_pf_done) {
+            e.l("v_mov_b32 %s, v113", Y1);
+          } else {
+            e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
+            e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
+            e.l("ds_read_b32 %s, %s", Y1, X1);
+            e.l("s_waitcnt lgkmcnt(0)");
+          }
           e.l("v_and_b32_e32 %s, 0xfffff, %s", X0, Y1);
           e.l("v_cmp_eq_u32_e32 vcc, 0xfffff, %s", X0);
           e.l("s_mov_b64 %s, vcc", T2);
@@ -2918,11 +2948,21 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     jobs.push_back({k, 1});
     jobs.push_back({size_t(post), 2});
   }
+  // runs an inlined call returns into (past their POST_CALL: Lpa) never read their RET
+  // record along with the POST_CALL (Em::ret_pf), which that path skips
+  std::vector<uint8_t> inl_target(runs.size(), 0);
+  for (size_t k = 0; k < runs.size(); k++) {
+    int64_t f, post;
+    inline_of(k, &f, &post);
+    if (post >= 0) inl_target[size_t(post)] = 1;
+  }
+  const bool ret_pf_on = !(getenv("WB_RET_PF") && getenv("WB_RET_PF")[0] == '0');
   for (size_t jb = 0; jb < jobs.size(); jb++) {
     const size_t k = jobs[jb].first;
     const int var = jobs[jb].second;
     const JitRun &r = runs[k];
     Em e;
+    e.ret_pf = ret_pf_on && !cost && !inl_target[k] && ret_prefetch_run(P, r);
     e.g = glog;
     e.run = uint32_t(k + size_t(var) * 2 * runs.size());   // (stub labels apart)
     const std::string K = std::to_string(k) + (var == 1 ? "c" : var == 2 ? "p" : "");
