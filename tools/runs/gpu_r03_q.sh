@@ -12,5 +12,7 @@ step c5 200 python bench.py --workload c5 --instances 262144 --steps 5 --warmup 
 step c1 200 python bench.py --workload c1 --steps 2 --warmup 1 --cpu-seconds 4
 step c1_nopf 200 env WB_RET_PF=0 python bench.py --workload c1 --steps 2 --warmup 1 --no-cpu-baseline
 step c3_4k 200 python bench.py --workload c3 --elements 4096 --steps 2 --warmup 1 --no-cpu-baseline
+step c3_4k_dup 200 env WB_TRIP_DUP=1 python bench.py --workload c3 --elements 4096 --steps 2 --warmup 1 --no-cpu-baseline
+step c4_dup 200 env WB_TRIP_DUP=1 python bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline
 step c2 200 python bench.py --no-cpu-baseline
 for f in $O/c*.log; do echo $f $(grep -h '"metric"' $f | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('%.3g'%d['value'], '%.3f'%d['ms_per_step'])" 2>/dev/null); done
