@@ -60,6 +60,16 @@ __global__ void kbench(const uint32_t *buf, uint64_t *out) {
   T("s_load_dwordx8 s[20:27], %0, 0x0\n s_waitcnt lgkmcnt(0)", :: "s"(buf) : "s20","s21","s22","s23","s24","s25","s26","s27")
   // 21: v_readfirstlane x4 then s_and on the last
   T("v_readfirstlane_b32 s20, v40\n v_readfirstlane_b32 s21, v41\n v_readfirstlane_b32 s22, v42\n v_readfirstlane_b32 s23, v43\n s_and_b32 s24, s20, s23", ::: "s20","s21","s22","s23","s24")
+  // 22: v_cmp -> s_and exec -> s_cbranch_scc0 not taken (a compiled branch's lane test)
+  T("v_cmp_le_i32_e32 vcc, 2, v41\n s_and_b64 s[20:21], vcc, exec\n s_cbranch_scc0 4f\n4:", ::: "s20","s21","vcc")
+  // 23: readfirstlane + nop + v_cmp_ne + s_and + cbranch (the return record's uniformity test)
+  T("v_readfirstlane_b32 s20, v40\n s_nop 1\n v_cmp_ne_u32_e64 s[22:23], s20, v40\n s_and_b64 s[22:23], s[22:23], exec\n s_cbranch_scc1 5f\n5:", ::: "s20","s22","s23")
+  // 24: 12 independent SALU (issue rate of a transfer's scalar checks)
+  T("s_add_u32 s20, s20, 4\n s_cmp_ge_u32 s20, s21\n s_cmp_le_u32 s22, s23\n s_cselect_b32 s24, s23, s24\n s_cmp_ge_u32 s22, s24\n s_add_u32 s25, s22, 0x20\n s_cmp_ge_u32 s25, s24\n s_mov_b32 s26, 0x60\n s_mov_b32 s27, 0x60\n s_mov_b32 s28, 0x60\n s_mov_b32 s29, 0x60\n s_mov_b32 s30, 0x60", ::: "s20","s21","s22","s23","s24","s25","s26","s27","s28","s29","s30")
+  // 25: v_cmp -> s_and exec -> s_cbranch taken to the next line
+  T("v_cmp_le_i32_e32 vcc, 0, v41\n s_and_b64 s[20:21], vcc, exec\n s_cbranch_scc1 6f\n s_nop 0\n6:", ::: "s20","s21","vcc")
+  // 26: DPP min step pair (s_nop 1 + v_min_u32_dpp), the scheduler's wave reduction
+  T("s_nop 1\n v_min_u32_dpp v40, v40, v40 row_shr:1 row_mask:0xf bank_mask:0xf", ::: "v40")
 }
 
 int main() {
@@ -71,14 +81,15 @@ int main() {
     "s_cmp+cbranch not taken", "getpc+add+addc+setpc", "readfirstlane->s_add", "global_load_x4+wait",
     "2x(s_load_x2+wait)", "ds_read x2+wait+v_add+ds_write", "v_add addr + ds_read + wait",
     "s_and+s_lshr", "2x s_mov_b64", "s_cmp+cbranch taken", "ds_write_b32", "s_load_x8+wait",
-    "4x readfirstlane + s_and"};
+    "4x readfirstlane + s_and", "v_cmp+s_and+cbranch nt", "rfl+nop+v_cmp_ne+s_and+cbr",
+    "12 SALU (transfer checks)", "v_cmp+s_and+cbranch taken", "s_nop1 + v_min_dpp"};
   for (int it = 0; it < 3; it++) {
     hipLaunchKernelGGL(kbench, dim3(1), dim3(64), 0, 0, buf, out);
     hipDeviceSynchronize();
   }
   uint64_t h[64];
   hipMemcpy(h, out, sizeof h, hipMemcpyDeviceToHost);
-  for (int i = 0; i < 22; i++)
+  for (int i = 0; i < 27; i++)
     printf("%2d %-34s %8.1f cyc/rep (memtime ticks)\n", i, names[i], (double)(h[i] - h[0]) / 64.0);
   // the memtime clock rate
   int rate = 0; hipDeviceGetAttribute(&rate, hipDeviceAttributeClockRate, 0);

@@ -303,12 +303,20 @@ struct Em {
   // is set
   std::string leave_if_t2() {
     if (trip) return trip_leave();
-    const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(stubs.size());
+    const std::string lab = leave_stub();
     l("s_and_b64 %s, %s, exec", T2, T2);
     l("s_cbranch_scc1 %s", lab.c_str());
+    return lab;
+  }
+  // a leave stub before instruction pc without a test here (the caller branches to it)
+  std::string leave_stub() {
+    const std::string lab = "Lx" + std::to_string(run) + "_" + std::to_string(stubs.size());
     stubs.push_back(Stub{lab, pc, done, cdone});
     return lab;
   }
+  // A run that starts with a POST_CALL and ends with a CALL checks the call stack once at
+  // its start, for the deeper of the two (jit_source): both instructions skip their own
+  bool call_checked = false;
   // Trip mode (jit_source): the lanes of T2 leave alone, before instruction pc -- each
   // records it as its pc (VPC v92) with the instructions the run retired before it (VCNT
   // v93), no longer runs in this trip (TPC v98 = -1) and waits outside the trips as an
@@ -839,8 +847,10 @@ bool emit(Em &e, const DInstr &I) {
       const uint32_t L = a, r = b, fb = e.fb;
       if (L < e.fb || uint64_t(L) + r > TC_VF_CELLS) return false;
       e.drain();
-      e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);   // call stack slots past LDS: the C++ step
-      e.leave_if_t2();
+      if (!e.call_checked) {
+        e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);   // call stack slots past LDS: the C++ step
+        e.leave_if_t2();
+      }
       for (uint32_t k = r; k-- > 0;)
         if (L != fb) e.l("v_mov_b32 %s, %s", e.v(L + k), e.v(fb + k));
       if (L > fb) {
@@ -1492,9 +1502,11 @@ std::vector<uint8_t> dead_zeros(const Program &P, const JitRun &r) {
 void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *dead) {
   const uint32_t L = I.w1 & 0xFFFFu, nargs = I.w1 >> 16, nloc = I.w2 & 0xFFFFu, fb = e.fb;
   const uint32_t n = L - fb;
-  e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
-  e.l("v_cmp_lt_u32_e64 %s, s93, %s", T2, X0);   // would pass the LDS part: the C++ step
-  e.leave_if_t2();
+  if (!e.call_checked) {
+    e.l("v_add_u32_e32 %s, %u, v102", X0, n + 1);
+    e.l("v_cmp_lt_u32_e64 %s, s93, %s", T2, X0);   // would pass the LDS part: the C++ step
+    e.leave_if_t2();
+  }
   e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
   for (uint32_t k = 0; k < n; k++) e.l("ds_write_b32 %s, %s offset:%u", X1, e.v(fb + k), k * 256u);
   e.l("v_mov_b32 %s, 0x%x", Y1, ((pc + 1) & 0xFFFFFu) | (L << 20));
@@ -1510,26 +1522,33 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *
 // not be the entry frame's), results a.. -> fb.., jump to the return pc.
 // split: (SIMT) where the lanes' return records disagree, go there (Y1 = the records);
 // else leave before the return. Returns the leave stub's label.
+// One test decides the common case: a lane whose call stack reaches past its LDS part
+// reads its record as ~0 (an entry-frame record: it leaves), and an entry-frame record in
+// the first lane counts as a disagreement, so a single branch takes every exception to
+// `split` (which leaves for entry-frame records) or to the leave stub. (An LDS read past
+// the allocation returns 0 and cannot fault; the record of such a lane is discarded.)
 std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
   const uint32_t a = I.w1 & 0xFFFFu, nres = I.w1 >> 16, fb = e.fb;
-  e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
-  const std::string out = e.leave_if_t2();
+  const std::string out = e.leave_stub();
   if (e.ret_pf_done) {
-    e.l("v_mov_b32 %s, v113", Y1);
+    e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
+    e.l("v_cndmask_b32_e64 %s, v113, -1, vcc", Y1);
   } else {
     e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
     e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
     e.l("ds_read_b32 %s, %s", Y1, X1);
+    e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
     e.l("s_waitcnt lgkmcnt(0)");
+    e.l("v_cndmask_b32_e64 %s, %s, -1, vcc", Y1, Y1);
   }
   e.l("v_readfirstlane_b32 s68, %s", Y1);
   e.l("s_nop 1");
   e.l("v_cmp_ne_u32_e64 %s, s68, %s", T2, Y1);
-  e.l("s_and_b64 %s, %s, exec", T2, T2);
-  e.l("s_cbranch_scc1 %s", split.empty() ? out.c_str() : split.c_str());
   e.l("s_and_b32 s68, s68, 0xfffff");
   e.l("s_cmp_eq_u32 s68, 0xfffff");
-  e.l("s_cbranch_scc1 %s", out.c_str());
+  e.l("s_cselect_b64 %s, exec, %s", T2, T2);
+  e.l("s_and_b64 %s, %s, exec", T2, T2);
+  e.l("s_cbranch_scc1 %s", split.empty() ? out.c_str() : split.c_str());
   e.l("v_subrev_u32_e32 v102, 1, v102");
   for (uint32_t k = 0; k < nres; k++)
     if (a != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(a + k));
@@ -1673,6 +1692,12 @@ void long_jump(Em &e, const std::string &to, const std::string &tag) {
   e.l("LJMP %s %s", to.c_str(), tag.c_str());
 }
 
+// conditional form: to label `to` when SCC is 1 (s_cbranch_scc1 when near, else around
+// a long jump)
+void cond_jump(Em &e, const std::string &to, const std::string &tag) {
+  e.l("LJCC %s %s", to.c_str(), tag.c_str());
+}
+
 std::string resolve_jumps(const std::string &body) {
   std::vector<std::string> lines;
   for (size_t at = 0; at < body.size();) {
@@ -1689,6 +1714,7 @@ std::string resolve_jumps(const std::string &body) {
     const std::string &ln = lines[i];
     uint64_t b = 12;
     if (ln.empty() || ln[0] == '.') b = ln.compare(0, 8, ".p2align") == 0 ? 64 : 0;
+    if (ln.compare(0, 5, "LJMP ") == 0 || ln.compare(0, 5, "LJCC ") == 0) b = 48;   // (the long form)
     if (!ln.empty() && ln.back() == ':') { lab[ln.substr(0, ln.size() - 1)] = i; b = 0; }
     pos[i + 1] = pos[i] + b;
   }
@@ -1696,7 +1722,8 @@ std::string resolve_jumps(const std::string &body) {
   out.reserve(body.size() + body.size() / 4);
   for (size_t i = 0; i < lines.size(); i++) {
     const std::string &ln = lines[i];
-    if (ln.compare(0, 5, "LJMP ") != 0) { out += ln; out += '\n'; continue; }
+    const bool cc = ln.compare(0, 5, "LJCC ") == 0;
+    if (ln.compare(0, 5, "LJMP ") != 0 && !cc) { out += ln; out += '\n'; continue; }
     const size_t sp = ln.find(' ', 5);
     const std::string to = ln.substr(5, sp - 5), tag = ln.substr(sp + 1);
     auto it = lab.find(to);
@@ -1704,7 +1731,13 @@ std::string resolve_jumps(const std::string &body) {
                                        : (pos[it->second] > pos[i] ? pos[it->second] - pos[i]
                                                                     : pos[i] - pos[it->second]);
     if (d < 100000) {
-      out += "s_branch " + to + "\n";
+      out += (cc ? "s_cbranch_scc1 " : "s_branch ") + to + "\n";
+    } else if (cc) {
+      out += "s_cbranch_scc0 " + tag + "_n\n";
+      out += "s_getpc_b64 s[68:69]\n" + tag + ":\n";
+      out += "s_add_u32 s68, s68, " + to + " - " + tag + "\n";
+      out += "s_addc_u32 s69, s69, (" + to + " - " + tag + ") >> 32\n";
+      out += "s_setpc_b64 s[68:69]\n" + tag + "_n:\n";
     } else {
       out += "s_getpc_b64 s[68:69]\n" + tag + ":\n";
       out += "s_add_u32 s68, s68, " + to + " - " + tag + "\n";
@@ -3020,6 +3053,29 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_or_b64 %s, %s, vcc", T2, T2);
       e.leave_if_t2();
     }
+    // POST_CALL ... CALL: one call-stack check at the start for both (the POST_CALL pops
+    // `pop` slots, the CALL pushes n + 1), leaving before the run when either would.
+    // Not where an inlined call enters past the POST_CALL (Lpa), nor for an inlined CALL.
+    {
+      int64_t f0 = -1, p0 = -1;
+      inline_of(k, &f0, &p0);
+      const DInstr &first = P.code[r.pc];
+      const uint32_t fbc = P.global_cells;
+      if (!scan && !inl_target[k] && f0 < 0 && lop == OP_CALL && r.len >= 2 &&
+          op_of(first) == OP_POST_CALL && (first.w1 & 0xFFFFu) >= fbc &&
+          (last.w1 & 0xFFFFu) >= fbc) {
+        const uint32_t pop = (first.w1 & 0xFFFFu) - fbc, push = (last.w1 & 0xFFFFu) - fbc + 1;
+        e.pc = r.pc;
+        if (push > pop) {
+          e.l("v_add_u32_e32 %s, %u, v102", X0, push - pop);
+          e.l("v_cmp_lt_u32_e64 %s, s93, %s", T2, X0);
+        } else {
+          e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);
+        }
+        e.leave_if_t2();
+        e.call_checked = true;
+      }
+    }
     std::string extra;   // SIMT split code, placed after the run
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
@@ -3093,10 +3149,36 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.l("s_cmp_ge_u32 s62, s63");
       e.l("s_cbranch_scc1 %s", xs.c_str());
     };
+    // The common case of a transfer to pc `to` that starts a compiled run, in one branch:
+    // (taken) the count limit is not reached, and after the re-aim that run stops short of
+    // OTHER -- the jump goes straight there; else the full checks below (go, taken_checks)
+    // run as before. `lim`: the limit is already in s68 (budget ? OTHER : 0) -- a return's
+    // shared prefix, see below.
+    int nfast = 0;
+    auto fast_to = [&](uint32_t to, bool taken, bool lim) {
+      auto it = start.find(to);
+      if (it == start.end()) return;
+      const uint32_t tend = (to + runs[it->second].len - 1) * 32u;
+      const std::string tl = "Lb" + std::to_string(it->second) +
+                             (var == 2 && loop_of.count(k) && loop_of[k] == it->second ? "c" : "");
+      if (lim) {
+        e.l("s_cmp_gt_u32 s68, 0x%x", tend);
+      } else if (taken) {
+        e.l("s_cmp_ge_u32 s95, 0x%x", to * 32u);   // to <= LOW: re-aim OTHER
+        e.l("s_cselect_b32 s63, s95, s63");
+        e.l("s_cmp_lt_u32 s65, s64");
+        e.l("s_cselect_b32 s68, s63, 0");
+        e.l("s_cmp_gt_u32 s68, 0x%x", tend);
+      } else {
+        e.l("s_cmp_gt_u32 s63, 0x%x", tend);
+      }
+      cond_jump(e, tl, "Lf" + K + "_" + std::to_string(nfast++));
+    };
     auto fallthrough = [&](uint32_t cnt) {   // next(): stop at the lowest waiting pc
       e.gas_add(c_fall);
       e.l("s_mov_b32 s62, 0x%x", fall * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", cnt);
+      fast_to(fall, false, false);
       e.l("s_cmp_ge_u32 s62, s63");
       e.l("s_cbranch_scc1 %s", xs.c_str());
       go(fall, preload);
@@ -3331,6 +3413,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.gas_add(c_fall);
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+      fast_to(tgt, true, false);
       taken_checks();
       go(tgt, preload);
     } else if (lop == OP_RET) {
@@ -3357,19 +3440,34 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       }
       e.gas_add(c_fall);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
-      taken_checks();
       // straight into the code after a known call site of this function, else dispatch
       std::vector<uint32_t> sites;
       const int64_t f = func_of(e.pc);
       if (f >= 0)
         for (uint32_t rs : ret_sites[uint32_t(f)])
           if (start.count(rs) && sites.size() < 6) sites.push_back(rs);
+      // the fast way: re-aim, s68 = the limit (budget ? OTHER : 0), then per known site
+      // one compare against the site's run end (fast_to)
+      if (!sites.empty()) {
+        e.l("s_cmp_le_u32 s62, s95");
+        e.l("s_cselect_b32 s63, s95, s63");
+        e.l("s_cmp_lt_u32 s65, s64");
+        e.l("s_cselect_b32 s68, s63, 0");
+        for (size_t q = 0; q < sites.size(); q++) {
+          e.l("s_cmp_eq_u32 s62, 0x%x", sites[q] * 32u);
+          e.l("s_cbranch_scc1 Lrf%s_%zu", K.c_str(), q);
+        }
+      }
+      taken_checks();
       for (size_t q = 0; q < sites.size(); q++) {
         e.l("s_cmp_eq_u32 s62, 0x%x", sites[q] * 32u);
         e.l("s_cbranch_scc1 Lrt%s_%zu", K.c_str(), q);
       }
       go(~0u, false);
       for (size_t q = 0; q < sites.size(); q++) {
+        e.l("Lrf%s_%zu:", K.c_str(), q);
+        fast_to(sites[q], true, true);
+        taken_checks();
         e.l("Lrt%s_%zu:", K.c_str(), q);
         go(sites[q], false);
       }
@@ -3468,6 +3566,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.gas_add(uint64_t(int64_t(c_fall) + c_adj));
       e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", taken_cnt);
+      fast_to(tgt, true, false);
       taken_checks();
       go(tgt, false);
       if (lop != OP_JMP) {
