@@ -16,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -1750,8 +1751,8 @@ std::string resolve_jumps(const std::string &body) {
 
 // min over the lanes of `mask` (an SGPR pair) of VPC into SGPR `dst` (~0 when none);
 // EXEC = all 64 lanes on entry and exit
-void wave_min_vpc(Em &e, const char *mask, const char *dst) {
-  e.l("v_cndmask_b32_e64 %s, -1, %s, %s", X0, VPC, mask);
+void wave_min_of(Em &e, const char *mask, const char *src, const char *dst) {
+  e.l("v_cndmask_b32_e64 %s, -1, %s, %s", X0, src, mask);
   static const char *const steps[6] = {"row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf",
                                        "row_shr:4 row_mask:0xf", "row_shr:8 row_mask:0xf",
                                        "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"};
@@ -1763,12 +1764,13 @@ void wave_min_vpc(Em &e, const char *mask, const char *dst) {
   e.l("v_readlane_b32 %s, %s, 63", dst, X0);
   e.l("s_nop 1");
 }
+void wave_min_vpc(Em &e, const char *mask, const char *dst) { wave_min_of(e, mask, VPC, dst); }
 
 // The scheduler's pick: the lanes of `mask` (ALL, or another SGPR pair: trip mode's
 // lanes outside the trips) at their lowest pc are the group, OTHER/LOW = the lowest pc of
 // the other lanes in ALL, the handler banks of the matching mode, and the group's TInstr
 // is dispatched. `p`: label prefix (Lsc for Lsched).
-void sched_block(Em &e, const std::string &p, const char *mask) {
+void sched_block(Em &e, const std::string &p, const char *mask, bool depth = false) {
   // every pick costs 16 of the budget as well: the core returns to the kernel (limits,
   // interrupts) even if the lanes retired nothing
   e.l("s_sub_u32 s64, s64, 16");
@@ -1844,6 +1846,80 @@ void sched_block(Em &e, const std::string &p, const char *mask) {
     e.l("s_setpc_b64 s[68:69]");
     return;
   }
+  if (!mask && depth) {
+    // Recursive modules (jit_source: depth_pick): the group is every lane at the pc of the
+    // lane lowest in its call stack (fewest stack slots; ties: the lowest pc). LOW = the
+    // lowest waiting pc, OTHER = the lowest waiting pc above the group's (= LOW when the
+    // group is the lowest): the group runs on until it reaches OTHER or jumps to or below
+    // LOW, so it follows its lanes' calls and returns past lanes waiting lower in the
+    // function instead of stopping at them -- lanes in different parts of their call trees
+    // meet at the pcs where the others wait (C1: 1.43 -> 1.04 group runs per run of the
+    // slowest lane in a model of its traces, tools/fib_probe.py)
+    e.l("s_mov_b64 exec, -1");
+    e.l("s_waitcnt lgkmcnt(0)");   // (a TInstr prefetch must land: s[76:77] is a temp here)
+    e.l("s_nop 4");
+    e.l("v_min_u32_e32 %s, 0xfff, v102", X1);
+    e.l("v_lshl_or_b32 %s, %s, 20, %s", X1, X1, VPC);
+    e.l("s_nop 1");
+    wave_min_of(e, "s[96:97]", X1, "s68");
+    e.l("s_and_b32 s68, s68, 0xfffff");                  // the group's pc
+    e.l("s_lshl_b32 s62, s68, 5");
+    e.l("v_cmp_eq_u32_e64 s[74:75], s68, %s", VPC);
+    e.l("s_and_b64 s[74:75], s[74:75], s[96:97]");       // the group: ALL at that pc
+    e.l("s_cmp_eq_u32 s95, -1");                         // were the banks converged?
+    e.l("s_cselect_b32 s69, 1, 0");
+    e.l("s_andn2_b64 vcc, s[96:97], s[74:75]");          // the lanes left waiting
+    e.l("s_cbranch_vccz %s_conv", p.c_str());
+    wave_min_vpc(e, "vcc", "s63");                       // LOW (a pc)
+    e.l("s_cmp_gt_u32 s63, s68");
+    e.l("s_cbranch_scc1 %s_ol", p.c_str());
+    e.l("s_lshl_b32 s95, s63, 5");
+    e.l("v_cmp_lt_u32_e64 s[76:77], s68, %s", VPC);
+    e.l("s_and_b64 s[76:77], s[76:77], vcc");            // waiting above the group's pc
+    wave_min_vpc(e, "s[76:77]", "s63");                  // OTHER (~0: none)
+    e.l("s_cmp_eq_u32 s63, -1");
+    e.l("s_cbranch_scc1 %s_od", p.c_str());
+    e.l("s_lshl_b32 s63, s63, 5");
+    e.l("s_branch %s_od", p.c_str());
+    e.l("%s_ol:", p.c_str());
+    e.l("s_lshl_b32 s63, s63, 5");
+    e.l("s_mov_b32 s95, s63");
+    e.l("%s_od:", p.c_str());
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+    e.l("s_cmp_eq_u32 s69, 0");
+    e.l("s_cbranch_scc1 %s_disp", p.c_str());
+    e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
+    e.l("s_addc_u32 s71, s71, 0");
+    e.l("s_branch %s_bankb", p.c_str());
+    e.l("%s_conv:", p.c_str());
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
+    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
+    e.l("s_mov_b32 s63, -1");
+    e.l("s_mov_b32 s95, -1");
+    e.l("s_cmp_eq_u32 s69, 1");
+    e.l("s_cbranch_scc1 %s_disp", p.c_str());
+    e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
+    e.l("s_subb_u32 s71, s71, 0");
+    e.l("%s_bankb:", p.c_str());
+    e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
+    e.l("s_addc_u32 s73, s71, 0");
+    e.l("%s_disp:", p.c_str());
+    e.l("s_mov_b64 exec, s[74:75]");
+    e.l("s_cmp_eq_u32 s64, 0");                          // budget spent: to the kernel
+    e.l("s_cbranch_scc1 %s_out", p.c_str());
+    e.l("s_waitcnt lgkmcnt(0)");
+    e.l("s_add_u32 s68, s70, s76");
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    e.l("%s_out:", p.c_str());
+    e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
+    e.l("s_addc_u32 s69, s71, 0");
+    e.l("s_setpc_b64 s[68:69]");
+    return;
+  }
   e.l("s_mov_b64 exec, -1");
   if (mask) e.l("s_mov_b64 s[74:75], %s", mask);   // (the TInstr load below overwrites s[76:91])
   e.l("s_nop 4");
@@ -1904,7 +1980,7 @@ void sched_block(Em &e, const std::string &p, const char *mask) {
 // hybrid (trip mode beside SIMT scheduling, jit_source): a wave whose lanes are not all at
 // one pc goes to the trips (Ltin) instead of picking a group; the trips come back here
 // once every lane is at one pc again.
-std::string simt_sched(bool hybrid) {
+std::string simt_sched(bool hybrid, bool depth) {
   Em e;
   e.l(".p2align 6");
   e.l("Lmerge:");
@@ -1922,7 +1998,7 @@ std::string simt_sched(bool hybrid) {
     long_jump(e, "Ltin", "Lsc_tq");
     e.l("Lsc_one:");
   }
-  sched_block(e, "Lsc", nullptr);
+  sched_block(e, "Lsc", nullptr, depth);
   return e.o;
 }
 
@@ -2883,6 +2959,42 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   return src;
 }
 
+// Whether a function can reach itself through calls: a cycle among direct calls (CALL,
+// TAIL_CALL), or any indirect call (its targets are not known here)
+bool recursive(const Program &P) {
+  std::map<uint32_t, uint32_t> fentry;   // entry pc -> function
+  for (uint32_t f = 0; f < P.funcs.size(); f++)
+    if (!P.funcs[f].imported) fentry[P.funcs[f].entry_pc] = f;
+  auto func_of = [&](uint32_t pc) -> int64_t {
+    auto it = fentry.upper_bound(pc);
+    return it == fentry.begin() ? -1 : int64_t(std::prev(it)->second);
+  };
+  const size_t nf = P.funcs.size();
+  std::vector<std::vector<uint32_t>> g(nf);
+  for (uint32_t pc = 0; pc < P.code.size(); pc++) {
+    const uint16_t o = op_of(P.code[pc]);
+    if (o == OP_CALL_INDIRECT || o == OP_TAIL_CALL_INDIRECT) return true;
+    if (o != OP_CALL && o != OP_TAIL_CALL) continue;
+    const int64_t a = func_of(pc), b = func_of(P.code[pc].w3);
+    if (a < 0 || b < 0) continue;
+    if (a == b) return true;
+    g[size_t(a)].push_back(uint32_t(b));
+  }
+  std::vector<uint8_t> st(nf, 0);   // 0 new, 1 on the path, 2 done
+  std::function<bool(uint32_t)> dfs = [&](uint32_t f) -> bool {
+    st[f] = 1;
+    for (uint32_t t : g[f]) {
+      if (st[t] == 1) return true;
+      if (st[t] == 0 && dfs(t)) return true;
+    }
+    st[f] = 2;
+    return false;
+  };
+  for (uint32_t f = 0; f < nf; f++)
+    if (st[f] == 0 && dfs(f)) return true;
+  return false;
+}
+
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost, bool simt, bool trip) {
   if (cost) simt = false;
@@ -2909,7 +3021,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           "s_mov_b32 %0, s6\ns_mov_b32 %1, s7\n"
           "s_getpc_b64 s[8:9]\nLpe:\ns_add_u32 s8, s8, Lend - Lpe\ns_addc_u32 s9, s9, 0\n"
           "s_setpc_b64 s[8:9]\n";
-  if (simt) body += simt_sched(hybrid);
+  // Recursive modules pick groups by call-stack height first (sched_block); their split
+  // branches go through that pick too (the pc-only shortcut, Lbf, would undo it).
+  // WB_DEPTH=0: pc-only picks everywhere (A/B aid)
+  const bool depth_pick = simt && !(getenv("WB_DEPTH") && getenv("WB_DEPTH")[0] == '0') &&
+                          recursive(P);
+  if (simt) body += simt_sched(hybrid, depth_pick);
   // run index by start pc: a transfer to one jumps straight to its code
   std::map<uint32_t, size_t> start;
   for (size_t k = 0; k < runs.size(); k++) start[runs[k].pc] = k;
@@ -3527,7 +3644,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
           x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
           flush(x);
-          if (fall != tgt && !hybrid) {   // (hybrid: every split goes to Lsched, hence the trips)
+          if (fall != tgt && !hybrid && !depth_pick) {   // (hybrid: every split goes to Lsched, hence the trips)
             // No waiting lane at or below the nearer destination `lo`: the lanes going
             // there are the next group, those going to `hi` wait, and the lowest waiting
             // pc becomes min(LOW, hi) -- a pick without the wave reductions of Lsched
