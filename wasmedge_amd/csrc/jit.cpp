@@ -3293,9 +3293,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     };
     auto fallthrough = [&](uint32_t cnt) {   // next(): stop at the lowest waiting pc
       e.gas_add(c_fall);
-      e.l("s_mov_b32 s62, 0x%x", fall * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", cnt);
       fast_to(fall, false, false);
+      e.l("s_mov_b32 s62, 0x%x", fall * 32u);
       e.l("s_cmp_ge_u32 s62, s63");
       e.l("s_cbranch_scc1 %s", xs.c_str());
       go(fall, preload);
@@ -3528,9 +3528,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
       emit_call(e, last, e.pc, dead.empty() ? nullptr : &dead);
       e.gas_add(c_fall);
-      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       fast_to(tgt, true, false);
+      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       taken_checks();
       go(tgt, preload);
     } else if (lop == OP_RET) {
@@ -3570,6 +3570,21 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         e.l("s_cselect_b32 s63, s95, s63");
         e.l("s_cmp_lt_u32 s65, s64");
         e.l("s_cselect_b32 s68, s63, 0");
+        // the limit clears every site's run (converged: always): straight to the site
+        uint32_t maxend = 0;
+        std::vector<std::string> tls;
+        for (uint32_t rs : sites) {
+          const size_t ri = start[rs];
+          maxend = std::max(maxend, (rs + runs[ri].len - 1) * 32u);
+          tls.push_back("Lb" + std::to_string(ri) + (var == 2 && loop_of.count(k) && loop_of[k] == ri ? "c" : ""));
+        }
+        e.l("s_cmp_gt_u32 s68, 0x%x", maxend);
+        e.l("s_cbranch_scc0 Lrg%s", K.c_str());
+        for (size_t q = 0; q < sites.size(); q++) {
+          e.l("s_cmp_eq_u32 s62, 0x%x", sites[q] * 32u);
+          cond_jump(e, tls[q], "Lrj" + K + "_" + std::to_string(q));
+        }
+        e.l("Lrg%s:", K.c_str());
         for (size_t q = 0; q < sites.size(); q++) {
           e.l("s_cmp_eq_u32 s62, 0x%x", sites[q] * 32u);
           e.l("s_cbranch_scc1 Lrf%s_%zu", K.c_str(), q);
@@ -3681,9 +3696,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         }
       }
       e.gas_add(uint64_t(int64_t(c_fall) + c_adj));
-      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       e.l("s_add_u32 s65, s65, 0x%x", taken_cnt);
       fast_to(tgt, true, false);
+      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
       taken_checks();
       go(tgt, false);
       if (lop != OP_JMP) {
