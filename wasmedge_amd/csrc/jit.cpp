@@ -3949,3 +3949,12 @@ extern "C" __attribute__((visibility("default"))) int wb_trip_choice(const uint8
   if (!wb::load_program(wasm, len, P, &ec).empty()) return -1;
   return P.divergent_mem || wb::trips_pay(P) ? 1 : 0;
 }
+
+// TEST hook (tests/test_depth_pick.py, CPU): whether the module counts as recursive for the
+// depth-keyed SIMT pick (wb::recursive). 1 / 0, or -1 when it fails to load.
+extern "C" __attribute__((visibility("default"))) int wb_recursive(const uint8_t *wasm, uint32_t len) {
+  wb::Program P;
+  uint8_t ec = 0;
+  if (!wb::load_program(wasm, len, P, &ec).empty()) return -1;
+  return wb::recursive(P) ? 1 : 0;
+}
