@@ -318,6 +318,9 @@ struct Em {
   // A run that starts with a POST_CALL and ends with a CALL checks the call stack once at
   // its start, for the deeper of the two (jit_source): both instructions skip their own
   bool call_checked = false;
+  // the run's POST_CALL checked the call stack at its start: a RET later in the run pops
+  // below that, so it needs no check of its own
+  bool stack_ok = false;
   // Trip mode (jit_source): the lanes of T2 leave alone, before instruction pc -- each
   // records it as its pc (VPC v92) with the instructions the run retired before it (VCNT
   // v93), no longer runs in this trip (TPC v98 = -1) and waits outside the trips as an
@@ -852,6 +855,7 @@ bool emit(Em &e, const DInstr &I) {
         e.l("v_cmp_lt_u32_e64 %s, s93, v102", T2);   // call stack slots past LDS: the C++ step
         e.leave_if_t2();
       }
+      e.stack_ok = !e.trip;
       for (uint32_t k = r; k-- > 0;)
         if (L != fb) e.l("v_mov_b32 %s, %s", e.v(L + k), e.v(fb + k));
       if (L > fb) {
@@ -1528,10 +1532,16 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *
 // the first lane counts as a disagreement, so a single branch takes every exception to
 // `split` (which leaves for entry-frame records) or to the leave stub. (An LDS read past
 // the allocation returns 0 and cannot fault; the record of such a lane is discarded.)
-std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
+// known: up to two (return record, label) pairs: where every lane's record is the same
+// known one the group goes straight to that label (the records of a function's direct call
+// sites are constants), before the agreement test.
+std::string emit_ret(Em &e, const DInstr &I, const std::string &split,
+                     const std::vector<std::pair<uint32_t, std::string>> &known = {}) {
   const uint32_t a = I.w1 & 0xFFFFu, nres = I.w1 >> 16, fb = e.fb;
   const std::string out = e.leave_stub();
-  if (e.ret_pf_done) {
+  if (e.ret_pf_done && e.stack_ok) {
+    e.l("v_mov_b32 %s, v113", Y1);
+  } else if (e.ret_pf_done) {
     e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
     e.l("v_cndmask_b32_e64 %s, v113, -1, vcc", Y1);
   } else {
@@ -1541,6 +1551,19 @@ std::string emit_ret(Em &e, const DInstr &I, const std::string &split) {
     e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
     e.l("s_waitcnt lgkmcnt(0)");
     e.l("v_cndmask_b32_e64 %s, %s, -1, vcc", Y1, Y1);
+  }
+  if (!known.empty()) {
+    if (known.size() > 1) e.l("v_mov_b32 %s, 0x%x", X0, known[1].first);
+    e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", known[0].first, Y1);
+    if (known.size() > 1) e.l("v_cmp_eq_u32_e64 s[68:69], %s, %s", X0, Y1);
+    e.l("s_and_b64 vcc, vcc, exec");
+    e.l("s_cmp_eq_u64 vcc, exec");
+    e.l("s_cbranch_scc1 %s", known[0].second.c_str());
+    if (known.size() > 1) {
+      e.l("s_and_b64 s[68:69], s[68:69], exec");
+      e.l("s_cmp_eq_u64 s[68:69], exec");
+      e.l("s_cbranch_scc1 %s", known[1].second.c_str());
+    }
   }
   e.l("v_readfirstlane_b32 s68, %s", Y1);
   e.l("s_nop 1");
@@ -3534,7 +3557,22 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       taken_checks();
       go(tgt, preload);
     } else if (lop == OP_RET) {
-      const std::string rout = emit_ret(e, last, (sx & 2) ? "Lrs" + K : std::string());
+      // a return's likely targets: the instruction after each direct call of its function
+      std::vector<uint32_t> sites;
+      const int64_t f = func_of(e.pc);
+      if (f >= 0)
+        for (uint32_t rs : ret_sites[uint32_t(f)])
+          if (start.count(rs) && sites.size() < 6) sites.push_back(rs);
+      // the first two sites' return records are constants: a group whose lanes all hold one
+      // of them goes straight to Lrk<K>_<q> (below)
+      std::vector<std::pair<uint32_t, std::string>> known;
+      for (size_t q = 0; q < sites.size() && q < 2 && !cost; q++) {
+        const DInstr &cl = P.code[sites[q] - 1];
+        const uint32_t L = cl.w1 & 0xFFFFu;
+        if (op_of(cl) == OP_CALL && L < 4096)
+          known.push_back({(sites[q] & 0xFFFFFu) | (L << 20), "Lrk" + K + "_" + std::to_string(q)});
+      }
+      const std::string rout = emit_ret(e, last, (sx & 2) ? "Lrs" + K : std::string(), known);
       if (sx & 2) {
         // lanes returning to different places: each records its return pc and count
         // (unless one leaves the entry function: the C++ step finishes those) and the
@@ -3558,11 +3596,6 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       e.gas_add(c_fall);
       e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
       // straight into the code after a known call site of this function, else dispatch
-      std::vector<uint32_t> sites;
-      const int64_t f = func_of(e.pc);
-      if (f >= 0)
-        for (uint32_t rs : ret_sites[uint32_t(f)])
-          if (start.count(rs) && sites.size() < 6) sites.push_back(rs);
       // the fast way: re-aim, s68 = the limit (budget ? OTHER : 0), then per known site
       // one compare against the site's run end (fast_to)
       if (!sites.empty()) {
@@ -3601,6 +3634,19 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         fast_to(sites[q], true, true);
         taken_checks();
         e.l("Lrt%s_%zu:", K.c_str(), q);
+        go(sites[q], false);
+      }
+      // every lane returns to known site q: pop, results, then the transfer's checks
+      for (size_t q = 0; q < known.size(); q++) {
+        const uint32_t a = last.w1 & 0xFFFFu, nres = last.w1 >> 16, fb = e.fb;
+        e.l("%s:", known[q].second.c_str());
+        e.l("v_subrev_u32_e32 v102, 1, v102");
+        for (uint32_t c = 0; c < nres; c++)
+          if (a != fb) e.l("v_mov_b32 %s, %s", e.V(fb + c).c_str(), e.V(a + c).c_str());
+        e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+        fast_to(sites[q], true, false);
+        e.l("s_mov_b32 s62, 0x%x", sites[q] * 32u);
+        taken_checks();
         go(sites[q], false);
       }
     } else if (lop == OP_BR_TABLE) {
