@@ -318,6 +318,14 @@ struct Em {
   // A run that starts with a POST_CALL and ends with a CALL checks the call stack once at
   // its start, for the deeper of the two (jit_source): both instructions skip their own
   bool call_checked = false;
+  // cells holding a splat of an f64 inline constant that was never materialized (jit_source
+  // fold_consts): the f64x2 ops reading them take the constant itself
+  std::map<uint32_t, std::string> kfold;
+  bool fuse_any = false;   // V_ANY_TRUE leaves its OR in R0 only (its cell is dead)
+  const char *kf(uint32_t c) const {
+    auto it = kfold.find(c);
+    return it == kfold.end() ? nullptr : it->second.c_str();
+  }
   // the run's POST_CALL checked the call stack at its start: a RET later in the run pops
   // below that, so it needs no check of its own
   bool stack_ok = false;
@@ -746,8 +754,11 @@ bool emit(Em &e, const DInstr &I) {
       const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, true, !e.nan_needed());
       const std::string res[2] = {e.dstp[0], e.dstp[1]};
       for (int k = 0; k < 2; k++) {
-        const char *x = e.src64(a + 2 * k, A0, A1, AP), *y = e.src64(b + 2 * k, B0, B1, BP);
+        const char *x = e.kf(a + 2 * k) ? e.kf(a + 2 * k) : e.src64(a + 2 * k, A0, A1, AP);
+        const char *y = e.kf(b + 2 * k) ? e.kf(b + 2 * k) : e.src64(b + 2 * k, B0, B1, BP);
         if (op == OP_V_F64X2_MUL) e.l("v_mul_f64 %s, %s, %s", res[k].c_str(), x, y);
+        else if (op == OP_V_F64X2_SUB && e.kf(b + 2 * k))   // (a folded constant: negate it)
+          e.l("v_add_f64 %s, %s, %s", res[k].c_str(), x, y[0] == '-' ? y + 1 : ("-" + std::string(y)).c_str());
         else e.l("v_add_f64 %s, %s, %s%s", res[k].c_str(), x, op == OP_V_F64X2_SUB ? "-" : "", y);
       }
       e.nan_fix({{r[0], r[1], res[0], a, b}, {r[2], r[3], res[1], a + 2, b + 2}}, 64);
@@ -772,7 +783,8 @@ bool emit(Em &e, const DInstr &I) {
       e.sync({a, a + 1, a + 2, a + 3, b, b + 1, b + 2, b + 3, c, c + 1, c + 2, c + 3});
       const char *const *r = e.res128(c, {{a, 4}, {b, 4}}, false, true);
       for (int q = 0; q < 2; q++) {
-        const char *x = e.src64(a + 2 * q, A0, A1, AP), *y = e.src64(b + 2 * q, B0, B1, BP);
+        const char *x = e.kf(a + 2 * q) ? e.kf(a + 2 * q) : e.src64(a + 2 * q, A0, A1, AP);
+        const char *y = e.kf(b + 2 * q) ? e.kf(b + 2 * q) : e.src64(b + 2 * q, B0, B1, BP);
         e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
         e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[2 * q]);
         e.l("v_mov_b32 %s, %s", r[2 * q + 1], r[2 * q]);
@@ -816,6 +828,7 @@ bool emit(Em &e, const DInstr &I) {
       e.sync({a, a + 1, a + 2, a + 3, c});
       e.l("v_or3_b32 %s, %s, %s, %s", R0, e.v(a), e.v(a + 1), e.v(a + 2));
       e.l("v_or_b32_e32 %s, %s, %s", R0, R0, e.v(a + 3));
+      if (e.fuse_any) return true;   // (jit_source: the branch after it tests R0 itself)
       e.l("v_cmp_ne_u32_e32 vcc, 0, %s", R0);
       e.l("v_cndmask_b32_e64 %s, 0, 1, vcc", e.v(c));
       return true;
@@ -2198,7 +2211,10 @@ bool written_exact(const DInstr &I, std::vector<uint32_t> *out) {
 // observable and kill nothing; calls, host calls and tail calls make every cell
 // observable; globals always are (the host reads them after a trap or an interrupt).
 // Returns per pc: 1 = the instruction's result may be observed.
-std::vector<uint8_t> nan_observable(const Program &P) {
+// live (non-null): plain liveness instead -- every source of a result is live when the
+// instruction runs (float compares and truncations included, their operands taken 4 cells
+// wide), and *live receives the cells live before each pc (bit sets of total_cells() + 8)
+std::vector<uint8_t> nan_observable(const Program &P, std::vector<std::vector<uint64_t>> *live = nullptr) {
   const size_t n = P.code.size();
   const uint32_t nc = P.total_cells() + 8;   // (+8: 4-wide over-approximations stay in range)
   const size_t W = (nc + 63) / 64;
@@ -2352,8 +2368,9 @@ std::vector<uint8_t> nan_observable(const Program &P) {
           const bool used = any(after, dst[0], dst[1]);
           if (dst[1]) res[pc] = used ? 1 : 0;
           kill(s, dst[0], dst[1]);
-          if (kind == PROP && used)
+          if (kind == PROP && (used || live))
             for (auto &x : src) put(s, x[0], x[1]);
+          if (kind == HIDE && live) { put(s, a, 4); put(s, b, 4); }
         } else if (is_store_op(op)) {   // the address and the stored bits
           put(s, a, 1);
           put(s, b, std::max(1u, mem_bytes(op) / 4));
@@ -2380,6 +2397,7 @@ std::vector<uint8_t> nan_observable(const Program &P) {
       }
     }
   }
+  if (live) *live = before;
   // (debugging aid: WB_NANOBS_LIST=<file> writes per pc the flag and the cells observable
   // before it)
   if (const char *lst = getenv("WB_NANOBS_LIST"))
@@ -2982,6 +3000,143 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   return src;
 }
 
+// ---------------------------------------------------------------- constant folding
+// Cells read and written by the instructions the planner below lets stand between a fold
+// and its uses: plain register ops that never leave the compiled code (no memory, no
+// traps, no calls). Returns false for anything else.
+bool pure_cells(const DInstr &I, std::vector<uint32_t> *rd, std::vector<uint32_t> *wr) {
+  const uint16_t op = op_of(I);
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu;
+  auto R = [&](uint32_t x, uint32_t n) { for (uint32_t k = 0; k < n; k++) rd->push_back(x + k); };
+  auto W = [&](uint32_t x, uint32_t n) { for (uint32_t k = 0; k < n; k++) wr->push_back(x + k); };
+  switch (op) {
+    case OP_V_F64X2_ADD: case OP_V_F64X2_SUB: case OP_V_F64X2_MUL: case OP_V_F64X2_EQ:
+    case OP_V_F64X2_NE: case OP_V_F64X2_LT: case OP_V_F64X2_GT: case OP_V_F64X2_LE:
+    case OP_V_F64X2_GE: case OP_V_I64X2_ADD: case OP_V_I64X2_SUB: case OP_V_I64X2_EQ:
+      R(a, 4); R(b, 4); W(c, 4); return true;
+    case OP_V_F64X2_SPLAT: case OP_V_I64X2_SPLAT: R(a, 2); W(c, 4); return true;
+    case OP_V_ANY_TRUE: R(a, 4); W(c, 1); return true;
+    case OP_V_EXTRACT64: R(a, 4); W(c, 2); return true;
+    case OP_V_REPLACE64: R(a, 4); R(b, 2); W(c, 4); return true;
+    case OP_CONST32: W(c, 1); return true;
+    case OP_CONST64: W(c, 2); return true;
+    case OP_CONST128: W(c, 4); return true;
+    case OP_MOV32: R(a, 1); W(c, 1); return true;
+    case OP_MOV64: R(a, 2); W(c, 2); return true;
+    case OP_MOV128: R(a, 4); W(c, 4); return true;
+    case OP_I32_ADD: case OP_I32_SUB: case OP_I32_AND: case OP_I32_OR: case OP_I32_XOR:
+      R(a, 1); R(b, 1); W(c, 1); return true;
+    case OP_I32_ADD_I: case OP_I32_SUB_I: case OP_I32_SHL_I: R(a, 1); W(c, 1); return true;
+    case OP_I64_EXTEND_I32_U: case OP_F64_CONVERT_I32_U: case OP_F64_CONVERT_I32_S:
+      R(a, 1); W(c, 2); return true;
+    default: return false;
+  }
+}
+
+// The f64 inline constants of a VOP3 operand (0 is left out: -0.0 is not one of them)
+const char *f64_inline(uint64_t v) {
+  switch (v) {
+    case 0x3FE0000000000000ull: return "0.5";
+    case 0xBFE0000000000000ull: return "-0.5";
+    case 0x3FF0000000000000ull: return "1.0";
+    case 0xBFF0000000000000ull: return "-1.0";
+    case 0x4000000000000000ull: return "2.0";
+    case 0xC000000000000000ull: return "-2.0";
+    case 0x4010000000000000ull: return "4.0";
+    case 0xC010000000000000ull: return "-4.0";
+    default: return nullptr;
+  }
+}
+
+// Per run: `CONST64 X, k; V_F64X2_SPLAT X -> X` where k is an inline constant and every
+// later read of X..X+3 in the run is an f64x2 add/sub/mul/compare taking X as a whole
+// operand (and whose NaN payload is never observed) is not materialized: those ops take
+// k itself. X..X+3 must be written again later in the run or be dead where the run goes
+// on (live: plain liveness, nan_observable), and nothing between the splat and the last
+// use can leave the compiled code. C5: the 4.0 and 2.0 of its iteration (8 moves).
+struct FoldPlan {
+  std::vector<uint8_t> skip;                    // body index: not emitted
+  std::map<uint32_t, std::vector<std::pair<uint32_t, std::string>>> at;   // body index -> (cell, constant)
+};
+FoldPlan plan_folds(const Program &P, const JitRun &r, uint32_t nbody,
+                    const std::vector<std::vector<uint64_t>> &live, const std::vector<uint8_t> &nob,
+                    const std::vector<LoadBatch> &batches) {
+  FoldPlan fp;
+  fp.skip.assign(r.len, 0);
+  if (live.empty()) return fp;
+  const DInstr &last = P.code[r.pc + r.len - 1];
+  const uint16_t lop = op_of(last);
+  std::vector<uint32_t> succ;
+  if (nbody == r.len) succ.push_back(r.pc + r.len);
+  else if (lop == OP_JMP) succ.push_back(last.w3);
+  else if (is_branch_op(lop)) { succ.push_back(r.pc + r.len); succ.push_back(last.w3); }
+  else return fp;   // (calls, returns, br_table: no folds)
+  auto live_at = [&](uint32_t pc, uint32_t c) {
+    return pc >= live.size() || (live[pc][c >> 6] >> (c & 63) & 1);
+  };
+  for (uint32_t i = 0; i + 1 < nbody; i++) {
+    const DInstr &I = P.code[r.pc + i], &J = P.code[r.pc + i + 1];
+    if (op_of(I) != OP_CONST64 || op_of(J) != OP_V_F64X2_SPLAT) continue;
+    const uint32_t X = I.w2 & 0xFFFFu;
+    if ((J.w1 & 0xFFFFu) != X || (J.w2 & 0xFFFFu) != X || uint64_t(X) + 4 > P.total_cells()) continue;
+    const char *txt = f64_inline(uint64_t(I.w3) | (uint64_t(I.w1) << 32));
+    if (!txt) continue;
+    bool inbatch = false;
+    for (const auto &b : batches) inbatch = inbatch || (b.i0 <= i + 1 && i < b.i1);
+    if (inbatch) continue;
+    std::vector<uint32_t> uses;
+    bool ok = true, redefined = false;
+    std::vector<uint8_t> cov(4, 0);   // cells of X..X+3 written again so far
+    for (uint32_t j = i + 2; j < r.len && ok && !redefined; j++) {
+      const DInstr &K = P.code[r.pc + j];
+      const uint16_t ko = op_of(K);
+      std::vector<uint32_t> rd, wr;
+      if (j + 1 == r.len && nbody < r.len) {   // the run's branch
+        const uint32_t ka = K.w1 & 0xFFFFu, kb = K.w1 >> 16;
+        if (ko != OP_JMP && ka >= X && ka < X + 4 && !cov[ka - X]) ok = false;
+        if (ko >= OP_BR_EQ && ko <= OP_BR_GE_U && kb >= X && kb < X + 4 && !cov[kb - X]) ok = false;
+        break;
+      }
+      if (!pure_cells(K, &rd, &wr)) { ok = false; break; }
+      const uint32_t ka = K.w1 & 0xFFFFu, kb = K.w1 >> 16, kc = K.w2 & 0xFFFFu;
+      bool reads = false;   // (of a cell of X..X+3 still holding the constant)
+      for (uint32_t x : rd) reads = reads || (x >= X && x < X + 4 && !cov[x - X]);
+      bool overlap_w = false;
+      for (uint32_t x : wr) overlap_w = overlap_w || (x >= X && x < X + 4);
+      const bool arith = ko == OP_V_F64X2_ADD || ko == OP_V_F64X2_SUB || ko == OP_V_F64X2_MUL;
+      const bool cmp = ko >= OP_V_F64X2_EQ && ko <= OP_V_F64X2_GE;
+      const bool partly = cov[0] || cov[1] || cov[2] || cov[3];
+      if (reads && partly) { ok = false; break; }
+      if (reads) {
+        const bool whole = (ka == X || kb == X) && !(ka != X && ka + 4 > X && ka < X + 4) &&
+                           !(kb != X && kb + 4 > X && kb < X + 4);
+        const bool quiet = !nob.empty() && r.pc + j < nob.size() && !nob[r.pc + j];
+        // (a use whose result lands on X itself, in place, is the last: X is written again)
+        if (!whole || (overlap_w && kc != X) || !((arith && quiet) || cmp)) { ok = false; break; }
+        uses.push_back(j);
+        if (overlap_w) redefined = true;
+        continue;
+      }
+      if (overlap_w) {
+        for (uint32_t x : wr) if (x >= X && x < X + 4) cov[x - X] = 1;
+        if (cov[0] && cov[1] && cov[2] && cov[3]) redefined = true;
+      }
+    }
+    if (!ok || uses.empty()) continue;
+    if (!redefined)
+      for (uint32_t t : succ)
+        for (uint32_t q = 0; q < 4; q++) ok = ok && (cov[q] || !live_at(t, X + q));
+    if (!ok) continue;
+    fp.skip[i] = fp.skip[i + 1] = 1;
+    for (uint32_t j : uses) {
+      fp.at[j].push_back({X, txt});
+      fp.at[j].push_back({X + 2, txt});
+    }
+    i++;
+  }
+  return fp;
+}
+
 // Whether a function can reach itself through calls: a cycle among direct calls (CALL,
 // TAIL_CALL), or any indirect call (its targets are not known here)
 bool recursive(const Program &P) {
@@ -3028,6 +3183,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // NaN fixes only where the payload can be observed (WB_NANOBS=0: everywhere)
   const bool nob_on = !(getenv("WB_NANOBS") && getenv("WB_NANOBS")[0] == '0');
   const std::vector<uint8_t> nob = nob_on ? nan_observable(P) : std::vector<uint8_t>();
+  // plain cell liveness (constant folds, fused any_true); WB_FOLD=0 turns both off
+  std::vector<std::vector<uint64_t>> live;
+  if (!(getenv("WB_FOLD") && getenv("WB_FOLD")[0] == '0')) nan_observable(P, &live);
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
@@ -3225,6 +3383,22 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const std::vector<LoadBatch> batches = batching ? load_batches(P, r, nbody, lead)
                                                     : std::vector<LoadBatch>();
     size_t nb = 0;
+    const FoldPlan fp = plan_folds(P, r, nbody, live, nob, batches);
+    // an any_true that only feeds the run's br_if / br_unless (its cell dead where the run
+    // goes on): the branch tests the OR of the vector's words itself (SIMT: a split stays in
+    // the compiled code, so nothing outside reads the cell)
+    uint32_t fuse_cell = ~0u;
+    if ((sx & 1) && !cost && nbody >= 1 && nbody < r.len && !live.empty() &&
+        (lop == OP_BR_IF || lop == OP_BR_UNLESS) && !fp.skip[nbody - 1]) {
+      const DInstr &A = P.code[r.pc + nbody - 1];
+      const uint32_t C = A.w2 & 0xFFFFu;
+      bool inb = false;
+      for (const auto &b : batches) inb = inb || (b.i0 <= nbody - 1 && nbody - 1 < b.i1);
+      auto lv = [&](uint32_t pc) { return pc >= live.size() || (live[pc][C >> 6] >> (C & 63) & 1); };
+      if (op_of(A) == OP_V_ANY_TRUE && (last.w1 & 0xFFFFu) == C && !inb &&
+          !lv(r.pc + r.len) && !lv(last.w3))
+        fuse_cell = C;
+    }
     for (uint32_t i = 0; i < nbody; i++) {
       if (nb < batches.size() && batches[nb].i0 == i) {
         const LoadBatch &b = batches[nb++];
@@ -3237,9 +3411,21 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
         continue;
       }
       const DInstr &I = P.code[r.pc + i];
+      if (fp.skip[i]) {   // a folded constant: counted, never materialized
+        e.done += (I.w0 >> 16) & 0xFFu;
+        if (cost) e.cdone += cost->full(P, r.pc + i);
+        continue;
+      }
       e.pc = r.pc + i;
       e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
-      if (!emit(e, I)) return "";   // jit_runs only picks compilable instructions
+      auto fit = fp.at.find(i);
+      if (fit != fp.at.end())
+        for (const auto &kv : fit->second) e.kfold[kv.first] = kv.second;
+      e.fuse_any = fuse_cell != ~0u && i + 1 == nbody;
+      const bool ok_emit = emit(e, I);
+      e.kfold.clear();
+      e.fuse_any = false;
+      if (!ok_emit) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
       if (cost) e.cdone += cost->full(P, r.pc + i);
       // an inlined call goes on here, after the POST_CALL it makes unnecessary
@@ -3687,7 +3873,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const uint32_t taken_cnt = uint32_t(int32_t(r.cnt) + tcnt);   // (cnt + tcnt >= 0)
       const std::string nt = "Lnt" + K;
       if (lop != OP_JMP) {
+        if (fuse_cell != ~0u) {   // (the fused any_true's OR is in R0)
+          e.alias_cell = int64_t(fuse_cell);
+          e.alias_reg = 114;
+        }
         branch_cond(e, last);
+        e.alias_cell = -1;
         e.l("s_and_b64 %s, vcc, exec", T2);
         e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
         e.l("s_cmp_eq_u64 %s, exec", T2);
