@@ -322,6 +322,10 @@ struct Em {
   // fold_consts): the f64x2 ops reading them take the constant itself
   std::map<uint32_t, std::string> kfold;
   bool fuse_any = false;   // V_ANY_TRUE leaves its OR in R0 only (its cell is dead)
+  // an f64x2 compare whose mask only an (also fused) any_true reads for the run's branch:
+  // the compare leaves the per-lane "any element true" mask in VCC (s[68:69] holds the
+  // first element's) and the any_true emits nothing
+  bool cmp_any = false;
   const char *kf(uint32_t c) const {
     auto it = kfold.find(c);
     return it == kfold.end() ? nullptr : it->second.c_str();
@@ -785,11 +789,13 @@ bool emit(Em &e, const DInstr &I) {
       for (int q = 0; q < 2; q++) {
         const char *x = e.kf(a + 2 * q) ? e.kf(a + 2 * q) : e.src64(a + 2 * q, A0, A1, AP);
         const char *y = e.kf(b + 2 * q) ? e.kf(b + 2 * q) : e.src64(b + 2 * q, B0, B1, BP);
-        e.l("v_cmp_%s_f64_e64 vcc, %s, %s", k[op - OP_V_F64X2_EQ], x, y);
-        e.l("v_cndmask_b32_e64 %s, 0, -1, vcc", r[2 * q]);
+        const char *m = e.cmp_any && q == 0 ? "s[68:69]" : "vcc";
+        e.l("v_cmp_%s_f64_e64 %s, %s, %s", k[op - OP_V_F64X2_EQ], m, x, y);
+        e.l("v_cndmask_b32_e64 %s, 0, -1, %s", r[2 * q], m);
         e.l("v_mov_b32 %s, %s", r[2 * q + 1], r[2 * q]);
       }
       e.put128(c, r);
+      if (e.cmp_any) e.l("s_or_b64 vcc, vcc, s[68:69]");   // lanes with any element true
       return true;
     }
     case OP_V_BITSELECT: {   // (a & d) | (b & ~d) per bit: v_bfi_b32(d, a, b)
@@ -825,6 +831,7 @@ bool emit(Em &e, const DInstr &I) {
       return true;
     }
     case OP_V_ANY_TRUE:
+      if (e.cmp_any) return true;   // (the compare before it left the lane mask in VCC)
       e.sync({a, a + 1, a + 2, a + 3, c});
       e.l("v_or3_b32 %s, %s, %s, %s", R0, e.v(a), e.v(a + 1), e.v(a + 2));
       e.l("v_or_b32_e32 %s, %s, %s", R0, R0, e.v(a + 3));
@@ -3186,6 +3193,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // plain cell liveness (constant folds, fused any_true); WB_FOLD=0 turns both off
   std::vector<std::vector<uint64_t>> live;
   if (!(getenv("WB_FOLD") && getenv("WB_FOLD")[0] == '0')) nan_observable(P, &live);
+  // (WB_CMPANY=1: an f64x2 compare feeding a fused any_true hands its lane masks to the
+  // branch; opt-in until measured)
+  const bool cmp_any_on = getenv("WB_CMPANY") && getenv("WB_CMPANY")[0] == '1';
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
@@ -3399,6 +3409,16 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           !lv(r.pc + r.len) && !lv(last.w3))
         fuse_cell = C;
     }
+    // ... and the f64x2 compare right before it whose mask it reads: the branch takes the
+    // compare's lane masks (WB_FOLD=0 turns this off with the rest)
+    bool cmp_any = false;
+    if (fuse_cell != ~0u && nbody >= 2 && !fp.skip[nbody - 2] && cmp_any_on) {
+      const DInstr &Cm = P.code[r.pc + nbody - 2], &A = P.code[r.pc + nbody - 1];
+      const uint16_t co = op_of(Cm);
+      bool inb = false;
+      for (const auto &b : batches) inb = inb || (b.i0 <= nbody - 2 && nbody - 2 < b.i1);
+      cmp_any = co >= OP_V_F64X2_EQ && co <= OP_V_F64X2_GE && (Cm.w2 & 0xFFFFu) == (A.w1 & 0xFFFFu) && !inb;
+    }
     for (uint32_t i = 0; i < nbody; i++) {
       if (nb < batches.size() && batches[nb].i0 == i) {
         const LoadBatch &b = batches[nb++];
@@ -3422,9 +3442,11 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       if (fit != fp.at.end())
         for (const auto &kv : fit->second) e.kfold[kv.first] = kv.second;
       e.fuse_any = fuse_cell != ~0u && i + 1 == nbody;
+      e.cmp_any = cmp_any && i + 2 >= nbody;
       const bool ok_emit = emit(e, I);
       e.kfold.clear();
       e.fuse_any = false;
+      e.cmp_any = false;
       if (!ok_emit) return "";   // jit_runs only picks compilable instructions
       e.done += (I.w0 >> 16) & 0xFFu;
       if (cost) e.cdone += cost->full(P, r.pc + i);
@@ -3873,12 +3895,16 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const uint32_t taken_cnt = uint32_t(int32_t(r.cnt) + tcnt);   // (cnt + tcnt >= 0)
       const std::string nt = "Lnt" + K;
       if (lop != OP_JMP) {
-        if (fuse_cell != ~0u) {   // (the fused any_true's OR is in R0)
-          e.alias_cell = int64_t(fuse_cell);
-          e.alias_reg = 114;
+        if (cmp_any) {   // VCC = the lanes whose any_true is 1
+          if (lop == OP_BR_UNLESS) e.l("s_not_b64 vcc, vcc");
+        } else {
+          if (fuse_cell != ~0u) {   // (the fused any_true's OR is in R0)
+            e.alias_cell = int64_t(fuse_cell);
+            e.alias_reg = 114;
+          }
+          branch_cond(e, last);
+          e.alias_cell = -1;
         }
-        branch_cond(e, last);
-        e.alias_cell = -1;
         e.l("s_and_b64 %s, vcc, exec", T2);
         e.l("s_cbranch_scc0 %s", nt.c_str());    // no lane takes it
         e.l("s_cmp_eq_u64 %s, exec", T2);
