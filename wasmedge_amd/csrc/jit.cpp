@@ -3560,11 +3560,18 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const size_t body2 = ei.o.size();
       const bool fc = fwd && var == 1;   // the forwarding copy: the callee's loads from F
       int64_t renamed = -1;              // the stack cell computed into a word's VGPR
+      // constant-address stores in the copy (WB_CST_STORE=1, opt-in until measured; else
+      // through the cell, as the first trip); cst_win: the 4 KiB window whose base is in XP, or -1
+      const bool cst_store = getenv("WB_CST_STORE") && getenv("WB_CST_STORE")[0] == '1';
+      int64_t cst_win = -1;
       std::vector<std::pair<uint32_t, uint32_t>> deferred;   // (cell, VGPR) read, then written
       const std::vector<LoadBatch> batches2 = batching && !fc ? load_batches(P, rf, rf.len - 1, lead2)
                                                               : std::vector<LoadBatch>();
       size_t nb2 = 0;
+      bool prev_cst = false;
       for (uint32_t i = 0; i + 1 < rf.len; i++) {
+        if (!prev_cst) cst_win = -1;   // (XP is a temporary of every other instruction)
+        prev_cst = false;
         if (nb2 < batches2.size() && batches2[nb2].i0 == i) {
           const LoadBatch &b = batches2[nb2++];
           emit_batch(ei, P, rf.pc, b, groups2, lead2);
@@ -3627,7 +3634,30 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
             if (ei.group) group_base(ei, *ei.group);
             ei.group = nullptr;
           }
-          emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
+          if (fc && ei.g != 0 && cst_store) {
+            // the copy's store goes to a constant address: its granule row and byte are
+            // known here, so the address is MEM + a constant (an immediate offset when it
+            // fits, else one add per 4 KiB window, shared by the next stores)
+            const uint64_t A = uint64_t(fa), gb = 4ull << ei.g;
+            const uint64_t Lo = ((A >> (2 + ei.g)) << (8 + ei.g)) + (A & (gb - 1));
+            ei.drain();
+            if (Lo <= 4095) {
+              ei.l("global_store_dword %s, %s, off offset:%u", MEM, fr.c_str(), uint32_t(Lo));
+            } else {
+              const uint64_t hi = Lo & ~0xFFFull;
+              if (int64_t(hi) != cst_win) {
+                ei.l("v_add_co_u32_e32 %s, vcc, 0x%x, v106", X0, uint32_t(hi));
+                ei.l("v_addc_co_u32_e32 %s, vcc, 0x%x, v107, vcc", X1, uint32_t(hi >> 32));
+                cst_win = int64_t(hi);
+              }
+              ei.l("global_store_dword %s, %s, off offset:%u", XP, fr.c_str(), uint32_t(Lo - hi));
+            }
+            ei.nvm++;
+            prev_cst = true;
+          } else {
+            emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
+            cst_win = -1;
+          }
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
         }
