@@ -3193,9 +3193,9 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   // plain cell liveness (constant folds, fused any_true); WB_FOLD=0 turns both off
   std::vector<std::vector<uint64_t>> live;
   if (!(getenv("WB_FOLD") && getenv("WB_FOLD")[0] == '0')) nan_observable(P, &live);
-  // (WB_CMPANY=1: an f64x2 compare feeding a fused any_true hands its lane masks to the
-  // branch; opt-in until measured)
-  const bool cmp_any_on = getenv("WB_CMPANY") && getenv("WB_CMPANY")[0] == '1';
+  // an f64x2 compare feeding a fused any_true hands its lane masks to the branch (C5
+  // 1.435e13 -> 1.475e13, profiles/r03ab_bench.json; WB_CMPANY=0 turns it off)
+  const bool cmp_any_on = !(getenv("WB_CMPANY") && getenv("WB_CMPANY")[0] == '0');
   // which divergence events stay in the core (debug aid): 1 split branches, 2 split
   // returns, 4 reaching a waiting lane / the count limit (else the core leaves as without
   // SIMT)
