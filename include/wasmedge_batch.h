@@ -60,10 +60,13 @@ typedef struct WasmEdge_Result {
 #define WASMEDGE_BATCH_TAIL_CALL_HOST 0xB2u   /* return_call_indirect reached a host import */
 
 typedef struct WasmEdge_BatchConfigure {
-  /* Page budget per instance; plays RuntimeConfigure::MaxMemPage
-   * (include/common/configure.h:123). 0 = the module's declared maximum, else its
-   * initial size. memory.grow beyond it returns -1 exactly like the reference. A
-   * module whose initial size exceeds a non-zero budget fails WasmEdge_BatchCreate with
+  /* Page limit per instance: RuntimeConfigure::MaxMemPage (include/common/configure.h:
+   * 112-123; 0 = its default, 65536). memory.grow returns -1 past it, past the module's
+   * declared maximum and past 65536 pages, or when the device has no memory left for the
+   * new pages -- MemoryInstance::growPage (include/runtime/instance/memory.h:87-115) with
+   * Allocator::resize failing (lib/system/allocator.cpp:101-129). Pages are committed on
+   * demand, as the reference's mmap'd reservation is: see MemoryReservePages. A module
+   * whose initial size exceeds a non-zero limit fails WasmEdge_BatchCreate with
    * MemoryOutOfBounds (0x88): the reference allocates no memory for it (memory.h:46-51). */
   uint32_t MaxMemoryPage;
   /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
@@ -111,7 +114,45 @@ typedef struct WasmEdge_BatchConfigure {
    * device call stack. A return_call to a host import fails BatchCreate (0x02), and a
    * return_call_indirect that reaches one ends the instance with 0xB2. */
   uint32_t TailCall;
+  /* Layout of linear memory on the device (results never depend on it). The first
+   * MemoryReservePages pages of every instance are allocated up front in the lane-
+   * interleaved layout every execution path addresses directly; pages an instance grows
+   * past them are committed on demand in 4 MiB rows (the page for all 64 instances of a
+   * wave) and reached through a page table by the per-lane step, more slowly. 0 = the
+   * module's initial size, raised toward the page limit while the whole batch's
+   * reservation stays within min(16 GiB, a quarter of the device's free memory); modules
+   * without memory.grow reserve their initial size. Clamped to [initial size, limit]. */
+  uint32_t MemoryReservePages;
+  /* Cap on the device memory committed for grown pages (bytes; 0 = until hipMalloc fails).
+   * A grow that would need more returns -1. */
+  uint64_t MemoryPoolBytes;
 } WasmEdge_BatchConfigure;
+
+#ifdef WASMEDGE_C_API_H
+/* The reference's configuration object as a batch configuration (header-inline: needs the
+ * reference's wasmedge.h included first). It carries over what the reference's
+ * WasmEdge_ConfigureContext decides for the interpreter path: the page limit
+ * (WasmEdge_ConfigureGetMaxMemoryPage, wasmedge.h:560; RuntimeConfigure::MaxMemPage,
+ * configure.h:112-123) and the TailCall proposal (WasmEdge_ConfigureHasProposal,
+ * wasmedge.h:495; off by default, configure.h:176-182). The proposals on by default
+ * (SIMD, bulk memory, reference types, multi-value, sign extension, saturating
+ * conversions, mutable globals) are always on in the batched path; MultiMemories is
+ * refused at WasmEdge_BatchCreate. Statistics: instruction counts are always reported;
+ * cost metering is set through CostLimit / CostTable (the reference keeps those on its
+ * StatisticsContext). Fields this does not set keep the caller's values; a NULL Conf
+ * leaves the reference defaults (MaxMemoryPage 0 = 65536, TailCall off). */
+static inline void WasmEdge_BatchConfigureFromContext(const WasmEdge_ConfigureContext *Conf,
+                                                      WasmEdge_BatchConfigure *Out) {
+  if (!Out) return;
+  if (!Conf) {
+    Out->MaxMemoryPage = 0;
+    Out->TailCall = 0;
+    return;
+  }
+  Out->MaxMemoryPage = WasmEdge_ConfigureGetMaxMemoryPage(Conf);
+  Out->TailCall = WasmEdge_ConfigureHasProposal(Conf, WasmEdge_Proposal_TailCall) ? 1u : 0u;
+}
+#endif
 
 typedef struct WasmEdge_BatchContext WasmEdge_BatchContext;
 

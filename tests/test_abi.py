@@ -14,9 +14,11 @@ LIB = os.path.join(ROOT, "wasmedge_amd", "libwasmedge_batch.so")
 
 
 def declared():
+    """Entry points the library must export (header-inline helpers excluded)."""
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(WasmEdge_Batch[A-Za-z]+)\s*\(", src)))
+    inline = set(re.findall(r"static inline [^(]*\b(WasmEdge_Batch[A-Za-z]+)\s*\(", src))
+    return sorted(set(re.findall(r"\b(WasmEdge_Batch[A-Za-z]+)\s*\(", src)) - inline)
 
 
 def test_header_declares_api():
@@ -70,9 +72,9 @@ def test_ctypes_layouts_match_the_header(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "%s/include/wasmedge_batch.h"\n'
                    'int main(void) {\n'
-                   '  printf("%%zu %%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchConfigure),\n'
+                   '  printf("%%zu %%zu %%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchConfigure),\n'
                    '         offsetof(WasmEdge_BatchConfigure, CostTable), offsetof(WasmEdge_BatchConfigure, MemoryGranule),\n'
-                   '         offsetof(WasmEdge_BatchConfigure, HostThreads));\n'
+                   '         offsetof(WasmEdge_BatchConfigure, HostThreads), offsetof(WasmEdge_BatchConfigure, MemoryPoolBytes));\n'
                    '  printf("%%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchImport), offsetof(WasmEdge_BatchImport, Value),\n'
                    '         offsetof(WasmEdge_BatchImport, Mutable));\n'
                    '  printf("%%zu\\n", sizeof(WasmEdge_Value));\n'
@@ -81,7 +83,8 @@ def test_ctypes_layouts_match_the_header(tmp_path):
     subprocess.check_call(["gcc", "-o", str(exe), str(src)])
     got = [list(map(int, line.split())) for line in subprocess.check_output([str(exe)]).decode().splitlines()]
     C, I = b._Conf, b._Import
-    assert got[0] == [ctypes.sizeof(C), C.CostTable.offset, C.MemoryGranule.offset, C.HostThreads.offset]
+    assert got[0] == [ctypes.sizeof(C), C.CostTable.offset, C.MemoryGranule.offset, C.HostThreads.offset,
+                      C.MemoryPoolBytes.offset]
     assert got[1] == [ctypes.sizeof(I), I.Value.offset, I.Mutable.offset]
     assert got[2] == [ctypes.sizeof(b._Value)]
 

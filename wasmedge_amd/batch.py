@@ -59,7 +59,8 @@ class _Conf(ctypes.Structure):
                 ("DeviceOrdinal", ctypes.c_int32), ("CostLimit", ctypes.c_uint64),
                 ("HostThreads", ctypes.c_uint32), ("CostTable", ctypes.c_void_p),
                 ("CostTableLen", ctypes.c_uint32), ("MemoryGranule", ctypes.c_uint32),
-                ("TailCall", ctypes.c_uint32)]
+                ("TailCall", ctypes.c_uint32), ("MemoryReservePages", ctypes.c_uint32),
+                ("MemoryPoolBytes", ctypes.c_uint64)]
 
 
 class _String(ctypes.Structure):
@@ -218,16 +219,20 @@ class BatchContext:
 
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
-                 memory_granule=0, imports=None, tail_call=False):
+                 memory_granule=0, imports=None, tail_call=False, memory_reserve_pages=0,
+                 memory_pool_bytes=0):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
-        metering is on when cost_limit > 0."""
+        metering is on when cost_limit > 0. max_memory_page 0 = the reference's default
+        page limit (65536); memory_reserve_pages / memory_pool_bytes: the device layout of
+        grown memory (WasmEdge_BatchConfigure)."""
         L = lib()
         tab = None
         if cost_table is not None:
             tab = np.ascontiguousarray(cost_table, np.uint64)
         conf = _Conf(max_memory_page, call_stack_cells, max_steps, time_limit, device, cost_limit,
                      host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
-                     len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0)
+                     len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0,
+                     memory_reserve_pages, memory_pool_bytes)
         res = _Result(0)
         imps = imports or []
         arr = (_Import * max(1, len(imps)))()

@@ -16,15 +16,17 @@
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s);
-extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, uint32_t threads, size_t lds_bytes);
+extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t threads, size_t lds_bytes);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
                                          const uint32_t *ls, uint32_t ls_slots, uint32_t full,
                                          uint32_t g, hipStream_t s);
-extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
+extern "C" hipError_t wb_launch_mem_hash(uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
-                                         uint32_t mem_words, uint32_t n, uint32_t g, hipStream_t s);
+                                         uint32_t mem_words, uint32_t n, uint32_t g,
+                                         const uint64_t *ptab, uint32_t ptab_w, uint32_t max_pages,
+                                         hipStream_t s);
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
                                            uint32_t global_cells, uint32_t ls_slots,
                                            uint32_t init_pages, uint32_t init_dropped,
@@ -71,14 +73,34 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   (void)hipEventCreate(&C->ev0);
   (void)hipEventCreate(&C->ev1);
   hipStream_t s = C->stream;
-  // memory budget (RuntimeConfigure::MaxMemPage analogue)
-  uint32_t budget = C->conf.MaxMemoryPage;
-  if (budget == 0) budget = P.mem_has_max ? P.mem_max : P.mem_min;
-  if (P.mem_has_max && budget > P.mem_max) budget = P.mem_max;
-  if (budget < P.mem_min) budget = P.mem_min;
-  if (!P.has_mem) budget = 0;
-  C->mem_max_pages = budget;
-  C->mem_words = budget << 14;
+  C->nwaves = (C->n + 63) / 64;
+  // page limit (memory.h:88-115 growPage: 65536, the module's max, PageLimit = MaxMemPage,
+  // configure.h:123) and the reserved layout (DESIGN.md "Linear memory"): a module that
+  // never grows reserves its initial pages; one that does, more of its limit while the
+  // batch's reservation stays small, the rest committed on demand from the pool
+  uint32_t limit = 65536;
+  if (P.mem_has_max) limit = std::min(limit, P.mem_max);
+  if (C->conf.MaxMemoryPage) limit = std::min(limit, C->conf.MaxMemoryPage);
+  const bool grows = std::any_of(P.code.begin(), P.code.end(),
+                                 [](const DInstr &d) { return (d.w0 & 0x7FFFu) == OP_MEM_GROW; });
+  uint32_t reserve = P.mem_min;
+  if (grows && limit > P.mem_min) {
+    if (C->conf.MemoryReservePages) {
+      reserve = std::min(limit, std::max(P.mem_min, C->conf.MemoryReservePages));
+    } else {
+      size_t free_b = 0, total_b = 0;
+      (void)hipMemGetInfo(&free_b, &total_b);
+      const uint64_t budget = std::min<uint64_t>(uint64_t(16) << 30, free_b / 4);
+      const uint64_t per_lane = budget / (uint64_t(C->nwaves) * (uint64_t(64) << 16));
+      reserve = uint32_t(std::max<uint64_t>(P.mem_min, std::min<uint64_t>(limit, per_lane)));
+    }
+  }
+  if (!P.has_mem) reserve = limit = 0;
+  C->mem_max_pages = limit;
+  C->rpages = reserve;
+  C->mem_words = reserve << 14;
+  C->grow_host = grows && limit > reserve;
+  C->pt_n.assign(C->nwaves, 0);
   // interleave granule of the wave's linear memories (DESIGN.md "Linear memory"): 4-byte
   // words when the module's addresses are wave-uniform, wider granules (a lane's
   // consecutive words together) when they diverge per lane (Program::divergent_mem)
@@ -89,7 +111,6 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     return C->fail(kRuntimeError, "MemoryGranule must be 0 or a power of two in [4, 128]");
   C->mlog = uint32_t(__builtin_ctz(gb)) - 2;
   C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
-  C->nwaves = (C->n + 63) / 64;
   // module image: active data segments over the initial pages
   std::vector<uint32_t> img;
   std::vector<uint8_t> pool;
@@ -257,7 +278,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
       (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
-      (P.n_imported && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
+      ((P.n_imported || C->grow_host) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
@@ -313,6 +334,10 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.mlog = C->mlog;
   k.init_pages = P.mem_min;
   k.mem_max_pages = C->mem_max_pages;
+  k.rpages = C->rpages;
+  k.ptab = C->pt_w ? C->ptab.ptr : nullptr;
+  k.ptab_w = C->pt_w;
+  k.grow_host = C->grow_host ? 1u : 0u;
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
   k.init_dropped = C->init_dropped;
@@ -345,7 +370,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   if (C->cap_threads != wpb * 64 || C->cap_lds != wave_lds * wpb + 256) {
     C->cap_threads = wpb * 64;
     C->cap_lds = wave_lds * wpb + 256;
-    C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, C->cap_threads, C->cap_lds);
+    C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, k.grow_host, C->cap_threads, C->cap_lds);
   }
   const char *pe = getenv("WB_PERSIST");
   if (C->cap_blocks && blocks > C->cap_blocks && !(pe && pe[0] == '0')) {
@@ -379,7 +404,7 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   if (C->stop_dirty.exchange(false) &&
       !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
-  if (e || !C->prog.n_imported) return e;
+  if (e || !(C->prog.n_imported || C->grow_host)) return e;
   for (;;) {
     // every round resumes the lanes the host serviced; lanes it ended keep its code
     const int64_t k = service_host_calls(C);
@@ -483,8 +508,10 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
 WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeconds) {
   if (!C) return R(kWrongVMWorkflow);
   const wb::Program &P = C->prog;
-  uint32_t init_words = P.mem_min << 14;
+  // the whole reserved layout: pages a lane grows into within it must read zero
+  const uint32_t init_words = C->mem_words;
   (void)hipEventRecord(C->ev0, C->stream);
+  if (!pool_reset(C)) return R(kRuntimeError);
   if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->lstate.ptr, C->ls_slots,
@@ -597,8 +624,20 @@ WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_S
 
 WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Hashes) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->settle()) return R(kRuntimeError);
+  // the grid covers the largest memory of the batch (a block per page and wave)
+  uint32_t maxp = 0;
+  if (C->prog.has_mem) {
+    const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+    std::vector<uint32_t> pages(size_t(C->nwaves) * 64);
+    if (!C->hip_ok(hipMemcpy2D(pages.data(), row, C->lstate.ptr + LS_PAGES * 64, pitch, row, C->nwaves,
+                               hipMemcpyDeviceToHost), "pages"))
+      return R(kRuntimeError);
+    for (uint32_t i = 0; i < C->n; i++) maxp = std::max(maxp, pages[i]);
+  }
   if (!C->hip_ok(wb_launch_mem_hash(C->mem.ptr, C->lstate.ptr, C->ls_slots, C->hashes.ptr,
-                                    C->mem_words, C->n, C->mlog, C->stream), "hash"))
+                                    C->mem_words, C->n, C->mlog, C->pt_w ? C->ptab.ptr : nullptr,
+                                    C->pt_w, maxp, C->stream), "hash"))
     return R(kRuntimeError);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "hash")) return R(kRuntimeError);
   if (!C->hip_ok(hipMemcpy(Hashes, C->hashes.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "hash"))
@@ -839,6 +878,7 @@ void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   if (C->ev0) (void)hipEventDestroy(C->ev0);
   if (C->ev1) (void)hipEventDestroy(C->ev1);
   hipStream_t s = C->stream;
+  for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
   delete C;
   if (s) (void)hipStreamDestroy(s);
 }

@@ -124,6 +124,33 @@ struct WasmEdge_BatchContext {
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0;
   uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
+  // Paged linear memory (DESIGN.md "Linear memory"): `mem_max_pages` is the page limit
+  // (65536, the module's max, MaxMemoryPage); pages [0, rpages) of every lane live in the
+  // reserved layout at `mem` (mem_words = rpages * 16384 words per lane), page q >= rpages
+  // of wave w in a pool row of 64 lanes x 64 KiB at pt_host[w * pt_w + q - rpages]. Rows
+  // come from hipMalloc'ed chunks, zeroed, handed out by the host when a lane parks at a
+  // memory.grow past its wave's rows (hostcall.cpp serve_grows) -- the batched
+  // Allocator::resize (lib/system/allocator.cpp:101-129), which commits pages on demand.
+  uint32_t rpages = 0;
+  bool grow_host = false;            // the module can grow past rpages
+  uint32_t pt_w = 0;                 // page-table width: pool pages per wave it can name
+  std::vector<uint64_t> pt_host;     // [nwaves][pt_w] row device addresses (0: none)
+  std::vector<uint32_t> pt_n;        // [nwaves] rows each wave holds (pages rpages.. +n)
+  DevBuf<uint64_t> ptab;             // the device copy of pt_host
+  bool pt_dirty = false;             // pt_host changed since the last upload
+  std::vector<uint64_t> pool_free;   // zeroed rows not handed out
+  std::vector<std::pair<void *, size_t>> pool_chunks;   // (base, bytes), freed at Delete
+  size_t pool_bytes = 0;             // bytes of chunks allocated
+  bool pool_used = false;            // rows were handed out since the last Reset
+  // device address of word-row `word` (a multiple of 64) of wave `wave`: that word of its
+  // 64 lanes, and the rows after it up to the end of its page; nullptr past the wave's rows
+  uint32_t *wave_rows(uint32_t wave, uint64_t word) const {
+    if (word < mem_words) return mem.ptr + (size_t(wave) * mem_words + word) * 64;
+    const uint64_t k = (word >> 14) - rpages;
+    if (k >= pt_w) return nullptr;
+    const uint64_t a = pt_host[size_t(wave) * pt_w + k];
+    return a ? reinterpret_cast<uint32_t *>(a) + size_t(word & 16383u) * 64 : nullptr;
+  }
   uint32_t mlog = 0;              // log2(words per memory interleave granule), KParams::mlog
   // current invocation
   int func = -1;
@@ -213,6 +240,11 @@ struct WaveView {
 
 uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t Len,
                uint8_t *Dst, const uint8_t *Src);
+// pool rows (hostcall.cpp): give wave `wave` rows up to `rows` pool pages (false: no
+// device memory for all of them; it keeps what it got); return every row at Reset
+bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows);
+bool pool_reset(WasmEdge_BatchContext *C);
+bool pool_upload(WasmEdge_BatchContext *C);
 int64_t service_host_calls(WasmEdge_BatchContext *C);
 uint64_t mem_size(const WasmEdge_BatchMemoryContext *M);   // bytes of the instance's memory
 

@@ -312,7 +312,10 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
   return npc;
 }
 
-template <bool VF, class Frame>
+// PG: the module can grow past the reserved layout (KParams::grow_host), so a lane's memory
+// may have pool pages: only then do the per-lane step's accesses go through the page table
+// and memory.size / memory.grow read the size from LS_PAGES (the fast paths never change).
+template <bool VF, bool PG, class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
                                        uint32_t *const gs, const GMem mem,
                                        uint32_t *const ls, uint32_t *const fs,
@@ -350,7 +353,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   // (own: the lane belongs to this launch wave -- half waves run a batch wave's lanes in
   // two launch waves, KParams::half)
   uint32_t status = own && inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
-  uint32_t pc = p.entry_pc, gsp = 0, pages = LS(LS_PAGES), dropped = LS(LS_DROPPED);
+  // `pages` = the lane's pages in the reserved layout, min(its memory size, rpages): the
+  // bound of every fast path. The size itself is LS_PAGES (memory.grow writes it there),
+  // read where it can exceed rpages (MEM_PAGES).
+  uint32_t pc = p.entry_pc, gsp = 0, pages = min(LS(LS_PAGES), p.rpages), dropped = LS(LS_DROPPED);
+  // (addressed from the kernel arguments, not `ls`: no extra pointer live through the loop)
+#define LS_PAGES_REF p.lstate[((size_t)__builtin_amdgcn_readfirstlane(inst >> 6) * p.ls_slots + LS_PAGES) * 64u + lane]
+#define MEM_PAGES (PG && pages >= p.rpages ? LS_PAGES_REF : pages)
   // one past the highest memory byte written since instantiation: Reset re-initialises
   // only [0, hwm) of each lane (plus the image), the rest is still the zero it was given
   uint32_t hwm = LS(LS_HWM);
@@ -520,6 +529,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define SLOW_OP() goto k_slow
 #define SLOW_IF(c) do { if (__ballot(c)) goto k_slow; } while (0)
 #define HOST_YIELD(f, base) SLOW_OP()
+#define MEM_BYTES ((uint64_t)pages << 16)
+#define WB_GROW(cur, n, res) ((void)0)
       uint32_t sc = 0, tick = 1024, xpc = 0, xpost = 0, tcode = 0;
       int32_t xadj = 0;
       uint64_t scost = 0;   // gas of the run so far (metered runs; wave-uniform)
@@ -624,6 +635,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_OP
 #undef SLOW_IF
 #undef HOST_YIELD
+#undef MEM_BYTES
+#undef WB_GROW
       count += (uint64_t)(int64_t)(int32_t)sc + asc;
       cost += scost;
       if (tcode == 0) {
@@ -656,7 +669,17 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define SLOW_OP() ((void)0)
 #define SLOW_IF(c) ((void)0)
 #define HOST_YIELD(f, base) do { status = WB_ERR_HOST_CALL; ycall = (f); ybase = (base); } while (0)
+#define MEM_BYTES ((uint64_t)slow_pages << 16)
+      // memory.grow (dbc_step.inc): within the reserved pages or the wave's pool rows it
+      // completes here; past them the lane parks for the host (hostcall.cpp grow service)
+#define WB_GROW(cur, n, res) do { const uint32_t _np = (cur) + (n); \
+    if (!PG) { pages = _np; res = (cur); } \
+    else if (_np <= p.rpages || (_np - 1u - p.rpages < p.ptab_w && \
+        p.ptab[(size_t)__builtin_amdgcn_readfirstlane(inst >> 6) * p.ptab_w + _np - 1u - p.rpages] != 0)) { \
+      LS_PAGES_REF = _np; pages = min(_np, p.rpages); res = (cur); \
+    } else { res = (n); HOST_YIELD(WB_GROW_CALL, C_); } } while (0)
       const uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(slowmask));
+      const uint32_t slow_pages = MEM_PAGES;   // the memory size (past the reserved layout too)
       const w4 I = code[pcs];
       const uint32_t w0 = I.x, w1 = I.y, w2 = I.z, w3 = I.w;
       const uint32_t op = w0 & 0x7FFFu;
@@ -673,8 +696,22 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         status = 0x03u;
         goto s_done;
       }
-      switch (op) {
+      if (!PG || !__ballot(pages >= p.rpages)) {
+        switch (op) {
 #include "dbc_step.inc"
+        }
+      } else {
+        // a lane of this group has grown past the reserved layout: the step's accesses go
+        // through the paged view (pool rows too); the fast paths only ever see the
+        // reserved layout (their bounds checks use min(pages, rpages)). A second copy of
+        // the step, so that the paged addressing costs the common case nothing.
+        const GMemP mem_pg{mem.p, mem.g, p.mem_words,
+                           p.ptab ? p.ptab + (size_t)__builtin_amdgcn_readfirstlane(inst >> 6) * p.ptab_w : nullptr,
+                           lane << p.mlog};
+        const GMemP &mem = mem_pg;
+        switch (op) {
+#include "dbc_step.inc"
+        }
       }
     s_next:
       if (p.cost_off && (status == WB_STATUS_RUNNING || status == WB_STATUS_OK) &&
@@ -696,6 +733,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef SLOW_OP
 #undef SLOW_IF
 #undef HOST_YIELD
+#undef MEM_BYTES
+#undef WB_GROW
     }
     WB_STAT_ADD(ST_CYC_SLOW, WB_NOW() - ts2);
     // budget, wall clock, and the host's interrupt request (every round: a core call
@@ -732,7 +771,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       for (uint32_t k = 0; k < p.hb_cells && ybase + k < p.total_cells; k++)
         p.hbuf[(size_t)inst * p.hb_cells + k] = F.get(ybase + k);
     }
-    LS(LS_PAGES) = pages;
+    if (!PG) LS(LS_PAGES) = pages;   // (PG: memory.grow wrote it)
     LS(LS_DROPPED) = dropped;
     LS(LS_HWM) = hwm;
     LS(LS_COST) = (uint32_t)cost;
@@ -742,6 +781,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   }
 #undef LS
 #undef WB_MARK
+#undef MEM_PAGES
+#undef LS_PAGES_REF
 }
 
 // General kernel: frames of any size in LDS (4 waves per block when they fit). VF: the
@@ -761,7 +802,7 @@ __device__ __forceinline__ uint32_t next_wave(const KParams &p, uint32_t &turn) 
   return w < nwaves ? w : 0xFFFFFFFFu;
 }
 
-template <bool VF>
+template <bool VF, bool PG>
 __device__ __forceinline__ void exec_body(const KParams &p) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
@@ -774,7 +815,7 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
     const uint32_t wave = lw >> p.half;
     const bool own = !p.half || (lane >> 5) == (lw & 1u);
     const uint32_t inst = wave * 64u + lane;
-    interp<VF>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+    interp<VF, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
                p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
                p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk,
@@ -783,10 +824,14 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4) wb_exec_kernel(const KParams p) {
-  exec_body<false>(p);
+  exec_body<false, false>(p);
+}
+extern "C" __global__ void __launch_bounds__(256, 4) wb_exec_pg_kernel(const KParams p) {
+  exec_body<false, true>(p);
 }
 // HBM frames: LDS holds only the waves' call-stack slots
-extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KParams p) {
+template <bool PG>
+__device__ __forceinline__ void exec_hbm_body(const KParams &p) {
   extern __shared__ uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
   lds_u32 *const stk = (lds_u32 *)(lds + ((wib * p.gs_lds) << 6) + lane);
@@ -794,14 +839,23 @@ extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KPara
   for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
     HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
-    interp<false>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
+    interp<false, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                   GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
                   p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
                   p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
   }
 }
+extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KParams p) {
+  exec_hbm_body<false>(p);
+}
+extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_pg_kernel(const KParams p) {
+  exec_hbm_body<true>(p);
+}
 extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_kernel(const KParams p) {
-  exec_body<true>(p);
+  exec_body<true, false>(p);
+}
+extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_pg_kernel(const KParams p) {
+  exec_body<true, true>(p);
 }
 
 // ======================================================================= helpers
@@ -813,6 +867,9 @@ extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_kernel(const KPa
 // and never written since (the kernel's every store path raises the mark), the way the
 // reference's fresh MAP_ANONYMOUS pages are zero without being written. `ls` = nullptr:
 // always full (per-lane table images).
+// `init_words` = the rows this covers: the whole reserved layout (rpages), so that pages a
+// lane grows into later read zero without memory.grow writing them; pool rows are zeroed
+// by the host (batch_api.cpp pool_reset).
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
                    uint32_t init_words, uint32_t mem_words, uint32_t nwaves,
@@ -834,7 +891,7 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
       rows = (rows + gm) & ~gm;
       if (rows > init_words) rows = init_words;
       __syncthreads();   // smax is reused by the next wave
-      uint32_t *wm = mem + wave * mem_words * 64u;
+      uint32_t *wm = mem + wave * mem_words * (size_t)64u;
       for (size_t i = threadIdx.x; i < (size_t)rows * 64u; i += blockDim.x) {
         const uint32_t word = (uint32_t)(((i >> (6 + g)) << g) | (i & ((1u << g) - 1u)));
         wm[i] = word < image_words ? image[word] : 0u;
@@ -862,7 +919,7 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
     }
     const uint32_t r1 = r0 + 1024u < rows ? r0 + 1024u : rows;
     if (r1 <= r0) continue;
-    uint32_t *wm = mem + wave * mem_words * 64u;
+    uint32_t *wm = mem + wave * mem_words * (size_t)64u;
     // size_t: rows past 2^26 (initial memories over 4096 pages) must not wrap
     for (size_t i = (size_t)r0 * 64u + threadIdx.x; i < (size_t)r1 * 64u; i += blockDim.x) {
       // linear index -> word: granule i >> (6 + g), word (i & (2^g - 1)) within it
@@ -894,53 +951,75 @@ wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_
 }
 
 // Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
+// The sum commutes, so the words are spread over the grid: block (wave, c) adds the terms
+// of u64 words [c*8192, (c+1)*8192) -- page c -- of its wave's 64 lanes (4 threads per
+// lane, coalesced across lanes) into hashes[] (zeroed first), and wb_mem_hash_fin_kernel
+// XORs the page-count term in. A lane's pages past the reserved layout are read through
+// the wave's pool rows (GMemP).
 extern "C" __global__ void __launch_bounds__(256)
-wb_mem_hash_kernel(const uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
-                   uint64_t *hashes, uint32_t mem_words, uint32_t n, uint32_t g) {
+wb_mem_hash_kernel(uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
+                   uint64_t *hashes, uint32_t mem_words, uint32_t n, uint32_t g,
+                   const uint64_t *ptab, uint32_t ptab_w) {
+  const uint32_t wave = blockIdx.x, lane = threadIdx.x & 63u, sub = threadIdx.x >> 6;
+  const uint32_t inst = wave * 64u + lane;
+  __shared__ uint64_t part[256];
+  uint64_t h = 0;
+  uint32_t pages = 0;
+  if (inst < n) {
+    pages = ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + lane];
+    if (blockIdx.y < pages) {
+      const GMemP m{mem + (size_t)wave * mem_words * 64u + (lane << g), g, mem_words,
+                    ptab ? ptab + (size_t)wave * ptab_w : nullptr, lane << g};
+      const uint64_t i0 = (uint64_t)blockIdx.y << 13;
+      for (uint64_t i = i0 + sub; i < i0 + 8192u; i += 4) {
+        const uint64_t w = (uint64_t)*mw(m, (uint32_t)(2 * i)) | ((uint64_t)*mw(m, (uint32_t)(2 * i + 1)) << 32);
+        h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
+      }
+    }
+  }
+  part[threadIdx.x] = h;
+  __syncthreads();
+  if (sub == 0 && inst < n && blockIdx.y < pages)
+    atomicAdd((unsigned long long *)&hashes[inst],
+              (unsigned long long)(part[lane] + part[lane + 64] + part[lane + 128] + part[lane + 192]));
+}
+extern "C" __global__ void __launch_bounds__(256)
+wb_mem_hash_fin_kernel(const uint32_t *ls, uint32_t ls_slots, uint64_t *hashes, uint32_t n) {
   const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
   if (inst >= n) return;
-  const uint32_t wave = inst >> 6, lane = inst & 63u;
-  const uint32_t *m = mem + (size_t)wave * mem_words * 64u + (lane << g);
-  const uint32_t pages = ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + lane];
-  const uint64_t nw = (uint64_t)pages << 13;
-  uint64_t h = 0;
-  for (uint64_t i = 0; i < nw; i++) {
-    const uint64_t w = (uint64_t)m[goff((uint32_t)(2 * i), g)] |
-                       ((uint64_t)m[goff((uint32_t)(2 * i + 1), g)] << 32);
-    h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
-  }
-  hashes[inst] = h ^ fmix64((uint64_t)pages + 0x1234567ull);
+  const uint32_t pages = ls[((size_t)(inst >> 6) * ls_slots + LS_PAGES) * 64u + (inst & 63u)];
+  hashes[inst] ^= fmix64((uint64_t)pages + 0x1234567ull);
 }
 
 // ======================================================================= launchers
 // (host stubs live in this translation unit; the C-ABI layer calls these)
+// the kernel for a launch: frames in HBM / LDS / VGPRs, and paged (PG) or not
+static const void *exec_kernel(int vframe, int hbm, int paged) {
+  if (hbm) return paged ? reinterpret_cast<const void *>(&wb_exec_hbm_pg_kernel)
+                        : reinterpret_cast<const void *>(&wb_exec_hbm_kernel);
+  if (vframe) return paged ? reinterpret_cast<const void *>(&wb_exec_vf_pg_kernel)
+                           : reinterpret_cast<const void *>(&wb_exec_vf_kernel);
+  return paged ? reinterpret_cast<const void *>(&wb_exec_pg_kernel)
+               : reinterpret_cast<const void *>(&wb_exec_kernel);
+}
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_vf_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&wb_exec_hbm_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (int k = 0; k < 8; k++)
+      (void)hipFuncSetAttribute(exec_kernel(k & 1, k >> 1 & 1, k >> 2 & 1),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (p->hframe)
-    hipLaunchKernelGGL(wb_exec_hbm_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
-  else if (vframe)
-    hipLaunchKernelGGL(wb_exec_vf_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
-  else
-    hipLaunchKernelGGL(wb_exec_kernel, dim3(blocks), dim3(threads), lds_bytes, s, *p);
-  return hipGetLastError();
+  const void *k = exec_kernel(vframe, p->hframe != nullptr, p->grow_host != 0);
+  void *args[] = {const_cast<KParams *>(p)};
+  return hipLaunchKernel(k, dim3(blocks), dim3(threads), args, lds_bytes, s);
 }
 // Blocks of the exec kernel the whole device holds at once (persistent waves, KParams::
 // wave_ctr): resident blocks per CU at this block size and LDS share x CUs; 0 on failure.
-extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, uint32_t threads, size_t lds_bytes) {
+extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t threads, size_t lds_bytes) {
   int per_cu = 0, cus = 0, dev = 0;
-  const void *k = hbm ? reinterpret_cast<const void *>(&wb_exec_hbm_kernel)
-                : vframe ? reinterpret_cast<const void *>(&wb_exec_vf_kernel)
-                         : reinterpret_cast<const void *>(&wb_exec_kernel);
+  const void *k = exec_kernel(vframe, hbm, paged);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, int(threads), lds_bytes) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -961,12 +1040,19 @@ extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                      image_words, init_words, mem_words, nwaves, ls, ls_slots, full, g);
   return hipGetLastError();
 }
-extern "C" hipError_t wb_launch_mem_hash(const uint32_t *mem, const uint32_t *ls,
+extern "C" hipError_t wb_launch_mem_hash(uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
-                                         uint32_t mem_words, uint32_t n, uint32_t g, hipStream_t s) {
+                                         uint32_t mem_words, uint32_t n, uint32_t g,
+                                         const uint64_t *ptab, uint32_t ptab_w, uint32_t max_pages,
+                                         hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mem, ls,
-                     ls_slots, hashes, mem_words, n, g);
+  hipError_t e = hipMemsetAsync(hashes, 0, size_t(n) * 8, s);
+  if (e != hipSuccess) return e;
+  if (max_pages)
+    hipLaunchKernelGGL(wb_mem_hash_kernel, dim3((n + 63) / 64, max_pages), dim3(256), 0, s, mem, ls,
+                       ls_slots, hashes, mem_words, n, g, ptab, ptab_w);
+  hipLaunchKernelGGL(wb_mem_hash_fin_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ls, ls_slots,
+                     hashes, n);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,

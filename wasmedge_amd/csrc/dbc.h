@@ -173,3 +173,6 @@ struct DFunc {
                                         // services it and resumes the lane. It stays the
                                         // final status only when no host function is
                                         // registered for that import.
+// The import index a lane parks with when its memory.grow needs pool rows the host has not
+// allocated yet (KParams::grow_host): the host allocates them and completes the grow.
+#define WB_GROW_CALL 0xFFFFFFFEu

@@ -401,6 +401,23 @@ WB_HD size_t goff(uint32_t w, uint32_t g) {
   return ((size_t)(w >> g) << (6 + g)) | (size_t)(w & ((1u << g) - 1u));
 }
 WB_HD uint32_t *mw(GMem m, uint32_t w) { return &m.p[goff(w, m.g)]; }
+// The paged view (the kernel's per-lane step): words below `rwords` (the reserved pages)
+// as GMem; word w of page q = w >> 14 beyond them in the wave's pool row pt[q - rpages],
+// the same 64-lane interleave within the row (`loff` = the lane's l * 2^g). Only accesses
+// the caller bounds-checked against the lane's pages come here, and every page below that
+// has a row.
+struct GMemP {
+  uint32_t *p;
+  uint32_t g;
+  uint32_t rwords;
+  const uint64_t *pt;
+  uint32_t loff;
+};
+WB_HD uint32_t *mw(GMemP m, uint32_t w) {
+  if (w < m.rwords) return &m.p[goff(w, m.g)];
+  uint32_t *row = (uint32_t *)(uintptr_t)m.pt[(w - m.rwords) >> 14];
+  return &row[m.loff + goff(w & 16383u, m.g)];
+}
 
 template <class M> WB_HD uint32_t mword(M m, uint32_t w) { return *mw(m, w); }
 template <class M> WB_HD uint64_t mload(M m, uint32_t ea, uint32_t n) {

@@ -127,10 +127,12 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   uint32_t pcells = 0, rcells = 0;
   for (uint8_t t : T.params) pcells += wb::cells_of(t);
   for (uint8_t t : T.results) rcells += wb::cells_of(t);
-  uint32_t budget = max_pages ? max_pages : (P.mem_has_max ? P.mem_max : P.mem_min);
-  if (P.mem_has_max && budget > P.mem_max) budget = P.mem_max;
-  if (budget < P.mem_min) budget = P.mem_min;
-  if (!P.has_mem) budget = 0;
+  // page limit as the library's (memory.h:88-115): 65536, the module's max, max_pages
+  uint32_t limit = 65536;
+  if (P.mem_has_max) limit = std::min(limit, P.mem_max);
+  if (max_pages) limit = std::min(limit, max_pages);
+  if (limit < P.mem_min) limit = P.mem_min;
+  if (!P.has_mem) limit = 0;
   if (!gs_depth) gs_depth = 4096;
   std::vector<DFunc> fv;
   for (const auto &fi : P.funcs) fv.push_back(DFunc{fi.imported ? 0xFFFFFFFFu : fi.entry_pc, P.type_canon[fi.type]});
@@ -149,7 +151,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   p.data_pool = pool.data(); p.data_off = doff.data(); p.data_len = dlen.data();
   p.results = results; p.param_cells = pcells; p.result_cells = rcells;
   p.global_cells = P.global_cells; p.total_cells = P.total_cells();
-  p.table_size = uint32_t(P.table0.size()); p.mem_max_pages = budget;
+  p.table_size = uint32_t(P.table0.size()); p.mem_max_pages = limit;
   p.gs_depth = gs_depth;
   p.mut_tables = P.mut_tables ? 1u : 0u; p.ntables = P.ntables; p.tab_words = P.tab_words;
   p.tabinfo = P.tabinfo.data(); p.elem_pool = P.elem_pool.data();
@@ -181,7 +183,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
                                P.types[P.funcs[f].type].results);
   for (uint32_t inst = 0; inst < n; inst++) {
     // instantiate: memory image + globals
-    memv.assign(size_t(budget) << 14, 0u);
+    memv.assign(size_t(P.mem_min) << 14, 0u);   // (memory.grow resizes it)
     uint8_t *mb = reinterpret_cast<uint8_t *>(memv.data());
     for (const auto &d : P.datas)
       if (d.active && !d.bytes.empty()) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
@@ -209,6 +211,10 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define SLOW_IF(c) ((void)0)
 #define HOST_YIELD(f, base) do { status = WB_ERR_HOST_CALL; ycall = (f); ybase = (base); } while (0)
 #define WB_FAST 0
+#define MEM_BYTES ((uint64_t)pages << 16)
+#define MEM_PAGES pages
+#define WB_GROW(cur, n, res) do { try { memv.resize(size_t((cur) + (n)) << 14, 0u); } catch (...) { break; } \
+    mem = memv.data(); mb = reinterpret_cast<uint8_t *>(mem); pages = (cur) + (n); res = (cur); } while (0)
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
     uint32_t pages = P.mem_min, dropped = init_dropped;

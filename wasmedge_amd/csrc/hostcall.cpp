@@ -31,6 +31,8 @@ void RoundCache::mark_dirty(uint32_t b) {
 
 uint32_t *RoundCache::get(uint32_t b, uint32_t wave, bool *fail) {
   if (wave < w0 || wave >= w0 + nw) return nullptr;
+  // pool pages sit at a different address per wave: left to the per-wave blocks
+  if (uint64_t(b + 1) * kRowWords > C->mem_words) return nullptr;
   Row *r;
   {
     std::lock_guard<std::mutex> lock(mu);
@@ -69,10 +71,11 @@ bool RoundCache::flush() {
 WaveView::Block *WaveView::block(uint32_t b) {
   for (auto &e : blocks)
     if (e.first == b) return &e.second;
-  const size_t rows = std::min<size_t>(kBlockWords, size_t(C->mem_words) - size_t(b) * kBlockWords);
+  // (a block never straddles a page: 16384 words per page, kBlockWords divides it)
+  const uint32_t *src = C->wave_rows(wave, uint64_t(b) * kBlockWords);
+  if (!src) { ok = false; return nullptr; }
   Block blk;
-  blk.w.resize(rows * 64);
-  const uint32_t *src = C->mem.ptr + (size_t(wave) * C->mem_words + size_t(b) * kBlockWords) * 64;
+  blk.w.resize(size_t(kBlockWords) * 64);
   if (hipMemcpy(blk.w.data(), src, blk.w.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) {
     ok = false;
     return nullptr;
@@ -133,8 +136,8 @@ uint8_t WaveView::rw(uint32_t lane, uint32_t off, uint32_t len, uint8_t *dst, co
 bool WaveView::flush() {
   for (auto &e : blocks) {
     if (!e.second.dirty) continue;
-    uint32_t *dst = C->mem.ptr + (size_t(wave) * C->mem_words + size_t(e.first) * kBlockWords) * 64;
-    if (hipMemcpy(dst, e.second.w.data(), e.second.w.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    uint32_t *dst = C->wave_rows(wave, uint64_t(e.first) * kBlockWords);
+    if (!dst || hipMemcpy(dst, e.second.w.data(), e.second.w.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       ok = false;
   }
   blocks.clear();
@@ -174,6 +177,123 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
   return 0;
 }
 
+// ---- pool rows for pages past the reserved layout ------------------------------------
+// A row = one pool page of a wave: 64 lanes x 64 KiB, interleaved like the reserved layout.
+constexpr size_t kRowBytes = size_t(64) << 16;
+
+// One more chunk of zeroed rows: at least `want` rows, growing with the pool (1/4 of what
+// it holds, at most 1 GiB at a time) so that few hipMallocs serve a growing batch; falls
+// back to exactly `want` when the larger chunk does not fit, and respects MemoryPoolBytes.
+static bool pool_chunk(WasmEdge_BatchContext *C, size_t want) {
+  size_t rows = std::max<size_t>(want, std::min<size_t>(256, std::max<size_t>(16, C->pool_bytes / kRowBytes / 4)));
+  const size_t cap = C->conf.MemoryPoolBytes;
+  if (cap) {   // within the cap: what is left of it, if that covers `want`
+    const size_t left = C->pool_bytes < cap ? (cap - C->pool_bytes) / kRowBytes : 0;
+    if (left < want) return false;
+    rows = std::min(rows, left);
+  }
+  for (int attempt = 0; attempt < 2; attempt++, rows = want) {
+    void *p = nullptr;
+    if (hipMalloc(&p, rows * kRowBytes) != hipSuccess) { (void)hipGetLastError(); continue; }
+    if (hipMemset(p, 0, rows * kRowBytes) != hipSuccess) { (void)hipFree(p); return false; }
+    C->pool_chunks.emplace_back(p, rows * kRowBytes);
+    C->pool_bytes += rows * kRowBytes;
+    for (size_t r = rows; r-- > 0;)
+      C->pool_free.push_back(reinterpret_cast<uint64_t>(p) + r * kRowBytes);
+    return true;
+  }
+  return false;
+}
+
+bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows) {
+  uint32_t &have = C->pt_n[wave];
+  if (rows <= have) return true;
+  if (rows > C->pt_w) {   // widen the page table (every wave's row of it)
+    uint32_t w = std::max<uint32_t>(rows, std::max<uint32_t>(16, C->pt_w * 2));
+    w = std::min<uint32_t>(w, C->mem_max_pages - C->rpages);
+    std::vector<uint64_t> t(size_t(C->nwaves) * w, 0);
+    for (uint32_t v = 0; v < C->nwaves; v++)
+      for (uint32_t k = 0; k < C->pt_n[v]; k++) t[size_t(v) * w + k] = C->pt_host[size_t(v) * C->pt_w + k];
+    C->pt_host.swap(t);
+    C->pt_w = w;
+    if (!C->ptab.alloc(C->pt_host.size())) return false;
+    C->pt_dirty = true;
+  }
+  while (have < rows) {
+    if (C->pool_free.empty() && !pool_chunk(C, rows - have)) return false;
+    C->pt_host[size_t(wave) * C->pt_w + have++] = C->pool_free.back();
+    C->pool_free.pop_back();
+    C->pool_used = C->pt_dirty = true;
+  }
+  return true;
+}
+
+bool pool_upload(WasmEdge_BatchContext *C) {
+  if (!C->pt_dirty) return true;
+  C->pt_dirty = false;
+  return C->hip_ok(hipMemcpy(C->ptab.ptr, C->pt_host.data(), C->pt_host.size() * 8, hipMemcpyHostToDevice),
+                   "page table");
+}
+
+// Reset (a fresh instantiation): every row back to the free list, zeroed again.
+bool pool_reset(WasmEdge_BatchContext *C) {
+  if (!C->pool_used) return true;
+  C->pool_used = false;
+  C->pool_free.clear();
+  for (const auto &ch : C->pool_chunks) {
+    if (!C->hip_ok(hipMemsetAsync(ch.first, 0, ch.second, C->stream), "pool reset")) return false;
+    for (size_t r = ch.second / kRowBytes; r-- > 0;)
+      C->pool_free.push_back(reinterpret_cast<uint64_t>(ch.first) + r * kRowBytes);
+  }
+  std::fill(C->pt_host.begin(), C->pt_host.end(), 0ull);
+  std::fill(C->pt_n.begin(), C->pt_n.end(), 0u);
+  C->pt_dirty = true;
+  if (!C->pt_host.empty() &&
+      !C->hip_ok(hipMemsetAsync(C->ptab.ptr, 0, C->pt_host.size() * 8, C->stream), "page table"))
+    return false;
+  C->pt_dirty = false;
+  return true;
+}
+
+// Lanes parked at a memory.grow past their wave's rows (WB_GROW_CALL; the request n in
+// their staged result cell): per wave, rows for the largest request (plus a quarter of what
+// the wave holds, so that a lane growing page by page parks rarely), then each lane's grow
+// completes -- old size, pages raised -- or returns -1 when the device has no memory for
+// its pages (growPage failing in Allocator::resize, memory.h:104-109).
+static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &parked,
+                        std::vector<uint32_t> &hcall, std::vector<uint32_t> &hbuf,
+                        std::vector<uint32_t> &pages, bool *pages_dirty, int64_t *resumed) {
+  const uint32_t hb = C->hb_cells, R = C->rpages;
+  // per wave, the lanes' requests smallest first: when the device runs out, the lanes
+  // that need fewer pages still get them
+  std::vector<std::pair<uint32_t, uint32_t>> need;   // (wave, rows)
+  for (uint32_t i : parked)
+    if (hcall[i] == WB_GROW_CALL) need.emplace_back(i / 64, pages[i] + hbuf[size_t(i) * hb] - R);
+  std::sort(need.begin(), need.end());
+  const uint32_t room = C->mem_max_pages - R;
+  for (size_t k = 0; k < need.size(); k++) {
+    const uint32_t w = need[k].first, rows = need[k].second;
+    if (rows <= C->pt_n[w]) continue;
+    if (k > 0 && need[k - 1].first == w && need[k - 1].second > C->pt_n[w]) continue;   // failed
+    const uint32_t slack = std::min<uint32_t>(room, std::max(rows, C->pt_n[w] + std::max<uint32_t>(4, C->pt_n[w] / 4)));
+    if (!pool_reserve(C, w, slack)) (void)pool_reserve(C, w, rows);
+  }
+  for (uint32_t i : parked) {
+    if (hcall[i] != WB_GROW_CALL) continue;
+    const uint32_t n = hbuf[size_t(i) * hb];
+    uint32_t &res = hbuf[size_t(i) * hb];
+    if (pages[i] + n - R <= C->pt_n[i / 64]) {
+      res = pages[i];
+      pages[i] += n;
+      *pages_dirty = true;
+    } else {
+      res = 0xFFFFFFFFu;
+    }
+    hcall[i] = 1;   // one result cell
+    ++*resumed;
+  }
+}
+
 // Serve every lane parked at a host import: call its host function with the args the
 // kernel staged in hbuf, stage the results (or end the lane with the host's ErrCode;
 // Terminated 0x01 ends it too, engine.cpp:62-64). Returns the number of lanes to resume,
@@ -208,6 +328,15 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
                               hipMemcpyDeviceToHost), "write marks")))
     return -1;
 
+  // memory.grow requests first: host functions of this round then see the grown pages
+  bool pages_dirty = false;
+  int64_t grown = 0;
+  std::vector<uint8_t> hcall_grow(parked.size(), 0);
+  for (size_t j = 0; j < parked.size(); j++) hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL;
+  if (C->grow_host) {
+    serve_grows(C, parked, hcall, hbuf, pages, &pages_dirty, &grown);
+    if (!pool_upload(C)) return -1;
+  }
   RoundCache rc;
   rc.C = C;
   rc.w0 = waves.front().first;
@@ -228,6 +357,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
       view.hwm = &hwm[size_t(view.wave) * 64];
       for (uint32_t j = waves[k].second; j < waves[k + 1].second; j++) {
         const uint32_t i = parked[j], f = hcall[i];
+        if (C->grow_host && hcall_grow[j]) continue;   // (served above)
         const WasmEdge_BatchContext::HostFn h =
             f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
         if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
@@ -280,10 +410,13 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
       !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
       !C->hip_ok(hipMemcpy(C->hbuf.ptr, hbuf.data(), hbuf.size() * 4, hipMemcpyHostToDevice), "hbuf"))
     return -1;
+  if (pages_dirty && !C->hip_ok(hipMemcpy2D(C->lstate.ptr + LS_PAGES * 64, pitch, pages.data(), row, row, nw,
+                                            hipMemcpyHostToDevice), "pages"))
+    return -1;
   if (hwm_dirty && !C->hip_ok(hipMemcpy2D(C->lstate.ptr + LS_HWM * 64, pitch, hwm.data(), row, row, nw,
                                           hipMemcpyHostToDevice), "write marks"))
     return -1;
-  return resumed.load();
+  return resumed.load() + grown;
 }
 
 }  // namespace wbh

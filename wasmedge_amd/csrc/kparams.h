@@ -36,9 +36,20 @@ struct KParams {
   uint32_t param_cells, result_cells;
   uint32_t global_cells, total_cells;
   uint32_t table_size;
-  uint32_t mem_words;           // words per lane reserved (= mem_max_pages * 16384)
+  uint32_t mem_words;           // words per lane in the reserved layout (= rpages * 16384)
   uint32_t mlog;                // log2 of the words per interleave granule (dbc_ops.h GMem)
-  uint32_t init_pages, mem_max_pages;
+  uint32_t init_pages;
+  uint32_t mem_max_pages;       // page limit: min(65536, the module's max, MaxMemoryPage)
+                                // (memory.h:88-115 growPage)
+  // Paged linear memory (DESIGN.md "Linear memory"): pages [0, rpages) of every lane live
+  // in the reserved, lane-interleaved layout at `mem`; page q >= rpages of a wave lives in a
+  // pool row (64 lanes x 64 KiB, same interleave) whose device address is
+  // ptab[wave * ptab_w + (q - rpages)] (0 = not allocated). Only the host allocates rows;
+  // a memory.grow past the wave's rows parks the lane (grow_host) for the host to do so.
+  uint32_t rpages;
+  const uint64_t *ptab;
+  uint32_t ptab_w;
+  uint32_t grow_host;           // 1: a grow past the allocated rows yields to the host
   uint32_t gs_depth;            // call-stack cells per lane
   uint32_t gs_lds;              // of which the first gs_lds live in LDS (after the frames)
   uint32_t init_dropped;        // data segments dropped after instantiation (bitmask)
