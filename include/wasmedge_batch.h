@@ -57,7 +57,6 @@ typedef struct WasmEdge_Result {
 #define WASMEDGE_BATCH_INTERRUPTED 0x07u      /* ErrCode::Interrupted: step/time limit */
 #define WASMEDGE_BATCH_STACK_EXHAUSTED 0xB0u  /* device call stack full */
 #define WASMEDGE_BATCH_HOST_CALL 0xB1u        /* reached a host import no host function is bound to */
-#define WASMEDGE_BATCH_TAIL_CALL_HOST 0xB2u   /* return_call_indirect reached a host import */
 
 typedef struct WasmEdge_BatchConfigure {
   /* Page limit per instance: RuntimeConfigure::MaxMemPage (include/common/configure.h:
@@ -111,8 +110,8 @@ typedef struct WasmEdge_BatchConfigure {
    * (Conf, WasmEdge_Proposal_TailCall), include/common/configure.h:176-182 leaves it off):
    * 0 = off, the opcodes fail BatchCreate with IllegalOpCode (0x37) as in the reference's
    * loader. On: a tail call reuses the caller's frame, so tail recursion never exhausts the
-   * device call stack. A return_call to a host import fails BatchCreate (0x02), and a
-   * return_call_indirect that reaches one ends the instance with 0xB2. */
+   * device call stack; a host import in tail position runs on the yield path and its results
+   * return from the caller (DESIGN.md "Tail calls"). */
   uint32_t TailCall;
   /* Layout of linear memory on the device (results never depend on it). The first
    * MemoryReservePages pages of every instance are allocated up front in the lane-
@@ -351,6 +350,10 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchCo
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *Cxt,
                                                          uint32_t Inst);
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *Cxt);
+/* Hash of the sources this library was built from (wasmedge_amd/csrc/srchash.py): lets a
+ * caller check that the library it loaded matches the checked-out tree (the batched form
+ * of the reference's WasmEdge_VersionGet, wasmedge.h). */
+WASMEDGE_BATCH_API const char *WasmEdge_BatchGetBuildHash(void);
 /* Human-readable description of the last failure on this context (or of the last
  * failed BatchCreate when Cxt is NULL). */
 WASMEDGE_BATCH_API const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *Cxt);

@@ -222,15 +222,11 @@ def test_runs_assemble(built, glog):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("jit", ["1", "0", "scan", "trip"])
+@pytest.mark.parametrize("jit", ["1", "0", "trip"])
 @pytest.mark.parametrize("granule", [4, 16, 128])
 def test_gpu_random_modules(built, monkeypatch, jit, granule):
-    """jit "scan": compiled runs with the opt-in unrolled scan loops (WB_SCAN=1); "trip":
-    trip mode forced on (WB_TRIP=1), "1" with it off"""
+    """jit "trip": trip mode forced on (WB_TRIP=1), "1" with it off"""
     monkeypatch.setenv("WB_TRIP", "1" if jit == "trip" else "0")
-    if jit == "scan":
-        monkeypatch.setenv("WB_SCAN", "1")
-        jit = "1"
     if jit == "trip":
         jit = "1"
     monkeypatch.setenv("WB_JIT", jit)

@@ -112,25 +112,60 @@ INDIRECT_TRAPS = assemble(r"""
 
 def test_indirect_traps_emulator(built):
     """Index 0 runs; 1: IndirectCallTypeMismatch 0x8C; 3: UninitializedElement 0x8A;
-    5: UndefinedElement 0x8B (controlInstr.cpp:101-158, the oracle's order); 2: a host import
-    through a tail call ends the instance with 0xB2 (DESIGN.md "Tail calls": the reference
-    would re-run its caller's caller's call instruction there)."""
+    5: UndefinedElement 0x8B (controlInstr.cpp:101-158, the oracle's order); 2: the host
+    import "fail" through the tail call, which fails (41 != 0): ExecutionFailed 0x8D."""
     rows = [[0], [1], [3], [5], [2]]
     m = O.Module(INDIRECT_TRAPS, tail_call=True)
-    ref = [m.run("go", r) for r in rows[:4]]
-    assert [r[0] for r in ref] == [0, 0x8C, 0x8A, 0x8B] and ref[0][1] == [42]
+    ref = [m.run("go", r) for r in rows]
+    assert [r[0] for r in ref] == [0, 0x8C, 0x8A, 0x8B, 0x8D] and ref[0][1] == [42]
     from hostfuncs import emu_host
     rets, st, cnt, h = emu_run(INDIRECT_TRAPS, "go", rows, [I32], [I32], tail_call=True,
                                host=emu_host(["fail"]))
-    assert compare(ref, rets[:4], st[:4], cnt[:4], h[:4], [I32]) == []
-    assert int(st[4]) == 0xB2
+    assert compare(ref, rets, st, cnt, h, [I32]) == []
 
 
-HOST_TAIL = assemble(r"""
+# Host imports in tail position (helper.cpp:35-97 with IsTailCall): the host function runs
+# in the reused frame and pops it. From the entry function (go, go_ind) the reference then
+# re-executes the entry's final `end` (the frame's From is RetIt - 1, helper.cpp:163) and
+# returns the host's results: the oracle restates it, the batched path matches it (one
+# counted `end` after the host call). From a nested frame (outer -> mid -> return_call) the
+# reference re-executes outer's `call` instead (the same off-by-one); the batched path
+# returns to outer, as `call $f` + `return` would (HOST_TWIN, which also counts the same two
+# instructions), a deliberate divergence (DESIGN.md "Tail calls").
+HOST_TAIL_WAT = r"""
 (module
+  (type $t (func (param i32) (result i32)))
   (import "env" "fail" (func $f (param i32) (result i32)))
-  (func (export "go") (param i32) (result i32) (return_call $f (local.get 0))))
-""")
+  (table 1 funcref)
+  (elem (i32.const 0) $f)
+  (func (export "go") (param i32) (result i32) (return_call $f (local.get 0)))
+  (func (export "go_ind") (param i32) (result i32)
+    (return_call_indirect (type $t) (local.get 0) (i32.const 0)))
+  (func $mid (param i32) (result i32) (local i32)
+    (local.set 1 (i32.const 5))
+    %s)
+  (func (export "outer") (param i32) (result i32)
+    (i32.add (call $mid (local.get 0)) (i32.const 100))))
+"""
+HOST_TAIL = assemble(HOST_TAIL_WAT % "(return_call $f (local.get 0))")
+HOST_TWIN = assemble(HOST_TAIL_WAT % "(return (call $f (local.get 0)))")
+
+
+def _host_tail_refs():
+    rows = [[0], [3], [0], [0]]
+    ref = {f: [O.Module(HOST_TAIL, tail_call=True).run(f, r) for r in rows] for f in ("go", "go_ind")}
+    ref["outer"] = [O.Module(HOST_TWIN, tail_call=True).run("outer", r) for r in rows]
+    assert [r[0] for r in ref["go"]] == [0, 0x8D, 0, 0] and ref["go"][0][1] == [7]
+    assert ref["outer"][0][1] == [107]
+    return rows, ref
+
+
+def test_host_tail_calls_emulator(built):
+    rows, ref = _host_tail_refs()
+    from hostfuncs import emu_host
+    for f in ("go", "go_ind", "outer"):
+        got = emu_run(HOST_TAIL, f, rows, [I32], [I32], tail_call=True, host=emu_host(["fail"]))
+        assert compare(ref[f], *got, [I32]) == [], f
 
 
 @pytest.mark.gpu
@@ -154,17 +189,29 @@ def test_gpu_tail_call_gate_and_host(built):
     with pytest.raises(batch.WasmEdgeError) as e:
         batch.BatchContext(TAIL, 64, device=0)
     assert e.value.code == 0x37
-    with pytest.raises(batch.WasmEdgeError) as e:
-        batch.BatchContext(HOST_TAIL, 64, device=0, tail_call=True)
-    assert e.value.code == 0x02
     import hostfuncs
+    rows = [[0], [1], [3], [5], [2]]
+    ref = [O.Module(INDIRECT_TRAPS, tail_call=True).run("go", r) for r in rows]
     ctx = batch.BatchContext(INDIRECT_TRAPS, 5, device=0, tail_call=True)
     try:
         hostfuncs.register(ctx)
-        rets, st, cnt = ctx.execute("go", batch.make_values([[0], [1], [3], [5], [2]], [I32]), 1)
-        assert [int(s) for s in st] == [0, 0x8C, 0x8A, 0x8B, 0xB2]
+        rets, st, cnt = ctx.execute("go", batch.make_values(rows, [I32]), 1)
+        got = [[int(x) for x in r] for r in batch.ret_ints(rets)]
+        assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32], check_hash=False) == []
+        assert [int(s) for s in st] == [0, 0x8C, 0x8A, 0x8B, 0x8D]
     finally:
         ctx.close()
+    # host imports in tail position: entry frame = the reference, nested = the twin
+    hrows, href = _host_tail_refs()
+    for f in ("go", "go_ind", "outer"):
+        ctx = batch.BatchContext(HOST_TAIL, len(hrows), device=0, tail_call=True)
+        try:
+            hostfuncs.register(ctx)
+            rets, st, cnt = ctx.execute(f, batch.make_values(hrows, [I32]), 1)
+            got = [[int(x) for x in r] if st[i] == 0 else [] for i, r in enumerate(batch.ret_ints(rets))]
+            assert compare(href[f], got, st, cnt, ctx.memory_hash(), [I32], check_hash=False) == [], f
+        finally:
+            ctx.close()
 
 
 # A direct call to a function defined AFTER its caller must zero the callee's locals too

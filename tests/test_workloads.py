@@ -106,12 +106,11 @@ def test_gpu_blake3_64k(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", ["0", "1", "4", "nosimt", "scan", "trip", "notrip"])
+@pytest.mark.parametrize("sched", ["0", "1", "4", "nosimt", "trip", "notrip"])
 def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
     """The wave scheduler only decides which lanes run together: the kernel's min-pc (0)
     and loop-aware largest-group policies (1, 4) between core calls, SIMT scheduling inside
-    the compiled runs (default) or not (nosimt: WB_SIMT=0), with or without the unrolled
-    scan loops (scan: WB_SCAN=1), trip mode forced on or off (WB_TRIP, jit.cpp "Trip
+    the compiled runs (default) or not (nosimt: WB_SIMT=0), trip mode forced on or off (WB_TRIP, jit.cpp "Trip
     mode": every lane runs its own compiled run in each trip), must give identical per-lane
     results on the divergent workloads (recursion with per-lane depth, quicksort with
     per-lane data, Collatz's br_table state machine with traps, Mandelbrot's per-lane
@@ -120,8 +119,6 @@ def test_gpu_scheduler_policies_bit_exact(built, sched, monkeypatch):
         monkeypatch.setenv("WB_TRIP", "1" if sched == "trip" else "0")
     elif sched == "nosimt":
         monkeypatch.setenv("WB_SIMT", "0")
-    elif sched == "scan":
-        monkeypatch.setenv("WB_SCAN", "1")
     else:
         monkeypatch.setenv("WB_SCHED", sched)
     cases = _cases()
@@ -262,9 +259,6 @@ def test_gpu_memory_granules_bit_exact(built, granule):
 ENGINES = {
     "simt": {},                                   # V frames, compiled runs, SIMT scheduling
     "trip": {"WB_TRIP": "1"},                     # V frames, trip mode
-    "half": {"WB_HALF": "1"},                     # half waves (32 lanes per launch wave)
-    "halftrip": {"WB_HALF": "1", "WB_TRIP": "1"},
-    "lsched": {"WB_LSCHED": "1"},                 # the pick by distinct-pc enumeration
     "nosimt": {"WB_SIMT": "0"},                   # V frames, compiled runs without SIMT
     "nojit": {"WB_JIT": "0"},                     # V frames, threaded core handlers only
     "lds": {"WB_VFRAME": "0"},                    # LDS frames, threaded core

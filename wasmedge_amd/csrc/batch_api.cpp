@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "batch_ctx.h"
+#include "build/srchash.h"
 #include "jit.h"
 #include "tc_slots.h"
 
@@ -225,9 +226,6 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
         C->jit_runs = uint32_t(runs.size());
         C->simt = want_simt;
         C->trip = want_trip;
-        // half waves (KParams::half): WB_HALF=1 (experiment)
-        const char *hw = getenv("WB_HALF");
-        C->half = want_simt && hw && hw[0] == '1';
       } else {
         C->last_error = err;
       }
@@ -257,7 +255,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // at the occupancy this batch reaches (nwaves over 256 CUs, at most 16 waves per CU)
   {
     const uint32_t tc = C->frame_hbm ? 0 : P.total_cells() ? P.total_cells() : 1;
-    const uint32_t lw = C->nwaves << (C->half ? 1 : 0);   // launch waves
+    const uint32_t lw = C->nwaves;   // launch waves
     const uint32_t per_cu = std::min<uint32_t>(C->vframe ? 8 : 16, std::max<uint32_t>(4, (lw + 255) / 256));
     const uint32_t wave_cells = (160 * 1024 - 1024) / 256 / per_cu;   // 256 B per cell row
     uint32_t s = wave_cells > tc + 1 ? wave_cells - tc - 1 : 0;
@@ -351,7 +349,6 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.sched = C->sched;
   k.loops = C->loops.ptr;
   k.simt = C->simt && k.tcode ? 1u : 0u;
-  k.half = C->half && k.simt && !k.hframe ? 1u : 0u;
   k.stats = C->stats;
 #ifdef WB_STATS
   (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 16 + 1024) * sizeof(uint64_t), C->stream);
@@ -362,7 +359,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     return C->fail(kRuntimeError, "internal: LDS share of a wave exceeds 160 KiB");
   uint32_t wpb = 4;
   while (wpb > 1 && wave_lds * wpb + 256 > 160 * 1024) wpb >>= 1;
-  uint32_t blocks = ((C->nwaves << k.half) + wpb - 1) / wpb;
+  uint32_t blocks = (C->nwaves + wpb - 1) / wpb;
   // persistent waves when the batch has more waves than the device holds at once (C5: 4,096
   // waves, 2 per SIMD): as many blocks as fit, each wave taking the next batch wave when
   // its own ends (batch_kernel.hip next_wave); WB_PERSIST=0 launches a wave per batch wave
@@ -841,6 +838,10 @@ WasmEdge_Result WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *M, cons
 }
 
 uint32_t WasmEdge_BatchGetInstanceCount(const WasmEdge_BatchContext *C) { return C ? C->n : 0; }
+
+// the marker keeps the hash findable in the file without loading it (srchash.py)
+static const char kBuildHash[] = "WB_SRC_HASH=" WB_SRC_HASH;
+const char *WasmEdge_BatchGetBuildHash(void) { return kBuildHash + 12; }
 
 
 uint32_t WasmEdge_BatchGetCodeSize(const WasmEdge_BatchContext *C) {

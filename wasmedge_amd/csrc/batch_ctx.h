@@ -82,7 +82,6 @@ struct WasmEdge_BatchContext {
   bool threaded = true;
   bool vframe = false;            // threaded core with the frame in VGPRs (wb_exec_vf_kernel)
   uint32_t jit_runs = 0;          // compiled straight-line runs (jit.h)
-  bool half = false;              // KParams::half: a batch wave runs as two launch waves
   bool simt = false;              // KParams::simt: the compiled runs schedule diverged lanes
   bool trip = false;              // ... in trip mode (jit.h)
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe

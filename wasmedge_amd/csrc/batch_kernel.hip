@@ -319,7 +319,7 @@ template <bool VF, bool PG, class Frame>
 __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_t inst,
                                        uint32_t *const gs, const GMem mem,
                                        uint32_t *const ls, uint32_t *const fs,
-                                       lds_u32 *const stk, const bool own = true) {
+                                       lds_u32 *const stk) {
   // the bytecode is read through the constant address space so every fetch is one
   // scalar s_load_dwordx4 (uniform pc) instead of a vector load + readfirstlanes
   typedef uint32_t w4 __attribute__((ext_vector_type(4)));
@@ -350,9 +350,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define TSIZE(t) LS(p.ls_tab + (t))
 #define TENT(t, i) lt[(size_t)(p.tabinfo[2u * (t)] + (i)) << 6]
 #define EDROP LS(p.ls_tab + p.ntables)
-  // (own: the lane belongs to this launch wave -- half waves run a batch wave's lanes in
-  // two launch waves, KParams::half)
-  uint32_t status = own && inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
+  uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   // `pages` = the lane's pages in the reserved layout, min(its memory size, rpages): the
   // bound of every fast path. The size itself is LS_PAGES (memory.grow writes it there),
   // read where it can exceed rpages (MEM_PAGES).
@@ -371,7 +369,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   if (status == WB_STATUS_RUNNING && istatus) status = istatus;   // instance never came up
   for (uint32_t c = 0; c < p.global_cells; c++) F.set(c, LS(LS_GLOBALS + c));
   uint32_t ycall = 0, ybase = 0;   // host import being called when the lane yields
-  bool active = own && inst < p.n;   // this launch owns the lane's outputs
+  bool active = inst < p.n;   // the lane has an instance (partial waves)
   if (p.resume) {
     // continue a lane parked at a host import: frame from fsave, the host function's
     // results (hcall = their cell count, ~0 = the host ended the lane) into its cells
@@ -399,6 +397,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t tpoll = t0 - 1000u;   // the last read of the interrupt flag (100 MHz ticks)
 #ifdef WB_STATS
   uint64_t *const stw = p.stats ? p.stats + (size_t)(inst >> 6) * ST_N : nullptr;
 #endif
@@ -737,13 +736,18 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef WB_GROW
     }
     WB_STAT_ADD(ST_CYC_SLOW, WB_NOW() - ts2);
-    // budget, wall clock, and the host's interrupt request (every round: a core call
-    // returns at least every 2^20 instructions), read from uncached device memory at
-    // system scope -- the reference's StopToken, checked on every branch, call and return
-    // (helper.cpp:24-27,184-187, controlInstr.cpp:75-78)
-    const bool stop = __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (status == WB_STATUS_RUNNING &&
-        (count >= p.max_steps || __builtin_amdgcn_s_memrealtime() - t0 > p.max_ticks || stop))
+    // budget, wall clock, and the host's interrupt request (a core call returns at least
+    // every 2^20 instructions) -- the reference's StopToken, checked on every branch, call
+    // and return (helper.cpp:24-27,184-187, controlInstr.cpp:75-78). The flag is an
+    // uncached system-scope read: at most one per 10 us of the wave's time (a round can be
+    // a single slow-step instruction), so a request lands within 10 us + one round.
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    bool stop = false;
+    if (now - tpoll >= 1000u) {
+      tpoll = now;
+      stop = __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (status == WB_STATUS_RUNNING && (count >= p.max_steps || now - t0 > p.max_ticks || stop))
       status = WB_ERR_INTERRUPTED;
   }
 #undef R32
@@ -794,7 +798,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 // block ends. Every instance-state buffer is indexed by the batch wave, so which launch
 // wave runs it does not matter. ~0: none left.
 __device__ __forceinline__ uint32_t next_wave(const KParams &p, uint32_t &turn) {
-  const uint32_t nwaves = ((p.n + 63u) >> 6) << p.half;
+  const uint32_t nwaves = (p.n + 63u) >> 6;
   if (!p.wave_ctr) return turn++ ? 0xFFFFFFFFu : (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   uint32_t w = 0;
   if ((threadIdx.x & 63u) == 0) w = __hip_atomic_fetch_add(p.wave_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -810,16 +814,12 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
   // LDS call-stack slots of this wave follow the frames of all the block's waves
   lds_u32 *const stk = (lds_u32 *)(lds + ((((blockDim.x >> 6) * p.total_cells) + wib * p.gs_lds) << 6) + lane);
   uint32_t turn = 0;
-  for (uint32_t lw; (lw = next_wave(p, turn)) != 0xFFFFFFFFu;) {
-    // half waves: launch wave lw runs lanes [32 (lw & 1), +32) of batch wave lw >> 1
-    const uint32_t wave = lw >> p.half;
-    const bool own = !p.half || (lane >> 5) == (lw & 1u);
+  for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
     interp<VF, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
                p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
-               p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk,
-               own);
+               p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
   }
 }
 

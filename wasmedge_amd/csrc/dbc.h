@@ -167,8 +167,6 @@ struct DFunc {
 #define WB_STATUS_OK 0x00u
 #define WB_ERR_INTERRUPTED 0x07u        // ErrCode::Interrupted (fuel / time limit)
 #define WB_ERR_STACK_EXHAUSTED 0xB0u    // device call stack full (no reference code)
-#define WB_ERR_TAIL_HOST 0xB2u          // return_call_indirect reached a host import (not
-                                        // supported: see DESIGN.md "Tail calls")
 #define WB_ERR_HOST_CALL 0xB1u          // lane yielded at a host import; BatchRun's host loop
                                         // services it and resumes the lane. It stays the
                                         // final status only when no host function is

@@ -1074,8 +1074,6 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
           for (size_t k = 0; k < args.size(); k++)
             if (args[k].var) set_var_local(callee, uint32_t(k));
         if (live()) {
-          if (!ind && P.funcs[callee].imported)
-            fail(E_UNSUPPORTED, "return_call to a host import is not supported by the batched path");
           for (auto &e : args) st.push_back(e);
           materialize_top(args.size());
           uint32_t argcells = 0;
@@ -1087,8 +1085,29 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
             if (ic + 1 > max_cell) max_cell = ic + 1;
           }
           st.resize(st.size() - args.size());
+          uint32_t rc = 0;
+          for (uint8_t rt : t.results) rc += cells_of(rt);
+          // A host import called in tail position runs in the caller's reused frame, which
+          // it then pops (helper.cpp:35-97 with IsTailCall, stackmgr.h:80-112): its results
+          // leave like a `return`. The reference resumes at the frame's From, which a
+          // native frame stores one instruction early (helper.cpp:163, RetIt - 1): from the
+          // entry function that re-executes the function's final `end` (counted and priced,
+          // then the run ends with the host's results), so the RET here retires one `end`.
+          // (From a nested frame the reference would re-execute its caller's call
+          // instruction instead; this returns to the caller -- DESIGN.md "Tail calls".)
+          // return_call_indirect may reach a host import at run time: its RET follows it,
+          // reached only then (dbc_step.inc).
+          auto host_ret = [&]() {
+            pending += 1;
+            pend_ops.push_back(0x0B);
+            emit(OP_RET, L, rc);
+          };
           if (ind) {
             emit(OP_TAIL_CALL_INDIRECT, L, argcells, ic, tab, P.type_canon[ti]);
+            host_ret();
+          } else if (P.funcs[callee].imported) {
+            emit(OP_HOST_CALL, L, argcells, rc, 0, callee);
+            host_ret();
           } else {
             emit(OP_TAIL_CALL, L, argcells, P.funcs[callee].local_cells, 0, 0);
             callfix->push_back(CallFix{uint32_t(last_emit), callee});
@@ -1913,6 +1932,9 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
       // local cells (the locals the call zeroes: helper.cpp:155-161) only now
       for (auto &c : callfix) {
         DInstr &I = P.code[c.instr];
+        // (the c field is 16 bits, as emit() checks for cell indices)
+        if (P.funcs[c.callee].local_cells > 0xFFFFu)
+          throw Err{E_UNSUPPORTED, "callee locals exceed the DBC encoding (65535 cells)"};
         I.w3 = P.funcs[c.callee].body_pc;
         I.w2 = (I.w2 & 0xFFFF0000u) | P.funcs[c.callee].local_cells;
       }

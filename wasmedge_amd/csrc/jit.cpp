@@ -1818,77 +1818,6 @@ void sched_block(Em &e, const std::string &p, const char *mask, bool depth = fal
   // interrupts) even if the lanes retired nothing
   e.l("s_sub_u32 s64, s64, 16");
   e.l("s_cselect_b32 s64, 0, s64");
-  const char *lse = getenv("WB_LSCHED");
-  if (!mask && lse && lse[0] == '1') {
-    // (A/B variant) the pick by enumerating the distinct pcs of ALL: each round takes the
-    // first remaining lane's pc and the lanes at it, keeping the lowest two pcs -- no wave
-    // reductions; a round per distinct pc
-    e.l("s_mov_b64 exec, s[96:97]");
-    e.l("s_waitcnt lgkmcnt(0)");            // (a TInstr prefetch into s[76:91] must land)
-    e.l("s_mov_b64 s[76:77], s[96:97]");    // lanes not yet visited
-    e.l("s_mov_b32 s82, -1");               // lowest pc
-    e.l("s_mov_b32 s83, -1");               // the next lowest
-    e.l("%s_lp:", p.c_str());
-    e.l("s_ff1_i32_b64 s78, s[76:77]");
-    e.l("s_nop 0");
-    e.l("v_readlane_b32 s79, %s, s78", VPC);
-    e.l("s_nop 1");
-    e.l("v_cmp_eq_u32_e64 s[80:81], s79, %s", VPC);
-    e.l("s_and_b64 s[80:81], s[80:81], s[76:77]");
-    e.l("s_andn2_b64 s[76:77], s[76:77], s[80:81]");
-    e.l("s_cmp_lt_u32 s79, s82");
-    e.l("s_cbranch_scc0 %s_nm", p.c_str());
-    e.l("s_mov_b32 s83, s82");
-    e.l("s_mov_b32 s82, s79");
-    e.l("s_mov_b64 s[74:75], s[80:81]");    // the group: the lanes at the lowest pc
-    e.l("s_branch %s_nx", p.c_str());
-    e.l("%s_nm:", p.c_str());
-    e.l("s_min_u32 s83, s83, s79");
-    e.l("%s_nx:", p.c_str());
-    e.l("s_cmp_lg_u64 s[76:77], 0");
-    e.l("s_cbranch_scc1 %s_lp", p.c_str());
-    e.l("s_lshl_b32 s62, s82, 5");
-    e.l("s_cmp_eq_u32 s95, -1");            // were the banks converged?
-    e.l("s_cselect_b32 s69, 1, 0");
-    e.l("s_cmp_eq_u32 s83, -1");
-    e.l("s_mov_b32 s63, -1");
-    e.l("s_cbranch_scc1 %s_lc", p.c_str());
-    e.l("s_lshl_b32 s63, s83, 5");
-    e.l("%s_lc:", p.c_str());
-    e.l("s_load_dwordx8 s[76:83], s[60:61], s62");
-    e.l("s_load_dwordx8 s[84:91], s[60:61], s62 offset:0x20");
-    e.l("s_cmp_eq_u32 s63, -1");
-    e.l("s_cbranch_scc1 %s_conv", p.c_str());
-    e.l("s_mov_b32 s95, s63");
-    e.l("s_cmp_eq_u32 s69, 0");
-    e.l("s_cbranch_scc1 %s_disp", p.c_str());
-    e.l("s_add_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // C -> D banks
-    e.l("s_addc_u32 s71, s71, 0");
-    e.l("s_branch %s_bankb", p.c_str());
-    e.l("%s_conv:", p.c_str());
-    e.l("s_mov_b32 s63, -1");
-    e.l("s_mov_b32 s95, -1");
-    e.l("s_cmp_eq_u32 s69, 1");
-    e.l("s_cbranch_scc1 %s_disp", p.c_str());
-    e.l("s_sub_u32 s70, s70, 0x%x", 2u * TC_BANK_BYTES);  // D -> C banks
-    e.l("s_subb_u32 s71, s71, 0");
-    e.l("%s_bankb:", p.c_str());
-    e.l("s_add_u32 s72, s70, 0x%x", TC_BANK_BYTES);
-    e.l("s_addc_u32 s73, s71, 0");
-    e.l("%s_disp:", p.c_str());
-    e.l("s_mov_b64 exec, s[74:75]");
-    e.l("s_cmp_eq_u32 s64, 0");
-    e.l("s_cbranch_scc1 %s_out", p.c_str());
-    e.l("s_waitcnt lgkmcnt(0)");
-    e.l("s_add_u32 s68, s70, s76");
-    e.l("s_addc_u32 s69, s71, 0");
-    e.l("s_setpc_b64 s[68:69]");
-    e.l("%s_out:", p.c_str());
-    e.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
-    e.l("s_addc_u32 s69, s71, 0");
-    e.l("s_setpc_b64 s[68:69]");
-    return;
-  }
   if (!mask && depth) {
     // Recursive modules (jit_source: depth_pick): the group is every lane at the pc of the
     // lane lowest in its call stack (fewest stack slots; ties: the lowest pc). LOW = the
@@ -2045,19 +1974,13 @@ std::string simt_sched(bool hybrid, bool depth) {
   return e.o;
 }
 
-// ---------------------------------------------------------------- SIMT scan loops
+// ---------------------------------------------------------------- scan loops
 // A run that IS a load-scan loop (Hoare partition's `while (a[i] < p) i++`): exactly
 //   x += d (I32_ADD_I / I32_SUB_I in place, d a multiple of 4, |d| <= 64)
 //   y = i32.load(x + off)
 //   br_<cmp> y, p (or p, y; p loop-invariant; an immediate form) back to the run's start
-// can run kScanUnroll iterations per trip (SIMT only, opt-in: WB_SCAN=1, see jit_source):
-// every lane's next kScanUnroll loads go
-// out together (one memory latency instead of one per iteration), then each lane's exit
-// iteration is found in order. A lane that leaves at iteration j gets x + d*j, the j-th
-// value and j iterations' count (j - 1 taken) and waits at the fall-through pc; the lanes
-// still looping go round again. Any lane whose kScanUnroll loads are not all in bounds and
-// aligned runs the plain run instead (which meets the failing access itself).
-constexpr uint32_t kScanUnroll = 8;
+// runs kTripScan iterations per trip in trip mode (trip_scan_stage): every lane's next
+// loads go out together, then each lane's exit iteration is found in order.
 constexpr uint32_t kTripScan = 4;   // trip mode: scan iterations per trip (trip_scan_stage)
 struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
 
@@ -2083,7 +2006,7 @@ bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
   } else {
     return false;
   }
-  if (uint64_t(i1.w3) + 64u * kScanUnroll + 4 > 0xFFFFFFFFull) return false;
+  if (uint64_t(i1.w3) + 64u * 2 * kTripScan + 4 > 0xFFFFFFFFull) return false;   // (the window, with room)
   *sl = ScanLoop{x, y, i1.w3, o0 == OP_I32_ADD_I ? int32_t(i0.w3) : -int32_t(i0.w3), y_first};
   return true;
 }
@@ -2102,82 +2025,6 @@ void scan_cond(Em &e, const DInstr &I, const ScanLoop &sl, const char *val) {
   }
 }
 
-// the block at the run's start (label Lb<K>); the plain run follows at Lbo<K>
-void scan_loop_block(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl,
-                     const std::string &K) {
-  const uint32_t U = kScanUnroll, fall = r.pc + 3;
-  const DInstr &br = P.code[r.pc + 2];
-  const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
-  const uint32_t x = sl.x, y = sl.y;
-  static const char *const T[kScanUnroll] = {"v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115"};
-  e.l("Lb%s:", K.c_str());
-  flush(e);   // counts per lane from here
-  // the window: bytes (x + d*j) + off .. +3 for j = 1..U, in bounds and aligned, x + d*j
-// not wrapping (the loop's i32.add / i32.sub wraps; the 33-bit address sum does not)
-  const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
-  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(x));
-  e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
-  e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
-  e.l("s_or_b64 %s, %s, vcc", T2, T2);
-  e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(x));
-  if (sl.d < 0) {   // x itself must not wrap below 0 (i32.sub), whatever the offset
-    e.l("v_cmp_gt_u32_e32 vcc, 0x%x, %s", uint32_t(-sl.d) * U, e.v(x));
-    e.l("s_or_b64 %s, %s, vcc", T2, T2);
-  }
-  e.l("v_and_b32_e32 %s, 3, %s", Y1, Y0);
-  e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y1);
-  e.l("s_or_b64 %s, %s, vcc", T2, T2);
-  e.l("s_and_b64 %s, %s, exec", T2, T2);
-  e.l("s_cbranch_scc1 Lbo%s", K.c_str());
-  for (uint32_t j = 1; j <= U; j++) {
-    e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(x));
-    if (e.g == 0) {
-      e.l("v_mov_b32 %s, %s", W0, Y0);
-      e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
-      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-    } else {
-      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
-      e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
-      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-      e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
-      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
-    }
-    e.l("global_load_dword %s, %s, off", T[j - 1], XP);
-  }
-  e.l("s_waitcnt vmcnt(0)");
-  // exits in iteration order; s[74:75] = the lanes still looping
-  e.l("s_mov_b64 s[74:75], exec");
-  for (uint32_t j = 1; j <= U; j++) {
-    const std::string nx = "Lsn" + K + "_" + std::to_string(j);
-    scan_cond(e, br, sl, T[j - 1]);
-    e.l("s_andn2_b64 s[68:69], s[74:75], vcc");   // leave in this iteration
-    e.l("s_and_b64 s[74:75], s[74:75], vcc");
-    e.l("s_cmp_eq_u64 s[68:69], 0");
-    e.l("s_cbranch_scc1 %s", nx.c_str());
-    e.l("s_mov_b64 exec, s[68:69]");
-    e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(j)), e.v(x));
-    e.l("v_mov_b32 %s, %s", e.v(y), T[j - 1]);
-    e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(int32_t(j * r.cnt) + int32_t(j - 1) * tcnt), VCNT);
-    e.l("v_mov_b32 %s, 0x%x", VPC, fall);
-    e.l("s_mov_b64 exec, s[74:75]");
-    e.l("%s:", nx.c_str());
-  }
-  // the lanes still looping: U iterations done, go round
-  e.l("s_mov_b64 exec, s[74:75]");
-  e.l("s_cbranch_execz Lsd%s", K.c_str());
-  const uint32_t per = U * uint32_t(int32_t(r.cnt) + tcnt);
-  e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(U)), e.v(x));
-  e.l("v_mov_b32 %s, %s", e.v(y), T[U - 1]);
-  e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, per, VCNT);
-  e.l("s_sub_u32 s64, s64, 0x%x", per);
-  e.l("s_cselect_b32 s64, 0, s64");
-  e.l("s_cmp_eq_u32 s64, 0");
-  e.l("s_cbranch_scc0 Lb%s", K.c_str());
-  e.l("v_mov_b32 %s, 0x%x", VPC, r.pc);   // budget spent: to the kernel through Lsched
-  e.l("Lsd%s:", K.c_str());
-  long_jump(e, "Lsched", "Lsq" + K);
-  e.l("Lbo%s:", K.c_str());
-}
 
 // the cells an instruction writes, exactly for the 32-bit results (written() counts c + 1
 // too; true), else as written() (false)
@@ -3309,23 +3156,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     const std::string K = std::to_string(k) + (var == 1 ? "c" : var == 2 ? "p" : "");
     if (!nob.empty()) e.nanobs = &nob;
     e.l(".p2align 6");
-    ScanLoop sl;
-    // Scan blocks are opt-in (WB_SCAN=1; WB_SCAN=p+1: only the loop at pc p): measured on
-    // C3 they do not pay (4K elements: 1.23e11 instr/s with, 1.26e11 without) -- Hoare
-    // scans over random data stop after ~2 iterations, so the 8 speculative loads and the
-    // exit search cost more than the latency they hide.
-    const char *sce = getenv("WB_SCAN");
-    const bool scan = var == 0 && simt && !cost && sce && atoi(sce) >= 1 &&
-                      (atoi(sce) == 1 || uint32_t(atoi(sce)) == r.pc + 1) && scan_loop_of(P, r, &sl);
-    if (scan) {
-      e.g = glog;
-      e.fb = P.global_cells;
-      e.prog = &P;
-      e.run = uint32_t(k);
-      scan_loop_block(e, P, r, sl, K);   // its own label Lb<K>; the plain run at Lbo<K>
-    } else {
-      e.l("Lb%s:", K.c_str());
-    }
+    e.l("Lb%s:", K.c_str());
     const DInstr &last = P.code[r.pc + r.len - 1];
     const uint16_t lop = op_of(last);
     // Where the run goes on: the instruction after it (fall-through, untaken branch), a
@@ -3369,7 +3200,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       inline_of(k, &f0, &p0);
       const DInstr &first = P.code[r.pc];
       const uint32_t fbc = P.global_cells;
-      if (!scan && !inl_target[k] && f0 < 0 && lop == OP_CALL && r.len >= 2 &&
+      if (!inl_target[k] && f0 < 0 && lop == OP_CALL && r.len >= 2 &&
           op_of(first) == OP_POST_CALL && (first.w1 & 0xFFFFu) >= fbc &&
           (last.w1 & 0xFFFFu) >= fbc) {
         const uint32_t pop = (first.w1 & 0xFFFFu) - fbc, push = (last.w1 & 0xFFFFu) - fbc + 1;
@@ -3560,18 +3391,11 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       const size_t body2 = ei.o.size();
       const bool fc = fwd && var == 1;   // the forwarding copy: the callee's loads from F
       int64_t renamed = -1;              // the stack cell computed into a word's VGPR
-      // constant-address stores in the copy (WB_CST_STORE=1, opt-in until measured; else
-      // through the cell, as the first trip); cst_win: the 4 KiB window whose base is in XP, or -1
-      const bool cst_store = getenv("WB_CST_STORE") && getenv("WB_CST_STORE")[0] == '1';
-      int64_t cst_win = -1;
       std::vector<std::pair<uint32_t, uint32_t>> deferred;   // (cell, VGPR) read, then written
       const std::vector<LoadBatch> batches2 = batching && !fc ? load_batches(P, rf, rf.len - 1, lead2)
                                                               : std::vector<LoadBatch>();
       size_t nb2 = 0;
-      bool prev_cst = false;
       for (uint32_t i = 0; i + 1 < rf.len; i++) {
-        if (!prev_cst) cst_win = -1;   // (XP is a temporary of every other instruction)
-        prev_cst = false;
         if (nb2 < batches2.size() && batches2[nb2].i0 == i) {
           const LoadBatch &b = batches2[nb2++];
           emit_batch(ei, P, rf.pc, b, groups2, lead2);
@@ -3634,30 +3458,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
             if (ei.group) group_base(ei, *ei.group);
             ei.group = nullptr;
           }
-          if (fc && ei.g != 0 && cst_store) {
-            // the copy's store goes to a constant address: its granule row and byte are
-            // known here, so the address is MEM + a constant (an immediate offset when it
-            // fits, else one add per 4 KiB window, shared by the next stores)
-            const uint64_t A = uint64_t(fa), gb = 4ull << ei.g;
-            const uint64_t Lo = ((A >> (2 + ei.g)) << (8 + ei.g)) + (A & (gb - 1));
-            ei.drain();
-            if (Lo <= 4095) {
-              ei.l("global_store_dword %s, %s, off offset:%u", MEM, fr.c_str(), uint32_t(Lo));
-            } else {
-              const uint64_t hi = Lo & ~0xFFFull;
-              if (int64_t(hi) != cst_win) {
-                ei.l("v_add_co_u32_e32 %s, vcc, 0x%x, v106", X0, uint32_t(hi));
-                ei.l("v_addc_co_u32_e32 %s, vcc, 0x%x, v107, vcc", X1, uint32_t(hi >> 32));
-                cst_win = int64_t(hi);
-              }
-              ei.l("global_store_dword %s, %s, off offset:%u", XP, fr.c_str(), uint32_t(Lo - hi));
-            }
-            ei.nvm++;
-            prev_cst = true;
-          } else {
-            emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
-            cst_win = -1;
-          }
+          emit_store(ei, OP_ST32, I.w1 & 0xFFFFu, I.w1 >> 16, I.w3, fr.c_str());
           ei.done += (I.w0 >> 16) & 0xFFu;
           continue;
         }

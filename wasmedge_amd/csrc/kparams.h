@@ -83,10 +83,6 @@ struct KParams {
   const uint32_t *loops;        // per pc: innermost loop (head, end), ~0 = none
   uint32_t *wave_ctr;           // persistent waves: the next wave to run (NULL: one launch
                                 // wave per wave of the batch, the block's own)
-  uint32_t half;                // 1: half waves -- every batch wave runs as two launch waves
-                                // of 32 lanes each (its lanes [0,32) and [32,64)), twice the
-                                // waves per SIMD for latency-bound modules (exec kernels
-                                // only; the HBM-frame kernel always runs whole waves)
   uint32_t simt;                // V frames + compiled runs: every running lane enters the
                                 // core, whose compiled runs schedule the lanes among
                                 // themselves (jit.cpp Lsched); the C++ loop only serves
