@@ -125,7 +125,31 @@ typedef struct WasmEdge_BatchConfigure {
   /* Cap on the device memory committed for grown pages (bytes; 0 = until hipMalloc fails).
    * A grow that would need more returns -1. */
   uint64_t MemoryPoolBytes;
+  /* Devices the batch spreads over from this one process (SURVEY.md 8(b) NumDevices, 8(e)).
+   * DeviceCount 0 or 1: one device, DeviceOrdinal. More: Devices[0..DeviceCount) are HIP
+   * ordinals -- a device may repeat (several shards on one device) -- and instance ids go to
+   * them by Partition: WASMEDGE_BATCH_PARTITION_BLOCKS, contiguous blocks of whole waves, or
+   * WASMEDGE_BATCH_PARTITION_INTERLEAVE, id mod DeviceCount (evens out work that varies
+   * with the id). Every call then drives every shard -- one host thread and one stream per
+   * shard, no collective -- and gathers per-instance outputs into the caller's
+   * [NumInstances] arrays in instance order (WasmEdge_BatchPlacement gives the map).
+   * Results never depend on it; like the reference's concurrent VM::execute
+   * (include/vm/vm.h:137-141), host functions are called from one shard at a time unless
+   * HostThreads > 1. */
+  const int32_t *Devices;
+  uint32_t DeviceCount;
+  uint32_t Partition;
 } WasmEdge_BatchConfigure;
+
+#define WASMEDGE_BATCH_PARTITION_BLOCKS 0u
+#define WASMEDGE_BATCH_PARTITION_INTERLEAVE 1u
+
+/* Where instance Inst of a NumInstances-instance batch over DeviceCount devices runs: the
+ * index into Devices (*Shard) and its lane on that device (*Local). No device is touched.
+ * WrongVMWorkflow (0x04) for Inst >= NumInstances, DeviceCount 0 or an unknown Partition. */
+WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchPlacement(uint32_t NumInstances, uint32_t DeviceCount,
+                                                          uint32_t Partition, uint32_t Inst,
+                                                          uint32_t *Shard, uint32_t *Local);
 
 #ifdef WASMEDGE_C_API_H
 /* The reference's configuration object as a batch configuration (header-inline: needs the

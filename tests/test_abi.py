@@ -108,9 +108,10 @@ def test_ctypes_layouts_match_the_header(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "%s/include/wasmedge_batch.h"\n'
                    'int main(void) {\n'
-                   '  printf("%%zu %%zu %%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchConfigure),\n'
+                   '  printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchConfigure),\n'
                    '         offsetof(WasmEdge_BatchConfigure, CostTable), offsetof(WasmEdge_BatchConfigure, MemoryGranule),\n'
-                   '         offsetof(WasmEdge_BatchConfigure, HostThreads), offsetof(WasmEdge_BatchConfigure, MemoryPoolBytes));\n'
+                   '         offsetof(WasmEdge_BatchConfigure, HostThreads), offsetof(WasmEdge_BatchConfigure, MemoryPoolBytes),\n'
+                   '         offsetof(WasmEdge_BatchConfigure, Devices), offsetof(WasmEdge_BatchConfigure, Partition));\n'
                    '  printf("%%zu %%zu %%zu\\n", sizeof(WasmEdge_BatchImport), offsetof(WasmEdge_BatchImport, Value),\n'
                    '         offsetof(WasmEdge_BatchImport, Mutable));\n'
                    '  printf("%%zu\\n", sizeof(WasmEdge_Value));\n'
@@ -120,7 +121,7 @@ def test_ctypes_layouts_match_the_header(tmp_path):
     got = [list(map(int, line.split())) for line in subprocess.check_output([str(exe)]).decode().splitlines()]
     C, I = b._Conf, b._Import
     assert got[0] == [ctypes.sizeof(C), C.CostTable.offset, C.MemoryGranule.offset, C.HostThreads.offset,
-                      C.MemoryPoolBytes.offset]
+                      C.MemoryPoolBytes.offset, C.Devices.offset, C.Partition.offset]
     assert got[1] == [ctypes.sizeof(I), I.Value.offset, I.Mutable.offset]
     assert got[2] == [ctypes.sizeof(b._Value)]
 

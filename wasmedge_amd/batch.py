@@ -60,7 +60,20 @@ class _Conf(ctypes.Structure):
                 ("HostThreads", ctypes.c_uint32), ("CostTable", ctypes.c_void_p),
                 ("CostTableLen", ctypes.c_uint32), ("MemoryGranule", ctypes.c_uint32),
                 ("TailCall", ctypes.c_uint32), ("MemoryReservePages", ctypes.c_uint32),
-                ("MemoryPoolBytes", ctypes.c_uint64)]
+                ("MemoryPoolBytes", ctypes.c_uint64), ("Devices", ctypes.POINTER(ctypes.c_int32)),
+                ("DeviceCount", ctypes.c_uint32), ("Partition", ctypes.c_uint32)]
+
+PARTITION_BLOCKS, PARTITION_INTERLEAVE = 0, 1
+
+
+def placement(n, device_count, partition, inst):
+    """(shard, lane) of instance `inst` in an n-instance batch over device_count devices
+    (WasmEdge_BatchPlacement; no device needed)."""
+    g, l = ctypes.c_uint32(), ctypes.c_uint32()
+    r = lib().WasmEdge_BatchPlacement(n, device_count, partition, inst, ctypes.byref(g), ctypes.byref(l))
+    if r.Code:
+        raise WasmEdgeError(r.Code, "placement")
+    return g.value, l.value
 
 
 class _String(ctypes.Structure):
@@ -165,6 +178,8 @@ def lib():
             f = getattr(L, name)
             f.restype = _Result
             f.argtypes = args
+        L.WasmEdge_BatchPlacement.restype = _Result
+        L.WasmEdge_BatchPlacement.argtypes = [u32, u32, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.WasmEdge_BatchInterrupt.restype = None
         L.WasmEdge_BatchInterrupt.argtypes = [vp]
         L.WasmEdge_BatchMemoryGetInstance.restype = u32
@@ -220,11 +235,12 @@ class BatchContext:
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
                  memory_granule=0, imports=None, tail_call=False, memory_reserve_pages=0,
-                 memory_pool_bytes=0):
+                 memory_pool_bytes=0, devices=None, partition=PARTITION_BLOCKS):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
         metering is on when cost_limit > 0. max_memory_page 0 = the reference's default
         page limit (65536); memory_reserve_pages / memory_pool_bytes: the device layout of
-        grown memory (WasmEdge_BatchConfigure)."""
+        grown memory (WasmEdge_BatchConfigure). devices: a list of HIP ordinals (repeats
+        allowed) to spread the instances over from this process, by `partition`."""
         L = lib()
         tab = None
         if cost_table is not None:
@@ -233,6 +249,13 @@ class BatchContext:
                      host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
                      len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0,
                      memory_reserve_pages, memory_pool_bytes)
+        if devices is not None and len(devices) == 1:
+            conf.DeviceOrdinal = devices[0]
+        if devices is not None and len(devices) > 1:
+            self._devices = (ctypes.c_int32 * len(devices))(*devices)
+            conf.Devices = self._devices
+            conf.DeviceCount = len(devices)
+            conf.Partition = partition
         res = _Result(0)
         imps = imports or []
         arr = (_Import * max(1, len(imps)))()

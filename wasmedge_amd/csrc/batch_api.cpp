@@ -13,6 +13,7 @@
 #include "batch_ctx.h"
 #include "build/srchash.h"
 #include "jit.h"
+#include "multi.h"
 #include "tc_slots.h"
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
@@ -432,6 +433,8 @@ WasmEdge_BatchContext *WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfi
     if (Res) *Res = R(kWrongVMWorkflow);
     return nullptr;
   }
+  if (Conf && Conf->DeviceCount > 1)   // several devices: a parent over one shard each
+    return wbm::create(*Conf, WasmBuf, WasmLen, NumInstances, Imports, ImportLen, Res);
   auto *C = new WasmEdge_BatchContext();
   if (Conf) C->conf = *Conf;
   else C->conf.DeviceOrdinal = -1;
@@ -466,6 +469,8 @@ WasmEdge_BatchContext *WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfi
 WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_String FuncName,
                                       const WasmEdge_Value *Params, const uint32_t ParamLen) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::set_args(C, FuncName, Params, ParamLen);
+  DevScope dev(C);
   std::string name(FuncName.Buf ? FuncName.Buf : "", FuncName.Length);
   int f = wb::find_export(C->prog, name);
   if (f < 0) return R(C->fail(kFuncNotFound, "function '" + name + "' not found"));
@@ -504,6 +509,8 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
 
 WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeconds) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::reset(C, KernelSeconds);
+  DevScope dev(C);
   const wb::Program &P = C->prog;
   // the whole reserved layout: pages a lane grows into within it must read zero
   const uint32_t init_words = C->mem_words;
@@ -562,6 +569,8 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
 
 WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSeconds) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::run(C, KernelSeconds);
+  DevScope dev(C);
   if (C->func < 0) return R(C->fail(kWrongVMWorkflow, "BatchSetArgs not called"));
   const wb::FuncInfo &F = C->prog.funcs[C->func];
   if (F.imported) return R(C->fail(kRuntimeError, "exported function is a host import"));
@@ -575,6 +584,7 @@ WasmEdge_Result WasmEdge_BatchResults(WasmEdge_BatchContext *C, WasmEdge_Value *
                                       const uint32_t ReturnLen, uint8_t *PerInstance,
                                       uint64_t *InstrCounts) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::results(C, Returns, ReturnLen, PerInstance, InstrCounts);
   if (!C->ran) return R(C->fail(kWrongVMWorkflow, "BatchRun not called"));
   std::vector<uint8_t> st(C->n);
   if (!C->hip_ok(hipMemcpy(st.data(), C->status.ptr, C->n, hipMemcpyDeviceToHost), "status"))
@@ -621,6 +631,8 @@ WasmEdge_Result WasmEdge_BatchExecute(WasmEdge_BatchContext *C, const WasmEdge_S
 
 WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Hashes) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::gather_u64(C, Hashes, WasmEdge_BatchMemoryHash);
+  DevScope dev(C);
   if (!C->settle()) return R(kRuntimeError);
   // the grid covers the largest memory of the batch (a block per page and wave)
   uint32_t maxp = 0;
@@ -642,10 +654,14 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
   return R(0);
 }
 
-uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) { return C ? C->jit_runs : 0; }
+uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) {
+  if (C && !C->shards.empty()) return WasmEdge_BatchGetCompiledRuns(wbm::first(C));
+  return C ? C->jit_runs : 0;
+}
 
 WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *Costs) {
   if (!C || !Costs) return R(kWrongVMWorkflow);
+  if (!C->shards.empty()) return wbm::gather_u64(C, Costs, WasmEdge_BatchGetTotalCosts);
   if (!C->settle()) return R(kRuntimeError);
   const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
   std::vector<uint32_t> lo(size_t(C->nwaves) * 64), hi(lo.size());
@@ -659,6 +675,9 @@ WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *
 }
 
 uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (C && !C->shards.empty()) return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchGetMemoryPages(s, l) : 0;
   if (!C || Inst >= C->n || !C->prog.has_mem || !C->settle()) return 0;
   uint32_t p = 0;
   const size_t at = (size_t(Inst / 64) * C->ls_slots + LS_PAGES) * 64 + Inst % 64;
@@ -669,12 +688,20 @@ uint32_t WasmEdge_BatchGetMemoryPages(WasmEdge_BatchContext *C, uint32_t Inst) {
 WasmEdge_Result WasmEdge_BatchGetMemory(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off,
                                         uint8_t *Dst, uint32_t Len) {
   if (!C) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchGetMemory(s, l, Off, Dst, Len) : R(kRuntimeError);
   return R(mem_rw(C, Inst, Off, Len, Dst, nullptr));
 }
 
 WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off,
                                         const uint8_t *Src, uint32_t Len) {
   if (!C) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchSetMemory(s, l, Off, Src, Len) : R(kRuntimeError);
   return R(mem_rw(C, Inst, Off, Len, nullptr, Src));
 }
 
@@ -713,6 +740,11 @@ extern "C" {
 WasmEdge_Result WasmEdge_BatchTableGetSize(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
                                            uint32_t Inst, uint32_t *Size) {
   if (!C || !Size) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchTableGetSize(s, TableName, l, Size)
+                                       : R(C->fail(kRuntimeError, "instance index out of range"));
   const int t = find_named(C->prog.table_exports, TableName);
   if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
   if (Inst >= C->n) return R(C->fail(kRuntimeError, "instance index out of range"));
@@ -723,6 +755,11 @@ WasmEdge_Result WasmEdge_BatchTableGetSize(WasmEdge_BatchContext *C, const WasmE
 WasmEdge_Result WasmEdge_BatchTableGetData(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
                                            uint32_t Inst, WasmEdge_Value *Data, uint32_t Offset) {
   if (!C || !Data) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchTableGetData(s, TableName, l, Data, Offset)
+                                       : R(C->fail(kRuntimeError, "instance index out of range"));
   uint32_t size = 0;
   WasmEdge_Result r = WasmEdge_BatchTableGetSize(C, TableName, Inst, &size);
   if (r.Code) return r;
@@ -740,6 +777,14 @@ WasmEdge_Result WasmEdge_BatchTableGetData(WasmEdge_BatchContext *C, const WasmE
 WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmEdge_String TableName,
                                            uint32_t Inst, WasmEdge_Value Data, uint32_t Offset) {
   if (!C) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty()) {
+    if (Inst == WASMEDGE_BATCH_ALL_INSTANCES)   // (every shard's bounds first: all or none)
+      return wbm::all(C, [&](WasmEdge_BatchContext *x) { return WasmEdge_BatchTableSetData(x, TableName, Inst, Data, Offset); });
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchTableSetData(s, TableName, l, Data, Offset)
+                                       : R(C->fail(kRuntimeError, "instance index out of range"));
+  }
   const wb::Program &P = C->prog;
   const int t = find_named(P.table_exports, TableName);
   if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
@@ -769,6 +814,11 @@ WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmE
 WasmEdge_Result WasmEdge_BatchGlobalGetValue(WasmEdge_BatchContext *C, const WasmEdge_String GlobalName,
                                              uint32_t Inst, WasmEdge_Value *Value) {
   if (!C || !Value) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchGlobalGetValue(s, GlobalName, l, Value)
+                                       : R(C->fail(kRuntimeError, "instance index out of range"));
   const wb::Program &P = C->prog;
   const int g = find_named(P.global_exports, GlobalName);
   if (g < 0) return R(C->fail(kFuncNotFound, "global export not found"));
@@ -790,6 +840,14 @@ WasmEdge_Result WasmEdge_BatchGlobalGetValue(WasmEdge_BatchContext *C, const Was
 WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchContext *C, const WasmEdge_String GlobalName,
                                              uint32_t Inst, WasmEdge_Value Value) {
   if (!C) return R(kWrongVMWorkflow);
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (!C->shards.empty()) {
+    if (Inst == WASMEDGE_BATCH_ALL_INSTANCES)
+      return wbm::all(C, [&](WasmEdge_BatchContext *x) { return WasmEdge_BatchGlobalSetValue(x, GlobalName, Inst, Value); });
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchGlobalSetValue(s, GlobalName, l, Value)
+                                       : R(C->fail(kRuntimeError, "instance index out of range"));
+  }
   const wb::Program &P = C->prog;
   const int g = find_named(P.global_exports, GlobalName);
   if (g < 0) return R(C->fail(kFuncNotFound, "global export not found"));
@@ -810,6 +868,8 @@ WasmEdge_Result WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *C,
                                               const WasmEdge_String FuncName,
                                               WasmEdge_BatchHostFunc_t Func, void *Data) {
   if (!C || !Func) return R(kWrongVMWorkflow);
+  if (!C->shards.empty())
+    return wbm::all(C, [&](WasmEdge_BatchContext *x) { return WasmEdge_BatchAddHostFunction(x, ModuleName, FuncName, Func, Data); });
   const std::string mod(ModuleName.Buf ? ModuleName.Buf : "", ModuleName.Length);
   const std::string name(FuncName.Buf ? FuncName.Buf : "", FuncName.Length);
   // every import of that (module, name) binds to it, as an import object would
@@ -820,7 +880,7 @@ WasmEdge_Result WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *C,
 }
 
 uint32_t WasmEdge_BatchMemoryGetInstance(const WasmEdge_BatchMemoryContext *M) {
-  return M ? M->inst : 0;
+  return M ? M->ctx->gid(M->inst) : 0;   // (the batch-wide id, on a multi-device batch too)
 }
 
 WasmEdge_Result WasmEdge_BatchMemoryGetData(const WasmEdge_BatchMemoryContext *M, uint8_t *Data,
@@ -845,6 +905,7 @@ const char *WasmEdge_BatchGetBuildHash(void) { return kBuildHash + 12; }
 
 
 uint32_t WasmEdge_BatchGetCodeSize(const WasmEdge_BatchContext *C) {
+  if (C && !C->shards.empty()) return WasmEdge_BatchGetCodeSize(wbm::first(C));
   return C ? uint32_t(C->prog.code.size()) : 0;
 }
 
@@ -863,6 +924,11 @@ __attribute__((visibility("default"))) uint32_t wb_stats_read(WasmEdge_BatchCont
 #endif
 
 void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *C) {
+  if (C && !C->shards.empty()) {
+    for (WasmEdge_BatchContext *s : C->shards)
+      if (s) WasmEdge_BatchInterrupt(s);
+    return;
+  }
   if (!C || !C->stop) return;
   static const uint32_t one = 1;
   (void)hipMemcpyAsync(C->stop, &one, 4, hipMemcpyHostToDevice, C->ctl_stream);
@@ -872,6 +938,11 @@ void WasmEdge_BatchInterrupt(WasmEdge_BatchContext *C) {
 
 void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   if (!C) return;
+  if (!C->shards.empty()) {
+    wbm::destroy(C);
+    return;
+  }
+  DevScope dev(C);
   if (C->stream) (void)hipStreamSynchronize(C->stream);
   if (C->ctl_stream) (void)hipStreamDestroy(C->ctl_stream);
   if (C->stop) (void)hipFree(C->stop);

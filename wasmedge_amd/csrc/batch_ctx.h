@@ -162,6 +162,18 @@ struct WasmEdge_BatchContext {
   // accessor settles first.
   bool reset_pending = false;
 
+  // Multi-device contexts (WasmEdge_BatchConfigure::Devices, multi.cpp): the parent holds
+  // one shard context per entry of Devices (nullptr: no instances there) and routes every
+  // call to them; a shard is a whole single-device context over its part of the ids.
+  std::vector<WasmEdge_BatchContext *> shards;
+  uint32_t part = 0;
+  WasmEdge_BatchContext *parent = nullptr;   // (a shard)
+  uint32_t shard_g = 0;
+  std::mutex *host_mu = nullptr;             // shards: one host service round at a time
+  std::mutex own_host_mu;                    // (the parent's, when HostThreads <= 1)
+  // the batch-wide instance id of this context's lane `local`
+  uint32_t gid(uint32_t local) const;
+
   uint8_t fail(uint8_t code, const std::string &m) {
     last_error = m;
     return code;
@@ -180,6 +192,26 @@ struct WasmEdge_BatchContext {
 };
 
 namespace wbh {
+
+// The context's device current on the calling thread for a call's span (restored after):
+// a multi-device batch drives each shard from its own thread, and a caller may have any
+// device current.
+struct DevScope {
+  int prev = -1;
+  explicit DevScope(const WasmEdge_BatchContext *C) {
+    int cur = -1;
+    if (C && C->stream && hipGetDevice(&cur) == hipSuccess && cur != C->device &&
+        hipSetDevice(C->device) == hipSuccess)
+      prev = cur;
+  }
+  ~DevScope() { if (prev >= 0) (void)hipSetDevice(prev); }
+  DevScope(const DevScope &) = delete;
+  DevScope &operator=(const DevScope &) = delete;
+};
+
+// multi.cpp: the placement of instance ids over shards, and the routed API
+bool placement(uint32_t n, uint32_t g_count, uint32_t part, uint32_t inst, uint32_t *g, uint32_t *local);
+uint32_t shard_size(uint32_t n, uint32_t g_count, uint32_t part, uint32_t g);
 
 constexpr uint32_t kBlockWords = 1024;   // host-view block: 4 KiB of each of a wave's 64 lanes
 

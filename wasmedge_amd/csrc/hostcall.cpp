@@ -299,6 +299,10 @@ static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &p
 // Terminated 0x01 ends it too, engine.cpp:62-64). Returns the number of lanes to resume,
 // or -1 on a device error.
 int64_t service_host_calls(WasmEdge_BatchContext *C) {
+  // the shards of a multi-device batch serve their rounds one at a time unless the caller
+  // declared its host functions reentrant (HostThreads > 1)
+  std::unique_lock<std::mutex> shard_lock;
+  if (C->host_mu) shard_lock = std::unique_lock<std::mutex>(*C->host_mu);
   const wb::Program &P = C->prog;
   const uint32_t n = C->n, hb = C->hb_cells, nw = C->nwaves;
   std::vector<uint8_t> st(n);

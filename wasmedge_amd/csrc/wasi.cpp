@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "batch_ctx.h"
+#include "multi.h"
 
 using namespace wbh;
 
@@ -29,7 +30,7 @@ WasmEdge_Result wasi_trampoline(void *Data, WasmEdge_BatchMemoryContext *M,
                                 const WasmEdge_Value *Params, WasmEdge_Value *Returns) {
   const auto *slot = static_cast<const WasmEdge_BatchContext::WasiSlot *>(Data);
   WasmEdge_BatchContext *C = slot->ctx;
-  const uint32_t inst = WasmEdge_BatchMemoryGetInstance(M);
+  const uint32_t inst = M->inst;   // (this context's own lane index: its WASI state)
   uint32_t a[4] = {0, 0, 0, 0}, ret = 0;
   const size_t f = size_t(slot - C->wasi_slots.data());   // the import's function index
   const wb::FuncType &t = C->prog.types[C->prog.funcs[f].type];
@@ -49,6 +50,8 @@ WasmEdge_Result WasmEdge_BatchInitWASI(WasmEdge_BatchContext *C, const char *con
                                        const uint32_t ArgLen, const char *const *Envs,
                                        const uint32_t EnvLen) {
   if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty())
+    return wbm::all(C, [&](WasmEdge_BatchContext *s) { return WasmEdge_BatchInitWASI(s, Args, ArgLen, Envs, EnvLen); });
   C->wasi_env.args.clear();
   C->wasi_env.envs.clear();
   for (uint32_t k = 0; k < ArgLen; k++) C->wasi_env.args.emplace_back(Args && Args[k] ? Args[k] : "");
@@ -68,12 +71,18 @@ WasmEdge_Result WasmEdge_BatchInitWASI(WasmEdge_BatchContext *C, const char *con
 }
 
 uint32_t WasmEdge_BatchWASIGetExitCode(const WasmEdge_BatchContext *C, uint32_t Inst) {
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (C && !C->shards.empty()) return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchWASIGetExitCode(s, l) : 0;
   if (!C || Inst >= C->wasi_lanes.size()) return 0;
   return C->wasi_lanes[Inst].exit_code;
 }
 
 uint32_t WasmEdge_BatchWASIGetOutput(const WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Fd,
                                      uint8_t *Buf, uint32_t Len) {
+  WasmEdge_BatchContext *sh;
+  uint32_t l;
+  if (C && !C->shards.empty()) return wbm::route(C, Inst, &sh, &l) ? WasmEdge_BatchWASIGetOutput(sh, l, Fd, Buf, Len) : 0;
   if (!C || Inst >= C->wasi_lanes.size() || (Fd != 1 && Fd != 2)) return 0;
   const std::string &s = C->wasi_lanes[Inst].out[Fd - 1];
   if (Buf) memcpy(Buf, s.data(), std::min<size_t>(Len, s.size()));
