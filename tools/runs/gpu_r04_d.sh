@@ -1,0 +1,12 @@
+# r04 d: longest-first wave order (LPT) for persistent launches -- C5 A/B, parity, timeline
+O=gpurun_out/r04d; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+step c5_lpt 200 python bench.py --workload c5 --instances 262144 --steps 10 --warmup 2 --no-cpu-baseline
+WB_LPT=0 step c5_nolpt 200 python bench.py --workload c5 --instances 262144 --steps 10 --warmup 2 --no-cpu-baseline
+step tests 400 python -u -m pytest tests/test_workloads.py -m gpu -v --timeout 200 --timeout-method thread -k "c5 or partial or mandel"
+step timeline 300 python -u tools/wave_timeline.py c5 --out $O/timeline.json

@@ -19,7 +19,7 @@ import re  # noqa: E402
 OPS = re.findall(r"X\((\w+)\)", _src[_i:_src.index("enum DOp", _i)])
 NAMES = ["rounds", "fast", "lanes", "tc", "cpp", "slow", "cyc_sched", "cyc_fast", "cyc_slow",
          "x_call", "x_ret", "x_post", "x_br", "x_other", "cyc_tc", "tc_sched"]
-NST = len(NAMES)
+NST = 32   # per-wave stride of the stats buffer (batch_kernel.hip ST_N <= 32)
 
 
 def run(name, wasm, func, rows, types):
@@ -38,7 +38,7 @@ def run(name, wasm, func, rows, types):
     buf = raw[:nw * NST].reshape(nw, NST)
     hist = raw[nw * NST:]
     m = buf.astype(np.float64).mean(0)
-    d = dict(zip(NAMES, m))
+    d = dict(zip(NAMES, m[:len(NAMES)]))
     cyc = (d["cyc_sched"] + d["cyc_fast"] + d["cyc_slow"]) * 16
     print("%-10s instr/s=%.3e wasm/inst=%.3e rounds=%.3e fast-lanes=%.1f tc=%.3e cpp=%.3e "
           "slow=%.3e | cycles/wave=%.3e sched=%.0f%% fast=%.0f%% slow=%.0f%% | cyc/round=%.0f"

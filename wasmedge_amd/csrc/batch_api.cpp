@@ -18,6 +18,8 @@
 
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s);
+extern "C" hipError_t wb_launch_wave_order(const uint32_t *ticks, uint32_t *order, uint32_t nwaves,
+                                           hipStream_t s);
 extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t threads, size_t lds_bytes);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
@@ -283,7 +285,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
                                       " MiB linear memory)");
 #ifdef WB_STATS
-  if (!C->hip_ok(hipMalloc(&C->stats, (nw * 16 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
+  if (!C->hip_ok(hipMalloc(&C->stats, (nw * 32 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
 #endif
   if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
   return 0;
@@ -352,7 +354,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.simt = C->simt && k.tcode ? 1u : 0u;
   k.stats = C->stats;
 #ifdef WB_STATS
-  (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 16 + 1024) * sizeof(uint64_t), C->stream);
+  (void)hipMemsetAsync(C->stats, 0, (size_t(C->nwaves) * 32 + 1024) * sizeof(uint64_t), C->stream);
 #endif
   // launch geometry: 4 waves per block when their LDS frames fit in 160 KB
   size_t wave_lds = size_t((C->frame_hbm ? 0 : k.total_cells) + k.gs_lds) * 64 * 4;
@@ -371,17 +373,32 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, k.grow_host, C->cap_threads, C->cap_lds);
   }
   const char *pe = getenv("WB_PERSIST");
+  if (const char *lp = getenv("WB_LPT")) C->lpt = lp[0] != '0';
   if (C->cap_blocks && blocks > C->cap_blocks && !(pe && pe[0] == '0')) {
     if (!C->wave_ctr.ptr && !C->wave_ctr.alloc(1)) return C->fail(kRuntimeError, "device allocation failed");
     if (!C->hip_ok(hipMemsetAsync(C->wave_ctr.ptr, 0, 4, C->stream), "wave counter")) return kRuntimeError;
     k.wave_ctr = C->wave_ctr.ptr;
     blocks = C->cap_blocks;
+    // longest-first order from the last launch of this function (batch_ctx.h wave_order)
+    if (C->lpt && !resume && !is_start) {
+      if (!C->wave_ticks.ptr && (!C->wave_ticks.alloc(C->nwaves) || !C->wave_order.alloc(C->nwaves)))
+        return C->fail(kRuntimeError, "device allocation failed");
+      k.wave_ticks = C->wave_ticks.ptr;
+      k.wave_order = C->order_pc == entry_pc ? C->wave_order.ptr : nullptr;
+    }
   }
   (void)hipEventRecord(C->ev0, C->stream);
   // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
   if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, vf, C->stream), "launch"))
     return kRuntimeError;
   (void)hipEventRecord(C->ev1, C->stream);
+  // the next launch of this function takes the longest waves first (sorted on the device,
+  // after the timed kernel; the order buffer is only read by later launches)
+  if (k.wave_ticks) {
+    if (!C->hip_ok(wb_launch_wave_order(k.wave_ticks, C->wave_order.ptr, C->nwaves, C->stream), "wave order"))
+      return kRuntimeError;
+    C->order_pc = entry_pc;
+  }
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;
   C->reset_pending = false;   // (the stream is drained)
   if (KernelSeconds) {
@@ -918,7 +935,7 @@ const char *WasmEdge_BatchGetLastError(const WasmEdge_BatchContext *C) {
 __attribute__((visibility("default"))) uint32_t wb_stats_read(WasmEdge_BatchContext *C,
                                                               uint64_t *out) {
   if (!C || !C->stats) return 0;
-  (void)hipMemcpy(out, C->stats, (size_t(C->nwaves) * 16 + 1024) * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out, C->stats, (size_t(C->nwaves) * 32 + 1024) * sizeof(uint64_t), hipMemcpyDeviceToHost);
   return C->nwaves;
 }
 #endif

@@ -91,6 +91,13 @@ struct WasmEdge_BatchContext {
   uint32_t cap_threads = 0, cap_blocks = 0;
   size_t cap_lds = 0;
   DevBuf<uint32_t> wave_ctr;
+  // Longest-first wave order (KParams::wave_order): each persistent launch records every
+  // batch wave's run time; the next launch of the same function takes the waves in
+  // descending order of it (LPT), so the heavy waves start first instead of wherever their
+  // ids put them. Scheduling only: results never depend on it (WB_LPT=0 turns it off).
+  DevBuf<uint32_t> wave_ticks, wave_order;
+  uint32_t order_pc = 0xFFFFFFFFu;   // entry pc of the launch the order was taken from
+  bool lpt = true;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
   DevBuf<uint32_t> loops;         // Program::loops (scheduler)
   DevBuf<uint32_t> brtab, vconst, table, global_init, image, data_off, data_len;

@@ -91,7 +91,10 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #ifdef WB_STATS
 enum { ST_ROUNDS, ST_FAST, ST_LANES, ST_TC, ST_CPP, ST_SLOW, ST_CYC_SCHED, ST_CYC_FAST,
        ST_CYC_SLOW, ST_X_CALL, ST_X_RET, ST_X_POST, ST_X_BR, ST_X_OTHER, ST_CYC_TC, ST_TC_SCHED,
+       ST_T0, ST_T1, ST_HW,   // the batch wave's start / end (s_memrealtime, 100 MHz) and where
+                              // it ran (HW_ID: SIMD, CU, SE, XCC bits) -- tools/wave_timeline.py
        ST_N };
+static_assert(ST_N <= 32, "per-wave stats stride is 32 (batch_api.cpp)");
 // one relaxed atomic add per event from the first active lane (also inside divergent
 // regions, where a per-wave count must be taken once); cycles in units of 16 clocks
 #define WB_STAT_ADD(k, v)                                                              \
@@ -397,9 +400,17 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     gsp = 1;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#ifdef WB_STATS
+  if (p.stats && !p.resume && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) {
+    uint64_t *const sw = p.stats + (size_t)(inst >> 6) * 32u;
+    sw[ST_T0] = t0;
+    sw[ST_HW] = __builtin_amdgcn_s_getreg((4 << 0) | (31 << 11)) |   // HW_REG_HW_ID (gfx9 id 4)
+                ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (31 << 11)) << 32);   // XCC_ID
+  }
+#endif
   uint64_t tpoll = t0 - 1000u;   // the last read of the interrupt flag (100 MHz ticks)
 #ifdef WB_STATS
-  uint64_t *const stw = p.stats ? p.stats + (size_t)(inst >> 6) * ST_N : nullptr;
+  uint64_t *const stw = p.stats ? p.stats + (size_t)(inst >> 6) * 32u : nullptr;
 #endif
   const uint32_t lane = __lane_id();
   const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
@@ -564,7 +575,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
                         : ST_X_OTHER, 1);
             // which op made the core exit: a histogram after the per-wave counters
             if (stw && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))
-              __hip_atomic_fetch_add(&p.stats[(size_t)((p.n + 63) >> 6) * ST_N + (xo & 1023u)], 1ull,
+              __hip_atomic_fetch_add(&p.stats[(size_t)((p.n + 63) >> 6) * 32u + (xo & 1023u)], 1ull,
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
 #endif
@@ -762,6 +773,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #undef GSF_BASE
 #undef GS_PTR
 #undef GS_CPTR
+#ifdef WB_STATS
+  if (p.stats && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))
+    p.stats[(size_t)(inst >> 6) * 32u + ST_T1] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (active) {
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
@@ -803,7 +818,8 @@ __device__ __forceinline__ uint32_t next_wave(const KParams &p, uint32_t &turn) 
   uint32_t w = 0;
   if ((threadIdx.x & 63u) == 0) w = __hip_atomic_fetch_add(p.wave_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   w = __builtin_amdgcn_readfirstlane(w);
-  return w < nwaves ? w : 0xFFFFFFFFu;
+  if (w >= nwaves) return 0xFFFFFFFFu;
+  return p.wave_order ? __builtin_amdgcn_readfirstlane(p.wave_order[w]) : w;
 }
 
 template <bool VF, bool PG>
@@ -816,10 +832,13 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
   uint32_t turn = 0;
   for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
+    const uint64_t ws = p.wave_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
     interp<VF, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
                p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
                p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+    if (p.wave_ticks && lane == 0)
+      p.wave_ticks[wave] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - ws, 0xFFFFFFFFull);
   }
 }
 
@@ -991,7 +1010,39 @@ wb_mem_hash_fin_kernel(const uint32_t *ls, uint32_t ls_slots, uint64_t *hashes, 
   hashes[inst] ^= fmix64((uint64_t)pages + 0x1234567ull);
 }
 
+// Longest-first order of the batch waves for the next persistent launch (KParams::
+// wave_order), from this launch's per-wave run times: a counting sort over 1024 buckets of
+// [0, max] (descending), in one block -- on the device, so no host round trip sits between
+// launches. Within a bucket the order is whatever the atomics give (scheduling only).
+extern "C" __global__ void __launch_bounds__(1024)
+wb_wave_order_kernel(const uint32_t *ticks, uint32_t *order, uint32_t nwaves) {
+  __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t mx;
+  const uint32_t t = threadIdx.x;
+  cnt[t] = 0;
+  if (t == 0) mx = 0;
+  __syncthreads();
+  for (uint32_t w = t; w < nwaves; w += 1024) atomicMax(&mx, ticks[w]);
+  __syncthreads();
+  const uint64_t span = (uint64_t)mx + 1;
+  for (uint32_t w = t; w < nwaves; w += 1024)
+    atomicAdd(&cnt[1023u - (uint32_t)((uint64_t)ticks[w] * 1024u / span)], 1u);
+  __syncthreads();
+  if (t == 0) {   // exclusive prefix sum, heaviest bucket first
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < 1024; b++) { const uint32_t c = cnt[b]; cnt[b] = run; run += c; }
+  }
+  __syncthreads();
+  for (uint32_t w = t; w < nwaves; w += 1024)
+    order[atomicAdd(&cnt[1023u - (uint32_t)((uint64_t)ticks[w] * 1024u / span)], 1u)] = w;
+}
+
 // ======================================================================= launchers
+extern "C" hipError_t wb_launch_wave_order(const uint32_t *ticks, uint32_t *order, uint32_t nwaves,
+                                           hipStream_t s) {
+  hipLaunchKernelGGL(wb_wave_order_kernel, dim3(1), dim3(1024), 0, s, ticks, order, nwaves);
+  return hipGetLastError();
+}
 // (host stubs live in this translation unit; the C-ABI layer calls these)
 // the kernel for a launch: frames in HBM / LDS / VGPRs, and paged (PG) or not
 static const void *exec_kernel(int vframe, int hbm, int paged) {

@@ -83,6 +83,10 @@ struct KParams {
   const uint32_t *loops;        // per pc: innermost loop (head, end), ~0 = none
   uint32_t *wave_ctr;           // persistent waves: the next wave to run (NULL: one launch
                                 // wave per wave of the batch, the block's own)
+  const uint32_t *wave_order;   // persistent waves: the batch waves in the order they are
+                                // taken (NULL: id order) -- longest first by the last launch
+  uint32_t *wave_ticks;         // persistent waves: each batch wave's run time (100 MHz ticks,
+                                // or NULL)
   uint32_t simt;                // V frames + compiled runs: every running lane enters the
                                 // core, whose compiled runs schedule the lanes among
                                 // themselves (jit.cpp Lsched); the C++ loop only serves
