@@ -79,6 +79,29 @@ def test_gpu_loaded_library_is_head(built):
         ctx.close()
 
 
+DRIVER = os.path.join(ROOT, "tests", "c", "abi_driver")
+
+
+def test_c_driver_is_built(built):
+    """tests/c/abi_driver.c -- a plain C embedder of the ABI -- is built against the header
+    and links the library (run on the GPU below)."""
+    assert os.access(DRIVER, os.X_OK)
+    out = subprocess.run(["ldd", DRIVER], capture_output=True, text=True).stdout
+    assert "libwasmedge_batch.so" in out and "not found" not in out
+
+
+@pytest.mark.gpu
+def test_gpu_c_driver(built):
+    """A C program calls the ABI on the GPU (no ctypes): Create / Execute / the staged
+    SetArgs-Reset-Run-Results path / MemoryHash / FuncNotFound, on one device and on two
+    shards, every result and instruction count checked in C against fib and the reference's
+    counting rule."""
+    r = subprocess.run([DRIVER, os.path.join(ROOT, "tests", "golden", "fibonacci.wasm")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "one device: 1000 instances ok" in r.stdout and "two shards: 1000 instances ok" in r.stdout
+
+
 def test_null_context_is_wrong_workflow(built):
     """Reference C API: NULL context -> WrongVMWorkflow (lib/api/wasmedge.cpp:266-277).
     Exercised without a GPU: no device call happens before the NULL check."""

@@ -8,11 +8,13 @@ pinned at their boundary, and one that is gone:
   -40,000, silently truncated (counts off by 65,536 per taken branch), and in front of a
   block end a "tcnt overflow" rejection. The reference counts every `nop`
   (engine.cpp:1618-1631), so this is counting parity, exact against the oracle.
-* at most 32 data segments when the module uses `data.drop` (the dropped set is one
-  32-bit word per instance), and at most 32 element segments in a module that mutates
-  its tables (per-lane tables, frontend.cpp). Both fail BatchCreate with 0x02 and a
-  message; one fewer is accepted and runs bit-exact. The reference has no such limit
-  (DESIGN.md "Module subset").
+* segment counts: data segments and element segments of any number, each dropped
+  per instance (a bit per segment in the instance state; round 3 refused more than 32
+  data segments with `data.drop` and more than 32 element segments in a table-mutating
+  module). Modules with 70 segments of each kind -- passive and active ones, memory.init /
+  table.init from segments in every mask word, data.drop / elem.drop on some lanes, state
+  kept across invocations -- run bit-exact against the oracle (the reference has no limit,
+  lib/executor/instantiate/data.cpp, elem.cpp).
 """
 import pytest
 
@@ -44,30 +46,48 @@ def nops_module(n):
 
 
 def data_module(nseg):
-    segs = "\n".join('  (data $d%d "\\%02x")' % (k, k) for k in range(nseg))
+    """nseg data segments: every 5th active (at 1024 + k), the rest passive; f(x) inits
+    bytes from segments 2, 33, nseg-4 (passive) and nseg-5 (active: dropped at
+    instantiation, so a 1-byte init traps 0x88 when x & 4), drops 33 and nseg-4 when x & 1."""
+    def seg(k):
+        return ('  (data $d%d (i32.const %d) "\\%02x")' % (k, 1024 + k, k) if k % 5 == 0
+                else '  (data $d%d "\\%02x\\%02x")' % (k, k, k + 1))
+    segs = "\n".join(seg(k) for k in range(nseg))
+    act = nseg - 5 - (nseg - 5) % 5
     return assemble(r"""
 (module
   (memory 1)
 %s
   (func (export "f") (param $x i32) (result i32)
-    (memory.init $d%d (i32.const 8) (i32.const 0) (i32.const 1))
-    (if (local.get $x) (then (data.drop $d%d)))
-    (i32.load8_u (i32.const 8))))
-""" % (segs, nseg - 1, nseg - 1))
+    (memory.init $d2 (i32.const 8) (i32.const 0) (i32.const 1))
+    (memory.init $d33 (i32.const 9) (i32.const 1) (i32.const 1))
+    (memory.init $d%d (i32.const 10) (i32.const 0) (i32.const 2))
+    (memory.init $d%d (i32.const 12) (i32.const 0) (i32.const 0))
+    (if (i32.and (local.get $x) (i32.const 4))
+      (then (memory.init $d%d (i32.const 12) (i32.const 0) (i32.const 1))))
+    (if (i32.and (local.get $x) (i32.const 1)) (then (data.drop $d33) (data.drop $d%d)))
+    (i32.add (i32.load (i32.const 8)) (i32.load8_u (i32.const %d)))))
+""" % (segs, nseg - 4, act, act, nseg - 4, 1024 + act))
 
 
 def elem_module(nseg):
-    segs = "\n".join("  (elem $e%d func $g)" % k for k in range(nseg))
+    """nseg element segments (every 7th active into table $t at 1, the rest passive);
+    f(x) table.inits from segments 36 and nseg-1, drops them when x & 1."""
+    segs = "\n".join(("  (elem $e%d (table $t) (i32.const 1) func $g)" % k) if k % 7 == 0
+                     else ("  (elem $e%d func %s)" % (k, "$g" if k % 2 else "$h")) for k in range(nseg))
     return assemble(r"""
 (module
-  (table $t 2 funcref)
+  (table $t 4 funcref)
   (type $v (func (result i32)))
   (func $g (result i32) (i32.const 7))
+  (func $h (result i32) (i32.const 11))
 %s
   (func (export "f") (param $x i32) (result i32)
-    (table.init $t $e%d (i32.const 0) (i32.const 0) (i32.const 1))
-    (if (local.get $x) (then (elem.drop $e%d)))
-    (call_indirect (type $v) (i32.const 0))))
+    (table.init $t $e36 (i32.const 0) (i32.const 0) (i32.const 1))
+    (table.init $t $e%d (i32.const 2) (i32.const 0) (i32.const 1))
+    (if (i32.and (local.get $x) (i32.const 1)) (then (elem.drop $e36) (elem.drop $e%d)))
+    (i32.add (call_indirect (type $v) (i32.const 0))
+             (i32.mul (i32.const 100) (call_indirect (type $v) (i32.const 2))))))
 """ % (segs, nseg - 1, nseg - 1))
 
 
@@ -82,25 +102,50 @@ def test_long_folded_prefix_counts_emulator(built, n):
     assert compare(ref, *got, [I32]) == []
 
 
-@pytest.mark.parametrize("kind,make", [("data", data_module), ("element", elem_module)])
-def test_segment_limit_boundary_emulator(built, kind, make):
-    ok = make(32)
-    ref = oracle_run(O.Module(ok), "f", ROWS)
-    assert compare(ref, *emu_run(ok, "f", ROWS, [I32], [I32]), [I32]) == []
-    # the oracle (the reference's behaviour) runs 33; this build refuses it at lowering
-    bad = make(33)
-    assert all(r[0] == 0 for r in oracle_run(O.Module(bad), "f", ROWS))
-    with pytest.raises(RuntimeError, match="0x2: more than 32 %s segments" % kind):
-        emu_run(bad, "f", ROWS, [I32], [I32])
+ROWS_SEG = [[x] for x in (0, 1, 2, 3, 4, 5, 6, 7)]
+
+
+@pytest.mark.parametrize("make", [data_module, elem_module])
+@pytest.mark.parametrize("nseg", [40, 70])
+def test_many_segments_emulator(built, make, nseg):
+    wasm = make(nseg)
+    ref = oracle_run(O.Module(wasm), "f", ROWS_SEG)
+    assert {r[0] for r in ref} <= {0, 0x88}
+    assert compare(ref, *emu_run(wasm, "f", ROWS_SEG, [I32], [I32]), [I32]) == []
 
 
 @pytest.mark.gpu
 def test_gpu_limits(built):
     from helpers import gpu_run
-    from wasmedge_amd import batch
-    for wasm in (nops_module(40000), data_module(32), elem_module(32)):
+    for wasm in (nops_module(40000), data_module(40), elem_module(40)):
         ref = oracle_run(O.Module(wasm), "f", ROWS)
         assert compare(ref, *gpu_run(wasm, "f", ROWS, [I32], [I32]), [I32]) == []
-    for make in (data_module, elem_module):
-        with pytest.raises(RuntimeError):
-            batch.BatchContext(make(33), 4, device=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("make", [data_module, elem_module])
+def test_gpu_many_segments(built, make):
+    """70 segments: masks past the first word, on 130 lanes (three waves), invoked twice on
+    the same instances -- the second call sees the first call's drops -- against an oracle
+    instance kept across the two calls."""
+    from wasmedge_amd import batch
+    wasm = make(70)
+    rows = [[x % 8] for x in range(130)]
+    m = O.Module(wasm)
+    want = []
+    for r in rows:
+        inst = O.Instance(m)
+        want.append([inst.invoke("f", r)[:2], inst.invoke("f", r)[:2]])
+    ctx = batch.BatchContext(wasm, len(rows), device=0)
+    try:
+        got = []
+        for rep in range(2):
+            rets, st, cnt = ctx.execute("f", batch.make_values(rows, [I32]), 1)
+            got.append([(int(st[i]), [int(batch.ret_ints(rets)[i][0])] if st[i] == 0 else [])
+                        for i in range(len(rows))])
+        for i in range(len(rows)):
+            for rep in range(2):
+                code, vals = want[i][rep]
+                assert got[rep][i] == (code, list(vals) if code == 0 else []), (i, rep)
+    finally:
+        ctx.close()

@@ -119,14 +119,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   std::vector<uint32_t> img;
   std::vector<uint8_t> pool;
   std::vector<uint32_t> doff, dlen;
-  uint32_t dropped = 0;
+  std::vector<uint32_t> dropped((P.datas.size() + 31) / 32 + 1, 0u);   // a bit per data segment
   for (size_t k = 0; k < P.datas.size(); k++) {
     const auto &d = P.datas[k];
     doff.push_back(uint32_t(pool.size()));
     dlen.push_back(uint32_t(d.bytes.size()));
     pool.insert(pool.end(), d.bytes.begin(), d.bytes.end());
     if (d.active) {
-      if (k < 32) dropped |= 1u << k;   // active segments are dropped after init
+      dropped[k >> 5] |= 1u << (k & 31);   // active segments are dropped after init
       uint64_t end = uint64_t(d.offset) + d.bytes.size();
       if (img.size() * 4 < end) img.resize((end + 3) / 4, 0);
       for (size_t b = 0; b < d.bytes.size(); b++) {
@@ -136,7 +136,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     }
   }
   C->image_words = uint32_t(img.size());
-  C->init_dropped = dropped;
+  C->init_dropped = dropped[0];
   std::vector<DFunc> fv;
   for (const auto &f : P.funcs)
     fv.push_back(DFunc{f.imported ? 0xFFFFFFFFu : f.entry_pc, P.type_canon[f.type]});
@@ -239,8 +239,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   std::vector<uint32_t> ls_init = P.global_init;
   if (P.mut_tables) {
     for (const auto &t : P.tables) ls_init.push_back(t.min);
-    ls_init.push_back(P.init_edropped);
+    ls_init.insert(ls_init.end(), P.init_edropped.begin(), P.init_edropped.end());
   }
+  // the dropped-data mask past its first word (data segments 32 on)
+  C->ls_drop_ext = LS_GLOBALS + uint32_t(ls_init.size());
+  ls_init.insert(ls_init.end(), dropped.begin() + 1, dropped.end());
   bool ok = C->code.upload(codepad, s) && C->loops.upload(P.loops, s) && (!C->threaded || C->tcode.upload(tcv, s)) && C->brtab.upload(P.brtab, s) &&
             C->vconst.upload(P.vconst, s) && C->table.upload(P.table0, s) &&
             C->global_init.upload(ls_init, s) && C->image.upload(img, s) &&
@@ -318,6 +321,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     k.mut_tables = 1; k.ntables = P.ntables; k.tab_words = P.tab_words;
   }
   k.ls_tab = LS_GLOBALS + P.global_cells;
+  k.ls_drop_ext = C->ls_drop_ext;
   k.mem = C->mem.ptr; k.gstack = C->gstack.ptr; k.lstate = C->lstate.ptr;
   k.fsave = C->fsave.ptr; k.hcall = C->hcall.ptr; k.hbuf = C->hbuf.ptr;
   k.hframe = C->frame_hbm ? C->hframe.ptr : nullptr;

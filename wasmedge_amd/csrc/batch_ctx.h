@@ -128,7 +128,7 @@ struct WasmEdge_BatchContext {
   std::vector<WasiSlot> wasi_slots;   // per function index (Data of its HostFn)
   DevBuf<uint8_t> status;
   DevBuf<uint64_t> counts, hashes;
-  uint32_t image_words = 0, init_dropped = 0;
+  uint32_t image_words = 0, init_dropped = 0, ls_drop_ext = 0;
   uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
   // Paged linear memory (DESIGN.md "Linear memory"): `mem_max_pages` is the page limit
   // (65536, the module's max, MaxMemoryPage); pages [0, rpages) of every lane live in the

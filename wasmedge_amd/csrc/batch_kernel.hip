@@ -352,7 +352,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   uint32_t *const lt = p.ltab ? p.ltab + (size_t)(inst >> 6) * p.tab_words * 64u + (inst & 63u) : nullptr;
 #define TSIZE(t) LS(p.ls_tab + (t))
 #define TENT(t, i) lt[(size_t)(p.tabinfo[2u * (t)] + (i)) << 6]
-#define EDROP LS(p.ls_tab + p.ntables)
+// dropped element segments: mask words after the table sizes; dropped data segments: the
+// first 32 in `dropped` (LS_DROPPED), the rest in mask words at ls_drop_ext (slow paths only)
+#define ELEM_DROPPED(e) ((LS(p.ls_tab + p.ntables + ((e) >> 5)) >> ((e) & 31u)) & 1u)
+#define SET_ELEM_DROPPED(e) (LS(p.ls_tab + p.ntables + ((e) >> 5)) |= 1u << ((e) & 31u))
+#define DATA_DROPPED(s) ((s) < 32u ? (dropped >> (s)) & 1u : (LS(p.ls_drop_ext + ((s) >> 5) - 1u) >> ((s) & 31u)) & 1u)
+#define SET_DATA_DROPPED(s) do { const uint32_t _s = (s); \
+    if (_s < 32u) dropped |= 1u << _s; else LS(p.ls_drop_ext + (_s >> 5) - 1u) |= 1u << (_s & 31u); } while (0)
   uint32_t status = inst < p.n ? WB_STATUS_RUNNING : WB_STATUS_OK;
   // `pages` = the lane's pages in the reserved layout, min(its memory size, rpages): the
   // bound of every fast path. The size itself is LS_PAGES (memory.grow writes it there),
@@ -800,6 +806,10 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   }
 #undef LS
 #undef WB_MARK
+#undef ELEM_DROPPED
+#undef SET_ELEM_DROPPED
+#undef DATA_DROPPED
+#undef SET_DATA_DROPPED
 #undef MEM_PAGES
 #undef LS_PAGES_REF
 }

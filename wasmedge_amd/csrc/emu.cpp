@@ -138,12 +138,12 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   for (const auto &fi : P.funcs) fv.push_back(DFunc{fi.imported ? 0xFFFFFFFFu : fi.entry_pc, P.type_canon[fi.type]});
   std::vector<uint8_t> pool;
   std::vector<uint32_t> doff, dlen;
-  uint32_t init_dropped = 0;
+  std::vector<uint32_t> init_dropped((P.datas.size() + 31) / 32 + 1, 0u);   // a bit per data segment
   for (size_t k = 0; k < P.datas.size(); k++) {
     doff.push_back(uint32_t(pool.size()));
     dlen.push_back(uint32_t(P.datas[k].bytes.size()));
     pool.insert(pool.end(), P.datas[k].bytes.begin(), P.datas[k].bytes.end());
-    if (P.datas[k].active && k < 32) init_dropped |= 1u << k;
+    if (P.datas[k].active) init_dropped[k >> 5] |= 1u << (k & 31);
   }
   KParams p{};
   p.code = P.code.data(); p.brtab = P.brtab.data(); p.vconst = P.vconst.data();
@@ -157,10 +157,13 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   p.tabinfo = P.tabinfo.data(); p.elem_pool = P.elem_pool.data();
   p.elem_off = P.elem_off.data(); p.elem_len = P.elem_len.data();
   std::vector<uint32_t> ltabv, tsz;   // this instance's tables (per-lane table mode)
-  uint32_t edrop = 0;
+  std::vector<uint32_t> edrop;
 #define TSIZE(t) tsz[(uint32_t)(t)]
 #define TENT(t, i) ltabv[P.tabinfo[2u * (t)] + (i)]
-#define EDROP edrop
+#define ELEM_DROPPED(e) ((edrop[(e) >> 5] >> ((e) & 31u)) & 1u)
+#define SET_ELEM_DROPPED(e) (edrop[(e) >> 5] |= 1u << ((e) & 31u))
+#define DATA_DROPPED(s) ((dropped[(s) >> 5] >> ((s) & 31u)) & 1u)
+#define SET_DATA_DROPPED(s) (dropped[(s) >> 5] |= 1u << ((s) & 31u))
   std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
   std::vector<uint32_t> memv;
   // gas metering: per DBC prefix sums of its instructions' costs (unit table by default)
@@ -217,11 +220,13 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     mem = memv.data(); mb = reinterpret_cast<uint8_t *>(mem); pages = (cur) + (n); res = (cur); } while (0)
 #define W128(c, v) do { for (int _k = 0; _k < 4; _k++) W32((c) + _k, (v)[_k]); } while (0)
 #define WLOOP(c, v) W32(c, v)
-    uint32_t pages = P.mem_min, dropped = init_dropped;
+    uint32_t pages = P.mem_min;
+    std::vector<uint32_t> dropped = init_dropped;
     ltabv = P.tab_image;
     tsz.clear();
     for (const auto &t : P.tables) tsz.push_back(t.min);
     edrop = P.init_edropped;
+    edrop.resize(edrop.size() + 1, 0u);
     for (uint32_t c = 0; c < P.global_cells; c++) W32(c, P.global_init[c]);
     // one invocation of the function at `entry` on this instance's state
     auto invoke = [&](uint32_t entry, const uint32_t *prm, uint32_t ncells, uint64_t &count) {

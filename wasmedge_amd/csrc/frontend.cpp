@@ -1288,7 +1288,6 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
       case 0xFC09: {
         uint32_t di = r.u32();
         if (di >= P.datas.size()) fail(E_TYPECHECK, "unknown data");
-        if (di >= 32) fail(E_UNSUPPORTED, "more than 32 data segments");
         if (live()) emit(OP_DATA_DROP, 0, 0, 0, 0, di);
         break;
       }
@@ -1954,7 +1953,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
     // per-lane table words: each table gets min + kTableGrowLimit slots (bounded by its
     // max); element segment pool for table.init; active and declarative segments
     // start dropped (elem.cpp)
-    if (P.elems.size() > 32) throw Err{E_UNSUPPORTED, "more than 32 element segments"};
+    P.init_edropped.assign((P.elems.size() + 31) / 32 + (P.elems.empty() ? 1 : 0), 0u);
     for (uint32_t t = 0; t < P.ntables; t++) {
       const TableInfo &T = P.tables[t];
       uint64_t cap = uint64_t(T.min) + kTableGrowLimit;
@@ -1972,7 +1971,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
       P.elem_off.push_back(uint32_t(P.elem_pool.size()));
       P.elem_len.push_back(uint32_t(e.items.size()));
       P.elem_pool.insert(P.elem_pool.end(), e.items.begin(), e.items.end());
-      if (e.active || e.declarative) P.init_edropped |= 1u << k;
+      if (e.active || e.declarative) P.init_edropped[k >> 5] |= 1u << (k & 31);
     }
   }
   fuse_arx(P);

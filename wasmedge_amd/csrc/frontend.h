@@ -92,7 +92,10 @@ struct Program {
   bool mut_tables = false;
   std::vector<uint32_t> tab_image, tabinfo;
   std::vector<uint32_t> elem_pool, elem_off, elem_len;
-  uint32_t tab_words = 0, init_edropped = 0;
+  uint32_t tab_words = 0;
+  // dropped element segments at instantiation (active and declarative ones, elem.cpp), a
+  // bit per segment, 32 per word; per-lane tables keep these words in the instance state
+  std::vector<uint32_t> init_edropped;
   int64_t start_func = -1;
   // lowered code
   std::vector<DInstr> code;

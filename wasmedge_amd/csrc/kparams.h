@@ -73,7 +73,10 @@ struct KParams {
   const uint32_t *elem_pool;    // element segment items (function index, ~0 = null)
   const uint32_t *elem_off, *elem_len;
   uint32_t mut_tables, ntables, tab_words;
-  uint32_t ls_tab;              // LS slot of table 0's size; ls_tab + ntables: dropped elems
+  uint32_t ls_tab;              // LS slot of table 0's size; ls_tab + ntables: the dropped-elem
+                                // mask words (32 segments each)
+  uint32_t ls_drop_ext;         // LS slot of the dropped-data mask's second word (segments
+                                // 32..63; LS_DROPPED holds 0..31)
   uint32_t *stop;               // host-set interrupt request (WasmEdge_BatchInterrupt)
   uint64_t max_ticks;           // wall-clock budget per wave in 100 MHz ticks
   uint64_t *stats;              // WB_STATS builds: per-wave counters (else unused)
