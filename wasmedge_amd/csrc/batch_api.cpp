@@ -19,22 +19,23 @@
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s);
 extern "C" hipError_t wb_launch_wave_order(const uint32_t *ticks, uint32_t *order, uint32_t nwaves,
-                                           hipStream_t s);
+                                           uint32_t *wave_ctr, hipStream_t s);
 extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t threads, size_t lds_bytes);
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
-                                         const uint32_t *ls, uint32_t ls_slots, uint32_t full,
-                                         uint32_t g, hipStream_t s);
+                                         uint32_t *ls, uint32_t ls_slots, uint32_t full,
+                                         uint32_t g, uint32_t fuse_state, const uint32_t *global_init,
+                                         uint32_t init_pages, uint32_t init_dropped,
+                                         uint64_t init_cost, hipStream_t s);
 extern "C" hipError_t wb_launch_mem_hash(uint32_t *mem, const uint32_t *ls,
                                          uint32_t ls_slots, uint64_t *hashes,
                                          uint32_t mem_words, uint32_t n, uint32_t g,
                                          const uint64_t *ptab, uint32_t ptab_w, uint32_t max_pages,
                                          hipStream_t s);
-extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
-                                           uint32_t global_cells, uint32_t ls_slots,
-                                           uint32_t init_pages, uint32_t init_dropped,
-                                           uint32_t nwaves, uint64_t init_cost, hipStream_t s);
+extern "C" hipError_t wb_launch_state_init(uint32_t *ls, uint32_t ls_slots, uint32_t nwaves,
+                                           const uint32_t *global_init, uint32_t init_pages,
+                                           uint32_t init_dropped, uint64_t init_cost, hipStream_t s);
 
 
 using namespace wbh;
@@ -380,7 +381,15 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   if (const char *lp = getenv("WB_LPT")) C->lpt = lp[0] != '0';
   if (C->cap_blocks && blocks > C->cap_blocks && !(pe && pe[0] == '0')) {
     if (!C->wave_ctr.ptr && !C->wave_ctr.alloc(1)) return C->fail(kRuntimeError, "device allocation failed");
-    if (!C->hip_ok(hipMemsetAsync(C->wave_ctr.ptr, 0, 4, C->stream), "wave counter")) return kRuntimeError;
+    // the last launch's wave-order kernel (its own stream): it zeroed the counter, and wrote
+    // the order this launch reads from the ticks this launch overwrites
+    if (C->order_pending && !C->hip_ok(hipStreamWaitEvent(C->stream, C->ev_order, 0), "wave order wait"))
+      return kRuntimeError;
+    C->order_pending = false;
+    // (the wave-order kernel after the last launch zeroed it already)
+    if (!C->ctr_zero && !C->hip_ok(hipMemsetAsync(C->wave_ctr.ptr, 0, 4, C->stream), "wave counter"))
+      return kRuntimeError;
+    C->ctr_zero = false;
     k.wave_ctr = C->wave_ctr.ptr;
     blocks = C->cap_blocks;
     // longest-first order from the last launch of this function (batch_ctx.h wave_order)
@@ -397,14 +406,27 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     return kRuntimeError;
   (void)hipEventRecord(C->ev1, C->stream);
   // the next launch of this function takes the longest waves first (sorted on the device,
-  // after the timed kernel; the order buffer is only read by later launches)
+  // after the timed kernel, on a stream of its own so that it overlaps the next Reset; the
+  // order buffer is only read by later launches)
   if (k.wave_ticks) {
-    if (!C->hip_ok(wb_launch_wave_order(k.wave_ticks, C->wave_order.ptr, C->nwaves, C->stream), "wave order"))
+    if (!C->order_stream &&
+        (!C->hip_ok(hipStreamCreateWithFlags(&C->order_stream, hipStreamNonBlocking), "stream") ||
+         !C->hip_ok(hipEventCreateWithFlags(&C->ev_order, hipEventDisableTiming), "event")))
       return kRuntimeError;
+    if (!C->hip_ok(hipStreamWaitEvent(C->order_stream, C->ev1, 0), "wave order wait") ||
+        !C->hip_ok(wb_launch_wave_order(k.wave_ticks, C->wave_order.ptr, C->nwaves, C->wave_ctr.ptr,
+                                        C->order_stream), "wave order") ||
+        !C->hip_ok(hipEventRecord(C->ev_order, C->order_stream), "wave order"))
+      return kRuntimeError;
+    C->order_pending = true;
     C->order_pc = entry_pc;
+    C->ctr_zero = true;
   }
-  if (!C->hip_ok(hipStreamSynchronize(C->stream), "interpreter kernel")) return kRuntimeError;
-  C->reset_pending = false;   // (the stream is drained)
+  // the interpreter kernel's end
+  if (!C->hip_ok(hipEventSynchronize(C->ev1), "interpreter kernel") ||
+      !C->hip_ok(hipGetLastError(), "interpreter kernel"))
+    return kRuntimeError;
+  C->reset_pending = false;   // (the instance state is final)
   if (KernelSeconds) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, C->ev0, C->ev1);
@@ -537,24 +559,28 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   const uint32_t init_words = C->mem_words;
   (void)hipEventRecord(C->ev0, C->stream);
   if (!pool_reset(C)) return R(kRuntimeError);
+  // after a run the memory kernel's write-mark path resets the instance state as well
+  const bool fused = P.has_mem && !C->mem_fresh && init_words;
   if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->lstate.ptr, C->ls_slots,
-                                    C->mem_fresh ? 1u : 0u, C->mlog, C->stream), "mem init"))
+                                    C->mem_fresh ? 1u : 0u, C->mlog, fused ? 1u : 0u, C->global_init.ptr, P.mem_min,
+                                    C->init_dropped, C->init_cost, C->stream), "mem init"))
     return R(kRuntimeError);
   C->mem_fresh = false;   // from now on every lane's write mark (LS_HWM) is valid
   // per-lane tables (instantiate/table.cpp + elem.cpp): every lane starts from the image
   if (P.mut_tables &&
       !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
-                                    P.tab_words, C->nwaves, nullptr, 0, 1u, 0u, C->stream), "table init"))
+                                    P.tab_words, C->nwaves, nullptr, 0, 1u, 0u, 0u, nullptr, 0, 0, 0,
+                                    C->stream), "table init"))
     return R(kRuntimeError);
   // gas: instantiation's constant expressions are priced first (module.cpp order); one
   // past the limit fails the instantiation like the reference's VM::instantiate
   if (C->conf.CostLimit && C->init_exceeded)
     return R(C->fail(0x03, "instantiation exceeds the cost limit (constant expressions)"));
-  if (!C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->global_init.ptr, P.global_cells,
-                                      C->ls_slots, P.mem_min, C->init_dropped, C->nwaves,
-                                      C->init_cost, C->stream), "state init"))
+  if (!fused && !C->hip_ok(wb_launch_state_init(C->lstate.ptr, C->ls_slots, C->nwaves, C->global_init.ptr,
+                                                P.mem_min, C->init_dropped, C->init_cost, C->stream),
+                           "state init"))
     return R(kRuntimeError);
   (void)hipEventRecord(C->ev1, C->stream);
   // without a start function and without a request for the time, the next launch on the
@@ -966,6 +992,11 @@ void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   DevScope dev(C);
   if (C->stream) (void)hipStreamSynchronize(C->stream);
   if (C->ctl_stream) (void)hipStreamDestroy(C->ctl_stream);
+  if (C->order_stream) {
+    (void)hipStreamSynchronize(C->order_stream);
+    (void)hipStreamDestroy(C->order_stream);
+  }
+  if (C->ev_order) (void)hipEventDestroy(C->ev_order);
   if (C->stop) (void)hipFree(C->stop);
   if (C->stats) (void)hipFree(C->stats);
   if (C->ev0) (void)hipEventDestroy(C->ev0);

@@ -91,6 +91,10 @@ struct WasmEdge_BatchContext {
   uint32_t cap_threads = 0, cap_blocks = 0;
   size_t cap_lds = 0;
   DevBuf<uint32_t> wave_ctr;
+  bool ctr_zero = false;           // wave_ctr is 0 (zeroed by the wave-order kernel)
+  hipStream_t order_stream = nullptr;   // the wave-order kernel (overlaps the next Reset)
+  hipEvent_t ev_order = nullptr;        // its end; the next persistent launch waits on it
+  bool order_pending = false;
   // Longest-first wave order (KParams::wave_order): each persistent launch records every
   // batch wave's run time; the next launch of the same function takes the waves in
   // descending order of it (LPT), so the heavy waves start first instead of wherever their

@@ -899,31 +899,54 @@ extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_pg_kernel(const 
 // `init_words` = the rows this covers: the whole reserved layout (rpages), so that pages a
 // lane grows into later read zero without memory.grow writing them; pool rows are zeroed
 // by the host (batch_api.cpp pool_reset).
+// Instance state at instantiation (instantiate/module.cpp: memory of `min` pages, active
+// data segments dropped, globals from their initialisers, no failure yet): LS slot `slot`.
+struct StateInit {
+  const uint32_t *global_init;
+  uint32_t init_pages, init_dropped;
+  uint64_t init_cost;
+  uint32_t on;   // (mem init) reset the state too
+};
+__device__ __forceinline__ uint32_t state_word(uint32_t slot, const StateInit &st) {
+  if (slot == LS_PAGES) return st.init_pages;
+  if (slot == LS_DROPPED) return st.init_dropped;
+  if (slot == LS_RPC) return 0xFFFFFFFFu;
+  if (slot == LS_COST) return (uint32_t)st.init_cost;
+  if (slot == LS_COST + 1) return (uint32_t)(st.init_cost >> 32);
+  if (slot >= LS_GLOBALS) return st.global_init[slot - LS_GLOBALS];
+  return 0;
+}
+
+// (write-mark path) with st.on set, the wave's instance state is reset too, after
+// its mark was read: one launch per Reset instead of two
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
                    uint32_t init_words, uint32_t mem_words, uint32_t nwaves,
-                   const uint32_t *ls, uint32_t ls_slots, uint32_t full, uint32_t g) {
+                   uint32_t *ls, uint32_t ls_slots, uint32_t full, uint32_t g, StateInit st) {
   const uint32_t chunks = (init_words + 1023u) / 1024u;
-  __shared__ uint32_t smax;
   if (!full && ls) {
-    // a Reset after a run: one block per wave reads the wave's write mark once and
-    // rewrites the rows below it (usually a few; the mark is per lane, the rows per wave)
-    for (size_t wave = blockIdx.x; wave < nwaves; wave += gridDim.x) {
-      if (threadIdx.x == 0) smax = 0;
-      __syncthreads();
-      if (threadIdx.x < 64) atomicMax(&smax, ls[((size_t)wave * ls_slots + LS_HWM) * 64u + threadIdx.x]);
-      __syncthreads();
-      const uint64_t hw = ((uint64_t)smax + 3u) / 4u;
+    // a Reset after a run: 64 threads per batch wave (4 per block) read the wave's write
+    // marks once (a shuffle max) and rewrite the rows below the highest (usually a few; the
+    // mark is per lane, the rows per wave)
+    const uint32_t lane = threadIdx.x & 63u;
+    for (size_t wave = (size_t)blockIdx.x * 4u + (threadIdx.x >> 6); wave < nwaves;
+         wave += (size_t)gridDim.x * 4u) {
+      uint32_t m = ls[((size_t)wave * ls_slots + LS_HWM) * 64u + lane];
+      for (uint32_t o = 32; o; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, 64));
+      const uint64_t hw = ((uint64_t)m + 3u) / 4u;
       uint32_t rows = (uint32_t)(hw < init_words ? hw : init_words);
       if (rows < image_words && image_words <= init_words) rows = image_words;
       const uint32_t gm = (1u << g) - 1u;
       rows = (rows + gm) & ~gm;
       if (rows > init_words) rows = init_words;
-      __syncthreads();   // smax is reused by the next wave
       uint32_t *wm = mem + wave * mem_words * (size_t)64u;
-      for (size_t i = threadIdx.x; i < (size_t)rows * 64u; i += blockDim.x) {
+      for (size_t i = lane; i < (size_t)rows * 64u; i += 64u) {
         const uint32_t word = (uint32_t)(((i >> (6 + g)) << g) | (i & ((1u << g) - 1u)));
         wm[i] = word < image_words ? image[word] : 0u;
+      }
+      if (st.on) {   // (after every lane's mark was read: the shuffle)
+        uint32_t *lw = ls + (size_t)wave * ls_slots * 64u;
+        for (uint32_t i = lane; i < ls_slots * 64u; i += 64u) lw[i] = state_word(i >> 6, st);
       }
     }
     return;
@@ -931,21 +954,7 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
   for (size_t b = blockIdx.x; b < (size_t)nwaves * chunks; b += gridDim.x) {
     const size_t wave = b / chunks;
     const uint32_t r0 = (uint32_t)(b - wave * chunks) * 1024u;
-    uint32_t rows = init_words;
-    if (!full && ls) {
-      if (threadIdx.x == 0) smax = 0;
-      __syncthreads();
-      if (threadIdx.x < 64) atomicMax(&smax, ls[((size_t)wave * ls_slots + LS_HWM) * 64u + threadIdx.x]);
-      __syncthreads();
-      const uint64_t hw = ((uint64_t)smax + 3u) / 4u;
-      rows = (uint32_t)(hw < init_words ? hw : init_words);
-      if (rows < image_words && image_words <= init_words) rows = image_words;
-      // whole granules: words [0, rows) of the 64 lanes are the linear range [0, rows*64)
-      const uint32_t gm = (1u << g) - 1u;
-      rows = (rows + gm) & ~gm;
-      if (rows > init_words) rows = init_words;
-      __syncthreads();   // smax is reused by the next iteration
-    }
+    const uint32_t rows = init_words;
     const uint32_t r1 = r0 + 1024u < rows ? r0 + 1024u : rows;
     if (r1 <= r0) continue;
     uint32_t *wm = mem + wave * mem_words * (size_t)64u;
@@ -958,25 +967,13 @@ wb_mem_init_kernel(uint32_t *mem, const uint32_t *image, uint32_t image_words,
   }
 }
 
-// Instance state at instantiation (instantiate/module.cpp: memory of `min` pages, active
-// data segments dropped, globals from their initialisers, no failure yet).
+// Instance state at instantiation, every wave (a Reset without the write-mark path).
 extern "C" __global__ void __launch_bounds__(256)
-wb_state_init_kernel(uint32_t *ls, const uint32_t *global_init, uint32_t global_cells,
-                     uint32_t ls_slots, uint32_t init_pages, uint32_t init_dropped,
-                     uint32_t nwaves, uint64_t init_cost) {
+wb_state_init_kernel(uint32_t *ls, uint32_t ls_slots, uint32_t nwaves, StateInit st) {
   const size_t total = (size_t)nwaves * ls_slots * 64u;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t slot = (uint32_t)((i >> 6) % ls_slots);
-    uint32_t v = 0;
-    if (slot == LS_PAGES) v = init_pages;
-    else if (slot == LS_DROPPED) v = init_dropped;
-    else if (slot == LS_RPC) v = 0xFFFFFFFFu;
-    else if (slot == LS_COST) v = (uint32_t)init_cost;
-    else if (slot == LS_COST + 1) v = (uint32_t)(init_cost >> 32);
-    else if (slot >= LS_GLOBALS) v = global_init[slot - LS_GLOBALS];
-    ls[i] = v;
-  }
+       i += (size_t)gridDim.x * blockDim.x)
+    ls[i] = state_word((uint32_t)((i >> 6) % ls_slots), st);
 }
 
 // Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
@@ -1025,12 +1022,16 @@ wb_mem_hash_fin_kernel(const uint32_t *ls, uint32_t ls_slots, uint64_t *hashes, 
 // [0, max] (descending), in one block -- on the device, so no host round trip sits between
 // launches. Within a bucket the order is whatever the atomics give (scheduling only).
 extern "C" __global__ void __launch_bounds__(1024)
-wb_wave_order_kernel(const uint32_t *ticks, uint32_t *order, uint32_t nwaves) {
+wb_wave_order_kernel(const uint32_t *ticks, uint32_t *order, uint32_t nwaves, uint32_t *wave_ctr) {
   __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t wsum[16];
   __shared__ uint32_t mx;
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   cnt[t] = 0;
-  if (t == 0) mx = 0;
+  if (t == 0) {
+    mx = 0;
+    *wave_ctr = 0;   // the next persistent launch starts from batch wave 0 (no memset)
+  }
   __syncthreads();
   for (uint32_t w = t; w < nwaves; w += 1024) atomicMax(&mx, ticks[w]);
   __syncthreads();
@@ -1038,10 +1039,19 @@ wb_wave_order_kernel(const uint32_t *ticks, uint32_t *order, uint32_t nwaves) {
   for (uint32_t w = t; w < nwaves; w += 1024)
     atomicAdd(&cnt[1023u - (uint32_t)((uint64_t)ticks[w] * 1024u / span)], 1u);
   __syncthreads();
-  if (t == 0) {   // exclusive prefix sum, heaviest bucket first
-    uint32_t run = 0;
-    for (uint32_t b = 0; b < 1024; b++) { const uint32_t c = cnt[b]; cnt[b] = run; run += c; }
+  // exclusive prefix sum over the buckets, heaviest first: a shuffle scan per wave, then
+  // the 16 wave totals
+  const uint32_t c = cnt[t];
+  uint32_t x = c;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t i = 0; i < wv; i++) off += wsum[i];
+  cnt[t] = off + x - c;
   __syncthreads();
   for (uint32_t w = t; w < nwaves; w += 1024)
     order[atomicAdd(&cnt[1023u - (uint32_t)((uint64_t)ticks[w] * 1024u / span)], 1u)] = w;
@@ -1049,8 +1059,8 @@ wb_wave_order_kernel(const uint32_t *ticks, uint32_t *order, uint32_t nwaves) {
 
 // ======================================================================= launchers
 extern "C" hipError_t wb_launch_wave_order(const uint32_t *ticks, uint32_t *order, uint32_t nwaves,
-                                           hipStream_t s) {
-  hipLaunchKernelGGL(wb_wave_order_kernel, dim3(1), dim3(1024), 0, s, ticks, order, nwaves);
+                                           uint32_t *wave_ctr, hipStream_t s) {
+  hipLaunchKernelGGL(wb_wave_order_kernel, dim3(1), dim3(1024), 0, s, ticks, order, nwaves, wave_ctr);
   return hipGetLastError();
 }
 // (host stubs live in this translation unit; the C-ABI layer calls these)
@@ -1090,15 +1100,19 @@ extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t th
 extern "C" hipError_t wb_launch_mem_init(uint32_t *mem, const uint32_t *image,
                                          uint32_t image_words, uint32_t init_words,
                                          uint32_t mem_words, uint32_t nwaves,
-                                         const uint32_t *ls, uint32_t ls_slots, uint32_t full,
-                                         uint32_t g, hipStream_t s) {
+                                         uint32_t *ls, uint32_t ls_slots, uint32_t full,
+                                         uint32_t g, uint32_t fuse_state, const uint32_t *global_init,
+                                         uint32_t init_pages, uint32_t init_dropped,
+                                         uint64_t init_cost, hipStream_t s) {
   const size_t total = (size_t)nwaves * ((init_words + 1023u) / 1024u);
   if (total == 0) return hipSuccess;
-  // full (re)initialisation: a block per 1024 rows of a wave; after a run: a block per
-  // wave (the kernel's write-mark path)
-  const size_t blocks = (!full && ls) ? nwaves : (total < 262144 ? total : 262144);
+  // full (re)initialisation: a block per 1024 rows of a wave; after a run: 64 threads per
+  // wave (the kernel's write-mark path, which also resets the instance state when
+  // fuse_state is set)
+  const size_t blocks = (!full && ls) ? (nwaves + 3u) / 4u : (total < 262144 ? total : 262144);
+  const StateInit st{global_init, init_pages, init_dropped, init_cost, (!full && ls && fuse_state) ? 1u : 0u};
   hipLaunchKernelGGL(wb_mem_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, mem, image,
-                     image_words, init_words, mem_words, nwaves, ls, ls_slots, full, g);
+                     image_words, init_words, mem_words, nwaves, ls, ls_slots, full, g, st);
   return hipGetLastError();
 }
 extern "C" hipError_t wb_launch_mem_hash(uint32_t *mem, const uint32_t *ls,
@@ -1116,15 +1130,14 @@ extern "C" hipError_t wb_launch_mem_hash(uint32_t *mem, const uint32_t *ls,
                      hashes, n);
   return hipGetLastError();
 }
-extern "C" hipError_t wb_launch_state_init(uint32_t *ls, const uint32_t *global_init,
-                                           uint32_t global_cells, uint32_t ls_slots,
-                                           uint32_t init_pages, uint32_t init_dropped,
-                                           uint32_t nwaves, uint64_t init_cost, hipStream_t s) {
+extern "C" hipError_t wb_launch_state_init(uint32_t *ls, uint32_t ls_slots, uint32_t nwaves,
+                                           const uint32_t *global_init, uint32_t init_pages,
+                                           uint32_t init_dropped, uint64_t init_cost, hipStream_t s) {
   const size_t total = (size_t)nwaves * ls_slots * 64u;
   size_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(wb_state_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ls,
-                     global_init, global_cells, ls_slots, init_pages, init_dropped, nwaves,
-                     init_cost);
+  const StateInit st{global_init, init_pages, init_dropped, init_cost, 1u};
+  hipLaunchKernelGGL(wb_state_init_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ls, ls_slots,
+                     nwaves, st);
   return hipGetLastError();
 }
