@@ -232,7 +232,7 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
                      "on those instances"
                      % (what, n1, i1, s1, nt, threads, it, st),
            "calibration": "the oracle on 1 thread takes 0.9-1.4x the reference interpreter's "
-                          "time on fib(30) and 3.5x on mt19937 (BASELINE.md 3)"}
+                          "time on fib(30) and 2-2.5x on mt19937 (BASELINE.md 3)"}
     return rec, state["mbytes"] / state["instrs"]
 
 

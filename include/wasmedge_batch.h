@@ -103,8 +103,10 @@ typedef struct WasmEdge_BatchConfigure {
   uint32_t CostTableLen;
   /* Bytes per granule in which the device interleaves the linear memories of a wave's 64
    * instances (4, 8, ..., 128; 0 = chosen from the module: 4 when its memory addresses
-   * are the same in every instance, 128 when they depend on per-instance data). Layout
-   * only: results never depend on it. */
+   * are the same in every instance, 128 when they depend on per-instance data; when they
+   * depend only on parameters of exported functions, the first WasmEdge_BatchSetArgs
+   * decides from the values passed: 4 if every instance passes the same ones, else 128).
+   * Layout only: results never depend on it. WasmEdge_BatchGetMemoryGranule reports it. */
   uint32_t MemoryGranule;
   /* The TailCall proposal (return_call, return_call_indirect; WasmEdge_ConfigureAddProposal
    * (Conf, WasmEdge_Proposal_TailCall), include/common/configure.h:176-182 leaves it off):
@@ -328,6 +330,10 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchCon
  * frames, metering, WB_JIT=0, or a compile failure, whose message WasmEdge_BatchGetLastError
  * then returns until the next error). Results never depend on it. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *Cxt);
+
+/* The interleave granule in use, in bytes (WasmEdge_BatchConfigure::MemoryGranule).
+ * Layout only: results never depend on it. */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *Cxt);
 
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */

@@ -195,6 +195,8 @@ def lib():
         L.WasmEdge_BatchWASIGetOutput.argtypes = [vp, u32, u32, vp, u32]
         L.WasmEdge_BatchGetCompiledRuns.restype = u32
         L.WasmEdge_BatchGetCompiledRuns.argtypes = [vp]
+        L.WasmEdge_BatchGetMemoryGranule.restype = u32
+        L.WasmEdge_BatchGetMemoryGranule.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -358,6 +360,10 @@ class BatchContext:
     def compiled_runs(self):
         """Straight-line runs compiled for the V-frame core (WasmEdge_BatchGetCompiledRuns)."""
         return lib().WasmEdge_BatchGetCompiledRuns(self._h)
+
+    def memory_granule(self):
+        """The interleave granule in use, bytes (WasmEdge_BatchGetMemoryGranule)."""
+        return lib().WasmEdge_BatchGetMemoryGranule(self._h)
 
     def interrupt(self):
         lib().WasmEdge_BatchInterrupt(self._h)

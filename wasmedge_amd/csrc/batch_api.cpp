@@ -42,6 +42,65 @@ using namespace wbh;
 
 namespace {
 
+// The compiled runs of a V-frame context (jit.h) at the context's current layout
+// (C->mlog): assembled, loaded, patched into the threaded code `tcv` and flagged in
+// `codepad`. A compile failure is not fatal (the core interprets) but is kept as the last
+// error.
+void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::vector<TInstr> &tcv) {
+  const wb::Program &P = C->prog;
+  const bool want_simt = C->want_simt;
+  bool want_trip = C->want_trip;
+  std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt, want_trip);
+  if (want_trip && runs.size() > wb::kTripMaxRuns) {   // (too many runs to visit per trip)
+    want_trip = false;
+    runs = wb::jit_runs(P, tcv, want_simt, false);
+  }
+  // debugging aids (tools/trip_debug.py): WB_TRIP_LIST=<file> writes the runs' start pcs,
+  // WB_TRIP_EXCL=<pc>,<pc>,... leaves the runs starting there to the handlers
+  if (const char *tl = getenv("WB_TRIP_LIST"))
+    if (FILE *f = fopen(tl, "w")) {
+      for (const auto &r : runs) fprintf(f, "%u %u\n", r.pc, r.len);
+      fclose(f);
+    }
+  if (const char *tx = getenv("WB_TRIP_EXCL")) {
+    std::vector<uint32_t> ex;
+    for (const char *q = tx; *q;) {
+      ex.push_back(uint32_t(strtoul(q, const_cast<char **>(&q), 10)));
+      if (*q == ',') q++;
+      else break;
+    }
+    runs.erase(std::remove_if(runs.begin(), runs.end(),
+                              [&](const wb::JitRun &r) { return std::find(ex.begin(), ex.end(), r.pc) != ex.end(); }),
+               runs.end());
+  }
+  if (!runs.empty()) {
+    std::vector<uint8_t> start(P.code.size() + 1, 0);
+    for (const auto &r : runs) start[r.pc] = 1;
+    std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
+    std::vector<uint64_t> addr;
+    const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
+    const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
+                                           want_trip);
+    const std::string err = src.empty() ? std::string("compiled runs: no source")
+                                        : wb::jit_load(src, runs.size(), C->device, &addr);
+    if (err.empty()) {
+      if (C->conf.CostLimit)   // metered: the core holds the runs and nothing else
+        for (size_t pc = 0; pc < P.code.size(); pc++) {
+          tcj[pc].w[0] = 0;
+          codepad[pc].w0 &= ~DBC_HOT;
+        }
+      wb::jit_patch(tcj, runs, addr);
+      for (const auto &r : runs) codepad[r.pc].w0 |= DBC_HOT;   // the core is entered there
+      tcv.swap(tcj);
+      C->jit_runs = uint32_t(runs.size());
+      C->simt = want_simt;
+      C->trip = want_trip;
+    } else {
+      C->last_error = err;
+    }
+  }
+}
+
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
   std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports,
@@ -111,6 +170,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // consecutive words together) when they diverge per lane (Program::divergent_mem)
   uint32_t gb = C->conf.MemoryGranule;
   if (const char *e = getenv("WB_GRANULE")) gb = uint32_t(atoi(e));
+  // a module whose addresses may differ between instances starts at 128-byte granules and
+  // tries 4-byte words on its second run (layout_trial; WB_GRANULE_TRIAL=0 turns it off)
+  const char *gte = getenv("WB_GRANULE_TRIAL");
+  if (gb == 0 && P.divergent_mem && P.has_mem && !(gte && gte[0] == '0')) {
+    C->trial = 1;
+    C->trial_mlog[0] = 5;   // 128 B
+    C->trial_mlog[1] = 0;   // 4 B
+  }
   if (gb == 0) gb = P.divergent_mem ? 128 : 4;   // profiles/r02h_c3_granules.json
   if (gb < 4 || gb > 128 || (gb & (gb - 1)))
     return C->fail(kRuntimeError, "MemoryGranule must be 0 or a power of two in [4, 128]");
@@ -184,57 +251,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // on (A/B measurement aid). SIMT contexts only.
   const char *tre = getenv("WB_TRIP");
   bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem || wb::trips_pay(P));
-  if (C->threaded && C->vframe && !(jte && jte[0] == '0')) {
-    std::vector<wb::JitRun> runs = wb::jit_runs(P, tcv, want_simt, want_trip);
-    if (want_trip && runs.size() > wb::kTripMaxRuns) {   // (too many runs to visit per trip)
-      want_trip = false;
-      runs = wb::jit_runs(P, tcv, want_simt, false);
-    }
-    // debugging aids (tools/trip_debug.py): WB_TRIP_LIST=<file> writes the runs' start pcs,
-    // WB_TRIP_EXCL=<pc>,<pc>,... leaves the runs starting there to the handlers
-    if (const char *tl = getenv("WB_TRIP_LIST"))
-      if (FILE *f = fopen(tl, "w")) {
-        for (const auto &r : runs) fprintf(f, "%u %u\n", r.pc, r.len);
-        fclose(f);
-      }
-    if (const char *tx = getenv("WB_TRIP_EXCL")) {
-      std::vector<uint32_t> ex;
-      for (const char *q = tx; *q;) {
-        ex.push_back(uint32_t(strtoul(q, const_cast<char **>(&q), 10)));
-        if (*q == ',') q++;
-        else break;
-      }
-      runs.erase(std::remove_if(runs.begin(), runs.end(),
-                                [&](const wb::JitRun &r) { return std::find(ex.begin(), ex.end(), r.pc) != ex.end(); }),
-                 runs.end());
-    }
-    if (!runs.empty()) {
-      std::vector<uint8_t> start(P.code.size() + 1, 0);
-      for (const auto &r : runs) start[r.pc] = 1;
-      std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
-      std::vector<uint64_t> addr;
-      const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
-      const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
-                                             want_trip);
-      const std::string err = src.empty() ? std::string("compiled runs: no source")
-                                          : wb::jit_load(src, runs.size(), C->device, &addr);
-      if (err.empty()) {
-        if (C->conf.CostLimit)   // metered: the core holds the runs and nothing else
-          for (size_t pc = 0; pc < P.code.size(); pc++) {
-            tcj[pc].w[0] = 0;
-            codepad[pc].w0 &= ~DBC_HOT;
-          }
-        wb::jit_patch(tcj, runs, addr);
-        for (const auto &r : runs) codepad[r.pc].w0 |= DBC_HOT;   // the core is entered there
-        tcv.swap(tcj);
-        C->jit_runs = uint32_t(runs.size());
-        C->simt = want_simt;
-        C->trip = want_trip;
-      } else {
-        C->last_error = err;
-      }
-    }
-  }
+  C->want_simt = want_simt;
+  C->want_trip = want_trip;
+  C->jit_on = C->threaded && C->vframe && !(jte && jte[0] == '0');
+  C->codepad0 = codepad;   // (pristine: a change of layout compiles the runs again)
+  if (C->jit_on) compile_runs(C, codepad, tcv);
   // LS image from slot LS_GLOBALS on: globals, then (per-lane tables) table sizes and
   // the dropped-elem mask
   std::vector<uint32_t> ls_init = P.global_init;
@@ -292,6 +313,51 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (!C->hip_ok(hipMalloc(&C->stats, (nw * 32 + 1024) * sizeof(uint64_t)), "stats")) return kRuntimeError;
 #endif
   if (!C->hip_ok(hipStreamSynchronize(s), "upload")) return kRuntimeError;
+  return 0;
+}
+
+// A new interleave granule (at a Reset, which then writes every page of every lane): the
+// compiled runs again at the new layout.
+uint8_t relayout(WasmEdge_BatchContext *C, uint32_t mlog) {
+  if (!C->settle()) return kRuntimeError;
+  C->mlog = mlog;
+  if (C->jit_on) {
+    std::vector<DInstr> codepad = C->codepad0;
+    std::vector<TInstr> tcv = wb::build_threaded(C->prog, codepad, C->vframe);
+    C->jit_runs = 0;
+    C->simt = C->trip = false;
+    compile_runs(C, codepad, tcv);
+    if (!C->code.upload(codepad, C->stream) || !C->tcode.upload(tcv, C->stream))
+      return C->fail(kRuntimeError, "device upload of the module failed");
+  }
+  C->mem_fresh = true;
+  return 0;
+}
+
+// Layout trial: the interleave granule from observed throughput, for modules whose
+// addresses may differ between instances (Program::divergent_mem; the static analysis
+// cannot tell a per-lane index from a wave-uniform one kept in memory, such as mt19937's
+// state index). The first run at 128-byte granules and the next one, after a Reset, at
+// 4-byte words each measure wasm instructions per kernel second; the 4-byte layout stays
+// when it is at least 10% faster on the same function, else the next Reset goes back.
+// Trial runs do not use the longest-first wave order, so both see the same schedule.
+// Results never depend on the layout (tests/test_workloads.py granule matrix).
+uint8_t layout_trial(WasmEdge_BatchContext *C, double secs) {
+  std::vector<uint64_t> cnt(C->n);
+  if (secs <= 0 || !C->hip_ok(hipMemcpy(cnt.data(), C->counts.ptr, size_t(C->n) * 8, hipMemcpyDeviceToHost), "counts")) {
+    C->trial = C->trial == 3 ? 4 : 0;
+    return secs <= 0 ? 0 : kRuntimeError;
+  }
+  double sum = 0;
+  for (uint64_t c : cnt) sum += double(c);
+  const double rate = sum / secs;
+  if (C->trial == 1) {
+    C->trial_rate = rate;
+    C->trial_func = C->func;
+    C->trial = 2;
+  } else {   // 3
+    C->trial = C->func == C->trial_func && rate >= 1.10 * C->trial_rate ? 0 : 4;
+  }
   return 0;
 }
 
@@ -397,7 +463,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
       if (!C->wave_ticks.ptr && (!C->wave_ticks.alloc(C->nwaves) || !C->wave_order.alloc(C->nwaves)))
         return C->fail(kRuntimeError, "device allocation failed");
       k.wave_ticks = C->wave_ticks.ptr;
-      k.wave_order = C->order_pc == entry_pc ? C->wave_order.ptr : nullptr;
+      k.wave_order = C->order_pc == entry_pc && C->trial != 1 && C->trial != 3 ? C->wave_order.ptr : nullptr;
     }
   }
   (void)hipEventRecord(C->ev0, C->stream);
@@ -555,6 +621,11 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   if (!C->shards.empty()) return wbm::reset(C, KernelSeconds);
   DevScope dev(C);
   const wb::Program &P = C->prog;
+  if (C->trial == 2 || C->trial == 4) {   // (layout_trial)
+    const uint8_t e = relayout(C, C->trial_mlog[C->trial == 2 ? 1 : 0]);
+    if (e) return R(e);
+    C->trial = C->trial == 2 ? 3 : 0;
+  }
   // the whole reserved layout: pages a lane grows into within it must read zero
   const uint32_t init_words = C->mem_words;
   (void)hipEventRecord(C->ev0, C->stream);
@@ -621,8 +692,12 @@ WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSecond
   if (C->func < 0) return R(C->fail(kWrongVMWorkflow, "BatchSetArgs not called"));
   const wb::FuncInfo &F = C->prog.funcs[C->func];
   if (F.imported) return R(C->fail(kRuntimeError, "exported function is a host import"));
-  uint8_t e = launch_exec(C, F.entry_pc, false, KernelSeconds);
+  const bool measure = C->trial == 1 || C->trial == 3;
+  double ks = 0;
+  uint8_t e = launch_exec(C, F.entry_pc, false, KernelSeconds || measure ? &ks : nullptr);
   if (e) return R(e);
+  if (KernelSeconds) *KernelSeconds = ks;
+  if (measure && (e = layout_trial(C, ks))) return R(e);
   C->ran = true;
   return R(0);
 }
@@ -704,6 +779,11 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
 uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) {
   if (C && !C->shards.empty()) return WasmEdge_BatchGetCompiledRuns(wbm::first(C));
   return C ? C->jit_runs : 0;
+}
+
+uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *C) {
+  if (C && !C->shards.empty()) return WasmEdge_BatchGetMemoryGranule(wbm::first(C));
+  return C ? 4u << C->mlog : 0;
 }
 
 WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchContext *C, uint64_t *Costs) {

@@ -84,6 +84,15 @@ struct WasmEdge_BatchContext {
   uint32_t jit_runs = 0;          // compiled straight-line runs (jit.h)
   bool simt = false;              // KParams::simt: the compiled runs schedule diverged lanes
   bool trip = false;              // ... in trip mode (jit.h)
+  bool want_simt = false, want_trip = false, jit_on = false;   // (compile_runs inputs)
+  std::vector<DInstr> codepad0;   // the module's DBC before compile_runs flags it
+  // layout trial (batch_api.cpp layout_trial): 1 = the next run measures the module's
+  // granule, 2 = the next Reset switches to the other one, 3 = the next run measures that,
+  // 4 = the next Reset switches back; 0 = decided
+  uint8_t trial = 0;
+  uint32_t trial_mlog[2] = {0, 0};   // (the module's granule, the other one)
+  int trial_func = -1;
+  double trial_rate = 0;
   bool frame_hbm = false;         // frames in HBM (wb_exec_hbm_kernel), KParams::hframe
   DevBuf<uint32_t> hframe;
   // persistent waves (KParams::wave_ctr): the exec kernel's resident blocks for the last
