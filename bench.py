@@ -82,6 +82,13 @@ def workload(name, args):
                 [batch.I32, batch.I64, batch.I64],
                 "mt19937 of test/thread/ThreadTest.cpp:31-163, %d draws from a per-instance seed" % n,
                 {"draws": n})
+    if name == "tail":
+        # not a BASELINE config: the TailCall proposal's return_call / return_call_indirect
+        # (tail recursion, mutual recursion through a table), 5000 + id mod 13 outer steps
+        return (workloads.tail_wasm(), "run",
+                lambda ids: np.stack([ids, np.full_like(ids, 5000)], 1), [I32, I32],
+                "tail-recursive countdown + mutual even/odd (return_call, return_call_indirect)",
+                {"steps": 5000})
     raise SystemExit("unknown workload " + name)
 
 
@@ -181,7 +188,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
+def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, tail_call=False):
     """The oracle (C restatement of the reference interpreter, oracle/) timed on the
     box's host cores over a bounded sample of the same workload: chunks of instances
     (ids 0, 1, 2, ...), first on ONE thread for about budget_s / 4 seconds, then on
@@ -191,7 +198,7 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what):
     record and the sample's linear-memory bytes per wasm instruction."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
-    m = oracle_py.Module(wasm)
+    m = oracle_py.Module(wasm, tail_call=tail_call)
     n_max = len(gpu["counts"])
     # chunks of about a quarter of a phase at the oracle's ~2e8 instr/s per thread
     t_inst = float(gpu["counts"].mean()) / 2e8
@@ -271,7 +278,7 @@ def main():
     ap.add_argument("--instances", type=int, default=INSTANCES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "mt"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "mt", "tail"])
     ap.add_argument("--mt-n", type=int, default=100000, help="mt19937 draws per instance")
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     ap.add_argument("--cost-limit", type=int, default=0,
@@ -298,6 +305,8 @@ def main():
     ids = shard_ids(dist.rank, args.instances, dist.world, args.scaling)
     n = len(ids)
     kw = {"max_memory_page": 17} if args.workload == "c3" else {}
+    if args.workload == "tail":
+        kw["tail_call"] = True
     if args.cost_limit:
         kw["cost_limit"] = args.cost_limit
     rows = build_rows(ids)
@@ -399,7 +408,8 @@ def main():
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads = host_cores()
         out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
-                                                threads, gpu, args.workload.upper())
+                                                threads, gpu, args.workload.upper(),
+                                                tail_call=args.workload == "tail")
         if args.workload == "c3":
             # qsort's bytes per instruction is stable across instances
             c3_bytes_per_instr, c3_bpi_src = bpi, " on the oracle sample"

@@ -538,6 +538,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     const int32_t _c0 = __builtin_amdgcn_readfirstlane(_tc); \
     if (__ballot(_t == _n0 && _tc == _c0) == act) JUMP(_n0, _c0); \
     xpc = _t; xadj = _tc; goto k_exit; } while (0)
+#define WB_UNIFORM(x) __builtin_amdgcn_readfirstlane(x)   // (dbc_step.inc: a wave-uniform value)
 #define TRAP(code) (tcode = (code))
 #define FINISH() (tcode = WB_TCODE_DONE)
 #define EXIT_IF_TRAPPED(t) do { if (__ballot(tcode != 0)) { xpc = (t); xadj = 0; goto k_exit; } } while (0)

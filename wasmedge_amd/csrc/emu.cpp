@@ -200,6 +200,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define GS_RD(s) GS(s)
 #define GS_WR(s, v) (GS(s) = (v))
 #define GS_FAST(hi) true
+#define WB_UNIFORM(x) (x)   // (one lane)
 #define GSF_BASE(s) (&GS(s))
 #define GS_PTR uint32_t *const
 #define GS_CPTR const uint32_t *const

@@ -482,6 +482,30 @@ def specs():
                      ["v_add_u32_e32 %s, 0x100, %s" % (X[0], X[0]), "s_add_u32 %s, %s, 1" % (di, di)])
         return out + g.next()
 
+    # return_call (dbc_step.inc OP_TAIL_CALL): the callee takes over the frame -- arguments
+    # L.. -> fb.. (L >= fb: ascending is safe), its locals zeroed, no spill and no return
+    # record. Fields: w1 = L, w2 = fb, w4 = target*32, w7 = nargs | nlocals << 16.
+    def tail_call_body(g):
+        n = "s68"
+        if g.vf:
+            si, di = T2L, T2H
+            out = ["s_and_b32 %s, %s, 0xffff" % (n, g.x(7)),
+                   "s_mov_b32 %s, %s" % (si, g.x(1)), "s_mov_b32 %s, %s" % (di, g.x(2))]
+            out += vmove(g, "ar", n, si, di, 1)
+            out += ["s_lshr_b32 %s, %s, 16" % (n, g.x(7)), "v_mov_b32 %s, 0" % Y[0]]
+            out += vloop(g, "zl", n, g.vwrites([(di, [Y[0]])]) + ["s_add_u32 %s, %s, 1" % (di, di)])
+            return out + g.taken(g.x(4), g.x(6))
+        out = ["s_and_b32 %s, %s, 0xffff" % (n, g.x(7)),
+               "v_add_u32_e64 %s, %s, %s" % (X[0], g.x(1), FR),
+               "v_add_u32_e64 %s, %s, %s" % (X[1], g.x(2), FR)]
+        out += copy(X[0], X[1], n, "ar", g)
+        out += ["s_lshr_b32 %s, %s, 16" % (n, g.x(7)), "v_mov_b32 %s, 0" % Y[0]]
+        zt, ze = g.lab("zl"), g.lab("zle")
+        out += ["%s:" % zt, "s_cmp_eq_u32 %s, 0" % n, "s_cbranch_scc1 %s" % ze,
+                "ds_write_b32 %s, %s" % (X[1], Y[0]), "v_add_u32_e32 %s, 0x100, %s" % (X[1], X[1]),
+                "s_sub_u32 %s, %s, 1" % (n, n), "s_branch %s" % zt, "%s:" % ze]
+        return out + g.taken(g.x(4), g.x(6))
+
     def call_body(g):
         if g.vf:
             return call_body_v(g)
@@ -717,6 +741,7 @@ def specs():
     add("CALL", ["CALL"], call_body, slots=2)
     add("RET", ["RET"], ret_body, slots=2)
     add("POST_CALL", ["POST_CALL"], post_call_body, slots=2)
+    add("TAIL_CALL", ["TAIL_CALL"], tail_call_body, slots=2)
     add("I32_CLZ", ["I32_CLZ"], lambda g: [
         "v_ffbh_u32_e32 %s, %s" % (X[0], A[0]),
         "v_min_u32_e32 %s, 32, %s" % (R[0], X[0])] + g.w32() + g.next())

@@ -2,6 +2,8 @@
 // dispatch core (gen_tc.py / tc_blob.inc). Field layout: tc.h.
 #include "tc.h"
 
+#include <cstdlib>
+
 #include "frontend.h"
 #include "tc_slots.h"
 
@@ -48,6 +50,8 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
   const uint32_t unit = vframe ? 1u : 256u;
   auto off = [T, unit](uint32_t cell) { return cell < T ? cell * unit : 0u; };
   std::vector<TInstr> tc(P.code.size() + 2, TInstr{{0, 0, 0, 0, 0, 0, 0, 0}});
+  const char *tte = getenv("WB_TC_TAIL");
+  const bool tail_off = tte && tte[0] == '0';
   for (size_t pc = 0; pc < P.code.size(); pc++) {
     const DInstr &I = P.code[pc];
     const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
@@ -109,6 +113,15 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
         w[4] = imm * 32u;
         w[7] = b | (c << 16);                     // nargs | nlocals << 16
       }
+    }
+    if (op == OP_TAIL_CALL) {   // gen_tc.py tail_call_body (WB_TC_TAIL=0: the C++ step, A/B aid)
+      const uint32_t fb = P.global_cells;
+      if (tail_off || a >= T || fb >= T || a < fb || imm >= (1u << 26) || b > 0xFFFFu) continue;
+      w[1] = a * unit;
+      w[2] = fb * unit;
+      w[3] = 0; w[5] = 0;
+      w[4] = imm * 32u;
+      w[7] = b | (c << 16);                       // nargs | locals to zero << 16
     }
     w[0] = uint32_t(slot) * TC_SLOT_BYTES;
     code[pc].w0 |= DBC_HOT;

@@ -347,6 +347,45 @@ def mandel_wasm():
     return assemble(mandel_wat())
 
 
+# ----------------------------------------------------------------- tail calls (not a config)
+def tail_wat():
+    return r"""
+(module
+  ;; Tail recursion with the TailCall proposal (return_call / return_call_indirect): a
+  ;; countdown accumulating a hash, which every 16th step calls a mutually tail-recursive
+  ;; even/odd pair over the low bits, one of them through a table. Frames never grow:
+  ;; run(iid, n) takes n + iid mod 13 outer steps.
+  (type $t (func (param i32 i32) (result i32)))
+  (table 2 funcref)
+  (elem (i32.const 0) $even $odd)
+  (func $even (type $t) (param $k i32) (param $acc i32) (result i32)
+    (if (result i32) (i32.eqz (local.get $k))
+      (then (i32.add (local.get $acc) (i32.const 1)))
+      (else (return_call_indirect (type $t) (i32.sub (local.get $k) (i32.const 1))
+                                  (i32.xor (local.get $acc) (local.get $k)) (i32.const 1)))))
+  (func $odd (type $t) (param $k i32) (param $acc i32) (result i32)
+    (if (result i32) (i32.eqz (local.get $k))
+      (then (local.get $acc))
+      (else (return_call $even (i32.sub (local.get $k) (i32.const 1))
+                               (i32.add (local.get $acc) (local.get $k))))))
+  (func $loop (param $n i32) (param $acc i32) (result i32)
+    (if (result i32) (i32.eqz (local.get $n))
+      (then (local.get $acc))
+      (else
+        (if (i32.eqz (i32.and (local.get $n) (i32.const 15)))
+          (then (local.set $acc (call $even (i32.and (local.get $acc) (i32.const 7)) (local.get $acc)))))
+        (return_call $loop (i32.sub (local.get $n) (i32.const 1))
+                           (i32.add (i32.mul (local.get $acc) (i32.const 31)) (local.get $n))))))
+  (func (export "run") (param $iid i32) (param $n i32) (result i32)
+    (return_call $loop (i32.add (local.get $n) (i32.rem_u (local.get $iid) (i32.const 13)))
+                       (local.get $iid))))
+"""
+
+
+def tail_wasm():
+    return assemble(tail_wat())
+
+
 WORKLOADS = {
     "blake3": (blake3_wasm, "run"),
     "qsort": (qsort_wasm, "sort"),
