@@ -489,9 +489,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
     C->ctr_zero = true;
   }
   // the interpreter kernel's end
-  if (!C->hip_ok(hipEventSynchronize(C->ev1), "interpreter kernel") ||
-      !C->hip_ok(hipGetLastError(), "interpreter kernel"))
-    return kRuntimeError;
+  if (!C->hip_ok(hipEventSynchronize(C->ev1), "interpreter kernel")) return kRuntimeError;
   C->reset_pending = false;   // (the instance state is final)
   if (KernelSeconds) {
     float ms = 0;
