@@ -87,3 +87,69 @@ def test_gpu_folds_match_oracle(built, fold, monkeypatch):
     r = rows()
     ref = oracle_run(O.Module(FOLD), "run", r)
     assert compare(ref, *gpu_run(FOLD, "run", r, [I32, I32], [I64]), [I64], exact=True) == []
+
+
+# The compare-mask branch (WB_CMPANY): an f64x2 compare feeding a fused any_true
+# branch hands its two lane masks to the branch (s_or_b64 of the masks) instead of
+# materializing the all-ones cells. br_if and br_unless (eqz) forms, f64x2.ne / lt / eq,
+# lanes holding NaN (0/0) and +-inf, so unordered compares take part.
+CMPANY = assemble(r"""
+(module
+  (func (export "run") (param $s i32) (param $n i32) (result i64)
+    (local $v v128) (local $i i32) (local $hits i32)
+    (local.set $v (f64x2.replace_lane 1 (f64x2.splat (f64.convert_i32_s (local.get $s)))
+                    (f64.div (f64.convert_i32_s (local.get $s)) (f64.const 0))))
+    (block $out (loop $l
+      (br_if $out (i32.ge_u (local.get $i) (local.get $n)))
+      (block $a
+        (br_if $a (v128.any_true (f64x2.ne (local.get $v) (f64x2.splat (f64.convert_i32_u (local.get $i))))))
+        (local.set $hits (i32.add (local.get $hits) (i32.const 1))))
+      (block $b
+        (br_if $b (i32.eqz (v128.any_true (f64x2.lt (local.get $v) (f64x2.splat (f64.const 2.0))))))
+        (local.set $hits (i32.add (local.get $hits) (i32.const 100))))
+      (block $c
+        (br_if $c (v128.any_true (f64x2.eq (local.get $v) (f64x2.splat (f64.convert_i32_u (local.get $i))))))
+        (local.set $hits (i32.add (local.get $hits) (i32.const 10000))))
+      (local.set $v (f64x2.add (local.get $v) (f64x2.splat (f64.const 0.5))))
+      (local.set $i (i32.add (local.get $i) (i32.const 1)))
+      (br $l)))
+    (i64.extend_i32_u (local.get $hits))))
+""")
+
+
+def cmpany_rows():
+    return [[s, n] for s in (-3, -1, 0, 1, 2, 5, -100, 7) for n in (0, 1, 5, 17)]
+
+
+def test_cmpany_emitted(built, tmp_path):
+    """The compiled code of CMPANY ORs the compare's two lane masks into the branch."""
+    from wasmedge_amd import batch
+    L = batch.lib()
+    L.wb_jit_check.restype = ctypes.c_int
+    L.wb_jit_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p, ctypes.c_uint32]
+    dump = tmp_path / "simt.s"
+    os.environ["WB_JIT_DUMP_SIMT"] = str(dump)
+    try:
+        err = ctypes.create_string_buffer(256)
+        n = ctypes.c_uint32()
+        assert L.wb_jit_check(CMPANY, len(CMPANY), 0, ctypes.byref(n), err, 256) > 0, err.value
+    finally:
+        del os.environ["WB_JIT_DUMP_SIMT"]
+    assert "s_or_b64 vcc, vcc, s[68:69]" in dump.read_text()
+
+
+def test_cmpany_rows_on_oracle():
+    """The rows reach both outcomes of each branch (NaN lanes included)."""
+    m = O.Module(CMPANY)
+    got = {m.run("run", r)[1][0] for r in cmpany_rows()}
+    assert len(got) > 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cmpany", ["1", "0"])
+def test_gpu_cmpany_matches_oracle(built, cmpany, monkeypatch):
+    monkeypatch.setenv("WB_CMPANY", cmpany)
+    r = cmpany_rows()
+    ref = oracle_run(O.Module(CMPANY), "run", r)
+    assert compare(ref, *gpu_run(CMPANY, "run", r, [I32, I32], [I64]), [I64], exact=True) == []

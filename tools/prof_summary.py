@@ -35,13 +35,31 @@ XCDS = 8
 SIMDS = 256 * 4
 
 
+# PROF_LAST=n: the interpreter kernel's figures over its last n launches only (the bench's
+# timed steps: a run before them may have had another memory layout, the layout trial)
+LAST = int(os.environ.get("PROF_LAST", "0"))
+EXEC = ("wb_exec_vf_kernel", "wb_exec_kernel", "wb_exec_hbm_kernel", "wb_exec_vf_pg_kernel",
+        "wb_exec_pg_kernel", "wb_exec_hbm_pg_kernel")
+
+
 def counters(path):
     agg = collections.defaultdict(list)
     if not os.path.exists(path):
         return {}
-    for r in csv.DictReader(open(path)):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+    for r in rows:
         agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    return {k: sum(v[-LAST:] if LAST and k[0] in EXEC else v) / len(v[-LAST:] if LAST and k[0] in EXEC else v)
+            for k, v in agg.items()}
+
+
+def last_avg_ns(d, kernel):
+    """Mean duration of the kernel's last LAST launches in the trace pass."""
+    rows = [r for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv")))
+            if r["Kernel_Name"] == kernel]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ds = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[-LAST:]]
+    return sum(ds) / len(ds)
 
 
 def bench_line(path):
@@ -72,19 +90,20 @@ def main():
         C.update(counters(os.path.join(d, p, "run_counter_collection.csv")))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(d, "trace",
                                                                     "run_kernel_stats.csv")))}
-    K = next(k for k in ("wb_exec_vf_kernel", "wb_exec_kernel", "wb_exec_hbm_kernel") if k in stats)
+    K = next(k for k in EXEC if k in stats)
     H = "wb_mem_hash_kernel"
     g = lambda c, k=K: C.get((k, c))
     hash_bytes = 65536.0 * pages * inst
     fetch_factor = hash_bytes / (g("FETCH_SIZE", H) * 1024.0) if pages and g("FETCH_SIZE", H) else 2.0
     fetch = g("FETCH_SIZE") * 1024.0 * fetch_factor
     write = g("WRITE_SIZE") * 1024.0
-    avg_ns = float(stats[K]["AverageNs"])
+    avg_ns = last_avg_ns(d, K) if LAST else float(stats[K]["AverageNs"])
     waves = g("SQ_WAVES")
     wc = g("SQ_WAVE_CYCLES")                 # quad-cycles, summed over waves
     gui = g("GRBM_GUI_ACTIVE")               # cycles, summed over the XCDs
     valu = g("SQ_INSTS_VALU")
     out = {"config": profile_key(cfg), "source": tag, "kernel": K, "kernel_avg_ns": avg_ns,
+           "launches_averaged": ("the last %d" % LAST) if LAST else "all",
            "waves": waves, "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch,
            "write_bytes": write, "fetch_factor": fetch_factor,
            "valu_insts_per_launch": valu, "salu_insts_per_launch": g("SQ_INSTS_SALU"),
@@ -108,7 +127,9 @@ def main():
         out["vmem_latency_cycles"] = g("VmemLatency")
     lines = ["# %s: rocprofv3 counters, `bench.py` %s" % (tag, json.dumps(out["config"])), "",
              "Per-kernel means over launches (counter passes run separately, see "
-             "tools/prof_bench.sh).", "",
+             "tools/prof_bench.sh)%s." % (
+                 "; the interpreter kernel over its last %d launches (the timed steps)" % LAST
+                 if LAST else ""), "",
              "| kernel | counter | mean per launch |", "|---|---|---|"]
     for (k, c), v in sorted(C.items()):
         if k.startswith("wb_"):
