@@ -891,6 +891,7 @@ bool emit(Em &e, const DInstr &I) {
       }
       return true;
     }
+    case OP_TAIL_CALL:   // the last instruction of a run (emit_tail_call)
     case OP_CALL: {   // the last instruction of a run (emit_call)
       const uint32_t L = a, nargs = b, nloc = c, fb = e.fb;
       return L >= fb && L < TC_VF_CELLS && imm < (1u << 26) && uint64_t(L) + nargs <= TC_VF_CELLS &&
@@ -1543,6 +1544,17 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *
     if (!dead || !(*dead)[fb + nargs + k]) e.l("v_mov_b32 %s, 0", e.v(fb + nargs + k));
 }
 
+// TAIL_CALL (return_call, dbc_step.inc OP_TAIL_CALL; gen_tc.py tail_call_body): the
+// callee takes over the frame -- arguments L.. -> fb.. (ascending: L >= fb), its live
+// locals zeroed; no spill, no return record, then the transfer to its body like a jump.
+void emit_tail_call(Em &e, const DInstr &I, const std::vector<uint8_t> *dead) {
+  const uint32_t L = I.w1 & 0xFFFFu, nargs = I.w1 >> 16, nloc = I.w2 & 0xFFFFu, fb = e.fb;
+  for (uint32_t k = 0; k < nargs; k++)
+    if (L != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(L + k));
+  for (uint32_t k = 0; k < nloc; k++)
+    if (!dead || !(*dead)[fb + nargs + k]) e.l("v_mov_b32 %s, 0", e.v(fb + nargs + k));
+}
+
 // RET (gen_tc.py ret_body_v): pop the return record (it must agree across the lanes and
 // not be the entry frame's), results a.. -> fb.., jump to the return pc.
 // split: (SIMT) where the lanes' return records disagree, go there (Y1 = the records);
@@ -1647,7 +1659,7 @@ bool is_xfer(uint16_t op) { return op == OP_CALL || op == OP_RET; }
 bool is_branch_op(uint16_t op) {
   return op == OP_JMP || op == OP_BR_IF || op == OP_BR_UNLESS || (op >= OP_BR_EQ && op <= OP_BR_GE_U_I);
 }
-bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op) || op == OP_BR_TABLE; }
+bool ends_run(uint16_t op) { return is_xfer(op) || is_branch_op(op) || op == OP_BR_TABLE || op == OP_TAIL_CALL; }
 
 
 // The compare of a branch into vcc (true = taken).
@@ -1679,7 +1691,8 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bo
   // (br_table only with SIMT: its splits stay in the core, and SIMT contexts are never
   // metered, whose compiled runs would have to price each table entry)
   for (size_t pc = 0; pc < n; pc++)
-    ok[pc] = jit_ok(P, P.code[pc]) && (simt || op_of(P.code[pc]) != OP_BR_TABLE);
+    ok[pc] = jit_ok(P, P.code[pc]) && (simt || op_of(P.code[pc]) != OP_BR_TABLE) &&
+             (op_of(P.code[pc]) != OP_TAIL_CALL || (simt && !trip));   // (SIMT transfers only)
   for (size_t pc = 0; pc < n;) {
     if (!ok[pc]) { pc++; continue; }
     // a run ends after a call, return or branch (the run's code makes the transfer)
@@ -1692,7 +1705,7 @@ std::vector<JitRun> jit_runs(const Program &P, const std::vector<TInstr> &tc, bo
     bool calls = false;   // the call protocol's handlers are long: worth a run of any length
     for (size_t k = pc; k < end; k++) {
       const uint16_t o = op_of(P.code[k]);
-      calls |= is_xfer(o) || o == OP_POST_CALL || o == OP_BR_TABLE;
+      calls |= is_xfer(o) || o == OP_POST_CALL || o == OP_BR_TABLE || o == OP_TAIL_CALL;
     }
     // a lone branch: only with SIMT, where its splits then stay in the core
     if (end - pc == 1 && is_branch_op(op_of(P.code[pc]))) calls = simt && op_of(P.code[pc]) != OP_JMP;
@@ -3164,8 +3177,8 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     // the run is prefetched into both banks while the run works, unless it starts a
     // compiled run itself (then the code jumps there) or the run calls.
     const uint32_t fall = r.pc + r.len;
-    const uint32_t tgt = (lop == OP_CALL || is_branch_op(lop)) ? last.w3 : 0;
-    const uint32_t pre = lop == OP_CALL ? tgt : fall;
+    const uint32_t tgt = (lop == OP_CALL || lop == OP_TAIL_CALL || is_branch_op(lop)) ? last.w3 : 0;
+    const uint32_t pre = lop == OP_CALL || lop == OP_TAIL_CALL ? tgt : fall;
     const bool preload = lop != OP_RET && lop != OP_JMP && lop != OP_BR_TABLE && !start.count(pre);
     e.fb = P.global_cells;
     e.prog = &P;
@@ -3585,6 +3598,16 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       // the caller's run)
       e.l("Li%s:", IK.c_str());
       e.o += ei.o;
+    } else if (lop == OP_TAIL_CALL) {
+      std::vector<uint8_t> dead;
+      if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
+      emit_tail_call(e, last, dead.empty() ? nullptr : &dead);
+      e.gas_add(c_fall);
+      e.l("s_add_u32 s65, s65, 0x%x", r.cnt);
+      fast_to(tgt, true, false);
+      e.l("s_mov_b32 s62, 0x%x", tgt * 32u);
+      taken_checks();
+      go(tgt, preload);
     } else if (lop == OP_CALL) {
       std::vector<uint8_t> dead;
       if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
