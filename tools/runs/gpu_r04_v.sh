@@ -1,6 +1,6 @@
 # r04 v: closing bench lines at HEAD with their CPU baselines (rooflines from the r04t/r04u
 # profiles of this same build, profiles/prof_<workload>.json)
-O=gpurun_out/r04v; mkdir -p $O
+O=${OUT:-gpurun_out/r04v}; mkdir -p $O
 step() {  # name, timeout, command...
   local n=$1 t=$2; shift 2
   timeout -k 10 $t "$@" > $O/$n.json 2> $O/$n.err; local rc=$?
