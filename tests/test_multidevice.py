@@ -130,3 +130,35 @@ def test_gpu_two_shards_host_calls_and_state(built, part):
         assert [ctx.global_get("g", i)[0] for i in (0, 77, 129)] == [5, 5, 5]
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_shards_run_the_layout_trial(built):
+    """mt19937 over two shards on one device through Reset cycles: each shard runs its own
+    layout trial (128-byte granules first, then 4-byte words), every run bit-identical to
+    the oracle sample."""
+    import oracle_py as O
+    from conftest import golden
+    from helpers import compare, oracle_run
+    from wasmedge_amd import batch
+    wasm = golden("mt19937.wasm")
+    n = 4096
+    rows = [[0, 5489 + i, 3000] for i in range(n)]
+    idx = list(range(0, n, 211)) + [n - 1]
+    ref = oracle_run(O.Module(wasm), "mt19937", [rows[i] for i in idx])
+    ctx = batch.BatchContext(wasm, n, devices=[0, 0], partition=batch.PARTITION_INTERLEAVE)
+    try:
+        vals = batch.make_values(rows, [0x7F, 0x7E, 0x7E])
+        granules = []
+        for k in range(3):
+            if k:
+                ctx.reset()
+            rets, st, cnt = ctx.execute("mt19937", vals, 1)
+            h = ctx.memory_hash()
+            ints = batch.ret_ints(rets)
+            got = [[int(ints[i][0])] if st[i] == 0 else [] for i in idx]
+            assert compare(ref, got, st[idx], cnt[idx], h[idx], [0x7E]) == [], k
+            granules.append(ctx.memory_granule())
+        assert granules[0] == 128 and granules[1] == 4
+    finally:
+        ctx.close()

@@ -169,11 +169,18 @@ def test_host_tail_calls_emulator(built):
 
 
 @pytest.mark.gpu
-def test_gpu_tail_calls_match_oracle(built):
+@pytest.mark.parametrize("engine", ["compiled", "core", "step"])
+def test_gpu_tail_calls_match_oracle(built, monkeypatch, engine):
     """Every tail-call shape on the GPU (direct, mutual with zeroed locals and stores,
     indirect through the table, from the entry function) against the oracle, on 192 lanes
     of mixed depths -- up to 100,000 frames deep, far past the device call stack's 4,096
-    cells, which a tail call never uses."""
+    cells, which a tail call never uses. Engines: return_call compiled into the runs
+    (default), the threaded core's handler (WB_JIT=0), the compiled C++ step (WB_JIT=0,
+    WB_TC_TAIL=0)."""
+    if engine != "compiled":
+        monkeypatch.setenv("WB_JIT", "0")
+    if engine == "step":
+        monkeypatch.setenv("WB_TC_TAIL", "0")
     m = O.Module(TAIL, tail_call=True)
     rows = [[i % 3, (i * 977) % 1500] for i in range(190)] + [[0, 100000], [1, 100000]]
     ref = [m.run("run", r) for r in rows]
