@@ -1,5 +1,5 @@
 # r04 s: the whole -m gpu suite and smoke() at HEAD (the round's closing record)
-O=gpurun_out/r04s; mkdir -p $O
+O=${OUT:-gpurun_out/r04s}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 tail -3 $O/gpu_tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" $O/gpu_tests.log | head -20; exit $rc; }
