@@ -235,6 +235,19 @@ WasmEdge_BatchExecute(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName
                       WasmEdge_Value *Returns, const uint32_t ReturnLen,
                       uint8_t *PerInstance, uint64_t *InstrCounts);
 
+/* SURVEY.md §8(b)'s form of the same call: the per-instance outcome as a WasmEdge_Result
+ * each (Code = the status byte above). WasmEdge_Result is one byte (wasmedge.h:55-60), so
+ * an array of them is the status array itself. */
+typedef char WasmEdge_BatchResultIsOneByte[sizeof(WasmEdge_Result) == 1 ? 1 : -1];
+static inline WasmEdge_Result
+WasmEdge_BatchExecuteResults(WasmEdge_BatchContext *Cxt, const WasmEdge_String FuncName,
+                             const WasmEdge_Value *Params, const uint32_t ParamLen,
+                             WasmEdge_Value *Returns, const uint32_t ReturnLen,
+                             WasmEdge_Result *PerInstance, uint64_t *InstrCounts) {
+  return WasmEdge_BatchExecute(Cxt, FuncName, Params, ParamLen, Returns, ReturnLen,
+                               (uint8_t *)PerInstance, InstrCounts);
+}
+
 /* Ask a running BatchExecute/BatchRun on this context to stop (any thread): every
  * instance still running ends with Interrupted (0x07) at the next scheduler round (the
  * flag is read every round; a core call runs at most 2^20 instructions), like the
