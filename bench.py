@@ -195,7 +195,8 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, t
     `threads` threads for the rest of the budget (or until every instance ran). The
     oracle is the checker here too: the GPU's final state for the same instances must
     match bit for bit (status, return value, count, memory hash). Returns the baseline
-    record and the sample's linear-memory bytes per wasm instruction."""
+    record, the sample's linear-memory bytes per wasm instruction, and those bytes split
+    into (load, store) bytes per wasm instruction."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     m = oracle_py.Module(wasm, tail_call=tail_call)
@@ -203,7 +204,7 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, t
     # chunks of about a quarter of a phase at the oracle's ~2e8 instr/s per thread
     t_inst = float(gpu["counts"].mean()) / 2e8
     rmask = 0xFFFFFFFF if gpu["ret32"] else 0xFFFFFFFFFFFFFFFF
-    state = {"done": 0, "mbytes": 0.0, "instrs": 0.0}
+    state = {"done": 0, "mbytes": 0.0, "sbytes": 0.0, "instrs": 0.0}
 
     def phase(nthr, budget):
         # ids wrap round: a phase that runs out of instances starts over (checked again)
@@ -224,6 +225,7 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, t
                 raise SystemExit("GPU/oracle mismatch in instances %d..%d" % (ids[0], ids[-1]))
             instrs += float(out["counts"].sum())
             state["mbytes"] += float(out["mem_bytes"].sum())
+            state["sbytes"] += float(out["store_bytes"].sum())
             secs += out["seconds"]
             state["done"] = int((ids[-1] + 1) % n_max)
             ran += k
@@ -240,7 +242,8 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, t
                      % (what, n1, i1, s1, nt, threads, it, st),
            "calibration": "the oracle on 1 thread takes 0.9-1.4x the reference interpreter's "
                           "time on fib(30) and 2-2.5x on mt19937 (BASELINE.md 3)"}
-    return rec, state["mbytes"] / state["instrs"]
+    ld = (state["mbytes"] - state["sbytes"]) / state["instrs"]
+    return rec, state["mbytes"] / state["instrs"], (ld, state["sbytes"] / state["instrs"])
 
 
 def load_profile(workload, config):
@@ -264,23 +267,180 @@ def elapsed_hint(args):
     return args.workload == "c3" and args.elements >= 65536
 
 
+# The job's instance count per workload when --instances is not given: the metric's "64K
+# instances" (configs[1..3]) and C5's "256K across 8 MI355X" (configs[4]). With --gpus N > 1
+# this is the FIXED TOTAL the ranks split (strong scaling, the metric's configuration);
+# --scaling weak gives every rank that many instead.
+DEFAULT_INSTANCES = {"c5": 262144}
+
+
+def default_instances(workload):
+    return DEFAULT_INSTANCES.get(workload, INSTANCES)
+
+
+# Every bench workload runs on the compiled runs (DESIGN.md "Execution engines"): a context
+# that reports none fell back to the threaded core (a hiprtc / assembly failure), and its
+# line would silently measure a slower engine (the r04g failure mode).
+def check_engine(workload, compiled_runs, engine, last_error=""):
+    """SystemExit when a workload that compiles its runs in the test suite reports 0
+    compiled runs (unless WB_JIT=0 asked for the interpreter)."""
+    if compiled_runs == 0 and os.environ.get("WB_JIT", "1") != "0":
+        raise SystemExit("bench.py: %s ran on %s with 0 compiled runs (silent fallback from the "
+                         "compiled runs; last error: %s)" % (workload, engine, last_error or "none"))
+
+
+def vary_ids(ids, step, workload):
+    """Fresh inputs for step `step` (--vary-args): every instance gets another id -- a new
+    tile, seed, block or start value -- shifted by a stride that is not a multiple of the
+    wave size, so no wave sees the inputs of any earlier launch. C5's ids stay tile indices
+    of the 4096^2 image (a permutation of its 262,144 tiles)."""
+    shift = (step + 1) * 4099
+    if workload == "c5":
+        return (ids + shift) % 262144
+    return (ids + shift) % (1 << 30)
+
+
+class Phase:
+    """One measured configuration: a context over `ids` (or over several devices), warmup,
+    then exactly `steps` timed steps of Reset + Run. fresh: every step passes new arguments
+    (vary_ids), uploaded before the step's clock starts -- the timed region is the same
+    Reset + Run, on inputs the learned schedules have not seen."""
+
+    def __init__(self, args, dist, ids, devices=None):
+        from wasmedge_amd import batch
+        self.args, self.dist, self.ids = args, dist, ids
+        self.wasm, self.func, self.build_rows, self.ptypes, self.desc, self.extra = workload(args.workload, args)
+        kw = {"max_memory_page": 17} if args.workload == "c3" else {}
+        if args.workload == "tail":
+            kw["tail_call"] = True
+        if args.cost_limit:
+            kw["cost_limit"] = args.cost_limit
+        if devices:
+            kw["devices"] = devices
+            kw["partition"] = batch.PARTITION_BLOCKS
+        else:
+            kw["device"] = dist.local_rank
+        self.kw = kw
+        self.batch = batch
+        self.n = len(ids)
+        self.values = batch.make_values(self.build_rows(ids), self.ptypes)
+        self.t_start = time.perf_counter()
+        self.t0 = time.perf_counter()
+        self.ctx = batch.BatchContext(self.wasm, self.n, **kw)
+        self.t_create = time.perf_counter() - self.t0
+        self.e2e_s = {}
+
+    def progress(self, msg):
+        if self.dist.rank == 0:
+            print("[bench] %s %.1fs" % (msg, time.perf_counter() - self.t_start), file=sys.stderr, flush=True)
+
+    def outcome(self):
+        _, st, cnt = self.ctx.results(1)
+        traps = int((st != 0).sum())
+        if traps and self.args.workload != "c4":
+            raise SystemExit("%s instances trapped: %s" % (self.args.workload, np.unique(st)))
+        return float(cnt.sum()), traps
+
+    def warm(self, warmup):
+        """End-to-end passes (SURVEY.md 8(d) variant ii), the warmup steps themselves:
+         cold = BatchCreate (decode, validate, lower, hiprtc compile of the compiled runs,
+                device allocation, instantiation) + SetArgs (params H2D) + Run + Results;
+         warm = the same on the live context: SetArgs + Reset + Run + Results."""
+        ctx = self.ctx
+        t = self.t0
+        ctx.set_args(self.func, self.values)
+        self.instrs_per_step, self.traps = None, 0
+        if warmup:
+            ctx.run()
+            self.instrs_per_step, self.traps = self.outcome()
+            self.e2e_s["cold"] = time.perf_counter() - t
+            self.progress("warmup 1/%d done (end-to-end cold)" % warmup)
+        for w in range(1, warmup):
+            t = time.perf_counter()
+            ctx.set_args(self.func, self.values)
+            ctx.reset()
+            ctx.run()
+            self.outcome()
+            if w == 1:
+                self.e2e_s["warm"] = time.perf_counter() - t
+            self.progress("warmup %d/%d done" % (w + 1, warmup))
+        check_engine(self.args.workload, ctx.compiled_runs(), ctx.engine(),
+                     self.batch.lib().WasmEdge_BatchGetLastError(ctx._h).decode())
+
+    def timed(self, steps):
+        """Exactly `steps` timed steps bracketed by a barrier on both sides (BatchRun
+        synchronises its stream); returns (max elapsed over ranks, kernel seconds)."""
+        ctx, dist = self.ctx, self.dist
+        dist.barrier()
+        t0 = time.perf_counter()
+        ksum = 0.0
+        for k in range(steps):
+            ctx.reset(timed=False)   # (no host round trip: the run orders after it)
+            ksum += ctx.run()        # HIP-event time of the interpreter kernel (its stream)
+            if elapsed_hint(self.args):
+                self.progress("step %d/%d done" % (k + 1, steps))
+        elapsed = time.perf_counter() - t0
+        dist.barrier()
+        if self.instrs_per_step is None:
+            self.instrs_per_step, self.traps = self.outcome()
+        _, st, cnt = ctx.results(1)
+        assert float(cnt.sum()) == self.instrs_per_step and int((st != 0).sum()) == self.traps
+        return dist.max(elapsed), ksum
+
+    def fresh(self, steps):
+        """--vary-args: `steps` steps, each on new arguments (vary_ids). SetArgs uploads them
+        before the step's clock starts; the clock covers Reset + Run as in timed(). Returns
+        (instructions, max over ranks of the summed step times, kernel seconds)."""
+        ctx, dist = self.ctx, self.dist
+        instrs, secs, ksum = 0.0, 0.0, 0.0
+        for k in range(steps):
+            vals = self.batch.make_values(self.build_rows(vary_ids(self.ids, k, self.args.workload)), self.ptypes)
+            ctx.set_args(self.func, vals)
+            dist.barrier()
+            t0 = time.perf_counter()
+            ctx.reset(timed=False)
+            ksum += ctx.run()
+            secs += time.perf_counter() - t0
+            dist.barrier()
+            _, st, cnt = ctx.results(1)
+            if int((st != 0).sum()) and self.args.workload != "c4":
+                raise SystemExit("fresh inputs: instances trapped: %s" % np.unique(st))
+            instrs += float(cnt.sum())
+        # (the repeated-input arguments again, for the hashes and checks after this)
+        ctx.set_args(self.func, self.values)
+        return dist.sum(instrs), dist.max(secs), ksum
+
+    def close(self):
+        self.ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: --instances per GPU; strong: --instances for the whole job")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): --instances is the whole job's, split over the GPUs "
+                         "(the metric's 64K instances; C5's 256K); weak: --instances per GPU")
+    ap.add_argument("--no-weak", action="store_true",
+                    help="with --gpus N > 1 and strong scaling: skip the extra weak-scaling phase")
+    ap.add_argument("--in-process", action="store_true",
+                    help="--gpus N from ONE process: one context over devices 0..N-1 "
+                         "(WasmEdge_BatchConfigure::Devices) instead of a process per GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: shards, barrier and reductions, no GPU")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default: 20 for C2, whose step is ~1.6 ms; 3 otherwise)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2 / 1)")
     ap.add_argument("--iters", type=int, default=ITERS)
-    ap.add_argument("--instances", type=int, default=INSTANCES)
+    ap.add_argument("--instances", type=int, default=None,
+                    help="instances (default 65536; 262144 for c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "mt", "tail"])
     ap.add_argument("--mt-n", type=int, default=100000, help="mt19937 draws per instance")
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
+    ap.add_argument("--vary-args", default="auto", choices=["auto", "on", "off"],
+                    help="also measure fresh inputs every step (the learned wave order and "
+                         "layout never see them); auto = on for c5 and mt")
     ap.add_argument("--cost-limit", type=int, default=0,
                     help="meter gas with the unit cost table up to this limit (measures the "
                          "cost of exact metering; not the headline configuration)")
@@ -289,101 +449,68 @@ def main():
         args.steps = 20 if args.workload == "c2" else 3
     if args.warmup is None:
         args.warmup = 2 if args.workload == "c2" else 1
+    if args.instances is None:
+        args.instances = default_instances(args.workload)
+    if args.vary_args == "auto":
+        args.vary_args = "on" if args.workload in ("c5", "mt") else "off"
 
     world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None and args.gpus > 1:
+    if world_env is None and args.gpus > 1 and not args.in_process:
         sys.exit(launch_workers(args.gpus, sys.argv[1:]))
     if world_env is not None and int(world_env) != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, world_env))
+    if args.in_process and world_env is not None and int(world_env) > 1:
+        raise SystemExit("bench.py: --in-process runs one process, not one per GPU")
     dist = Dist()
     if args.dry_run:
         return dry_run(args, dist)
-    from wasmedge_amd import batch
-    wasm, func, build_rows, ptypes, desc, extra = workload(args.workload, args)
-    # this rank's shard first: the context holds exactly its instances (strong scaling
-    # splits --instances over the ranks, weak gives every rank --instances of its own)
+    n_gpus = args.gpus if args.in_process else dist.world
+    devices = list(range(args.gpus)) if args.in_process and args.gpus > 1 else None
+    # this rank's shard: the context holds exactly its instances (strong scaling splits
+    # --instances over the ranks, weak gives every rank --instances of its own; in-process,
+    # one context holds the whole job and the library splits it over the devices)
     ids = shard_ids(dist.rank, args.instances, dist.world, args.scaling)
-    n = len(ids)
-    kw = {"max_memory_page": 17} if args.workload == "c3" else {}
-    if args.workload == "tail":
-        kw["tail_call"] = True
-    if args.cost_limit:
-        kw["cost_limit"] = args.cost_limit
-    rows = build_rows(ids)
-    values = batch.make_values(rows, ptypes)
-    nret = 1
-    t_start = time.perf_counter()
-
-    def progress(msg):
-        if dist.rank == 0:
-            print("[bench] %s %.1fs" % (msg, time.perf_counter() - t_start), file=sys.stderr, flush=True)
-
-    def outcome():
-        _, st, cnt = ctx.results(nret)
-        traps = int((st != 0).sum())
-        if traps and args.workload != "c4":
-            raise SystemExit("%s instances trapped: %s" % (args.workload, np.unique(st)))
-        return float(cnt.sum()), traps
-
-    # End-to-end passes (SURVEY.md 8(d) variant ii), the warmup steps themselves:
-    #  cold = BatchCreate (decode, validate, lower, hiprtc compile of the compiled runs,
-    #         device allocation, instantiation) + SetArgs (params H2D) + Run + Results
-    #         (returns, statuses, counts D2H);
-    #  warm = the same on the live context: SetArgs + Reset + Run + Results.
-    t = time.perf_counter()
-    ctx = batch.BatchContext(wasm, n, device=dist.local_rank, **kw)
-    t_create = time.perf_counter() - t
-    ctx.set_args(func, values)
-    e2e_s = {}
-    if args.warmup:
-        ctx.run()
-        instrs_per_step, traps = outcome()
-        e2e_s["cold"] = time.perf_counter() - t
-        progress("warmup 1/%d done (end-to-end cold)" % args.warmup)
-    for w in range(1, args.warmup):
-        t = time.perf_counter()
-        ctx.set_args(func, values)
-        ctx.reset()
-        ctx.run()
-        outcome()
-        if w == 1:
-            e2e_s["warm"] = time.perf_counter() - t
-        progress("warmup %d/%d done" % (w + 1, args.warmup))
+    ph = Phase(args, dist, ids, devices)
+    ph.warm(args.warmup)
     dist.init()
-
-    dist.barrier()
-    t0 = time.perf_counter()
-    ksum = 0.0
-    for k in range(args.steps):
-        ctx.reset(timed=False)   # (no host round trip: the run orders after it)
-        ksum += ctx.run()        # HIP-event time of the interpreter kernel (its stream)
-        if elapsed_hint(args):
-            progress("step %d/%d done" % (k + 1, args.steps))
-    elapsed = time.perf_counter() - t0   # BatchRun synchronises its stream
-    dist.barrier()
-    elapsed = dist.max(elapsed)
-    if not args.warmup:
-        instrs_per_step, traps = outcome()
-    rets, st, cnt = ctx.results(nret)
-    assert float(cnt.sum()) == instrs_per_step and int((st != 0).sum()) == traps
+    elapsed, ksum = ph.timed(args.steps)
+    instrs_per_step, traps, ctx, n = ph.instrs_per_step, ph.traps, ph.ctx, ph.n
     total_instrs = dist.sum(instrs_per_step) * args.steps
+    fresh = None
+    if args.vary_args == "on":
+        fi, fs, fk = ph.fresh(args.steps)
+        fresh = {"value": fi / fs, "ms_per_step": 1e3 * fs / args.steps,
+                 "kernel_instr_per_s": fi / (dist.max(fk)),
+                 "steps": args.steps,
+                 "note": "every step on new arguments (instance i takes id (i + 4099*(k+1)) "
+                         "mod %s): the wave order learned from earlier launches is keyed on "
+                         "the arguments and is not reused; SetArgs before each step's clock, "
+                         "the clock covers Reset + Run as for `value`"
+                         % ("262144" if args.workload == "c5" else "2^30")}
     # checksum of checksums over every instance's final linear memory (hash kernel, after
     # the timed region)
+    rets, st, cnt = ctx.results(1)
     hashes = ctx.memory_hash()
     checksum = int(hashes.sum(dtype=np.uint64))
     gpu = {"counts": cnt, "hashes": hashes, "status": st, "ret": rets["lo"][:, 0],
            "ret32": args.workload not in ("c5", "mt")}
     kernel_avg = ksum / args.steps
-    e2e = {"create_s": dist.max(t_create)}
+    e2e = {"create_s": dist.max(ph.t_create)}
     for k in ("cold", "warm"):
-        if k in e2e_s:
-            e2e["e2e_%s_s" % k] = dist.max(e2e_s[k])
+        if k in ph.e2e_s:
+            e2e["e2e_%s_s" % k] = dist.max(ph.e2e_s[k])
             e2e["e2e_%s_instr_per_s" % k] = dist.sum(instrs_per_step) / e2e["e2e_%s_s" % k]
+    wasm, func, build_rows, ptypes, desc, extra = ph.wasm, ph.func, ph.build_rows, ph.ptypes, ph.desc, ph.extra
+    if devices:
+        par = "instance-sharded, 1 process over %d devices (WasmEdge_BatchConfigure::Devices, " \
+              "contiguous wave blocks)" % len(devices)
+    else:
+        par = "instance-sharded, 1 process per GPU"
     out = {
         "metric": METRIC,
         "value": total_instrs / elapsed,
         "unit": "instr/s",
-        "n_gpus": dist.world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
@@ -393,23 +520,28 @@ def main():
         "dtype": {"c5": "f64", "mt": "i64"}.get(args.workload, "i32"),
         "data": "synthetic: per-instance inputs derived from the instance id inside the "
                 "wasm module",
-        "config": dict({"workload": desc, "instances_per_gpu": n,
+        "config": dict({"workload": desc, "instances_per_gpu": n // (len(devices) if devices else 1),
                         "instances": int(dist.sum(float(n))),
                         "instrs_per_instance": instrs_per_step / n,
-                        "parallelism": "instance-sharded, 1 process per GPU"}, **extra),
+                        "parallelism": par,
+                        "compiled_runs": ctx.compiled_runs(), "engine": ctx.engine(),
+                        "granule": ctx.memory_granule()}, **extra),
         "memory_checksum": "%016x" % checksum,
         "kernel_instr_per_s": total_instrs / (dist.max(kernel_avg) * args.steps),
     }
+    if fresh:
+        out["fresh_input"] = fresh
     if args.workload == "c4":
         out["config"]["trapped_instances"] = traps
     if args.cost_limit:
         out["config"]["cost_limit"] = args.cost_limit
     c3_bytes_per_instr, c3_bpi_src = C3_BYTES_PER_INSTR, ", committed oracle figure"
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+    c3_split = None
+    if dist.rank == 0 and dist.world == 1 and not devices and not args.no_cpu_baseline:
         threads = host_cores()
-        out["cpu_baseline"], bpi = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
-                                                threads, gpu, args.workload.upper(),
-                                                tail_call=args.workload == "tail")
+        out["cpu_baseline"], bpi, c3_split = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
+                                                          threads, gpu, args.workload.upper(),
+                                                          tail_call=args.workload == "tail")
         if args.workload == "c3":
             # qsort's bytes per instruction is stable across instances
             c3_bytes_per_instr, c3_bpi_src = bpi, " on the oracle sample"
@@ -419,6 +551,28 @@ def main():
     out.update(e2e)
     prof = load_profile(args.workload, out["config"])
     kernel_max = dist.max(kernel_avg)
+    rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_instr, c3_bpi_src, c3_split)
+    ph.close()
+    # the metric's configuration at N > 1 is the fixed total (strong); the weak-scaling
+    # figure (every rank --instances of its own) rides along as an extra key
+    if n_gpus > 1 and args.scaling == "strong" and not args.no_weak:
+        wids = shard_ids(dist.rank, args.instances, dist.world, "weak") if not devices else \
+            np.arange(args.instances * len(devices), dtype=np.int64)
+        wp = Phase(args, dist, wids, devices)
+        wp.warm(1)
+        we, _ = wp.timed(args.steps)
+        wi = dist.sum(wp.instrs_per_step) * args.steps
+        out["weak_scaling"] = {"value": wi / we, "ms_per_step": 1e3 * we / args.steps,
+                               "instances": int(dist.sum(float(len(wids)))),
+                               "instances_per_gpu": args.instances,
+                               "note": "every GPU runs --instances of its own (ids disjoint)"}
+        wp.close()
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_instr, c3_bpi_src, c3_split):
+    traffic = prof.get("hbm_bytes_per_launch")
     # The interpreter's bound is vector issue (VALU), not HBM, for every config but C3:
     # SQ_INSTS_VALU per launch (committed PMC pass of this same command) x 64 lanes over
     # this run's live kernel time (HIP events on the library's stream), against 256 CU x
@@ -442,7 +596,6 @@ def main():
                       "SQ_WAVE_CYCLES per launch)" % prof.get("source")})
     else:
         issue["note"] = "no PMC summary for this configuration (tools/prof_bench.sh)"
-    traffic = prof.get("hbm_bytes_per_launch")
     if args.workload == "c3":
         # HBM-bound config: algorithmic bytes = the linear-memory bytes of the wasm loads and
         # stores, per wasm instruction as the oracle counts them on the CPU-baseline sample
@@ -455,7 +608,14 @@ def main():
                            "traffic": traffic,
                            "note": "algorithmic = linear-memory bytes of the wasm loads and "
                                    "stores (%.4f B per wasm instr%s); traffic = HBM bytes per "
-                                   "launch from FETCH_SIZE + WRITE_SIZE" % (bpi, c3_bpi_src)}
+                                   "launch, FETCH_SIZE x 2 (MI355X_MICROARCH.md 'HBM') + "
+                                   "WRITE_SIZE" % (bpi, c3_bpi_src)}
+        if c3_split:
+            ld, stb = c3_split
+            out["roofline"]["algorithmic_load_bytes"] = ld * instrs_per_step
+            out["roofline"]["algorithmic_store_bytes"] = stb * instrs_per_step
+        if prof.get("write_bytes") and c3_split:
+            out["roofline"]["write_over_store_bytes"] = prof["write_bytes"] / (c3_split[1] * instrs_per_step)
         out["issue_roofline"] = issue
     else:
         out["roofline"] = dict(issue)
@@ -469,9 +629,6 @@ def main():
                            "compiled loop forwards its loads in registers: the counters see the "
                            "stores only" % hbm["wasm_level_bytes"])
         out["hbm_roofline"] = hbm
-    if dist.rank == 0:
-        print(json.dumps(out), flush=True)
-    ctx.close()
 
 
 def dry_run(args, dist):

@@ -344,6 +344,15 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchGetTotalCosts(WasmEdge_BatchCon
  * then returns until the next error). Results never depend on it. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *Cxt);
 
+/* The execution engine the context runs, for reports (DESIGN.md "Execution engines"):
+ * "<core>/<frames>", core one of "compiled-runs" (with "+simt" / "+trip" for the
+ * scheduling inside them), "threaded-core" (the hand-written handlers, no compiled runs),
+ * "compiled-step"; frames "vgpr-frames", "lds-frames" or "hbm-frames"; "+metered" when the
+ * context meters gas. A context that wanted compiled runs and got none (a compile failure)
+ * says "threaded-core (compiled runs failed)". Valid until the next call on the context;
+ * "" for NULL. Results never depend on it. */
+WASMEDGE_BATCH_API const char *WasmEdge_BatchGetEngine(const WasmEdge_BatchContext *Cxt);
+
 /* The interleave granule in use, in bytes (WasmEdge_BatchConfigure::MemoryGranule).
  * Layout only: results never depend on it. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *Cxt);

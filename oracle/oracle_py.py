@@ -69,6 +69,9 @@ def lib():
         L.om_run_batch_mb.restype = ctypes.c_double
         L.om_run_batch_mb.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 6 + [ctypes.c_int]
+        L.om_run_batch_ms.restype = ctypes.c_double
+        L.om_run_batch_ms.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + \
+            [ctypes.c_void_p] * 7 + [ctypes.c_int]
         L.om_clear_imports.restype = None
         L.om_add_import.restype = None
         L.om_add_import.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_uint32] * 5 + \
@@ -185,11 +188,13 @@ class Module:
         counts = np.zeros(n, dtype=np.uint64)
         hashes = np.zeros(n, dtype=np.uint64)
         mem_bytes = np.zeros(n, dtype=np.uint64)
-        secs = L.om_run_batch_mb(self._h, idx, n, params.ctypes.data, results.ctypes.data,
+        store_bytes = np.zeros(n, dtype=np.uint64)
+        secs = L.om_run_batch_ms(self._h, idx, n, params.ctypes.data, results.ctypes.data,
                                  codes.ctypes.data, counts.ctypes.data, hashes.ctypes.data,
-                                 mem_bytes.ctypes.data, threads)
+                                 mem_bytes.ctypes.data, store_bytes.ctypes.data, threads)
         return {"results": results[:, :len(rt), :], "codes": codes, "counts": counts,
-                "hashes": hashes, "mem_bytes": mem_bytes, "seconds": secs}
+                "hashes": hashes, "mem_bytes": mem_bytes, "store_bytes": store_bytes,
+                "seconds": secs}
 
 
 class Instance:

@@ -115,6 +115,7 @@ struct OInst {
   const uint64_t *cost_tab;         /* 65536 entries by OpCode; NULL = the unit table */
   uint64_t mem_bytes;               /* linear-memory bytes the last invoke accessed (not
                                        in the reference: the roofline's algorithmic bytes) */
+  uint64_t mem_store_bytes;         /* ... of them written (stores, bulk destinations) */
   /* WASI subset (wasifunc.cpp): captured fd 1 / fd 2 bytes and the proc_exit code */
   uint8_t *wasi_out[2]; uint64_t wasi_len[2], wasi_cap[2];
   uint32_t wasi_exit;

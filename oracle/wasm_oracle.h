@@ -101,6 +101,11 @@ double om_run_batch(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
 double om_run_batch_mb(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
                        uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
                        uint64_t *mem_bytes, int threads);
+/* om_run_batch_mb plus store_bytes[n]: the part of mem_bytes that was written (stores,
+   bulk-op destinations, host-function writes) */
+double om_run_batch_ms(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *params,
+                       uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
+                       uint64_t *mem_bytes, uint64_t *store_bytes, int threads);
 
 #ifdef __cplusplus
 }

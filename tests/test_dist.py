@@ -67,10 +67,21 @@ def _run_bench(*argv):
     return out.returncode, [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
 
 
+def test_bench_launcher_default_is_the_metric_config():
+    """`bench.py --gpus 2` with no other option measures the metric's configuration: the
+    job's 64K instances split over the GPUs (strong scaling)."""
+    rc, lines = _run_bench("--gpus", "2", "--dry-run")
+    assert rc == 0 and len(lines) == 1
+    assert lines[0] == {"dry_run": True, "n_gpus": 2, "scaling": "strong", "instances": 65536,
+                        "first_id": 0, "last_id": 65535, "max_over_ranks": 2.0}
+    rc, lines = _run_bench("--gpus", "2", "--dry-run", "--workload", "c5")
+    assert rc == 0 and lines[0]["instances"] == 262144
+
+
 def test_bench_launcher_spawns_ranks_weak():
-    """`bench.py --gpus 2` run directly spawns one worker per GPU through its own launcher
-    (no torchrun); the ranks rendezvous on 127.0.0.1, shard by id and reduce."""
-    rc, lines = _run_bench("--gpus", "2", "--dry-run", "--instances", "65536")
+    """`bench.py --gpus 2 --scaling weak` run directly spawns one worker per GPU through its
+    own launcher (no torchrun); the ranks rendezvous on 127.0.0.1, shard by id and reduce."""
+    rc, lines = _run_bench("--gpus", "2", "--dry-run", "--scaling", "weak", "--instances", "65536")
     assert rc == 0 and len(lines) == 1
     assert lines[0] == {"dry_run": True, "n_gpus": 2, "scaling": "weak", "instances": 131072,
                         "first_id": 0, "last_id": 131071, "max_over_ranks": 2.0}

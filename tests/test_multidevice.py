@@ -134,9 +134,10 @@ def test_gpu_two_shards_host_calls_and_state(built, part):
 
 @pytest.mark.gpu
 def test_gpu_shards_run_the_layout_trial(built):
-    """mt19937 over two shards on one device through Reset cycles: each shard runs its own
-    layout trial (128-byte granules first, then 4-byte words), every run bit-identical to
-    the oracle sample."""
+    """mt19937 over two shards on one device through Reset cycles: the shards run the layout
+    trial together (128-byte granules for the warm-up and the measured run, then 4-byte
+    words; the first shard's verdict stands for both), every run bit-identical to the
+    oracle sample."""
     import oracle_py as O
     from conftest import golden
     from helpers import compare, oracle_run
@@ -150,7 +151,7 @@ def test_gpu_shards_run_the_layout_trial(built):
     try:
         vals = batch.make_values(rows, [0x7F, 0x7E, 0x7E])
         granules = []
-        for k in range(3):
+        for k in range(4):
             if k:
                 ctx.reset()
             rets, st, cnt = ctx.execute("mt19937", vals, 1)
@@ -159,6 +160,6 @@ def test_gpu_shards_run_the_layout_trial(built):
             got = [[int(ints[i][0])] if st[i] == 0 else [] for i in idx]
             assert compare(ref, got, st[idx], cnt[idx], h[idx], [0x7E]) == [], k
             granules.append(ctx.memory_granule())
-        assert granules[0] == 128 and granules[1] == 4
+        assert granules[:3] == [128, 128, 4] and granules[3] in (4, 128)
     finally:
         ctx.close()

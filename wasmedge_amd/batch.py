@@ -197,6 +197,8 @@ def lib():
         L.WasmEdge_BatchGetCompiledRuns.argtypes = [vp]
         L.WasmEdge_BatchGetMemoryGranule.restype = u32
         L.WasmEdge_BatchGetMemoryGranule.argtypes = [vp]
+        L.WasmEdge_BatchGetEngine.restype = ctypes.c_char_p
+        L.WasmEdge_BatchGetEngine.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -364,6 +366,11 @@ class BatchContext:
     def memory_granule(self):
         """The interleave granule in use, bytes (WasmEdge_BatchGetMemoryGranule)."""
         return lib().WasmEdge_BatchGetMemoryGranule(self._h)
+
+    def engine(self):
+        """The execution engine the context runs, e.g. "compiled-runs+simt/vgpr-frames"
+        (WasmEdge_BatchGetEngine)."""
+        return lib().WasmEdge_BatchGetEngine(self._h).decode()
 
     def interrupt(self):
         lib().WasmEdge_BatchInterrupt(self._h)

@@ -174,7 +174,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // tries 4-byte words on its second run (layout_trial; WB_GRANULE_TRIAL=0 turns it off)
   const char *gte = getenv("WB_GRANULE_TRIAL");
   if (gb == 0 && P.divergent_mem && P.has_mem && !(gte && gte[0] == '0')) {
-    C->trial = 1;
+    C->trial = 5;   // (the first run warms up unmeasured: a cold run would favour a switch)
     C->trial_mlog[0] = 5;   // 128 B
     C->trial_mlog[1] = 0;   // 4 B
   }
@@ -337,9 +337,10 @@ uint8_t relayout(WasmEdge_BatchContext *C, uint32_t mlog) {
 // Layout trial: the interleave granule from observed throughput, for modules whose
 // addresses may differ between instances (Program::divergent_mem; the static analysis
 // cannot tell a per-lane index from a wave-uniform one kept in memory, such as mt19937's
-// state index). The first run at 128-byte granules and the next one, after a Reset, at
-// 4-byte words each measure wasm instructions per kernel second; the 4-byte layout stays
-// when it is at least 10% faster on the same function, else the next Reset goes back.
+// state index). After one unmeasured warm-up run, a run at 128-byte granules and the next
+// one, after a Reset, at 4-byte words each measure wasm instructions per kernel second; the
+// 4-byte layout stays when it is at least 10% faster on the same function, else the next
+// Reset goes back. The rate is per instruction, so runs on different arguments compare.
 // Trial runs do not use the longest-first wave order, so both see the same schedule.
 // Results never depend on the layout (tests/test_workloads.py granule matrix).
 uint8_t layout_trial(WasmEdge_BatchContext *C, double secs) {
@@ -463,7 +464,10 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
       if (!C->wave_ticks.ptr && (!C->wave_ticks.alloc(C->nwaves) || !C->wave_order.alloc(C->nwaves)))
         return C->fail(kRuntimeError, "device allocation failed");
       k.wave_ticks = C->wave_ticks.ptr;
-      k.wave_order = C->order_pc == entry_pc && C->trial != 1 && C->trial != 3 ? C->wave_order.ptr : nullptr;
+      // (only for the same function on the same arguments: waves of other inputs take
+      // other times, and an order learned from them is noise -- the fresh-input bench)
+      k.wave_order = C->order_pc == entry_pc && C->order_fp == C->args_fp && C->trial != 1 && C->trial != 3
+                         ? C->wave_order.ptr : nullptr;
     }
   }
   (void)hipEventRecord(C->ev0, C->stream);
@@ -486,6 +490,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
       return kRuntimeError;
     C->order_pending = true;
     C->order_pc = entry_pc;
+    C->order_fp = C->args_fp;
     C->ctr_zero = true;
   }
   // the interpreter kernel's end
@@ -607,6 +612,10 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
                                 hipMemcpyHostToDevice, C->stream), "params upload"))
     return R(kRuntimeError);
   if (!C->hip_ok(hipStreamSynchronize(C->stream), "params upload")) return R(kRuntimeError);
+  // fingerprint of the arguments (the longest-first wave order is reused only on equal ones)
+  uint64_t fp = 0x9E3779B97F4A7C15ull ^ uint64_t(f);
+  for (uint32_t c : cells) fp = (fp ^ c) * 0x100000001B3ull + (fp >> 29);
+  C->args_fp = fp;
   C->func = f;
   C->param_cells = pc;
   C->result_cells = rc;
@@ -695,7 +704,8 @@ WasmEdge_Result WasmEdge_BatchRun(WasmEdge_BatchContext *C, double *KernelSecond
   uint8_t e = launch_exec(C, F.entry_pc, false, KernelSeconds || measure ? &ks : nullptr);
   if (e) return R(e);
   if (KernelSeconds) *KernelSeconds = ks;
-  if (measure && (e = layout_trial(C, ks))) return R(e);
+  if (C->trial == 5) C->trial = 1;   // (the warm-up run of the layout trial)
+  else if (measure && (e = layout_trial(C, ks))) return R(e);
   C->ran = true;
   return R(0);
 }
@@ -777,6 +787,19 @@ WasmEdge_Result WasmEdge_BatchMemoryHash(WasmEdge_BatchContext *C, uint64_t *Has
 uint32_t WasmEdge_BatchGetCompiledRuns(const WasmEdge_BatchContext *C) {
   if (C && !C->shards.empty()) return WasmEdge_BatchGetCompiledRuns(wbm::first(C));
   return C ? C->jit_runs : 0;
+}
+
+const char *WasmEdge_BatchGetEngine(const WasmEdge_BatchContext *C) {
+  if (!C) return "";
+  if (!C->shards.empty()) return WasmEdge_BatchGetEngine(wbm::first(C));
+  std::string e;
+  if (!C->threaded) e = "compiled-step";
+  else if (C->jit_runs) e = std::string("compiled-runs") + (C->simt ? "+simt" : "") + (C->trip ? "+trip" : "");
+  else e = C->jit_on ? "threaded-core (compiled runs failed)" : "threaded-core";
+  e += C->frame_hbm ? "/hbm-frames" : C->vframe ? "/vgpr-frames" : "/lds-frames";
+  if (C->conf.CostLimit) e += "+metered";
+  C->engine_desc = e;
+  return C->engine_desc.c_str();
 }
 
 uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *C) {

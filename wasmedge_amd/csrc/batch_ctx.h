@@ -76,6 +76,7 @@ struct WasmEdge_BatchContext {
   uint64_t *stats = nullptr;         // WB_STATS builds: per-wave counters (WB_STATS_OUT)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string last_error;
+  mutable std::string engine_desc;   // (WasmEdge_BatchGetEngine's string)
   // module buffers
   DevBuf<DInstr> code;
   DevBuf<TInstr> tcode;           // threaded code for the dispatch core (tc.h)
@@ -86,9 +87,9 @@ struct WasmEdge_BatchContext {
   bool trip = false;              // ... in trip mode (jit.h)
   bool want_simt = false, want_trip = false, jit_on = false;   // (compile_runs inputs)
   std::vector<DInstr> codepad0;   // the module's DBC before compile_runs flags it
-  // layout trial (batch_api.cpp layout_trial): 1 = the next run measures the module's
-  // granule, 2 = the next Reset switches to the other one, 3 = the next run measures that,
-  // 4 = the next Reset switches back; 0 = decided
+  // layout trial (batch_api.cpp layout_trial): 5 = the next run is the warm-up, 1 = the
+  // next run measures the module's granule, 2 = the next Reset switches to the other one,
+  // 3 = the next run measures that, 4 = the next Reset switches back; 0 = decided
   uint8_t trial = 0;
   uint32_t trial_mlog[2] = {0, 0};   // (the module's granule, the other one)
   int trial_func = -1;
@@ -110,6 +111,7 @@ struct WasmEdge_BatchContext {
   // ids put them. Scheduling only: results never depend on it (WB_LPT=0 turns it off).
   DevBuf<uint32_t> wave_ticks, wave_order;
   uint32_t order_pc = 0xFFFFFFFFu;   // entry pc of the launch the order was taken from
+  uint64_t order_fp = 0, args_fp = 1;   // its arguments' fingerprint; the staged arguments'
   bool lpt = true;
   uint32_t sched = 1;             // KParams::sched (WB_SCHED=k; 0: min-pc scheduling only)
   DevBuf<uint32_t> loops;         // Program::loops (scheduler)

@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <vector>
+
 #include "dbc.h"
 #include "kparams.h"
 
@@ -868,11 +871,15 @@ __device__ __forceinline__ void exec_hbm_body(const KParams &p) {
   uint32_t turn = 0;
   for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
+    const uint64_t ws = p.wave_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
     HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
     interp<false, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                   GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
                   p.lstate + (size_t)wave * p.ls_slots * 64u + lane,
                   p.fsave ? p.fsave + (size_t)wave * (p.total_cells + p.gs_lds) * 64u + lane : nullptr, stk);
+    // (the longest-first order of the next launch reads these, as for the other frames)
+    if (p.wave_ticks && lane == 0)
+      p.wave_ticks[wave] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - ws, 0xFFFFFFFFull);
   }
 }
 extern "C" __global__ void __launch_bounds__(256) wb_exec_hbm_kernel(const KParams p) {
@@ -979,37 +986,114 @@ wb_state_init_kernel(uint32_t *ls, uint32_t ls_slots, uint32_t nwaves, StateInit
 
 // Memory hash: sum over u64 words of fmix64(w ^ (i*K1 + K2)), ^ fmix64(pages+K3).
 // The sum commutes, so the words are spread over the grid: block (wave, c) adds the terms
-// of u64 words [c*8192, (c+1)*8192) -- page c -- of its wave's 64 lanes (4 threads per
-// lane, coalesced across lanes) into hashes[] (zeroed first), and wb_mem_hash_fin_kernel
-// XORs the page-count term in. A lane's pages past the reserved layout are read through
-// the wave's pool rows (GMemP).
+// of u64 words [c*8192, (c+1)*8192) -- page c -- of its wave's 64 lanes into hashes[]
+// (zeroed first), and wb_mem_hash_fin_kernel XORs the page-count term in.
+//
+// Page c of a wave's 64 lanes is ONE contiguous 4 MiB region in the interleaved layout
+// (the reserved layout, or the wave's pool row for a page past it), so the block streams
+// it front to back in 16-byte pieces -- a wave's load is 1 KiB contiguous, the access the
+// guide calibrates FETCH_SIZE on (MI355X_MICROARCH.md "HBM": 16 B per lane). Which lane
+// and word a piece holds follows from the granule of 2^g words:
+//   g >= 2: 4 consecutive words of one lane (a granule is 2^(g-2) pieces);
+//   g == 1: a u64 word of each of two adjacent lanes;
+//   g == 0: a lane's u64 word is two words a 64-word row apart, so a thread reads the same
+//           piece of two consecutive rows (a u64 word of each of 4 lanes).
+// A thread serves fixed lanes (one or two; four at g == 0) over its whole loop, so its
+// terms add up in registers, then per lane in LDS, then one global atomic per lane.
+typedef uint32_t wb_u32x4 __attribute__((ext_vector_type(4)));
+#define WB_HK(x, i) fmix64((x) ^ ((uint64_t)(i) * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull))
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_hash_kernel(uint32_t *mem, const uint32_t *ls, uint32_t ls_slots,
                    uint64_t *hashes, uint32_t mem_words, uint32_t n, uint32_t g,
                    const uint64_t *ptab, uint32_t ptab_w) {
-  const uint32_t wave = blockIdx.x, lane = threadIdx.x & 63u, sub = threadIdx.x >> 6;
-  const uint32_t inst = wave * 64u + lane;
-  __shared__ uint64_t part[256];
-  uint64_t h = 0;
-  uint32_t pages = 0;
-  if (inst < n) {
-    pages = ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + lane];
-    if (blockIdx.y < pages) {
-      const GMemP m{mem + (size_t)wave * mem_words * 64u + (lane << g), g, mem_words,
-                    ptab ? ptab + (size_t)wave * ptab_w : nullptr, lane << g};
-      const uint64_t i0 = (uint64_t)blockIdx.y << 13;
-      for (uint64_t i = i0 + sub; i < i0 + 8192u; i += 4) {
-        const uint64_t w = (uint64_t)*mw(m, (uint32_t)(2 * i)) | ((uint64_t)*mw(m, (uint32_t)(2 * i + 1)) << 32);
-        h += fmix64(w ^ (i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
+  const uint32_t wave = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  __shared__ unsigned long long acc[64];
+  __shared__ uint32_t ok[64];
+  __shared__ uint32_t any;
+  if (t == 0) any = 0;
+  __syncthreads();
+  if (t < 64) {
+    const uint32_t inst = wave * 64u + t;
+    ok[t] = inst < n && c < ls[((size_t)wave * ls_slots + LS_PAGES) * 64u + t];
+    acc[t] = 0;
+    if (ok[t]) any = 1;   // (benign race: every writer writes 1)
+  }
+  __syncthreads();
+  if (!any) return;
+  const uint32_t rp = mem_words >> 14;   // pages in the reserved layout
+  const wb_u32x4 *src;
+  if (c < rp) {
+    src = (const wb_u32x4 *)(mem + ((size_t)wave * mem_words + ((size_t)c << 14)) * 64u);
+  } else {
+    const uint64_t row = ptab ? ptab[(size_t)wave * ptab_w + (c - rp)] : 0;
+    if (!row) return;   // (no lane of the wave is that large: `any` was 0)
+    src = (const wb_u32x4 *)(uintptr_t)row;
+  }
+  const uint64_t i0 = (uint64_t)c << 13;   // the page's first u64 word
+  uint64_t h[4] = {0, 0, 0, 0};
+  uint32_t ln[4];
+  if (g >= 2) {
+    const uint32_t s = g - 2;
+    ln[0] = (t >> s) & 63u;
+    ln[1] = ((t >> s) + (256u >> s)) & 63u;   // (== ln[0] unless s == 3)
+    const bool v0 = ok[ln[0]], v1 = ok[ln[1]];
+#pragma unroll 4
+    for (uint32_t k = 0; k < 1024u; k++) {
+      const uint32_t j = t + 256u * k;
+      if (!((k & 1u) ? v1 : v0)) continue;
+      const wb_u32x4 x = __builtin_nontemporal_load(&src[j]);
+      const uint64_t i = i0 + ((((uint64_t)(j >> (s + 6)) << g) + ((j & ((1u << s) - 1u)) << 2)) >> 1);
+      h[k & 1u] += WB_HK((uint64_t)x.x | ((uint64_t)x.y << 32), i) + WB_HK((uint64_t)x.z | ((uint64_t)x.w << 32), i + 1);
+    }
+    if (s == 3) {
+      if (v0) atomicAdd(&acc[ln[0]], (unsigned long long)h[0]);
+      if (v1) atomicAdd(&acc[ln[1]], (unsigned long long)h[1]);
+    } else if (v0) {
+      atomicAdd(&acc[ln[0]], (unsigned long long)(h[0] + h[1]));
+    }
+  } else if (g == 1) {
+    ln[0] = (2u * t) & 63u;
+    ln[1] = ln[0] + 1u;
+    const bool v0 = ok[ln[0]], v1 = ok[ln[1]];
+    if (v0 || v1) {
+#pragma unroll 4
+      for (uint32_t k = 0; k < 1024u; k++) {
+        const uint32_t j = t + 256u * k;
+        const wb_u32x4 x = __builtin_nontemporal_load(&src[j]);
+        const uint64_t i = i0 + (j >> 5);
+        h[0] += WB_HK((uint64_t)x.x | ((uint64_t)x.y << 32), i);
+        h[1] += WB_HK((uint64_t)x.z | ((uint64_t)x.w << 32), i);
       }
+      if (v0) atomicAdd(&acc[ln[0]], (unsigned long long)h[0]);
+      if (v1) atomicAdd(&acc[ln[1]], (unsigned long long)h[1]);
+    }
+  } else {
+    const uint32_t m = t & 15u;   // piece of the 64-word row: lanes 4m .. 4m+3
+    bool v[4];
+    for (uint32_t q = 0; q < 4; q++) {
+      ln[q] = 4u * m + q;
+      v[q] = ok[ln[q]];
+    }
+    if (v[0] || v[1] || v[2] || v[3]) {
+#pragma unroll 4
+      for (uint32_t k = 0; k < 512u; k++) {
+        const uint32_t r = (t >> 4) + 16u * k;   // u64 word r: rows 2r and 2r+1
+        const wb_u32x4 lo = __builtin_nontemporal_load(&src[(2u * r) * 16u + m]);
+        const wb_u32x4 hi = __builtin_nontemporal_load(&src[(2u * r + 1u) * 16u + m]);
+        const uint64_t i = i0 + r;
+        h[0] += WB_HK((uint64_t)lo.x | ((uint64_t)hi.x << 32), i);
+        h[1] += WB_HK((uint64_t)lo.y | ((uint64_t)hi.y << 32), i);
+        h[2] += WB_HK((uint64_t)lo.z | ((uint64_t)hi.z << 32), i);
+        h[3] += WB_HK((uint64_t)lo.w | ((uint64_t)hi.w << 32), i);
+      }
+      for (uint32_t q = 0; q < 4; q++)
+        if (v[q]) atomicAdd(&acc[ln[q]], (unsigned long long)h[q]);
     }
   }
-  part[threadIdx.x] = h;
   __syncthreads();
-  if (sub == 0 && inst < n && blockIdx.y < pages)
-    atomicAdd((unsigned long long *)&hashes[inst],
-              (unsigned long long)(part[lane] + part[lane + 64] + part[lane + 128] + part[lane + 192]));
+  if (t < 64 && ok[t]) atomicAdd((unsigned long long *)&hashes[wave * 64u + t], acc[t]);
 }
+#undef WB_HK
 extern "C" __global__ void __launch_bounds__(256)
 wb_mem_hash_fin_kernel(const uint32_t *ls, uint32_t ls_slots, uint64_t *hashes, uint32_t n) {
   const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1074,15 +1158,24 @@ static const void *exec_kernel(int vframe, int hbm, int paged) {
   return paged ? reinterpret_cast<const void *>(&wb_exec_pg_kernel)
                : reinterpret_cast<const void *>(&wb_exec_kernel);
 }
+// The 160 KiB dynamic-LDS attribute of every exec kernel variant, once per device: HIP keeps
+// function attributes per device, and a multi-device batch (multi.cpp) launches on several.
+static void exec_attrs() {
+  static std::mutex mu;
+  static std::vector<bool> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return;
+  std::lock_guard<std::mutex> g(mu);
+  if (size_t(dev) < done.size() && done[dev]) return;
+  if (done.size() <= size_t(dev)) done.resize(size_t(dev) + 1, false);
+  for (int k = 0; k < 8; k++)
+    (void)hipFuncSetAttribute(exec_kernel(k & 1, k >> 1 & 1, k >> 2 & 1),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done[dev] = true;
+}
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    for (int k = 0; k < 8; k++)
-      (void)hipFuncSetAttribute(exec_kernel(k & 1, k >> 1 & 1, k >> 2 & 1),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  exec_attrs();
   const void *k = exec_kernel(vframe, p->hframe != nullptr, p->grow_host != 0);
   void *args[] = {const_cast<KParams *>(p)};
   return hipLaunchKernel(k, dim3(blocks), dim3(threads), args, lds_bytes, s);
@@ -1091,6 +1184,7 @@ extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t
 // wave_ctr): resident blocks per CU at this block size and LDS share x CUs; 0 on failure.
 extern "C" uint32_t wb_exec_capacity(int vframe, int hbm, int paged, uint32_t threads, size_t lds_bytes) {
   int per_cu = 0, cus = 0, dev = 0;
+  exec_attrs();
   const void *k = exec_kernel(vframe, hbm, paged);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, int(threads), lds_bytes) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess ||

@@ -211,12 +211,20 @@ bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows) {
   if (rows > C->pt_w) {   // widen the page table (every wave's row of it)
     uint32_t w = std::max<uint32_t>(rows, std::max<uint32_t>(16, C->pt_w * 2));
     w = std::min<uint32_t>(w, C->mem_max_pages - C->rpages);
+    // the new device table first: when it cannot be had, the old table, its width and its
+    // device copy stay as they were and the grow yields -1 (Allocator::resize failing)
+    wbh::DevBuf<uint64_t> nt;
+    if (!nt.alloc(size_t(C->nwaves) * w)) {
+      (void)hipGetLastError();
+      return false;
+    }
     std::vector<uint64_t> t(size_t(C->nwaves) * w, 0);
     for (uint32_t v = 0; v < C->nwaves; v++)
       for (uint32_t k = 0; k < C->pt_n[v]; k++) t[size_t(v) * w + k] = C->pt_host[size_t(v) * C->pt_w + k];
     C->pt_host.swap(t);
     C->pt_w = w;
-    if (!C->ptab.alloc(C->pt_host.size())) return false;
+    std::swap(C->ptab.ptr, nt.ptr);
+    std::swap(C->ptab.n, nt.n);   // (nt frees the old table)
     C->pt_dirty = true;
   }
   while (have < rows) {

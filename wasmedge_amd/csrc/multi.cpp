@@ -185,6 +185,13 @@ WasmEdge_Result run(Ctx *C, double *secs) {
     return WasmEdge_BatchRun(s, secs ? &t[s->shard_g] : nullptr);
   });
   if (secs) *secs = *std::max_element(t.begin(), t.end());
+  // one memory layout for the whole batch (batch_api.cpp layout_trial): the shards run the
+  // same module through the same calls, so their trials step together and only a verdict
+  // can differ; the first shard's stands for all of them
+  if (!r.Code)
+    if (Ctx *f = first(C))
+      for (Ctx *s : C->shards)
+        if (s && s != f) s->trial = f->trial;
   return r;
 }
 
