@@ -102,11 +102,15 @@ typedef struct WasmEdge_BatchConfigure {
   const uint64_t *CostTable;
   uint32_t CostTableLen;
   /* Bytes per granule in which the device interleaves the linear memories of a wave's 64
-   * instances (4, 8, ..., 128; 0 = chosen from the module: 4 when its memory addresses
-   * are the same in every instance, 128 when they depend on per-instance data; when they
-   * depend only on parameters of exported functions, the first WasmEdge_BatchSetArgs
-   * decides from the values passed: 4 if every instance passes the same ones, else 128).
-   * Layout only: results never depend on it. WasmEdge_BatchGetMemoryGranule reports it. */
+   * instances (4, 8, ..., 128; 0 = chosen: 4 when the module's load/store addresses are the
+   * same in every instance; when an address may depend on per-instance data, a layout trial
+   * decides from measured throughput -- the first Run is an unmeasured warm-up at 128, the
+   * second is measured at 128, the next Reset re-lays memory in 4-byte words and the Run
+   * after it is measured again; 4 stays if at least 10% faster per wasm instruction on the
+   * same function, else the following Reset goes back to 128 (WB_GRANULE_TRIAL=0: 128, no
+   * trial). The shards of a multi-device batch take the first shard's verdict.) Layout
+   * only: results never depend on it. WasmEdge_BatchGetMemoryGranule reports the layout in
+   * use. */
   uint32_t MemoryGranule;
   /* The TailCall proposal (return_call, return_call_indirect; WasmEdge_ConfigureAddProposal
    * (Conf, WasmEdge_Proposal_TailCall), include/common/configure.h:176-182 leaves it off):
@@ -299,6 +303,18 @@ WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *Cxt, const WasmEdge_String ModuleName,
                               const WasmEdge_String FuncName, WasmEdge_BatchHostFunc_t Func,
                               void *Data);
+/* The same with the host function's gas cost: the Cost of WasmEdge_FunctionInstanceCreate
+ * (Type, Func, Data, Cost) (include/api/wasmedge/wasmedge.h:2324; HostFunctionBase::Cost,
+ * include/runtime/hostfunc.h:28-46). In a metered context (CostLimit) every call adds Cost
+ * to the instance's gas total before the function runs; a call that would take the total
+ * past CostLimit ends the instance with CostLimitExceeded (0x03) instead -- the call
+ * instruction counted, the host function not run, the total unchanged -- as
+ * Stat->addCost(HostFunc.getCost()) does (lib/executor/helper.cpp:59-64). The built-in WASI
+ * functions cost 0, as the reference's do (include/host/wasi/wasibase.h:15). */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchAddHostFunctionWithCost(WasmEdge_BatchContext *Cxt, const WasmEdge_String ModuleName,
+                                      const WasmEdge_String FuncName, WasmEdge_BatchHostFunc_t Func,
+                                      void *Data, uint64_t Cost);
 /* Inside a host function: the calling instance and its memory
  * (WasmEdge_MemoryInstanceGetData / SetData, wasmedge.h:2552-2569). */
 WASMEDGE_BATCH_API uint32_t

@@ -55,6 +55,8 @@ def lib():
         L.om_hash_bytes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
         L.om_set_lazy_imports.restype = None
         L.om_set_lazy_imports.argtypes = [ctypes.c_int]
+        L.om_set_host_cost.restype = None
+        L.om_set_host_cost.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
         L.om_set_extern_value.restype = None
         L.om_set_extern_value.argtypes = [ctypes.c_uint32, ctypes.c_int32]
         L.om_table_set.restype = ctypes.c_int
@@ -289,6 +291,15 @@ def set_imports(imports):
         L.om_add_import(i["module"].encode(), i["name"].encode(), i["kind"], i.get("type", 0),
                         1 if i.get("mut") else 0, i.get("min", 0), mx or 0, 0 if mx is None else 1,
                         v & ((1 << 64) - 1), v >> 64)
+
+
+def set_host_costs(costs):
+    """Costs of the test host functions, {(module, name): cost} (HostFunctionBase::Cost);
+    charged under metering before the function runs (helper.cpp:59-64). {} clears them."""
+    L = lib()
+    L.om_set_host_cost(None, None, 0)
+    for (mod, name), c in (costs or {}).items():
+        L.om_set_host_cost(mod.encode(), name.encode(), int(c))
 
 
 def set_extern_value(handle, value):

@@ -107,6 +107,10 @@ double om_run_batch_ms(OMod *m, uint32_t fidx, uint32_t n, const uint64_t *param
                        uint64_t *results, uint8_t *codes, uint64_t *counts, uint64_t *hashes,
                        uint64_t *mem_bytes, uint64_t *store_bytes, int threads);
 
+/* TEST INFRASTRUCTURE: a test host function's cost (HostFunctionBase::Cost), by import
+   module / name, for instances created afterwards; mod NULL clears every cost */
+void om_set_host_cost(const char *mod, const char *name, uint64_t cost);
+
 #ifdef __cplusplus
 }
 #endif

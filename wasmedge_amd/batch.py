@@ -162,6 +162,7 @@ def lib():
         for name, args in [
             ("WasmEdge_BatchSetMemory", [vp, u32, u32, ctypes.c_char_p, u32]),
             ("WasmEdge_BatchAddHostFunction", [vp, _String, _String, HOST_FUNC, vp]),
+            ("WasmEdge_BatchAddHostFunctionWithCost", [vp, _String, _String, HOST_FUNC, vp, u64]),
             ("WasmEdge_BatchMemoryGetData", [vp, vp, u32, u32]),
             ("WasmEdge_BatchMemorySetData", [vp, ctypes.c_char_p, u32, u32]),
         ]:
@@ -405,11 +406,11 @@ class BatchContext:
         self._check(lib().WasmEdge_BatchGlobalSetValue(self._h, self._name(name), inst,
                                                        _Value.make(value, vtype)))
 
-    def add_host_function(self, module, name, fn, nparams, nresults):
+    def add_host_function(self, module, name, fn, nparams, nresults, cost=0):
         """Bind `fn(mem: HostMemory, args: list[int]) -> (code, results: list[int])` to
-        the import module.name (WasmEdge_BatchAddHostFunction). Values are raw bits
-        (uint128 as python ints); code 0 = success, else the ErrCode ending the instance
-        (0x01 Terminated)."""
+        the import module.name (WasmEdge_BatchAddHostFunction; with a gas `cost`,
+        WasmEdge_BatchAddHostFunctionWithCost). Values are raw bits (uint128 as python
+        ints); code 0 = success, else the ErrCode ending the instance (0x01 Terminated)."""
         def tramp(_data, memcxt, params, returns):
             pv = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * max(nparams, 1))).from_address(params)) \
                 if nparams else None
@@ -430,8 +431,8 @@ class BatchContext:
             return code
         cb = HOST_FUNC(tramp)
         self._hosts = getattr(self, "_hosts", []) + [cb]   # keep the trampoline alive
-        self._check(lib().WasmEdge_BatchAddHostFunction(self._h, self._name(module),
-                                                        self._name(name), cb, None))
+        self._check(lib().WasmEdge_BatchAddHostFunctionWithCost(self._h, self._name(module),
+                                                                self._name(name), cb, None, cost))
 
 
     # built-in WASI subset (WasmEdge_BatchInitWASI): args/envs shared by every instance

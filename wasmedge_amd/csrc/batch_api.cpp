@@ -1015,15 +1015,25 @@ WasmEdge_Result WasmEdge_BatchAddHostFunction(WasmEdge_BatchContext *C,
                                               const WasmEdge_String ModuleName,
                                               const WasmEdge_String FuncName,
                                               WasmEdge_BatchHostFunc_t Func, void *Data) {
+  return WasmEdge_BatchAddHostFunctionWithCost(C, ModuleName, FuncName, Func, Data, 0);
+}
+
+WasmEdge_Result WasmEdge_BatchAddHostFunctionWithCost(WasmEdge_BatchContext *C,
+                                                      const WasmEdge_String ModuleName,
+                                                      const WasmEdge_String FuncName,
+                                                      WasmEdge_BatchHostFunc_t Func, void *Data,
+                                                      uint64_t Cost) {
   if (!C || !Func) return R(kWrongVMWorkflow);
   if (!C->shards.empty())
-    return wbm::all(C, [&](WasmEdge_BatchContext *x) { return WasmEdge_BatchAddHostFunction(x, ModuleName, FuncName, Func, Data); });
+    return wbm::all(C, [&](WasmEdge_BatchContext *x) {
+      return WasmEdge_BatchAddHostFunctionWithCost(x, ModuleName, FuncName, Func, Data, Cost);
+    });
   const std::string mod(ModuleName.Buf ? ModuleName.Buf : "", ModuleName.Length);
   const std::string name(FuncName.Buf ? FuncName.Buf : "", FuncName.Length);
   // every import of that (module, name) binds to it, as an import object would
   for (uint32_t f = 0; f < C->prog.n_imported; f++)
     if (C->prog.funcs[f].import_module == mod && C->prog.funcs[f].import_name == name)
-      C->hosts[f] = WasmEdge_BatchContext::HostFn{Func, Data};
+      C->hosts[f] = WasmEdge_BatchContext::HostFn{Func, Data, Cost};
   return R(0);
 }
 

@@ -132,7 +132,8 @@ struct WasmEdge_BatchContext {
   // host-import yield path (only allocated when the module imports functions)
   DevBuf<uint32_t> fsave, hcall, hbuf;
   uint32_t hb_cells = 0;
-  struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; };
+  // a bound import: the function, its Data and its gas cost (HostFunctionBase::Cost)
+  struct HostFn { WasmEdge_BatchHostFunc_t fn = nullptr; void *data = nullptr; uint64_t cost = 0; };
   std::vector<HostFn> hosts;      // per function index (imports only)
   uint32_t host_threads = 0;      // service-round worker threads (0 or 1: one, serial)
   // built-in WASI subset (wasi.cpp): args/envs shared by every instance, captured

@@ -340,6 +340,23 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
                               hipMemcpyDeviceToHost), "write marks")))
     return -1;
 
+  // gas (metered contexts): the running totals of the waves with a parked lane whose host
+  // function has a cost, charged below before the function runs (helper.cpp:59-64)
+  const uint64_t limit = C->conf.CostLimit;
+  bool charge = false;
+  if (limit)
+    for (uint32_t i : parked)
+      if (hcall[i] < C->hosts.size() && C->hosts[hcall[i]].fn && C->hosts[hcall[i]].cost) charge = true;
+  std::vector<uint32_t> cost_lo, cost_hi;
+  if (charge) {
+    cost_lo.assign(size_t(nw) * 64, 0);
+    cost_hi.assign(size_t(nw) * 64, 0);
+    if (!C->hip_ok(hipMemcpy2D(cost_lo.data(), row, C->lstate.ptr + LS_COST * 64, pitch, row, nw,
+                               hipMemcpyDeviceToHost), "costs") ||
+        !C->hip_ok(hipMemcpy2D(cost_hi.data(), row, C->lstate.ptr + (LS_COST + 1) * 64, pitch, row, nw,
+                               hipMemcpyDeviceToHost), "costs"))
+      return -1;
+  }
   // memory.grow requests first: host functions of this round then see the grown pages
   bool pages_dirty = false;
   int64_t grown = 0;
@@ -373,6 +390,16 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
         const WasmEdge_BatchContext::HostFn h =
             f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
         if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
+        if (charge && h.cost) {   // Stat->addCost(HostFunc.getCost()) before the call
+          const uint64_t sum = (uint64_t(cost_hi[i]) << 32) | cost_lo[i], nsum = sum + h.cost;
+          if (nsum > limit) {     // CostLimitExceeded: the function never runs
+            st[i] = 0x03;
+            hcall[i] = 0xFFFFFFFFu;
+            continue;
+          }
+          cost_lo[i] = uint32_t(nsum);
+          cost_hi[i] = uint32_t(nsum >> 32);
+        }
         const wb::FuncType &t = P.types[P.funcs[f].type];
         uint32_t *cells = &hbuf[size_t(i) * hb];
         args.assign(t.params.size(), WasmEdge_Value{});
@@ -421,6 +448,11 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
   if (!C->hip_ok(hipMemcpy(C->status.ptr, st.data(), n, hipMemcpyHostToDevice), "status") ||
       !C->hip_ok(hipMemcpy(C->hcall.ptr, hcall.data(), size_t(n) * 4, hipMemcpyHostToDevice), "hcall") ||
       !C->hip_ok(hipMemcpy(C->hbuf.ptr, hbuf.data(), hbuf.size() * 4, hipMemcpyHostToDevice), "hbuf"))
+    return -1;
+  if (charge && (!C->hip_ok(hipMemcpy2D(C->lstate.ptr + LS_COST * 64, pitch, cost_lo.data(), row, row, nw,
+                                        hipMemcpyHostToDevice), "costs") ||
+                 !C->hip_ok(hipMemcpy2D(C->lstate.ptr + (LS_COST + 1) * 64, pitch, cost_hi.data(), row, row, nw,
+                                        hipMemcpyHostToDevice), "costs")))
     return -1;
   if (pages_dirty && !C->hip_ok(hipMemcpy2D(C->lstate.ptr + LS_PAGES * 64, pitch, pages.data(), row, row, nw,
                                             hipMemcpyHostToDevice), "pages"))
