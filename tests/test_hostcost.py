@@ -51,11 +51,15 @@ ROWS = [[i] for i in range(64)]
 
 
 def _oracle(limit, costs=COSTS, rows=ROWS):
-    """[(code, results, count, hash)], [gas total] of a fresh metered instance per row."""
+    """[(code, results, count, hash)], [gas total] of a fresh metered instance per row;
+    (None, None) when the instantiation itself runs out of gas."""
     O.set_host_costs(costs)
     try:
         m = O.Module(HOSTCOST, tail_call=True)
         insts = [O.Instance(m, cost_limit=limit) for _ in rows]
+        if not insts[0]._h:
+            assert insts[0].error == 0x03
+            return None, None
         ref = [x.invoke("run", r) for x, r in zip(insts, rows)]
         return ref, [x.cost_sum() for x in insts]
     finally:
@@ -74,6 +78,8 @@ def _host_trip_limits(row):
     prev = None
     for limit in range(1, full[0] + 1):
         ref, _ = _oracle(limit, rows=[row])
+        if ref is None:
+            continue
         code, _, cnt, _ = ref[0]
         if code == 0x03 and prev is not None and prev[0] == 0x03 and prev[2] == cnt:
             out.append(limit)
@@ -111,6 +117,11 @@ def test_gpu_host_cost_metering(built):
                          max(full) - 1, max(full), max(full) + 1, BIG] + trips[:24]))
     for limit in limits:
         ref, rcost = _oracle(limit)
+        if ref is None:   # the instantiation (the elem offset) runs out of gas
+            with pytest.raises(batch.WasmEdgeError) as e:
+                batch.BatchContext(HOSTCOST, len(ROWS), device=0, cost_limit=limit, tail_call=True)
+            assert e.value.code == 0x03
+            continue
         ctx = batch.BatchContext(HOSTCOST, len(ROWS), device=0, cost_limit=limit, tail_call=True)
         try:
             for (mod, name), c in COSTS.items():
