@@ -9,6 +9,10 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
+# (an API refusal exits 1 and is not fatal here; anything else stops the script)
+timeout -k 10 60 $R/tools/ubench/vmm > $O/vmm.log 2>&1; rc=$?
+echo "vmm rc=$rc $(tail -1 $O/vmm.log)"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after vmm"; exit $rc; fi
 step wcal 60 $R/tools/ubench/wcal
 cd /tmp && export TMPDIR=/tmp
 step wcal_trace 60 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wcal_trace -o run -- $R/tools/ubench/wcal
