@@ -84,6 +84,45 @@ int main() {
     CK(hipMemUnmap((char *)va + offs[k], row));
     CK(hipMemRelease(hs[k]));
   }
+  // steady-state costs per phase: 64 rows one by one, then one 1 GiB chunk
+  {
+    using clk = std::chrono::steady_clock;
+    double tc = 0, tm = 0, ta = 0, tu = 0;
+    std::vector<hipMemGenericAllocationHandle_t> h64(64);
+    for (int k = 0; k < 64; k++) {
+      char *p = (char *)va + (size_t(k) << 30);
+      auto t0 = clk::now();
+      CK(hipMemCreate(&h64[k], row, &prop, 0));
+      auto t1 = clk::now();
+      CK(hipMemMap(p, row, 0, h64[k], 0));
+      auto t2 = clk::now();
+      CK(hipMemSetAccess(p, row, &acc, 1));
+      auto t3 = clk::now();
+      tc += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      tm += std::chrono::duration<double, std::micro>(t2 - t1).count();
+      ta += std::chrono::duration<double, std::micro>(t3 - t2).count();
+    }
+    for (int k = 0; k < 64; k++) {
+      auto t0 = clk::now();
+      CK(hipMemUnmap((char *)va + (size_t(k) << 30), row));
+      CK(hipMemRelease(h64[k]));
+      tu += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    }
+    printf("per 4 MiB row (64 rows): create %.1f us, map %.1f us, access %.1f us, unmap+release %.1f us\n",
+           tc / 64, tm / 64, ta / 64, tu / 64);
+    const size_t big = size_t(1) << 30;
+    hipMemGenericAllocationHandle_t hb;
+    auto t0 = clk::now();
+    CK(hipMemCreate(&hb, big, &prop, 0));
+    CK(hipMemMap(va, big, 0, hb, 0));
+    CK(hipMemSetAccess(va, big, &acc, 1));
+    const double tb = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+    CK(hipMemset(va, 0, big));
+    CK(hipDeviceSynchronize());
+    CK(hipMemUnmap(va, big));
+    CK(hipMemRelease(hb));
+    printf("one 1 GiB chunk: create+map+access %.1f us\n", tb);
+  }
   CK(hipMemAddressFree(va, span));
   printf("vmm ok\n");
   return 0;

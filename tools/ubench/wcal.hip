@@ -67,6 +67,32 @@ __global__ void k_scan_swap(uint32_t *m) {
   }
 }
 
+// read every dword of granule r, store to every other dword of granule r - gap (read gap
+// granules earlier): how long a line read into L2 keeps taking stores without a write miss
+template <uint32_t kGap>
+__global__ void k_scan_swap_gap(uint32_t *m) {
+  const uint32_t wave = blockIdx.x, lane = threadIdx.x;
+  uint32_t acc = 0;
+  for (uint32_t r = 0; r < kRows + kGap; r++) {
+    if (r < kRows) {
+      const uint32_t *g = gran(m, wave, lane, r);
+      for (uint32_t w = 0; w < 32; w++) acc += g[w];   // (plain loads, as the compiled runs issue)
+    }
+    if (r >= kGap) {
+      uint32_t *s = gran(m, wave, lane, r - kGap);
+      for (uint32_t w = 0; w < 32; w += 2) s[w] = acc + w;
+    }
+  }
+}
+// stores only, but to granules the previous kernel just read (is the L2 still holding them?)
+__global__ void k_read_all(const uint32_t *m, uint32_t *out) {
+  const uint32_t wave = blockIdx.x, lane = threadIdx.x;
+  uint32_t acc = 0;
+  for (uint32_t r = 0; r < kRows; r++)
+    for (uint32_t w = 0; w < 32; w += 8) acc += gran(const_cast<uint32_t *>(m), wave, lane, r)[w];
+  if (acc == 0x1234567u) out[0] = acc;
+}
+
 int main(int argc, char **argv) {
   uint32_t *m = nullptr, *out = nullptr;
   if (hipMalloc(&m, kWords * 4) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
@@ -96,5 +122,10 @@ int main(int argc, char **argv) {
   run("half_seq", double(kWords) * 2, [&] { k_half_seq<<<g, b>>>(m); });
   run("dense_spread", double(kWords) * 4, [&] { k_dense_spread<<<g, b>>>(m); });
   run("scan_swap", double(kWords) * 2, [&] { k_scan_swap<<<g, b>>>(m); });
+  run("gap1", double(kWords) * 2, [&] { k_scan_swap_gap<1><<<g, b>>>(m); });
+  run("gap4", double(kWords) * 2, [&] { k_scan_swap_gap<4><<<g, b>>>(m); });
+  run("gap16", double(kWords) * 2, [&] { k_scan_swap_gap<16><<<g, b>>>(m); });
+  run("gap64", double(kWords) * 2, [&] { k_scan_swap_gap<64><<<g, b>>>(m); });
+  run("read_all", 0, [&] { k_read_all<<<g, b>>>(m, out); });
   return 0;
 }
