@@ -6,6 +6,9 @@ the same order):
   noswap    the partition's two swap stores dropped (the sort is wrong; its reads are not)
   nofill    the fill loop stores nothing (sorts zeroed memory: scans stop at once)
   trip0     base with trip mode off (WB_TRIP=0: SIMT scheduling only)
+  scan0 / chain0 / split0   base without the trips' scan windows / forward chaining /
+            stage A-B split (WB_TRIP_SCAN=0, WB_TRIP_CHAIN=0, WB_TRIP_SPLIT=0)
+  hyb0      trips alone, no SIMT phases (WB_HYBRID=0)
 usage: python tools/c3_writes.py [--elements N] [--only name,name]"""
 import argparse
 import os
@@ -33,7 +36,9 @@ def variants(n_el):
     assert fill in src
     nofill = src.replace(fill, "(drop (local.get $x))")
     return [("base", assemble(src), {}), ("noswap", assemble(noswap), {}),
-            ("nofill", assemble(nofill), {}), ("trip0", assemble(src), {"WB_TRIP": "0"})]
+            ("nofill", assemble(nofill), {}), ("trip0", assemble(src), {"WB_TRIP": "0"}),
+            ("scan0", assemble(src), {"WB_TRIP_SCAN": "0"}), ("chain0", assemble(src), {"WB_TRIP_CHAIN": "0"}),
+            ("split0", assemble(src), {"WB_TRIP_SPLIT": "0"}), ("hyb0", assemble(src), {"WB_HYBRID": "0"})]
 
 
 def main():
