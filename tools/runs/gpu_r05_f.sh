@@ -8,6 +8,8 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
+timeout -k 10 60 $R/tools/ubench/vmm > $O/vmm.log 2>&1; rc=$?; echo "vmm rc=$rc $(tail -1 $O/vmm.log)"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step plain 200 python3 $R/tools/c3_writes.py --only base,trip0,scan0,chain0,split0,hyb0
 cd /tmp && export TMPDIR=/tmp
 step write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/tools/c3_writes.py --only base,trip0,scan0,chain0,split0,hyb0

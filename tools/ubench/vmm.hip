@@ -123,6 +123,37 @@ int main() {
     CK(hipMemRelease(hb));
     printf("one 1 GiB chunk: create+map+access %.1f us\n", tb);
   }
+  // 2D copies over mapped rows a large pitch apart (the host service round's RoundCache:
+  // one row of every wave, the waves `pitch` apart)
+  {
+    int maxpitch = 0;
+    (void)hipDeviceGetAttribute(&maxpitch, hipDeviceAttributeMaxPitch, dev);
+    printf("hipDeviceAttributeMaxPitch = %d\n", maxpitch);
+    for (size_t pitch : {size_t(1) << 30, size_t(3) << 30, size_t(32) << 30}) {
+      std::vector<hipMemGenericAllocationHandle_t> hh(4);
+      for (int k = 0; k < 4; k++) {
+        char *p = (char *)va + k * pitch;
+        CK(hipMemCreate(&hh[k], row, &prop, 0));
+        CK(hipMemMap(p, row, 0, hh[k], 0));
+        CK(hipMemSetAccess(p, row, &acc, 1));
+        k_fill<<<64, 256>>>((uint32_t *)p, 4096, uint32_t(k));
+      }
+      CK(hipDeviceSynchronize());
+      std::vector<uint32_t> hb(4 * 4096, 0);
+      hipError_t e = hipMemcpy2D(hb.data(), 4096 * 4, va, pitch, 4096 * 4, 4, hipMemcpyDeviceToHost);
+      uint32_t bad = 0;
+      for (int k = 0; k < 4 && e == hipSuccess; k++)
+        for (uint32_t i = 0; i < 4096; i++) bad += hb[k * 4096 + i] != (i ^ uint32_t(k));
+      e = e == hipSuccess ? hipMemcpy2D(va, pitch, hb.data(), 4096 * 4, 4096 * 4, 4, hipMemcpyHostToDevice) : e;
+      printf("2D copy, pitch %zu GiB: %s, %u bad words\n", pitch >> 30, hipGetErrorString(e), bad);
+      (void)hipGetLastError();
+      CK(hipDeviceSynchronize());
+      for (int k = 0; k < 4; k++) {
+        CK(hipMemUnmap((char *)va + k * pitch, row));
+        CK(hipMemRelease(hh[k]));
+      }
+    }
+  }
   CK(hipMemAddressFree(va, span));
   printf("vmm ok\n");
   return 0;
