@@ -62,6 +62,13 @@ def workload(name, args):
         return (workloads.qsort_wasm(), "sort", lambda ids: np.stack([ids, np.full_like(ids, el)], 1),
                 [I32, I32], "C3 quicksort of %d i32 per instance (configs[2])" % el,
                 {"elements": el})
+    if name == "c3grow":
+        # not a BASELINE config: C3's sort in a module that starts with one page and
+        # memory.grows to the pages the sort needs (the cost of growth)
+        el = args.elements
+        return (workloads.qsort_grow_wasm(), "sort", lambda ids: np.stack([ids, np.full_like(ids, el)], 1),
+                [I32, I32], "C3 quicksort of %d i32 per instance, memory grown from 1 page by "
+                            "memory.grow (no declared max)" % el, {"elements": el})
     if name == "c4":
         return (workloads.collatz_wasm(), "collatz",
                 lambda ids: np.stack([ids, np.full_like(ids, 10000)], 1), [I32, I32],
@@ -264,7 +271,7 @@ def load_profile(workload, config):
 def elapsed_hint(args):
     """Long steps (full-size C3) report progress on stderr so a run is never silent for
     minutes; short ones stay quiet inside the timed region."""
-    return args.workload == "c3" and args.elements >= 65536
+    return args.workload in ("c3", "c3grow") and args.elements >= 65536
 
 
 # The job's instance count per workload when --instances is not given: the metric's "64K
@@ -435,7 +442,7 @@ def main():
                     help="instances (default 65536; 262144 for c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "mt", "tail"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3grow", "c4", "c5", "mt", "tail"])
     ap.add_argument("--mt-n", type=int, default=100000, help="mt19937 draws per instance")
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     ap.add_argument("--vary-args", default="auto", choices=["auto", "on", "off"],
@@ -542,7 +549,7 @@ def main():
         out["cpu_baseline"], bpi, c3_split = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
                                                           threads, gpu, args.workload.upper(),
                                                           tail_call=args.workload == "tail")
-        if args.workload == "c3":
+        if args.workload in ("c3", "c3grow"):
             # qsort's bytes per instruction is stable across instances
             c3_bytes_per_instr, c3_bpi_src = bpi, " on the oracle sample"
     if args.workload != "c2":
@@ -596,7 +603,7 @@ def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_inst
                       "SQ_WAVE_CYCLES per launch)" % prof.get("source")})
     else:
         issue["note"] = "no PMC summary for this configuration (tools/prof_bench.sh)"
-    if args.workload == "c3":
+    if args.workload in ("c3", "c3grow"):
         # HBM-bound config: algorithmic bytes = the linear-memory bytes of the wasm loads and
         # stores, per wasm instruction as the oracle counts them on the CPU-baseline sample
         # (or the committed figure when the baseline leg is skipped) x this launch's count

@@ -158,20 +158,26 @@ def test_gpu_grow_default_config(built):
 
 
 @pytest.mark.gpu
-def test_gpu_grow_through_the_pool(built):
-    """The same with two reserved pages: every grown page comes from the device pool
-    (lanes park at memory.grow, the host commits rows, the page table widens), over two
-    waves; bit-exact against the oracle, and again after a Reset."""
+@pytest.mark.parametrize("vmm", ["1", "0"])
+def test_gpu_grow_through_the_pool(built, monkeypatch, vmm):
+    """The same with two pages committed up front: every grown page is committed on demand
+    (lanes park at memory.grow and the host commits 4 MiB wave rows) -- into the
+    virtual-memory layout's VA range (vmm 1: every engine then addresses them directly), or
+    from the device pool through the page table (WB_VMM=0) -- over two waves; bit-exact
+    against the oracle, and again after a Reset."""
+    monkeypatch.setenv("WB_VMM", vmm)
     wasm = grow_wasm()
     rows = rows_for(128, 1200, mult=419)
     _gpu_grow(wasm, rows, oracle_rows(wasm, rows), memory_reserve_pages=2)
 
 
 @pytest.mark.gpu
-def test_gpu_grow_pool_exhausted(built):
-    """A cap on the pool (MemoryPoolBytes = 16 rows of 4 MiB): growPage's allocation
-    failure (memory.h:104-109) -- lanes asking for more pages than the wave can get see
-    -1, the others grow."""
+@pytest.mark.parametrize("vmm", ["1", "0"])
+def test_gpu_grow_pool_exhausted(built, monkeypatch, vmm):
+    """A cap on the committed pages (MemoryPoolBytes = 16 rows of 4 MiB): growPage's
+    allocation failure (memory.h:104-109) -- lanes asking for more pages than the wave can
+    get see -1, the others grow (virtual-memory layout and pool rows alike)."""
+    monkeypatch.setenv("WB_VMM", vmm)
     from wasmedge_amd import batch
     wasm = assemble("""(module (memory 1)
       (func (export "g") (param i32) (result i32 i32)

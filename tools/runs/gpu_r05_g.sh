@@ -1,0 +1,23 @@
+# r05 g: virtual-memory linear memory (VA reservation, 4 MiB wave rows committed on demand):
+# memgrow / layout / multidevice tests, the VMM probe (2D copy pitch), C3 write traffic by
+# trip feature (tools/c3_writes.py), and C3 vs the growing C3 (c3grow) at 4K and 1 MiB
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r05g; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+timeout -k 10 60 $R/tools/ubench/vmm > $O/vmm.log 2>&1; rc=$?; echo "vmm rc=$rc $(tail -1 $O/vmm.log)"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+step tests 600 python -u -m pytest tests/test_memgrow.py tests/test_layout.py tests/test_multidevice.py tests/test_hostcall.py -m gpu -v --timeout 300 --timeout-method thread
+step c3k 300 python bench.py --workload c3 --elements 4096 --steps 3 --warmup 3 --no-cpu-baseline
+step c3gk 300 python bench.py --workload c3grow --elements 4096 --steps 3 --warmup 3 --no-cpu-baseline
+step knobs 300 python3 $R/tools/c3_writes.py --only base,trip0,scan0,chain0,split0,hyb0
+cd /tmp && export TMPDIR=/tmp
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/tools/c3_writes.py --only base,trip0,scan0,chain0,split0,hyb0
+cd $R
+step c3 400 python bench.py --workload c3 --steps 2 --warmup 3 --no-cpu-baseline
+step c3g 400 python bench.py --workload c3grow --steps 2 --warmup 3 --no-cpu-baseline
+echo all done

@@ -226,6 +226,23 @@ def qsort_wasm(pages=17):
     return assemble(qsort_wat(pages))
 
 
+def qsort_grow_wat():
+    """C3's quicksort in a module that starts with ONE page and grows to what the sort
+    needs (1 + ceil((65536 + 4n) / 65536) pages) before filling it -- the allocator-driven
+    shape (a Rust/C module's heap) whose pages all come from memory.grow. No declared max:
+    the reference's default limit (65536) applies."""
+    src = qsort_wat(1)
+    old = "    (local.set $x (i32.add (i32.mul (local.get $iid) (i32.const 2654435761)) (i32.const 1)))"
+    assert old in src
+    grow = ("    (drop (memory.grow (i32.sub (i32.shr_u (i32.add (i32.const %d) (i32.add (i32.shl (local.get $n)"
+            " (i32.const 2)) (i32.const 65535))) (i32.const 16)) (memory.size))))\n" % QSORT_BASE)
+    return src.replace(old, grow + old)
+
+
+def qsort_grow_wasm():
+    return assemble(qsort_grow_wat())
+
+
 # ---------------------------------------------------------------------------- C4
 def collatz_wat():
     return r"""
