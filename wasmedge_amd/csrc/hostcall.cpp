@@ -31,12 +31,10 @@ void RoundCache::mark_dirty(uint32_t b) {
 
 uint32_t *RoundCache::get(uint32_t b, uint32_t wave, bool *fail) {
   if (wave < w0 || wave >= w0 + nw) return nullptr;
-  // pool pages sit at a different address per wave, and the virtual-memory layout's waves
-  // differ in the pages they have committed: past the pages every wave has, rows are left to
-  // the per-wave blocks (which see each wave's own); so are rows whose waves lie further
-  // apart than a 2D copy's pitch may be
-  if (uint64_t(b + 1) * kRowWords > C->direct_words()) return nullptr;
-  if (C->vmm && C->max_pitch && size_t(C->mem_words) * 256 > C->max_pitch) return nullptr;
+  // pool pages sit at a different address per wave: left to the per-wave blocks; so is the
+  // whole virtual-memory layout (hipMemcpy2D refuses its mapped ranges -- "invalid
+  // argument" at any pitch, tools/ubench/vmm.hip -- while 1D copies work)
+  if (C->vmm || uint64_t(b + 1) * kRowWords > C->direct_words()) return nullptr;
   Row *r;
   {
     std::lock_guard<std::mutex> lock(mu);
