@@ -7,6 +7,6 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
-step dbg64 120 python3 tools/vmm_debug.py 64
-step dbg128 120 python3 tools/vmm_debug.py 128
+step dbg64 120 env WB_VMM_DEBUG=1 python3 tools/vmm_debug.py 64
+
 echo all done

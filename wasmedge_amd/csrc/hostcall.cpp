@@ -17,6 +17,8 @@
 // thread), so host functions must be reentrant, as the reference's are under its
 // concurrent VM::execute (include/vm/vm.h:137-141).
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <thread>
 
@@ -184,8 +186,19 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
 // mapped at its place in the wave's VA, read-write for the device, zeroed (a fresh page reads
 // zero, as the reference's MAP_ANONYMOUS pages do). The device copy of the counts is
 // uploaded by the caller (vcommit_dirty).
+static bool vm_dbg() {
+  static const bool on = getenv("WB_VMM_DEBUG") != nullptr;
+  return on;
+}
+static bool vm_fail(const char *what, hipError_t e) {
+  if (vm_dbg()) fprintf(stderr, "[vmm] %s: %s\n", what, hipGetErrorString(e));
+  (void)hipGetLastError();
+  return false;
+}
+
 bool vm_commit(WasmEdge_BatchContext *C, uint32_t wave, uint32_t pages) {
   uint32_t &have = C->vcommit_h[wave];
+  if (vm_dbg()) fprintf(stderr, "[vmm] commit wave %u: %u -> %u pages\n", wave, have, pages);
   if (pages <= have) return true;
   const size_t bytes = size_t(pages - have) << 22;
   if (C->conf.MemoryPoolBytes && have >= C->vm_commit0 &&
@@ -196,25 +209,21 @@ bool vm_commit(WasmEdge_BatchContext *C, uint32_t wave, uint32_t pages) {
   prop.location.type = hipMemLocationTypeDevice;
   prop.location.id = C->device;
   hipMemGenericAllocationHandle_t h;
-  if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
+  hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
+  if (e != hipSuccess) return vm_fail("hipMemCreate", e);
   void *at = C->mem.ptr + (size_t(wave) * C->mem_words + (size_t(have) << 14)) * 64;
-  if (hipMemMap(at, bytes, 0, h, 0) != hipSuccess) {
-    (void)hipGetLastError();
+  if ((e = hipMemMap(at, bytes, 0, h, 0)) != hipSuccess) {
     (void)hipMemRelease(h);
-    return false;
+    return vm_fail("hipMemMap", e);
   }
   hipMemAccessDesc acc = {};
   acc.location = prop.location;
   acc.flags = hipMemAccessFlagsProtReadWrite;
-  if (hipMemSetAccess(at, bytes, &acc, 1) != hipSuccess ||
-      hipMemsetAsync(at, 0, bytes, C->stream) != hipSuccess) {
-    (void)hipGetLastError();
+  if ((e = hipMemSetAccess(at, bytes, &acc, 1)) != hipSuccess ||
+      (e = hipMemsetAsync(at, 0, bytes, C->stream)) != hipSuccess) {
     (void)hipMemUnmap(at, bytes);
     (void)hipMemRelease(h);
-    return false;
+    return vm_fail("hipMemSetAccess / hipMemsetAsync", e);
   }
   C->vm_maps.push_back(WasmEdge_BatchContext::VmMap{at, bytes, h});
   if (have >= C->vm_commit0) C->vm_grown_bytes += bytes;
@@ -388,6 +397,8 @@ static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &p
     // the pages exist: all within the wave's committed pages, or (past the VA range, or no
     // virtual-memory layout) every page below R backed and the rest in the wave's pool rows
     const uint32_t direct = C->vmm ? C->vcommit_h[i / 64] : R;
+    if (vm_dbg() && i % 64 < 2)
+      fprintf(stderr, "[vmm] lane %u: %u pages + %u, wave has %u (R %u)\n", i, pages[i], n, direct, R);
     if (pages[i] + n <= direct || (direct >= R && pages[i] + n - R <= C->pt_n[i / 64])) {
       res = pages[i];
       pages[i] += n;
