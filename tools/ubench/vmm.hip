@@ -154,6 +154,44 @@ int main() {
       }
     }
   }
+  // adjacent commits like batch_api.cpp vm_commit: [0,2), [2,8), [8,98), [98,195) rows of
+  // 4 MiB, each SetAccess'ed and zeroed with hipMemsetAsync on a non-blocking stream (or
+  // hipMemset, or a kernel) -- which call refuses what
+  {
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const uint32_t cuts[] = {0, 2, 8, 98, 195, 196, 200};
+    std::vector<std::pair<void *, size_t>> maps;
+    std::vector<hipMemGenericAllocationHandle_t> hh;
+    for (int mode = 0; mode < 3; mode++) {
+      for (size_t k = 0; k + 1 < sizeof cuts / sizeof cuts[0]; k++) {
+        const size_t bytes = size_t(cuts[k + 1] - cuts[k]) * row;
+        char *at = (char *)va + (size_t(mode) << 34) + size_t(cuts[k]) * row;
+        hipMemGenericAllocationHandle_t h;
+        hipError_t e1 = hipMemCreate(&h, bytes, &prop, 0);
+        hipError_t e2 = e1 == hipSuccess ? hipMemMap(at, bytes, 0, h, 0) : e1;
+        hipError_t e3 = e2 == hipSuccess ? hipMemSetAccess(at, bytes, &acc, 1) : e2;
+        hipError_t e4 = hipErrorUnknown;
+        if (e3 == hipSuccess) {
+          if (mode == 0) e4 = hipMemsetAsync(at, 0, bytes, st);
+          else if (mode == 1) e4 = hipMemset(at, 0, bytes);
+          else { k_fill<<<256, 256, 0, st>>>((uint32_t *)at, bytes / 4, 0); e4 = hipGetLastError(); }
+          hipError_t e5 = hipStreamSynchronize(st);
+          if (e4 == hipSuccess) e4 = e5;
+        }
+        printf("mode %d rows [%u,%u) at +%zu MiB: create %s map %s access %s zero %s\n", mode, cuts[k], cuts[k + 1],
+               (size_t(cuts[k]) * row) >> 20, hipGetErrorString(e1), hipGetErrorString(e2), hipGetErrorString(e3),
+               hipGetErrorString(e4));
+        (void)hipGetLastError();
+        if (e2 == hipSuccess) maps.emplace_back(at, bytes);
+        if (e1 == hipSuccess) hh.push_back(h);
+      }
+    }
+    CK(hipDeviceSynchronize());
+    for (auto &m : maps) (void)hipMemUnmap(m.first, m.second);
+    for (auto &h : hh) (void)hipMemRelease(h);
+    (void)hipStreamDestroy(st);
+  }
   CK(hipMemAddressFree(va, span));
   printf("vmm ok\n");
   return 0;
