@@ -192,6 +192,52 @@ int main() {
     for (auto &h : hh) (void)hipMemRelease(h);
     (void)hipStreamDestroy(st);
   }
+  // strategies for adjacent commits (which SetAccess call works), each verified by a
+  // kernel fill + check of every committed row before anything else touches it:
+  //  S2: SetAccess over the wave's whole committed range [0, new end) after each map
+  //  S6: one mapping + SetAccess per 4 MiB row
+  for (int strat : {2, 6}) {
+    const uint32_t cuts[] = {0, 2, 8, 98, 195, 196, 200};
+    std::vector<std::pair<void *, size_t>> maps;
+    std::vector<hipMemGenericAllocationHandle_t> hh;
+    char *base = (char *)va + (size_t(4 + strat) << 34);
+    bool all_ok = true;
+    for (size_t k = 0; k + 1 < sizeof cuts / sizeof cuts[0]; k++) {
+      hipError_t e = hipSuccess;
+      if (strat == 6) {
+        for (uint32_t r = cuts[k]; r < cuts[k + 1] && e == hipSuccess; r++) {
+          hipMemGenericAllocationHandle_t h;
+          char *at = base + size_t(r) * row;
+          e = hipMemCreate(&h, row, &prop, 0);
+          if (e == hipSuccess) { hh.push_back(h); e = hipMemMap(at, row, 0, h, 0); }
+          if (e == hipSuccess) { maps.emplace_back(at, row); e = hipMemSetAccess(at, row, &acc, 1); }
+        }
+      } else {
+        const size_t bytes = size_t(cuts[k + 1] - cuts[k]) * row;
+        char *at = base + size_t(cuts[k]) * row;
+        hipMemGenericAllocationHandle_t h;
+        e = hipMemCreate(&h, bytes, &prop, 0);
+        if (e == hipSuccess) { hh.push_back(h); e = hipMemMap(at, bytes, 0, h, 0); }
+        if (e == hipSuccess) { maps.emplace_back(at, bytes); e = hipMemSetAccess(base, size_t(cuts[k + 1]) * row, &acc, 1); }
+      }
+      printf("strategy S%d rows [%u,%u): %s\n", strat, cuts[k], cuts[k + 1], hipGetErrorString(e));
+      (void)hipGetLastError();
+      if (e != hipSuccess) { all_ok = false; break; }
+    }
+    if (all_ok) {
+      const size_t words = size_t(200) * row / 4;
+      CK(hipMemset(bad, 0, 4));
+      k_fill<<<1024, 256>>>((uint32_t *)base, words, 77u);
+      k_check<<<1024, 256>>>((uint32_t *)base, words, 77u, bad);
+      CK(hipDeviceSynchronize());
+      uint32_t nb = 0;
+      CK(hipMemcpy(&nb, bad, 4, hipMemcpyDeviceToHost));
+      printf("strategy S%d: kernel check over 200 rows: %u bad words\n", strat, nb);
+    }
+    CK(hipDeviceSynchronize());
+    for (auto &m : maps) (void)hipMemUnmap(m.first, m.second);
+    for (auto &h : hh) (void)hipMemRelease(h);
+  }
   CK(hipMemAddressFree(va, span));
   printf("vmm ok\n");
   return 0;
