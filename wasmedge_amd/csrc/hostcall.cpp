@@ -219,7 +219,11 @@ bool vm_commit(WasmEdge_BatchContext *C, uint32_t wave, uint32_t pages) {
   hipMemAccessDesc acc = {};
   acc.location = prop.location;
   acc.flags = hipMemAccessFlagsProtReadWrite;
-  if ((e = hipMemSetAccess(at, bytes, &acc, 1)) != hipSuccess ||
+  // access over the wave's whole committed range, not the new mapping alone: the runtime
+  // refuses a range that starts where another mapping ends ("invalid argument", at random;
+  // tools/ubench/vmm.hip strategy S2 is the form that held on every try)
+  void *wave_base = C->mem.ptr + size_t(wave) * C->mem_words * 64;
+  if ((e = hipMemSetAccess(wave_base, size_t(pages) << 22, &acc, 1)) != hipSuccess ||
       (e = hipMemsetAsync(at, 0, bytes, C->stream)) != hipSuccess) {
     (void)hipMemUnmap(at, bytes);
     (void)hipMemRelease(h);
