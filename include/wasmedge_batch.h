@@ -126,7 +126,10 @@ typedef struct WasmEdge_BatchConfigure {
    * wave) and reached through a page table by the per-lane step, more slowly. 0 = the
    * module's initial size, raised toward the page limit while the whole batch's
    * reservation stays within min(16 GiB, a quarter of the device's free memory); modules
-   * without memory.grow reserve their initial size. Clamped to [initial size, limit]. */
+   * without memory.grow reserve their initial size. Clamped to [initial size, limit]. After
+   * a run whose instances grew past it, the next BatchReset re-lays memory with the largest
+   * size they reached in the reserved layout (WasmEdge_BatchGetReservedPages), so later runs
+   * address every page directly. */
   uint32_t MemoryReservePages;
   /* Cap on the device memory committed for grown pages (bytes; 0 = until hipMalloc fails).
    * A grow that would need more returns -1. */
@@ -372,6 +375,14 @@ WASMEDGE_BATCH_API const char *WasmEdge_BatchGetEngine(const WasmEdge_BatchConte
 /* The interleave granule in use, in bytes (WasmEdge_BatchConfigure::MemoryGranule).
  * Layout only: results never depend on it. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *Cxt);
+
+/* Pages of every instance's memory in the reserved layout, which every execution path
+ * addresses directly (pages past it come from pool rows through a page table). It starts at
+ * MemoryReservePages (or the module's choice) and, at a BatchReset after a run whose
+ * instances grew past it, takes the largest memory they reached (within 3/4 of the device
+ * memory, and MemoryPoolBytes past the initial layout). Layout only: results never depend
+ * on it. */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetReservedPages(const WasmEdge_BatchContext *Cxt);
 
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */

@@ -158,26 +158,45 @@ def test_gpu_grow_default_config(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("vmm", ["1", "0"])
-def test_gpu_grow_through_the_pool(built, monkeypatch, vmm):
-    """The same with two pages committed up front: every grown page is committed on demand
-    (lanes park at memory.grow and the host commits 4 MiB wave rows) -- into the
-    virtual-memory layout's VA range (vmm 1: every engine then addresses them directly), or
-    from the device pool through the page table (WB_VMM=0) -- over two waves; bit-exact
-    against the oracle, and again after a Reset."""
-    monkeypatch.setenv("WB_VMM", vmm)
+def test_gpu_grow_through_the_pool(built):
+    """The same with two reserved pages: every grown page comes from the device pool
+    (lanes park at memory.grow, the host commits rows, the page table widens), over two
+    waves; bit-exact against the oracle, and again after a Reset."""
     wasm = grow_wasm()
     rows = rows_for(128, 1200, mult=419)
     _gpu_grow(wasm, rows, oracle_rows(wasm, rows), memory_reserve_pages=2)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("vmm", ["1", "0"])
-def test_gpu_grow_pool_exhausted(built, monkeypatch, vmm):
-    """A cap on the committed pages (MemoryPoolBytes = 16 rows of 4 MiB): growPage's
-    allocation failure (memory.h:104-109) -- lanes asking for more pages than the wave can
-    get see -1, the others grow (virtual-memory layout and pool rows alike)."""
-    monkeypatch.setenv("WB_VMM", vmm)
+def test_gpu_layout_takes_the_grown_pages(built):
+    """A run whose lanes grow past the reserved layout (two pages, pool rows past them):
+    the next Reset re-lays memory with every page they reached in the reserved layout
+    (WasmEdge_BatchGetReservedPages), where every engine addresses it directly; the run
+    after it is bit-exact again, and a fixed layout (WB_RELAYOUT=0) gives the same."""
+    from wasmedge_amd import batch
+    wasm = grow_wasm()
+    rows = rows_for(128, 300, mult=419)
+    ref = oracle_rows(wasm, rows)
+    ctx = batch.BatchContext(wasm, len(rows), device=0, memory_reserve_pages=2)
+    try:
+        vals = batch.make_values(rows, [I32, I32])
+        assert ctx.reserved_pages() == 2
+        for rep in range(3):
+            rets, st, cnt = ctx.execute("grow", vals, 1)
+            ints = batch.ret_ints(rets)
+            got = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == [], rep
+            ctx.reset()
+            assert ctx.reserved_pages() == 1 + max(r[0] for r in rows), rep
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_grow_pool_exhausted(built):
+    """A cap on the pool (MemoryPoolBytes = 16 rows of 4 MiB): growPage's allocation
+    failure (memory.h:104-109) -- lanes asking for more pages than the wave can get see
+    -1, the others grow."""
     from wasmedge_amd import batch
     wasm = assemble("""(module (memory 1)
       (func (export "g") (param i32) (result i32 i32)

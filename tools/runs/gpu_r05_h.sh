@@ -1,4 +1,4 @@
-# r05 h: the virtual-memory grow path (tools/vmm_debug.py), then the memgrow tests and the
+# r05 h: reserved layout grown at Reset to the pages the lanes reached; memgrow tests and the
 # C3 / growing-C3 benches
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r05h; mkdir -p $O
@@ -8,7 +8,7 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
-step dbg64 120 env WB_VMM_DEBUG=1 python3 tools/vmm_debug.py 128
+
 step tests 600 python -u -m pytest tests/test_memgrow.py tests/test_layout.py tests/test_multidevice.py tests/test_hostcall.py -m gpu -v --timeout 300 --timeout-method thread
 step c3k 300 python bench.py --workload c3 --elements 4096 --steps 3 --warmup 3 --no-cpu-baseline
 step c3gk 300 python bench.py --workload c3grow --elements 4096 --steps 3 --warmup 3 --no-cpu-baseline

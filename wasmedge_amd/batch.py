@@ -198,6 +198,8 @@ def lib():
         L.WasmEdge_BatchGetCompiledRuns.argtypes = [vp]
         L.WasmEdge_BatchGetMemoryGranule.restype = u32
         L.WasmEdge_BatchGetMemoryGranule.argtypes = [vp]
+        L.WasmEdge_BatchGetReservedPages.restype = u32
+        L.WasmEdge_BatchGetReservedPages.argtypes = [vp]
         L.WasmEdge_BatchGetEngine.restype = ctypes.c_char_p
         L.WasmEdge_BatchGetEngine.argtypes = [vp]
         _lib = L
@@ -367,6 +369,11 @@ class BatchContext:
     def memory_granule(self):
         """The interleave granule in use, bytes (WasmEdge_BatchGetMemoryGranule)."""
         return lib().WasmEdge_BatchGetMemoryGranule(self._h)
+
+    def reserved_pages(self):
+        """Pages of every instance in the directly addressed layout
+        (WasmEdge_BatchGetReservedPages)."""
+        return lib().WasmEdge_BatchGetReservedPages(self._h)
 
     def engine(self):
         """The execution engine the context runs, e.g. "compiled-runs+simt/vgpr-frames"

@@ -101,50 +101,6 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
   }
 }
 
-// VA reserved per context for a growing module's linear memory (of the 256 TiB a 48-bit VA
-// gives; 64K instances: 2,048 pages = 128 MiB per instance at full speed, pool rows past it)
-constexpr uint64_t kVaBudget = uint64_t(8) << 40;
-
-// The virtual-memory layout (batch_ctx.h): reserve vpages pages per lane of VA for the
-// whole batch and commit the first commit0 of every wave. false (nothing kept): the device
-// has no VMM or refused a call; the caller then allocates the reserved layout and pool rows
-// as before.
-bool vm_setup(WasmEdge_BatchContext *C, uint32_t commit0, uint32_t vpages) {
-  int vm = 0;
-  if (hipDeviceGetAttribute(&vm, hipDeviceAttributeVirtualMemoryManagementSupported, C->device) != hipSuccess ||
-      !vm)
-    return false;
-  const size_t wave_bytes = size_t(vpages) << 22;
-  void *va = nullptr;
-  if (hipMemAddressReserve(&va, size_t(C->nwaves) * wave_bytes, 0, nullptr, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  C->mem.ptr = static_cast<uint32_t *>(va);   // (not hipMalloc'ed: vm_release frees it)
-  C->mem.n = 0;
-  C->va_bytes = size_t(C->nwaves) * wave_bytes;
-  C->vmm = true;
-  const uint32_t old_words = C->mem_words;
-  C->mem_words = vpages << 14;                // (vm_commit addresses rows through it)
-  C->vcommit_h.assign(C->nwaves, 0);
-  int mp = 0;
-  (void)hipDeviceGetAttribute(&mp, hipDeviceAttributeMaxPitch, C->device);
-  C->max_pitch = mp > 0 ? size_t(mp) : 0;
-  for (uint32_t w = 0; w < C->nwaves; w++)
-    if (!wbh::vm_commit(C, w, commit0)) {
-      wbh::vm_release(C);
-      C->mem_words = old_words;
-      (void)hipGetLastError();
-      return false;
-    }
-  C->vm_commit0 = commit0;
-  C->vm_grown_bytes = 0;
-  if (C->vcommit.upload(C->vcommit_h, C->stream)) return true;
-  wbh::vm_release(C);
-  C->mem_words = old_words;
-  return false;
-}
-
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
   std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports,
@@ -205,23 +161,10 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   }
   if (!P.has_mem) reserve = limit = 0;
   C->mem_max_pages = limit;
-  C->rpages = reserve;
+  C->rpages = C->rpages0 = reserve;
   C->mem_words = reserve << 14;
   C->grow_host = grows && limit > reserve;
   C->pt_n.assign(C->nwaves, 0);
-  // a module that grows past its reserved pages: the pages it may grow into are a VA
-  // reservation committed on demand (batch_ctx.h "Virtual-memory layout"; WB_VMM=0 keeps
-  // the pool rows and page table for every page past the reserved layout)
-  const char *vme = getenv("WB_VMM");
-  if (C->grow_host && !(vme && vme[0] == '0')) {
-    const uint64_t wave_page = uint64_t(64) << 16;   // a page of a wave's 64 lanes
-    const uint32_t vpages = uint32_t(std::min<uint64_t>(limit, kVaBudget / (uint64_t(C->nwaves) * wave_page)));
-    if (vpages > reserve && vm_setup(C, reserve, vpages)) {
-      C->rpages = vpages;
-      C->mem_words = vpages << 14;
-      C->grow_host = limit > vpages;   // pool rows past the VA range only
-    }
-  }
   // interleave granule of the wave's linear memories (DESIGN.md "Linear memory"): 4-byte
   // words when the module's addresses are wave-uniform, wider granules (a lane's
   // consecutive words together) when they diverge per lane (Program::divergent_mem)
@@ -355,13 +298,13 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     for (uint8_t t : P.types[P.funcs[f].type].results) r += wb::cells_of(t);
     C->hb_cells = std::max(C->hb_cells, std::max(a, r));
   }
-  if ((!C->vmm && !C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64)) ||
+  if (!C->mem.alloc(nw * size_t(C->mem_words) * 64 + 64) ||
       !C->gstack.alloc(nw * size_t(C->gs_depth) * 64) ||
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
       !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
       (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
-      ((P.n_imported || C->grow_host || C->vmm) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
+      ((P.n_imported || C->grow_host) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
@@ -421,6 +364,60 @@ uint8_t layout_trial(WasmEdge_BatchContext *C, double secs) {
 
 uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
 
+// The reserved layout grown to what the instances reached (at a Reset after a run whose
+// lanes grew into pool rows): every page up to the batch's largest memory then sits in the
+// reserved layout, where every engine addresses it directly -- a module that memory.grows
+// runs its later invocations at full speed, and only the first pays the per-lane step's
+// page-table path (DESIGN.md "Paged growth"). Bounded by 3/4 of the device memory this
+// context holds or could get, and by MemoryPoolBytes past the initial layout;
+// WB_RELAYOUT=0 keeps the layout fixed (A/B aid). Reset rewrites every page anyway
+// (mem_fresh), so results never depend on it.
+uint8_t grow_layout(WasmEdge_BatchContext *C) {
+  if (const char *e = getenv("WB_RELAYOUT"))
+    if (e[0] == '0') return 0;
+  if (!C->settle()) return kRuntimeError;
+  const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+  std::vector<uint32_t> pages(size_t(C->nwaves) * 64);
+  if (!C->hip_ok(hipMemcpy2D(pages.data(), row, C->lstate.ptr + LS_PAGES * 64, pitch, row, C->nwaves,
+                             hipMemcpyDeviceToHost), "pages"))
+    return kRuntimeError;
+  uint32_t target = 0;
+  for (uint32_t i = 0; i < C->n; i++) target = std::max(target, pages[i]);
+  target = std::min(target, C->mem_max_pages);
+  const uint64_t wave_page = uint64_t(64) << 16;   // one page of a wave's 64 lanes
+  size_t free_b = 0, total_b = 0;
+  (void)hipMemGetInfo(&free_b, &total_b);
+  const uint64_t held = uint64_t(C->nwaves) * C->rpages * wave_page + C->pool_bytes;
+  uint64_t cap = (uint64_t(free_b) + held) / 4 * 3 / (uint64_t(C->nwaves) * wave_page);
+  if (C->conf.MemoryPoolBytes)
+    cap = std::min<uint64_t>(cap, C->rpages0 + C->conf.MemoryPoolBytes / (uint64_t(C->nwaves) * wave_page));
+  target = uint32_t(std::min<uint64_t>(target, cap));
+  if (target <= C->rpages) return 0;
+  // the pool rows go (their pages now live in the layout), then the old layout
+  for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
+  C->pool_chunks.clear();
+  C->pool_free.clear();
+  C->pool_bytes = 0;
+  C->pool_used = false;
+  std::fill(C->pt_host.begin(), C->pt_host.end(), 0ull);
+  std::fill(C->pt_n.begin(), C->pt_n.end(), 0u);
+  if (!C->pt_host.empty() && !C->hip_ok(hipMemset(C->ptab.ptr, 0, C->pt_host.size() * 8), "page table"))
+    return kRuntimeError;
+  C->pt_dirty = false;
+  if (!C->mem.alloc(size_t(C->nwaves) * (size_t(target) << 14) * 64 + 64)) {
+    (void)hipGetLastError();   // (no room after all: the layout it had)
+    if (!C->mem.alloc(size_t(C->nwaves) * C->mem_words * 64 + 64))
+      return C->fail(kRuntimeError, "device allocation of the memory layout failed");
+    C->mem_fresh = true;
+    return 0;
+  }
+  C->rpages = target;
+  C->mem_words = target << 14;
+  C->grow_host = C->mem_max_pages > target;
+  C->mem_fresh = true;   // (this Reset writes every page of the new layout)
+  return 0;
+}
+
 // One interpreter launch over every instance: entry_pc with the staged params (or the
 // start function when is_start). Shared by BatchRun and BatchReset.
 uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, bool resume,
@@ -468,7 +465,6 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.ptab = C->pt_w ? C->ptab.ptr : nullptr;
   k.ptab_w = C->pt_w;
   k.grow_host = C->grow_host ? 1u : 0u;
-  k.vcommit = C->vmm ? C->vcommit.ptr : nullptr;
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
   k.init_dropped = C->init_dropped;
@@ -572,7 +568,7 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   if (C->stop_dirty.exchange(false) &&
       !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
-  if (e || !(C->prog.n_imported || C->grow_host || C->vmm)) return e;
+  if (e || !(C->prog.n_imported || C->grow_host)) return e;
   for (;;) {
     // every round resumes the lanes the host serviced; lanes it ended keep its code
     const int64_t k = service_host_calls(C);
@@ -691,17 +687,13 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
     if (e) return R(e);
     C->trial = C->trial == 2 ? 3 : 0;
   }
-  // the whole reserved layout: pages a lane grows into within it must read zero (a
-  // virtual-memory layout: the write-mark path stays below each wave's marks, which its
-  // committed rows cover; a full init covers the rows every wave has, and the rows a wave
-  // committed past them are zeroed apart, below)
-  const uint32_t init_words = C->vmm && C->mem_fresh ? C->vm_commit0 << 14 : C->mem_words;
-  if (C->vmm && C->mem_fresh)
-    for (uint32_t w = 0; w < C->nwaves; w++)
-      if (C->vcommit_h[w] > C->vm_commit0 &&
-          !C->hip_ok(hipMemsetAsync(C->mem.ptr + (size_t(w) * C->mem_words + (size_t(C->vm_commit0) << 14)) * 64, 0,
-                                    size_t(C->vcommit_h[w] - C->vm_commit0) << 22, C->stream), "vm rows"))
-        return R(kRuntimeError);
+  // lanes grew into pool rows: the layout takes every page they reached (grow_layout)
+  if (C->grow_host && C->pool_used) {
+    const uint8_t e = grow_layout(C);
+    if (e) return R(e);
+  }
+  // the whole reserved layout: pages a lane grows into within it must read zero
+  const uint32_t init_words = C->mem_words;
   (void)hipEventRecord(C->ev0, C->stream);
   if (!pool_reset(C)) return R(kRuntimeError);
   // after a run the memory kernel's write-mark path resets the instance state as well
@@ -867,6 +859,11 @@ const char *WasmEdge_BatchGetEngine(const WasmEdge_BatchContext *C) {
   if (C->conf.CostLimit) e += "+metered";
   C->engine_desc = e;
   return C->engine_desc.c_str();
+}
+
+uint32_t WasmEdge_BatchGetReservedPages(const WasmEdge_BatchContext *C) {
+  if (C && !C->shards.empty()) return WasmEdge_BatchGetReservedPages(wbm::first(C));
+  return C ? C->rpages : 0;
 }
 
 uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *C) {
@@ -1181,7 +1178,6 @@ void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   if (C->ev1) (void)hipEventDestroy(C->ev1);
   hipStream_t s = C->stream;
   for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
-  if (C->vmm) wbh::vm_release(C);
   delete C;
   if (s) (void)hipStreamDestroy(s);
 }

@@ -154,6 +154,8 @@ struct WasmEdge_BatchContext {
   // memory.grow past its wave's rows (hostcall.cpp serve_grows) -- the batched
   // Allocator::resize (lib/system/allocator.cpp:101-129), which commits pages on demand.
   uint32_t rpages = 0;
+  uint32_t rpages0 = 0;              // rpages at BatchCreate (grow_layout bounds the growth
+                                     // past it by MemoryPoolBytes)
   bool grow_host = false;            // the module can grow past rpages
   uint32_t pt_w = 0;                 // page-table width: pool pages per wave it can name
   std::vector<uint64_t> pt_host;     // [nwaves][pt_w] row device addresses (0: none)
@@ -164,28 +166,9 @@ struct WasmEdge_BatchContext {
   std::vector<std::pair<void *, size_t>> pool_chunks;   // (base, bytes), freed at Delete
   size_t pool_bytes = 0;             // bytes of chunks allocated
   bool pool_used = false;            // rows were handed out since the last Reset
-  // Virtual-memory layout (batch_api.cpp vm_setup; MI355X-native form of the reference's
-  // mmap'd reservation committed on demand, lib/system/allocator.cpp:60-142): `mem` is a VA
-  // range of rpages pages per lane, wave w's first vcommit_h[w] pages backed by device
-  // memory, each 4 MiB row (a page of the wave's 64 lanes) mapped once and kept until
-  // Delete. Every engine addresses every page below rpages directly (no page table), so a
-  // grown page costs what an initial one does; only the commit itself is the host's.
-  bool vmm = false;
-  size_t va_bytes = 0;                 // the reservation
-  uint32_t vm_commit0 = 0;             // pages every wave has from the start
-  std::vector<uint32_t> vcommit_h;     // [nwaves] committed pages per wave
-  DevBuf<uint32_t> vcommit;            // its device copy (KParams::vcommit)
-  bool vcommit_dirty = false;
-  struct VmMap { void *at; size_t bytes; hipMemGenericAllocationHandle_t h; };
-  std::vector<VmMap> vm_maps;          // every mapping, unmapped and released at Delete
-  size_t vm_grown_bytes = 0;           // committed past vm_commit0 (counts to MemoryPoolBytes)
-  size_t max_pitch = 0;                // hipDeviceAttributeMaxPitch (RoundCache 2D copies)
-  // words of every lane addressable directly at `mem` in every wave (the host views' rows)
-  uint64_t direct_words() const { return vmm ? uint64_t(vm_commit0) << 14 : mem_words; }
   // device address of word-row `word` (a multiple of 64) of wave `wave`: that word of its
   // 64 lanes, and the rows after it up to the end of its page; nullptr past the wave's rows
   uint32_t *wave_rows(uint32_t wave, uint64_t word) const {
-    if (vmm && word < mem_words && (word >> 14) >= vcommit_h[wave]) return nullptr;
     if (word < mem_words) return mem.ptr + (size_t(wave) * mem_words + word) * 64;
     const uint64_t k = (word >> 14) - rpages;
     if (k >= pt_w) return nullptr;
@@ -316,11 +299,6 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
 // pool rows (hostcall.cpp): give wave `wave` rows up to `rows` pool pages (false: no
 // device memory for all of them; it keeps what it got); return every row at Reset
 bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows);
-// virtual-memory layout (hostcall.cpp): commit wave `wave`'s pages up to `pages` (zeroed,
-// mapped, readable and writable by the device; false: out of device memory or past
-// MemoryPoolBytes, keeping what it got); unmap and release everything and the VA range
-bool vm_commit(WasmEdge_BatchContext *C, uint32_t wave, uint32_t pages);
-void vm_release(WasmEdge_BatchContext *C);
 bool pool_reset(WasmEdge_BatchContext *C);
 bool pool_upload(WasmEdge_BatchContext *C);
 int64_t service_host_calls(WasmEdge_BatchContext *C);

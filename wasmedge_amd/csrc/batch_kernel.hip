@@ -690,19 +690,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
 #define SLOW_IF(c) ((void)0)
 #define HOST_YIELD(f, base) do { status = WB_ERR_HOST_CALL; ycall = (f); ybase = (base); } while (0)
 #define MEM_BYTES ((uint64_t)slow_pages << 16)
-      // memory.grow (dbc_step.inc): within the pages its wave has -- the reserved layout's,
-      // the committed ones of a virtual-memory layout (KParams::vcommit), then the wave's pool
-      // rows -- it completes here; past them the lane parks for the host (hostcall.cpp grow
-      // service)
+      // memory.grow (dbc_step.inc): within the reserved pages or the wave's pool rows it
+      // completes here; past them the lane parks for the host (hostcall.cpp grow service)
 #define WB_GROW(cur, n, res) do { const uint32_t _np = (cur) + (n); \
-    const uint32_t _w = __builtin_amdgcn_readfirstlane(inst >> 6); \
-    const uint32_t _dp = p.vcommit ? p.vcommit[_w] : p.rpages; \
-    if (_np <= _dp) { \
-      if (PG) LS_PAGES_REF = _np; \
-      pages = min(_np, p.rpages); res = (cur); \
-    } else if (PG && _dp >= p.rpages && _np - 1u - p.rpages < p.ptab_w && \
-               p.ptab[(size_t)_w * p.ptab_w + _np - 1u - p.rpages] != 0) { \
-      LS_PAGES_REF = _np; pages = p.rpages; res = (cur); \
+    if (!PG) { pages = _np; res = (cur); } \
+    else if (_np <= p.rpages || (_np - 1u - p.rpages < p.ptab_w && \
+        p.ptab[(size_t)__builtin_amdgcn_readfirstlane(inst >> 6) * p.ptab_w + _np - 1u - p.rpages] != 0)) { \
+      LS_PAGES_REF = _np; pages = min(_np, p.rpages); res = (cur); \
     } else { res = (n); HOST_YIELD(WB_GROW_CALL, C_); } } while (0)
       const uint32_t pcs = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(slowmask));
       const uint32_t slow_pages = MEM_PAGES;   // the memory size (past the reserved layout too)

@@ -17,8 +17,6 @@
 // thread), so host functions must be reentrant, as the reference's are under its
 // concurrent VM::execute (include/vm/vm.h:137-141).
 #include <algorithm>
-#include <cstdio>
-#include <cstdlib>
 #include <atomic>
 #include <thread>
 
@@ -33,10 +31,8 @@ void RoundCache::mark_dirty(uint32_t b) {
 
 uint32_t *RoundCache::get(uint32_t b, uint32_t wave, bool *fail) {
   if (wave < w0 || wave >= w0 + nw) return nullptr;
-  // pool pages sit at a different address per wave: left to the per-wave blocks; so is the
-  // whole virtual-memory layout (hipMemcpy2D refuses its mapped ranges -- "invalid
-  // argument" at any pitch, tools/ubench/vmm.hip -- while 1D copies work)
-  if (C->vmm || uint64_t(b + 1) * kRowWords > C->direct_words()) return nullptr;
+  // pool pages sit at a different address per wave: left to the per-wave blocks
+  if (uint64_t(b + 1) * kRowWords > C->mem_words) return nullptr;
   Row *r;
   {
     std::lock_guard<std::mutex> lock(mu);
@@ -181,81 +177,6 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
   return 0;
 }
 
-// ---- the virtual-memory layout (batch_ctx.h) -------------------------------------------
-// Commit wave `wave`'s pages [vcommit_h[wave], pages): one device allocation for the range,
-// mapped at its place in the wave's VA, read-write for the device, zeroed (a fresh page reads
-// zero, as the reference's MAP_ANONYMOUS pages do). The device copy of the counts is
-// uploaded by the caller (vcommit_dirty).
-static bool vm_dbg() {
-  static const bool on = getenv("WB_VMM_DEBUG") != nullptr;
-  return on;
-}
-static bool vm_fail(const char *what, hipError_t e) {
-  if (vm_dbg()) fprintf(stderr, "[vmm] %s: %s\n", what, hipGetErrorString(e));
-  (void)hipGetLastError();
-  return false;
-}
-
-bool vm_commit(WasmEdge_BatchContext *C, uint32_t wave, uint32_t pages) {
-  uint32_t &have = C->vcommit_h[wave];
-  if (vm_dbg()) fprintf(stderr, "[vmm] commit wave %u: %u -> %u pages\n", wave, have, pages);
-  if (pages <= have) return true;
-  const size_t bytes = size_t(pages - have) << 22;
-  if (C->conf.MemoryPoolBytes && have >= C->vm_commit0 &&
-      C->vm_grown_bytes + C->pool_bytes + bytes > C->conf.MemoryPoolBytes)
-    return false;
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = C->device;
-  hipMemGenericAllocationHandle_t h;
-  hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
-  if (e != hipSuccess) return vm_fail("hipMemCreate", e);
-  void *at = C->mem.ptr + (size_t(wave) * C->mem_words + (size_t(have) << 14)) * 64;
-  if ((e = hipMemMap(at, bytes, 0, h, 0)) != hipSuccess) {
-    (void)hipMemRelease(h);
-    return vm_fail("hipMemMap", e);
-  }
-  hipMemAccessDesc acc = {};
-  acc.location = prop.location;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  // access over the wave's whole committed range, not the new mapping alone: the runtime
-  // refuses a range that starts where another mapping ends ("invalid argument", at random;
-  // tools/ubench/vmm.hip strategy S2 is the form that held on every try)
-  void *wave_base = C->mem.ptr + size_t(wave) * C->mem_words * 64;
-  if ((e = hipMemSetAccess(wave_base, size_t(pages) << 22, &acc, 1)) != hipSuccess ||
-      (e = hipMemsetAsync(at, 0, bytes, C->stream)) != hipSuccess) {
-    (void)hipMemUnmap(at, bytes);
-    (void)hipMemRelease(h);
-    return vm_fail("hipMemSetAccess / hipMemsetAsync", e);
-  }
-  C->vm_maps.push_back(WasmEdge_BatchContext::VmMap{at, bytes, h});
-  if (have >= C->vm_commit0) C->vm_grown_bytes += bytes;
-  have = pages;
-  C->vcommit_dirty = true;
-  return true;
-}
-
-void vm_release(WasmEdge_BatchContext *C) {
-  if (C->stream) (void)hipStreamSynchronize(C->stream);
-  for (const auto &m : C->vm_maps) {
-    (void)hipMemUnmap(m.at, m.bytes);
-    (void)hipMemRelease(m.h);
-  }
-  C->vm_maps.clear();
-  if (C->mem.ptr && C->va_bytes) (void)hipMemAddressFree(C->mem.ptr, C->va_bytes);
-  C->mem.ptr = nullptr;   // (DevBuf must not hipFree a VA reservation)
-  C->va_bytes = 0;
-  C->vmm = false;
-}
-
-bool vm_upload(WasmEdge_BatchContext *C) {
-  if (!C->vcommit_dirty) return true;
-  C->vcommit_dirty = false;
-  return C->hip_ok(hipMemcpy(C->vcommit.ptr, C->vcommit_h.data(), C->vcommit_h.size() * 4, hipMemcpyHostToDevice),
-                   "committed pages");
-}
-
 // ---- pool rows for pages past the reserved layout ------------------------------------
 // A row = one pool page of a wave: 64 lanes x 64 KiB, interleaved like the reserved layout.
 constexpr size_t kRowBytes = size_t(64) << 16;
@@ -267,8 +188,7 @@ static bool pool_chunk(WasmEdge_BatchContext *C, size_t want) {
   size_t rows = std::max<size_t>(want, std::min<size_t>(256, std::max<size_t>(16, C->pool_bytes / kRowBytes / 4)));
   const size_t cap = C->conf.MemoryPoolBytes;
   if (cap) {   // within the cap: what is left of it, if that covers `want`
-    const size_t used = C->pool_bytes + C->vm_grown_bytes;   // (grown VM pages count too)
-    const size_t left = used < cap ? (cap - used) / kRowBytes : 0;
+    const size_t left = C->pool_bytes < cap ? (cap - C->pool_bytes) / kRowBytes : 0;
     if (left < want) return false;
     rows = std::min(rows, left);
   }
@@ -352,39 +272,11 @@ static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &p
                         std::vector<uint32_t> &hcall, std::vector<uint32_t> &hbuf,
                         std::vector<uint32_t> &pages, bool *pages_dirty, int64_t *resumed) {
   const uint32_t hb = C->hb_cells, R = C->rpages;
-  if (C->vmm) {
-    // the virtual-memory layout: per wave, its pages up to the largest request (a quarter of
-    // what it has as slack, so that a lane growing page by page parks rarely), within the
-    // VA range; what lies past it comes from pool rows below
-    // When the device (or MemoryPoolBytes) cannot give a wave all of it, the largest
-    // request that fits is committed, so the lanes that need fewer pages still get them.
-    std::vector<std::pair<uint32_t, uint32_t>> req;   // (wave, pages), largest first per wave
-    for (uint32_t i : parked)
-      if (hcall[i] == WB_GROW_CALL)
-        req.emplace_back(i / 64, std::min(R, pages[i] + hbuf[size_t(i) * hb]));
-    std::sort(req.begin(), req.end(), [](const std::pair<uint32_t, uint32_t> &a, const std::pair<uint32_t, uint32_t> &b) {
-      return a.first != b.first ? a.first < b.first : a.second > b.second;
-    });
-    for (size_t k = 0; k < req.size();) {
-      const uint32_t w = req[k].first, have = C->vcommit_h[w];
-      size_t e = k;
-      while (e < req.size() && req[e].first == w) e++;
-      if (req[k].second > have) {
-        const uint32_t slack = std::min(R, std::max(req[k].second, have + std::max<uint32_t>(4, have / 4)));
-        if (!vm_commit(C, w, slack))
-          for (size_t q = k; q < e && req[q].second > have; q++)
-            if (vm_commit(C, w, req[q].second)) break;
-      }
-      k = e;
-    }
-  }
   // per wave, the lanes' requests smallest first: when the device runs out, the lanes
   // that need fewer pages still get them
   std::vector<std::pair<uint32_t, uint32_t>> need;   // (wave, rows)
   for (uint32_t i : parked)
-    if (hcall[i] == WB_GROW_CALL && pages[i] + hbuf[size_t(i) * hb] > R &&
-        (!C->vmm || C->vcommit_h[i / 64] >= R))
-      need.emplace_back(i / 64, pages[i] + hbuf[size_t(i) * hb] - R);
+    if (hcall[i] == WB_GROW_CALL) need.emplace_back(i / 64, pages[i] + hbuf[size_t(i) * hb] - R);
   std::sort(need.begin(), need.end());
   const uint32_t room = C->mem_max_pages - R;
   for (size_t k = 0; k < need.size(); k++) {
@@ -398,12 +290,7 @@ static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &p
     if (hcall[i] != WB_GROW_CALL) continue;
     const uint32_t n = hbuf[size_t(i) * hb];
     uint32_t &res = hbuf[size_t(i) * hb];
-    // the pages exist: all within the wave's committed pages, or (past the VA range, or no
-    // virtual-memory layout) every page below R backed and the rest in the wave's pool rows
-    const uint32_t direct = C->vmm ? C->vcommit_h[i / 64] : R;
-    if (vm_dbg() && i % 64 < 2)
-      fprintf(stderr, "[vmm] lane %u: %u pages + %u, wave has %u (R %u)\n", i, pages[i], n, direct, R);
-    if (pages[i] + n <= direct || (direct >= R && pages[i] + n - R <= C->pt_n[i / 64])) {
+    if (pages[i] + n - R <= C->pt_n[i / 64]) {
       res = pages[i];
       pages[i] += n;
       *pages_dirty = true;
@@ -475,9 +362,9 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
   int64_t grown = 0;
   std::vector<uint8_t> hcall_grow(parked.size(), 0);
   for (size_t j = 0; j < parked.size(); j++) hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL;
-  if (C->grow_host || C->vmm) {
+  if (C->grow_host) {
     serve_grows(C, parked, hcall, hbuf, pages, &pages_dirty, &grown);
-    if (!pool_upload(C) || !vm_upload(C)) return -1;
+    if (!pool_upload(C)) return -1;
   }
   RoundCache rc;
   rc.C = C;
@@ -499,7 +386,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
       view.hwm = &hwm[size_t(view.wave) * 64];
       for (uint32_t j = waves[k].second; j < waves[k + 1].second; j++) {
         const uint32_t i = parked[j], f = hcall[i];
-        if ((C->grow_host || C->vmm) && hcall_grow[j]) continue;   // (served above)
+        if (C->grow_host && hcall_grow[j]) continue;   // (served above)
         const WasmEdge_BatchContext::HostFn h =
             f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
         if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1

@@ -94,12 +94,6 @@ struct KParams {
                                 // core, whose compiled runs schedule the lanes among
                                 // themselves (jit.cpp Lsched); the C++ loop only serves
                                 // what the core leaves to it
-  // Virtual-memory linear memory (batch_api.cpp vm_*): `mem` is a VA reservation of rpages
-  // pages per lane, of which wave w has its first vcommit[w] pages backed by device memory
-  // (committed in 4 MiB rows: one page of the wave's 64 lanes). A memory.grow within them
-  // completes in the kernel; past them the lane parks for the host to commit more. NULL:
-  // every page below rpages is backed.
-  const uint32_t *vcommit;
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
