@@ -158,10 +158,14 @@ def test_gpu_grow_default_config(built):
 
 
 @pytest.mark.gpu
-def test_gpu_grow_through_the_pool(built):
-    """The same with two reserved pages: every grown page comes from the device pool
-    (lanes park at memory.grow, the host commits rows, the page table widens), over two
-    waves; bit-exact against the oracle, and again after a Reset."""
+@pytest.mark.parametrize("relayout", ["1", "0"])
+def test_gpu_grow_through_the_pool(built, monkeypatch, relayout):
+    """The same with two reserved pages: lanes park at memory.grow and the host gives them
+    the pages -- by growing the reserved layout (relayout 1: the old rows copied over, every
+    engine then addresses the grown pages directly) or from the device pool (WB_RELAYOUT=0:
+    rows through the page table, which widens) -- over two waves; bit-exact against the
+    oracle, and again after a Reset."""
+    monkeypatch.setenv("WB_RELAYOUT", relayout)
     wasm = grow_wasm()
     rows = rows_for(128, 1200, mult=419)
     _gpu_grow(wasm, rows, oracle_rows(wasm, rows), memory_reserve_pages=2)
@@ -169,14 +173,16 @@ def test_gpu_grow_through_the_pool(built):
 
 @pytest.mark.gpu
 def test_gpu_layout_takes_the_grown_pages(built):
-    """A run whose lanes grow past the reserved layout (two pages, pool rows past them):
-    the next Reset re-lays memory with every page they reached in the reserved layout
-    (WasmEdge_BatchGetReservedPages), where every engine addresses it directly; the run
-    after it is bit-exact again, and a fixed layout (WB_RELAYOUT=0) gives the same."""
+    """Lanes that grow past the reserved layout (two pages): the service round grows the
+    layout to every page they ask for (WasmEdge_BatchGetReservedPages), where every engine
+    addresses it directly; bit-exact on every run, across Resets. With the growth done in
+    the run, a Reset after a pool-served run (WB_RELAYOUT=0 for the first run) re-lays memory
+    with the pages the lanes reached."""
     from wasmedge_amd import batch
     wasm = grow_wasm()
     rows = rows_for(128, 300, mult=419)
     ref = oracle_rows(wasm, rows)
+    top = 1 + max(r[0] for r in rows)
     ctx = batch.BatchContext(wasm, len(rows), device=0, memory_reserve_pages=2)
     try:
         vals = batch.make_values(rows, [I32, I32])
@@ -186,8 +192,25 @@ def test_gpu_layout_takes_the_grown_pages(built):
             ints = batch.ret_ints(rets)
             got = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
             assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == [], rep
+            assert ctx.reserved_pages() >= top, rep
             ctx.reset()
-            assert ctx.reserved_pages() == 1 + max(r[0] for r in rows), rep
+    finally:
+        ctx.close()
+    os.environ["WB_RELAYOUT"] = "0"
+    try:
+        ctx = batch.BatchContext(wasm, len(rows), device=0, memory_reserve_pages=2)
+        vals = batch.make_values(rows, [I32, I32])
+        rets, st, cnt = ctx.execute("grow", vals, 1)
+        assert ctx.reserved_pages() == 2
+    finally:
+        del os.environ["WB_RELAYOUT"]
+    try:
+        ctx.reset()   # (the pool-served run's pages: the Reset takes them into the layout)
+        assert ctx.reserved_pages() == top
+        rets, st, cnt = ctx.execute("grow", vals, 1)
+        ints = batch.ret_ints(rets)
+        got = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
+        assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == []
     finally:
         ctx.close()
 

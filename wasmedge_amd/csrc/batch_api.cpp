@@ -364,60 +364,6 @@ uint8_t layout_trial(WasmEdge_BatchContext *C, double secs) {
 
 uint32_t cells_of_value(uint8_t t) { return wb::cells_of(t); }
 
-// The reserved layout grown to what the instances reached (at a Reset after a run whose
-// lanes grew into pool rows): every page up to the batch's largest memory then sits in the
-// reserved layout, where every engine addresses it directly -- a module that memory.grows
-// runs its later invocations at full speed, and only the first pays the per-lane step's
-// page-table path (DESIGN.md "Paged growth"). Bounded by 3/4 of the device memory this
-// context holds or could get, and by MemoryPoolBytes past the initial layout;
-// WB_RELAYOUT=0 keeps the layout fixed (A/B aid). Reset rewrites every page anyway
-// (mem_fresh), so results never depend on it.
-uint8_t grow_layout(WasmEdge_BatchContext *C) {
-  if (const char *e = getenv("WB_RELAYOUT"))
-    if (e[0] == '0') return 0;
-  if (!C->settle()) return kRuntimeError;
-  const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
-  std::vector<uint32_t> pages(size_t(C->nwaves) * 64);
-  if (!C->hip_ok(hipMemcpy2D(pages.data(), row, C->lstate.ptr + LS_PAGES * 64, pitch, row, C->nwaves,
-                             hipMemcpyDeviceToHost), "pages"))
-    return kRuntimeError;
-  uint32_t target = 0;
-  for (uint32_t i = 0; i < C->n; i++) target = std::max(target, pages[i]);
-  target = std::min(target, C->mem_max_pages);
-  const uint64_t wave_page = uint64_t(64) << 16;   // one page of a wave's 64 lanes
-  size_t free_b = 0, total_b = 0;
-  (void)hipMemGetInfo(&free_b, &total_b);
-  const uint64_t held = uint64_t(C->nwaves) * C->rpages * wave_page + C->pool_bytes;
-  uint64_t cap = (uint64_t(free_b) + held) / 4 * 3 / (uint64_t(C->nwaves) * wave_page);
-  if (C->conf.MemoryPoolBytes)
-    cap = std::min<uint64_t>(cap, C->rpages0 + C->conf.MemoryPoolBytes / (uint64_t(C->nwaves) * wave_page));
-  target = uint32_t(std::min<uint64_t>(target, cap));
-  if (target <= C->rpages) return 0;
-  // the pool rows go (their pages now live in the layout), then the old layout
-  for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
-  C->pool_chunks.clear();
-  C->pool_free.clear();
-  C->pool_bytes = 0;
-  C->pool_used = false;
-  std::fill(C->pt_host.begin(), C->pt_host.end(), 0ull);
-  std::fill(C->pt_n.begin(), C->pt_n.end(), 0u);
-  if (!C->pt_host.empty() && !C->hip_ok(hipMemset(C->ptab.ptr, 0, C->pt_host.size() * 8), "page table"))
-    return kRuntimeError;
-  C->pt_dirty = false;
-  if (!C->mem.alloc(size_t(C->nwaves) * (size_t(target) << 14) * 64 + 64)) {
-    (void)hipGetLastError();   // (no room after all: the layout it had)
-    if (!C->mem.alloc(size_t(C->nwaves) * C->mem_words * 64 + 64))
-      return C->fail(kRuntimeError, "device allocation of the memory layout failed");
-    C->mem_fresh = true;
-    return 0;
-  }
-  C->rpages = target;
-  C->mem_words = target << 14;
-  C->grow_host = C->mem_max_pages > target;
-  C->mem_fresh = true;   // (this Reset writes every page of the new layout)
-  return 0;
-}
-
 // One interpreter launch over every instance: entry_pc with the staged params (or the
 // start function when is_start). Shared by BatchRun and BatchReset.
 uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, bool resume,
@@ -687,10 +633,18 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
     if (e) return R(e);
     C->trial = C->trial == 2 ? 3 : 0;
   }
-  // lanes grew into pool rows: the layout takes every page they reached (grow_layout)
+  // lanes grew into pool rows: the layout takes every page they reached (hostcall.cpp
+  // grow_layout; this Reset rewrites every page, so nothing is copied)
   if (C->grow_host && C->pool_used) {
-    const uint8_t e = grow_layout(C);
-    if (e) return R(e);
+    if (!C->settle()) return R(kRuntimeError);
+    const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+    std::vector<uint32_t> pages(size_t(C->nwaves) * 64);
+    if (!C->hip_ok(hipMemcpy2D(pages.data(), row, C->lstate.ptr + LS_PAGES * 64, pitch, row, C->nwaves,
+                               hipMemcpyDeviceToHost), "pages"))
+      return R(kRuntimeError);
+    uint32_t reached = 0;
+    for (uint32_t i = 0; i < C->n; i++) reached = std::max(reached, pages[i]);
+    if (!grow_layout(C, reached, reached, false)) return R(kRuntimeError);
   }
   // the whole reserved layout: pages a lane grows into within it must read zero
   const uint32_t init_words = C->mem_words;

@@ -300,6 +300,11 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
 // device memory for all of them; it keeps what it got); return every row at Reset
 bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows);
 bool pool_reset(WasmEdge_BatchContext *C);
+// grow the reserved layout to at least `need` pages per instance (up to `want`), within the
+// device memory and MemoryPoolBytes; live: keep the instances' memory (pool rows move into
+// the layout), else the next Reset rewrites it (mem_fresh). false only on a device error;
+// a layout that cannot grow stays as it was (true)
+bool grow_layout(WasmEdge_BatchContext *C, uint32_t need, uint32_t want, bool live);
 bool pool_upload(WasmEdge_BatchContext *C);
 int64_t service_host_calls(WasmEdge_BatchContext *C);
 uint64_t mem_size(const WasmEdge_BatchMemoryContext *M);   // bytes of the instance's memory

@@ -188,7 +188,9 @@ static bool pool_chunk(WasmEdge_BatchContext *C, size_t want) {
   size_t rows = std::max<size_t>(want, std::min<size_t>(256, std::max<size_t>(16, C->pool_bytes / kRowBytes / 4)));
   const size_t cap = C->conf.MemoryPoolBytes;
   if (cap) {   // within the cap: what is left of it, if that covers `want`
-    const size_t left = C->pool_bytes < cap ? (cap - C->pool_bytes) / kRowBytes : 0;
+    // (the reserved layout's growth past its initial size counts too: grow_layout)
+    const size_t used = C->pool_bytes + size_t(C->rpages - C->rpages0) * C->nwaves * kRowBytes;
+    const size_t left = used < cap ? (cap - used) / kRowBytes : 0;
     if (left < want) return false;
     rows = std::min(rows, left);
   }
@@ -263,6 +265,107 @@ bool pool_reset(WasmEdge_BatchContext *C) {
   return true;
 }
 
+// The reserved layout grown (DESIGN.md "Paged growth"): every page below the new rpages in
+// the lane-interleaved layout, where every engine -- compiled runs, threaded core, compiled
+// step -- addresses it directly, instead of pool rows that only the per-lane step reaches
+// through the page table. Grown between launches, when no lane runs: in a service round
+// (live: the old layout's rows and the pool rows are copied to their places in the new one,
+// device to device) or at a Reset (which rewrites every page anyway). Bounded by 3/4 of the
+// device memory this context holds or could get, and by MemoryPoolBytes past the initial
+// layout; WB_RELAYOUT=0 keeps the layout fixed (A/B aid). Results never depend on it.
+bool grow_layout(WasmEdge_BatchContext *C, uint32_t need, uint32_t want, bool live) {
+  if (const char *e = getenv("WB_RELAYOUT"))
+    if (e[0] == '0') return true;
+  need = std::min(need, C->mem_max_pages);
+  want = std::min(std::max(want, need), C->mem_max_pages);
+  if (need <= C->rpages) return true;
+  const uint64_t wave_page = uint64_t(64) << 16;   // one page of a wave's 64 lanes
+  const uint64_t per_page = uint64_t(C->nwaves) * wave_page;
+  size_t free_b = 0, total_b = 0;
+  (void)hipMemGetInfo(&free_b, &total_b);
+  // (live: the old layout and the pool stay until their rows are copied)
+  const uint64_t held = live ? 0 : uint64_t(C->rpages) * per_page + C->pool_bytes;
+  uint64_t cap = (uint64_t(free_b) + held) / 4 * 3 / per_page;
+  if (C->conf.MemoryPoolBytes) cap = std::min<uint64_t>(cap, C->rpages0 + C->conf.MemoryPoolBytes / per_page);
+  if (cap < need) return true;
+  const uint32_t target = uint32_t(std::min<uint64_t>(want, cap));
+  const size_t old_words = C->mem_words, new_words = size_t(target) << 14;
+  if (!live) {   // (the next Reset writes every page: drop the old layout first)
+    for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
+    C->pool_chunks.clear();
+    C->pool_free.clear();
+    C->pool_bytes = 0;
+    if (!C->mem.alloc(size_t(C->nwaves) * new_words * 64 + 64)) {
+      (void)hipGetLastError();   // (no room after all: the layout it had)
+      if (!C->mem.alloc(size_t(C->nwaves) * old_words * 64 + 64))
+        return C->hip_ok(hipErrorOutOfMemory, "memory layout");
+      C->pool_used = true;   // (its pool rows went with it: pool_reset restarts the table)
+      C->mem_fresh = true;
+      return true;
+    }
+    C->mem_fresh = true;
+  } else {
+    uint32_t *nm = nullptr;
+    if (hipMalloc(&nm, (size_t(C->nwaves) * new_words * 64 + 64) * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return true;
+    }
+    hipStream_t s = C->stream;
+    bool ok = hipMemsetAsync(nm, 0, (size_t(C->nwaves) * new_words * 64 + 64) * 4, s) == hipSuccess;
+    // each wave's rows of the old layout (one 2D copy while its pitches allow), then its
+    // pool rows as the pages after them
+    const bool one = new_words * 256 < (size_t(1) << 31);
+    if (ok && one)
+      ok = hipMemcpy2DAsync(nm, new_words * 256, C->mem.ptr, old_words * 256, old_words * 256, C->nwaves,
+                            hipMemcpyDeviceToDevice, s) == hipSuccess;
+    for (uint32_t w = 0; ok && w < C->nwaves; w++) {
+      if (!one)
+        ok = hipMemcpyAsync(nm + size_t(w) * new_words * 64, C->mem.ptr + size_t(w) * old_words * 64, old_words * 256,
+                            hipMemcpyDeviceToDevice, s) == hipSuccess;
+      for (uint32_t k = 0; ok && k < C->pt_n[w] && C->rpages + k < target; k++)
+        ok = hipMemcpyAsync(nm + (size_t(w) * new_words + (size_t(C->rpages + k) << 14)) * 64,
+                            reinterpret_cast<const void *>(C->pt_host[size_t(w) * C->pt_w + k]),
+                            size_t(1) << 22, hipMemcpyDeviceToDevice, s) == hipSuccess;
+    }
+    if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipFree(nm);
+      return C->hip_ok(hipGetLastError(), "memory layout copy");
+    }
+    (void)hipFree(C->mem.ptr);
+    C->mem.ptr = nm;
+    C->mem.n = size_t(C->nwaves) * new_words * 64 + 64;
+    // pool rows past the new layout (none when it covers every page the lanes hold) stay
+    const uint32_t moved = target - C->rpages;
+    bool any_left = false;
+    for (uint32_t w = 0; w < C->nwaves; w++) {
+      const uint32_t have = C->pt_n[w], keep = have > moved ? have - moved : 0;
+      for (uint32_t k = 0; k < keep; k++)
+        C->pt_host[size_t(w) * C->pt_w + k] = C->pt_host[size_t(w) * C->pt_w + moved + k];
+      for (uint32_t k = keep; k < have; k++) C->pt_host[size_t(w) * C->pt_w + k] = 0;
+      C->pt_n[w] = keep;
+      any_left |= keep != 0;
+    }
+    if (!any_left) {   // every row moved: the pool goes
+      for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
+      C->pool_chunks.clear();
+      C->pool_free.clear();
+      C->pool_bytes = 0;
+      C->pool_used = false;
+    }
+    C->pt_dirty = true;
+  }
+  if (!C->pt_host.empty() && C->pool_bytes == 0) {
+    std::fill(C->pt_host.begin(), C->pt_host.end(), 0ull);
+    std::fill(C->pt_n.begin(), C->pt_n.end(), 0u);
+    C->pt_dirty = true;
+  }
+  C->rpages = target;
+  C->mem_words = uint32_t(new_words);
+  C->grow_host = C->mem_max_pages > target;
+  if (!live) C->pool_used = false;
+  return pool_upload(C);
+}
+
 // Lanes parked at a memory.grow past their wave's rows (WB_GROW_CALL; the request n in
 // their staged result cell): per wave, rows for the largest request (plus a quarter of what
 // the wave holds, so that a lane growing page by page parks rarely), then each lane's grow
@@ -271,12 +374,22 @@ bool pool_reset(WasmEdge_BatchContext *C) {
 static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &parked,
                         std::vector<uint32_t> &hcall, std::vector<uint32_t> &hbuf,
                         std::vector<uint32_t> &pages, bool *pages_dirty, int64_t *resumed) {
-  const uint32_t hb = C->hb_cells, R = C->rpages;
+  const uint32_t hb = C->hb_cells;
+  // first the reserved layout grows to take every request (with a quarter of slack, so a
+  // lane growing page by page rarely parks again): the grown pages then run on every engine
+  uint32_t top = 0;
+  for (uint32_t i : parked)
+    if (hcall[i] == WB_GROW_CALL) top = std::max(top, pages[i] + hbuf[size_t(i) * hb]);
+  for (uint32_t w = 0; w < C->nwaves; w++) top = std::max(top, C->rpages + C->pt_n[w]);
+  if (top > C->rpages)
+    (void)grow_layout(C, top, top + std::max<uint32_t>(4, top / 4), true);
+  const uint32_t R = C->rpages;
   // per wave, the lanes' requests smallest first: when the device runs out, the lanes
   // that need fewer pages still get them
   std::vector<std::pair<uint32_t, uint32_t>> need;   // (wave, rows)
   for (uint32_t i : parked)
-    if (hcall[i] == WB_GROW_CALL) need.emplace_back(i / 64, pages[i] + hbuf[size_t(i) * hb] - R);
+    if (hcall[i] == WB_GROW_CALL && pages[i] + hbuf[size_t(i) * hb] > R)
+      need.emplace_back(i / 64, pages[i] + hbuf[size_t(i) * hb] - R);
   std::sort(need.begin(), need.end());
   const uint32_t room = C->mem_max_pages - R;
   for (size_t k = 0; k < need.size(); k++) {
@@ -290,7 +403,7 @@ static void serve_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &p
     if (hcall[i] != WB_GROW_CALL) continue;
     const uint32_t n = hbuf[size_t(i) * hb];
     uint32_t &res = hbuf[size_t(i) * hb];
-    if (pages[i] + n - R <= C->pt_n[i / 64]) {
+    if (pages[i] + n <= R || pages[i] + n - R <= C->pt_n[i / 64]) {
       res = pages[i];
       pages[i] += n;
       *pages_dirty = true;
