@@ -182,7 +182,11 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   if (gb < 4 || gb > 128 || (gb & (gb - 1)))
     return C->fail(kRuntimeError, "MemoryGranule must be 0 or a power of two in [4, 128]");
   C->mlog = uint32_t(__builtin_ctz(gb)) - 2;
+  // the call stack: a fixed CallStackCells, or (0) 4096 cells that grow on demand
+  // (WB_STACK_GROW=0 keeps them fixed: A/B and test aid)
   C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
+  const char *sge = getenv("WB_STACK_GROW");
+  C->gs_grow = !C->conf.CallStackCells && !(sge && sge[0] == '0');
   // module image: active data segments over the initial pages
   std::vector<uint32_t> img;
   std::vector<uint8_t> pool;
@@ -304,7 +308,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
       (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
-      ((P.n_imported || C->grow_host) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
+      ((P.n_imported || C->grow_host || C->gs_grow) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
@@ -413,6 +417,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.grow_host = C->grow_host ? 1u : 0u;
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
+  k.gs_grow = C->gs_grow ? 1u : 0u;
   k.init_dropped = C->init_dropped;
   k.ls_slots = C->ls_slots;
   k.is_start = is_start ? 1u : 0u;
@@ -514,7 +519,7 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   if (C->stop_dirty.exchange(false) &&
       !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
-  if (e || !(C->prog.n_imported || C->grow_host)) return e;
+  if (e || !(C->prog.n_imported || C->grow_host || C->gs_grow)) return e;
   for (;;) {
     // every round resumes the lanes the host serviced; lanes it ended keep its code
     const int64_t k = service_host_calls(C);

@@ -146,6 +146,9 @@ struct WasmEdge_BatchContext {
   DevBuf<uint64_t> counts, hashes;
   uint32_t image_words = 0, init_dropped = 0, ls_drop_ext = 0;
   uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
+  // the call stack grows on demand (CallStackCells 0): a call past gs_depth parks, the host
+  // doubles the stack (grow_stack) while device memory allows (KParams::gs_grow)
+  bool gs_grow = false;
   // Paged linear memory (DESIGN.md "Linear memory"): `mem_max_pages` is the page limit
   // (65536, the module's max, MaxMemoryPage); pages [0, rpages) of every lane live in the
   // reserved layout at `mem` (mem_words = rpages * 16384 words per lane), page q >= rpages
@@ -300,6 +303,10 @@ uint8_t mem_rw(WasmEdge_BatchContext *C, uint32_t Inst, uint32_t Off, uint32_t L
 // device memory for all of them; it keeps what it got); return every row at Reset
 bool pool_reserve(WasmEdge_BatchContext *C, uint32_t wave, uint32_t rows);
 bool pool_reset(WasmEdge_BatchContext *C);
+// the call stack grown to hold `need` cells per lane (at least twice its size; between
+// launches, its contents copied); false: no device memory for it (the caller then stops
+// growing it: calls past it trap 0xB0 as with a fixed CallStackCells)
+bool grow_stack(WasmEdge_BatchContext *C, uint64_t need);
 // grow the reserved layout to at least `need` pages per instance (up to `want`), within the
 // device memory and MemoryPoolBytes; live: keep the instances' memory (pool rows move into
 // the layout), else the next Reset rewrites it (mem_fresh). false only on a device error;

@@ -712,6 +712,19 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
       // limit it fails with CostLimitExceeded before it executes. Here: the instructions
       // up to the main op first, then (if it did not trap) the ones after it, then a
       // taken branch's adjustment (gas_step in dbc_ops.h)
+      // a call past the call stack's cells while the stack may still grow (KParams::
+      // gs_grow; the reference's StackManager is a growing vector, stackmgr.h:44-47): the
+      // lane parks at the call for the host to grow the stack (hostcall.cpp grow_stack) and
+      // runs it again on resume -- counted and priced once, then
+      if (p.gs_grow && (op == OP_CALL || op == OP_CALL_INDIRECT) &&
+          gsp + ((w1 & 0xFFFFu) - p.global_cells) + 1 > p.gs_depth) {
+        status = WB_ERR_HOST_CALL;
+        ycall = WB_STACK_CALL;
+        ybase = p.global_cells;
+        add = 0;
+        npc = pcs;
+        goto s_done;
+      }
       if (p.cost_off && gas_step(p.cost_pool + coff, 0, cnt8 - post8, p.cost_limit, cost, add)) {
         status = 0x03u;
         goto s_done;

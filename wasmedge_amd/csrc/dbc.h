@@ -174,3 +174,7 @@ struct DFunc {
 // The import index a lane parks with when its memory.grow needs pool rows the host has not
 // allocated yet (KParams::grow_host): the host allocates them and completes the grow.
 #define WB_GROW_CALL 0xFFFFFFFEu
+// ... when a call would pass the call stack's reserved cells while the stack may still grow
+// (KParams::gs_grow): the host grows it and the lane runs the call again (hostcall.cpp
+// grow_stack)
+#define WB_STACK_CALL 0xFFFFFFFDu

@@ -366,6 +366,38 @@ bool grow_layout(WasmEdge_BatchContext *C, uint32_t need, uint32_t want, bool li
   return pool_upload(C);
 }
 
+// The call stack's HBM part doubled (at least), between launches: [wave][slot][64] at the
+// old depth copied into the new one (one 2D copy while its pitch allows), the old freed.
+// Bounded by 3/4 of the device memory left; false when that does not hold `need` cells.
+bool grow_stack(WasmEdge_BatchContext *C, uint64_t need) {
+  const uint64_t old_d = C->gs_depth;
+  uint64_t d = std::max<uint64_t>(old_d * 2, need);
+  size_t free_b = 0, total_b = 0;
+  (void)hipMemGetInfo(&free_b, &total_b);
+  const uint64_t per_cell = uint64_t(C->nwaves) * 256;   // one cell of every lane
+  const uint64_t cap = std::min<uint64_t>(uint64_t(free_b) / 4 * 3 / per_cell, 0x7FFFFFFFull / 256);
+  d = std::min(d, cap);
+  if (d <= old_d || d < need) return false;
+  uint32_t *ns = nullptr;
+  if (hipMalloc(&ns, size_t(C->nwaves) * d * 256) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  bool ok = hipMemcpy2DAsync(ns, d * 256, C->gstack.ptr, old_d * 256, old_d * 256, C->nwaves,
+                             hipMemcpyDeviceToDevice, C->stream) == hipSuccess &&
+            hipStreamSynchronize(C->stream) == hipSuccess;
+  if (!ok) {
+    (void)hipFree(ns);
+    (void)hipGetLastError();
+    return false;
+  }
+  (void)hipFree(C->gstack.ptr);
+  C->gstack.ptr = ns;
+  C->gstack.n = size_t(C->nwaves) * d * 64;
+  C->gs_depth = uint32_t(d);
+  return true;
+}
+
 // Lanes parked at a memory.grow past their wave's rows (WB_GROW_CALL; the request n in
 // their staged result cell): per wave, rows for the largest request (plus a quarter of what
 // the wave holds, so that a lane growing page by page parks rarely), then each lane's grow
@@ -474,10 +506,33 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
   bool pages_dirty = false;
   int64_t grown = 0;
   std::vector<uint8_t> hcall_grow(parked.size(), 0);
-  for (size_t j = 0; j < parked.size(); j++) hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL;
+  for (size_t j = 0; j < parked.size(); j++)
+    hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL || hcall[parked[j]] == WB_STACK_CALL;
   if (C->grow_host) {
     serve_grows(C, parked, hcall, hbuf, pages, &pages_dirty, &grown);
     if (!pool_upload(C)) return -1;
+  }
+  // calls past the call stack (WB_STACK_CALL): the stack doubles (or takes what the deepest
+  // parked lane needs), every such lane runs its call again -- or, with no device memory
+  // left for it, the stack stops growing and the call traps 0xB0 as with a fixed size
+  if (C->gs_grow) {
+    bool any = false;
+    for (uint32_t i : parked) any |= hcall[i] == WB_STACK_CALL;
+    if (any) {
+      std::vector<uint32_t> gsp(size_t(nw) * 64, 0);
+      if (!C->hip_ok(hipMemcpy2D(gsp.data(), row, C->lstate.ptr + LS_GSP * 64, pitch, row, nw,
+                                 hipMemcpyDeviceToHost), "call stack depth"))
+        return -1;
+      uint64_t need = 0;
+      for (uint32_t i : parked)
+        if (hcall[i] == WB_STACK_CALL) need = std::max<uint64_t>(need, uint64_t(gsp[i]) + C->prog.total_cells() + 1);
+      if (!grow_stack(C, need)) C->gs_grow = false;
+      for (uint32_t i : parked)
+        if (hcall[i] == WB_STACK_CALL) {
+          hcall[i] = 0;   // (no result cells: the call runs again)
+          grown++;
+        }
+    }
   }
   RoundCache rc;
   rc.C = C;

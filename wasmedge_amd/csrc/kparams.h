@@ -94,6 +94,8 @@ struct KParams {
                                 // core, whose compiled runs schedule the lanes among
                                 // themselves (jit.cpp Lsched); the C++ loop only serves
                                 // what the core leaves to it
+  uint32_t gs_grow;             // 1: a call past gs_depth parks for the host to grow the call
+                                // stack (WB_STACK_CALL) instead of trapping 0xB0
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
