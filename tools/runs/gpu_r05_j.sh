@@ -8,7 +8,7 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-300)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
-step tests 600 python -u -m pytest tests/test_memgrow.py tests/test_deepstack.py tests/test_layout.py tests/test_hostcall.py tests/test_limits.py tests/test_scalar.py tests/test_depth_pick.py -m gpu -v --timeout 300 --timeout-method thread
+step tests 600 python -u -m pytest tests/test_deepstack.py tests/test_hostcall.py tests/test_hostcost.py -m gpu -v --timeout 300 --timeout-method thread
 step c3gk 300 python bench.py --workload c3grow --elements 4096 --steps 3 --warmup 3 --no-cpu-baseline
 step c3g 600 python bench.py --workload c3grow --steps 2 --warmup 3 --no-cpu-baseline
 echo all done

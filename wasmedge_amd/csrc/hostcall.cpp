@@ -554,7 +554,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
       view.hwm = &hwm[size_t(view.wave) * 64];
       for (uint32_t j = waves[k].second; j < waves[k + 1].second; j++) {
         const uint32_t i = parked[j], f = hcall[i];
-        if (C->grow_host && hcall_grow[j]) continue;   // (served above)
+        if (hcall_grow[j]) continue;   // (memory.grow and call-stack growth: served above)
         const WasmEdge_BatchContext::HostFn h =
             f < C->hosts.size() ? C->hosts[f] : WasmEdge_BatchContext::HostFn{};
         if (!h.fn) { hcall[i] = 0xFFFFFFFFu; continue; }   // no host function: stays 0xB1
