@@ -68,7 +68,12 @@ typedef struct WasmEdge_BatchConfigure {
    * whose initial size exceeds a non-zero limit fails WasmEdge_BatchCreate with
    * MemoryOutOfBounds (0x88): the reference allocates no memory for it (memory.h:46-51). */
   uint32_t MaxMemoryPage;
-  /* Device call-stack depth per instance in 32-bit cells (0 = 4096). */
+  /* Device call-stack depth per instance in 32-bit cells. 0 (the default): the stack
+   * starts at 4096 cells and grows on demand, as the reference's StackManager vectors do
+   * (include/runtime/stackmgr.h:44-47) -- a call past it parks the instance, the stack
+   * doubles between launches and the call runs again (counted once); only when the device
+   * has no memory left for it does a call end the instance with 0xB0. Non-zero: a fixed
+   * bound, 0xB0 past it. */
   uint32_t CallStackCells;
   /* Instruction budget per instance (0 = unlimited; counted in the reference's
    * Statistics units; checked every scheduler round, and a device-side core call never
