@@ -339,6 +339,12 @@ struct Em {
   // escape (OUTSIDE s[76:77], ESC s[78:79]: the C++ step executes that instruction);
   // the other lanes go on (past the stage's end when none is left). Out of line.
   bool trip = false;
+  // Trip-mode load cache (trip_source): loads whose value a scan's exit left in a VGPR --
+  // pc -> {the cache's address VGPR, its value VGPR}: the load becomes a move (the lanes
+  // running this code matched the address first) -- and the address VGPRs every store
+  // invalidates (-1)
+  std::map<uint32_t, std::pair<uint32_t, uint32_t>> fwd;
+  std::vector<uint32_t> inval;
   std::string stage_end;   // label: the end of the run's current stage (EXEC = its lanes)
   int nleave = 0;
   std::string trip_leave() {
@@ -499,6 +505,15 @@ bool emit_load(Em &e, uint16_t op, uint32_t a, uint32_t c, uint32_t imm) {
     }
     return true;
   }
+  if (op == OP_LD32) {
+    const auto f = e.fwd.find(e.pc);
+    if (f != e.fwd.end()) {   // (trip load cache: these lanes' word is in the value VGPR)
+      e.sync({a, c});
+      if (e.group) group_check(e, *e.group);
+      e.l("v_mov_b32 %s, v%u", e.v(c), f->second.second);
+      return true;
+    }
+  }
   const char *ins = n == 1 ? (op == OP_LD8S32 || op == OP_LD8S64 ? "global_load_sbyte" : "global_load_ubyte")
                     : n == 2 ? (op == OP_LD16S32 || op == OP_LD16S64 ? "global_load_sshort" : "global_load_ushort")
                              : "global_load_dword";
@@ -535,6 +550,7 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const 
       e.l("global_store_dword %s, %s%s", w[q].substr(0, k).c_str(), e.v(b + q), w[q].substr(k).c_str());
       e.nvm++;
     }
+    for (uint32_t r : e.inval) e.l("v_mov_b32 v%u, -1", r);   // (trip load cache: stale now)
     return true;
   }
   std::string w1, w2;
@@ -547,6 +563,7 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const 
     e.l("global_store_dword %s, %s%s", w2.substr(0, k2).c_str(), e.v(b + 1), w2.substr(k2).c_str());
     e.nvm++;
   }
+  for (uint32_t r : e.inval) e.l("v_mov_b32 v%u, -1", r);   // (trip load cache: stale now)
   return true;
 }
 
@@ -2441,12 +2458,15 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
 // stage code that follows (exec = them; the stage ends at once when there are none).
 // Entered with EXEC = the run's lanes in this trip. Temporaries survive from stage A to
 // stage B per lane (other runs execute under disjoint EXEC masks).
+// slot: the run's load-cache VGPRs {address, value} (-1: none) -- invalidated for all its
+// lanes in stage A, set to (x + off, y) by the window lanes that leave the scan in stage B.
 void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl, uint32_t U,
-                     int st, bool fall_in, const std::string &L) {
+                     int st, bool fall_in, const std::string &L, std::pair<int, int> slot) {
   static const char *const T[kTripScan] = {"v108", "v109", "v110", "v111"};
   const uint32_t x = sl.x, y = sl.y, fall = r.pc + 3;
   const DInstr &br = P.code[r.pc + 2];
   const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
+  if (st == 0 && slot.first >= 0) e.l("v_mov_b32 v%d, -1", slot.first);
   if (st == 0) {
     // the window: bytes (x + d*j) + off .. +3 for j = 1..U in bounds and aligned, and x +
     // d*j not wrapping (as the SIMT scan block)
@@ -2504,6 +2524,10 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
     e.l("s_mov_b64 exec, s[68:69]");
     e.l("v_add_u32_e32 %s, 0x%x, %s", e.v(x), uint32_t(sl.d * int32_t(j)), e.v(x));
     e.l("v_mov_b32 %s, %s", e.v(y), T[j - 1]);
+    if (slot.first >= 0) {   // (the load cache: the word that ended the scan, and its address)
+      e.l("v_add_u32_e32 v%d, 0x%x, %s", slot.first, sl.off, e.v(x));
+      e.l("v_mov_b32 v%d, %s", slot.second, T[j - 1]);
+    }
     e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(int32_t(j * r.cnt) + int32_t(j - 1) * tcnt), VCNT);
     e.l("v_mov_b32 %s, 0x%x", VPC, fall);
     if (!fall_in) e.l("s_or_b64 s[76:77], s[76:77], exec");   // (waits outside the trips)
@@ -2571,9 +2595,34 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     flush(h);
     long_jump(h, "Ltin", "Ltiq" + std::to_string(k));
   }
+  // ---- the load cache (WB_TRIP_FWD=0 turns it off). A lane's scan that ends leaves the
+  // word it ended on and that word's address in VGPRs above the frame (a slot per scan
+  // run); a later run of the same trip loop whose every stage-A load is a 32-bit load at a
+  // slot's address (C3's swap re-reads a[i] and a[j], which the two Hoare scans just ended
+  // on) runs, for the lanes that arrived at it in this trip and whose addresses match, in
+  // this same trip, its loads as moves -- instead of waiting for the next trip's stage A.
+  // A slot is invalid (-1) from the trips' entry (Ltin: code outside the trips may have
+  // stored), from its scan's stage A, and after any store of the lane (emit_store).
+  const bool fwd_on = !(getenv("WB_TRIP_FWD") && getenv("WB_TRIP_FWD")[0] == '0');
+  std::vector<std::pair<int, int>> slot_of(runs.size(), {-1, -1});
+  std::vector<uint32_t> slot_regs;   // address VGPRs
+  {
+    uint32_t ns = 0;
+    for (size_t k = 0; k < runs.size(); k++) {
+      ScanLoop sl;
+      if (!fwd_on || !scan_loop_of(P, runs[k], &sl)) continue;
+      const int a = 255 - 2 * int(ns), v = a - 1;
+      // (above the frame, above what inlined callees may use of it, never the frame's)
+      if (uint32_t(v) < 128 + 2 * P.total_cells() + 16) break;
+      slot_of[k] = {a, v};
+      slot_regs.push_back(uint32_t(a));
+      ns++;
+    }
+  }
   h.l(".p2align 6");
   h.l("Ltin:");
   h.l("s_mov_b64 exec, s[96:97]");
+  for (uint32_t r : slot_regs) h.l("v_mov_b32 v%u, -1", r);
   h.l("s_mov_b64 s[76:77], s[96:97]");
   h.l("s_mov_b64 s[78:79], 0");
   for (const auto &r : runs) {
@@ -2614,6 +2663,29 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   std::vector<uint8_t> is_scan(nr, 0);
   for (uint32_t k = 0; k < nr && scan_k >= 2; k++)
     is_scan[k] = split[k] == 2 && scan_loop_of(P, runs[k], &scans[k]);
+  for (uint32_t k = 0; k < nr; k++)
+    if (!is_scan[k]) slot_of[k] = {-1, -1};   // (its cache slot is never set: unused)
+  // the load cache's consumers: runs with a stage A of 32-bit loads at scan slots only
+  std::vector<std::map<uint32_t, std::pair<uint32_t, uint32_t>>> fwd(nr);
+  std::vector<uint8_t> fwd_ok(nr, 0);
+  for (uint32_t k = 0; k < nr && !slot_regs.empty(); k++) {
+    if (!split[k] || is_scan[k]) continue;
+    bool ok = true, any = false;
+    for (uint32_t i = 0; i < split[k] && ok; i++) {
+      const DInstr &I = P.code[runs[k].pc + i];
+      const uint16_t op = op_of(I);
+      if (!mem_bytes(op)) continue;
+      ok = false;
+      if (op != OP_LD32) break;
+      for (uint32_t q = 0; q < nr; q++)
+        if (is_scan[q] && slot_of[q].first >= 0 && scans[q].x == (I.w1 & 0xFFFFu) && scans[q].off == I.w3) {
+          fwd[k][runs[k].pc + i] = {uint32_t(slot_of[q].first), uint32_t(slot_of[q].second)};
+          ok = any = true;
+          break;
+        }
+    }
+    fwd_ok[k] = ok && any;
+  }
   h.l("Ltrip:");
   for (uint32_t k = 0; k < nr; k++) {
     if (!split[k]) continue;
@@ -2638,6 +2710,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     }
     h.l("s_cbranch_scc1 LtB%u", k);
     h.l("LtBr%u:", k);
+    if (fwd_ok[k]) {   // the lanes that arrived this trip (not at its start there): LtF
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, VPC);
+      h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
+      h.l("s_andn2_b64 s[74:75], s[74:75], vcc");
+      h.l("s_cbranch_scc1 LtF%u", k);
+      h.l("LtFr%u:", k);
+    }
   }
   if (hybrid) {
     // ---- every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL)
@@ -2666,7 +2746,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   for (uint32_t k = 0; k < nr; k++) {
     const JitRun &r = runs[k];
     trip_cost = std::max(trip_cost, r.cnt);
-    chained += r.cnt + 64;   // (+ a taken branch's correction)
+    chained += (fwd_ok[k] ? 2 : 1) * (r.cnt + 64);   // (+ a taken branch's correction)
     if (is_scan[k])
       trip_cost = std::max<uint32_t>(trip_cost, scan_k * uint32_t(std::max<int32_t>(
                                                     0, int32_t(r.cnt) + int16_t(P.code[r.pc + 2].w2 >> 16))) + r.cnt);
@@ -2715,10 +2795,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
     uint32_t done = 0;
-    for (int st = 0; st < 2; st++) {
+    // st 0: stage A, 1: stage B, 2: the whole run for the lanes the load cache serves (LtF)
+    for (int st = 0; st < 3; st++) {
       if (st == 0 && !split[k]) continue;
+      if (st == 2 && !fwd_ok[k]) continue;
       Em e;
       e.trip = true;
+      e.inval = slot_regs;
+      if (st == 2) e.fwd = fwd[k];
       if (!nob.empty()) e.nanobs = &nob;
       if (ret_pf_on && ret_prefetch_run(P, r)) {   // (POST_CALL in stage A: RET reads v113 in B)
         e.ret_pf = true;
@@ -2728,23 +2812,34 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       e.fb = P.global_cells;
       e.prog = &P;
       e.run = (hybrid ? 8 * nr : 0) + k + uint32_t(st) * nr;   // (labels apart from the SIMT runs')
-      e.done = done;
-      const std::string L = (st ? "LtB" : "LtA") + std::to_string(k);
+      e.done = st == 2 ? 0 : done;
+      const std::string L = (st == 2 ? "LtF" : st ? "LtB" : "LtA") + std::to_string(k);
       e.stage_end = L + "e";
       e.l(".p2align 2");
       e.l("%s:", L.c_str());
       e.l("s_mov_b64 exec, s[74:75]");
-      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, st, in_region(r.pc + 3), L);
+      if (st == 2) {   // the lanes whose every cached word is at its load's address
+        for (const auto &f : fwd[k]) {
+          const DInstr &I = P.code[f.first];
+          if (I.w3) e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, I.w3, e.v(I.w1 & 0xFFFFu));
+          else e.l("v_mov_b32 %s, %s", Y0, e.v(I.w1 & 0xFFFFu));
+          e.l("v_cmp_eq_u32_e32 vcc, v%u, %s", f.second.first, Y0);
+          e.l("s_and_b64 exec, exec, vcc");
+        }
+        e.l("s_cbranch_execz %s", e.stage_end.c_str());
+      }
+      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, st, in_region(r.pc + 3), L, slot_of[k]);
       const size_t at = e.o.size();
-      for (uint32_t i = st ? split[k] : 0; i < (st ? nbody : split[k]); i++) {
+      const uint32_t i0 = st == 1 ? split[k] : 0, i1 = st == 0 ? split[k] : nbody;
+      for (uint32_t i = i0; i < i1; i++) {
         const DInstr &I = P.code[r.pc + i];
         e.pc = r.pc + i;
         e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
         if (!emit(e, I)) return "";
         e.done += (I.w0 >> 16) & 0xFFu;
       }
-      done = e.done;
-      if (st == 1) {
+      if (st < 2) done = e.done;
+      if (st >= 1) {
         // (loads in flight land first: the transfer reads cells -- a branch's operands, a
         // call's spill, a return's results)
         e.drain();
@@ -2838,7 +2933,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       std::string code = sched_on ? e.o.substr(0, at) + schedule(e.o.substr(at)) : e.o;
       code += e.stage_end + ":\n";
       code += "s_mov_b64 exec, s[96:97]\n";
-      code += "s_branch " + std::string(st ? "LtBr" : "LtAr") + std::to_string(k) + "\n";
+      code += "s_branch " + std::string(st == 2 ? "LtFr" : st ? "LtBr" : "LtAr") + std::to_string(k) + "\n";
       code += e.tail;
       (st ? oob : ooa) += code;
     }
