@@ -2460,6 +2460,64 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
 // stage B per lane (other runs execute under disjoint EXEC masks).
 // slot: the run's load-cache VGPRs {address, value} (-1: none) -- invalidated for all its
 // lanes in stage A, set to (x + off, y) by the window lanes that leave the scan in stage B.
+// T2 = the lanes whose scan window (bytes (x + d*j) + off .. +3 for j = 1..U) is out of
+// bounds, unaligned or wraps x + d*j (as the SIMT scan block)
+void scan_window_fails(Em &e, const ScanLoop &sl, uint32_t U) {
+  const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
+  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(sl.x));
+  e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
+  e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(sl.x));
+  if (sl.d < 0) {
+    e.l("v_cmp_gt_u32_e32 vcc, 0x%x, %s", uint32_t(-sl.d) * U, e.v(sl.x));
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  }
+  e.l("v_and_b32_e32 %s, 3, %s", Y1, Y0);
+  e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y1);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+}
+
+// the scan window's U words into dst[0..U-1] (the window checked)
+void scan_window_loads(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<std::string> &dst) {
+  for (uint32_t j = 1; j <= U; j++) {
+    e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(sl.x));
+    if (e.g == 0) {
+      e.l("v_mov_b32 %s, %s", W0, Y0);
+      e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+    } else {
+      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
+      e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
+      e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+    }
+    e.l("global_load_dword %s, %s, off", dst[j - 1].c_str(), XP);
+  }
+}
+
+// The successor-window prefetch (trip_source): in stage A of a scan run that falls into
+// another scan run (Hoare's i-scan into its j-scan), every lane also loads the successor's
+// window at the successor's current x into pf.v[0..U-1] and records that x in pf.x (-1:
+// none). The lanes that leave the first scan in this trip then run the successor's stage B
+// in the same trip (LtS) when their x still equals pf.x -- the words are still the
+// memory's: pf.x is invalidated by every store of the lane and at the trips' entry.
+struct ScanPrefetch { uint32_t x = 0; std::vector<std::string> v; };
+
+void trip_scan_prefetch(Em &e, const ScanLoop &succ, uint32_t U, const ScanPrefetch &pf,
+                        const std::string &L) {
+  e.l("v_mov_b32 v%u, -1", pf.x);
+  scan_window_fails(e, succ, U);
+  e.l("s_and_b64 s[84:85], exec, %s", T2);     // (no prefetch)
+  e.l("s_andn2_b64 exec, exec, %s", T2);
+  e.l("s_cbranch_execz %s_pf", L.c_str());
+  e.l("v_mov_b32 v%u, %s", pf.x, e.v(succ.x));
+  scan_window_loads(e, succ, U, pf.v);
+  e.l("%s_pf:", L.c_str());
+  e.l("s_or_b64 exec, exec, s[84:85]");
+}
+
 void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl, uint32_t U,
                      int st, bool fall_in, const std::string &L, std::pair<int, int> slot) {
   static const char *const T[kTripScan] = {"v108", "v109", "v110", "v111"};
@@ -2468,40 +2526,12 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
   const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
   if (st == 0 && slot.first >= 0) e.l("v_mov_b32 v%d, -1", slot.first);
   if (st == 0) {
-    // the window: bytes (x + d*j) + off .. +3 for j = 1..U in bounds and aligned, and x +
-    // d*j not wrapping (as the SIMT scan block)
-    const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
-    e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(x));
-    e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
-    e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
-    e.l("s_or_b64 %s, %s, vcc", T2, T2);
-    e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(x));
-    if (sl.d < 0) {
-      e.l("v_cmp_gt_u32_e32 vcc, 0x%x, %s", uint32_t(-sl.d) * U, e.v(x));
-      e.l("s_or_b64 %s, %s, vcc", T2, T2);
-    }
-    e.l("v_and_b32_e32 %s, 3, %s", Y1, Y0);
-    e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y1);
-    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+    scan_window_fails(e, sl, U);
     e.l("s_and_b64 s[84:85], exec, %s", T2);     // plain lanes
     e.l("s_andn2_b64 exec, exec, %s", T2);       // window lanes
     e.l("s_cbranch_execz %s_sp", L.c_str());
     e.l("v_mov_b32 v112, 1");
-    for (uint32_t j = 1; j <= U; j++) {
-      e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(x));
-      if (e.g == 0) {
-        e.l("v_mov_b32 %s, %s", W0, Y0);
-        e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
-        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-      } else {
-        e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
-        e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
-        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-        e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
-        e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
-      }
-      e.l("global_load_dword %s, %s, off", T[j - 1], XP);
-    }
+    scan_window_loads(e, sl, U, std::vector<std::string>(T, T + U));
     e.l("%s_sp:", L.c_str());
     e.l("s_mov_b64 exec, s[84:85]");
     e.l("s_cbranch_execz %s", e.stage_end.c_str());
@@ -2619,24 +2649,6 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       ns++;
     }
   }
-  h.l(".p2align 6");
-  h.l("Ltin:");
-  h.l("s_mov_b64 exec, s[96:97]");
-  for (uint32_t r : slot_regs) h.l("v_mov_b32 v%u, -1", r);
-  h.l("s_mov_b64 s[76:77], s[96:97]");
-  h.l("s_mov_b64 s[78:79], 0");
-  for (const auto &r : runs) {
-    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", r.pc, VPC);
-    h.l("s_andn2_b64 s[76:77], s[76:77], vcc");
-  }
-  // TPC for the next trip: the pc of every lane in the runs, -1 outside
-  h.l("Ltp:");
-  h.l("s_mov_b64 exec, s[96:97]");
-  h.l("v_mov_b32 %s, %s", TPC, VPC);
-  h.l("s_mov_b64 exec, s[76:77]");
-  h.l("v_mov_b32 %s, -1", TPC);
-  h.l("s_mov_b64 exec, s[96:97]");
-  // ---- the trip (EXEC = ALL between the runs)
   std::string ooa, oob;   // the runs' stage code, out of line
   std::vector<uint32_t> split(runs.size());
   const uint32_t nr = uint32_t(runs.size());
@@ -2686,6 +2698,45 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     }
     fwd_ok[k] = ok && any;
   }
+  // the successor-window prefetch (trip_scan_prefetch; WB_TRIP_PF=0 turns it off):
+  // pf_to[q] = the scan run scan q falls into, pf_from[s] = q
+  const bool pf_on = !(getenv("WB_TRIP_PF") && getenv("WB_TRIP_PF")[0] == '0');
+  std::vector<int> pf_to(nr, -1), pf_from(nr, -1);
+  std::vector<ScanPrefetch> pfr(nr);
+  std::vector<uint32_t> inval = slot_regs;   // (what a store invalidates: Em::inval)
+  {
+    uint32_t next = 255 - 2 * uint32_t(slot_regs.size());   // below the cache slots
+    for (uint32_t q = 0; q < nr && pf_on && scan_k >= 2; q++) {
+      if (!is_scan[q] || !start.count(runs[q].pc + 3)) continue;
+      const uint32_t s = uint32_t(start[runs[q].pc + 3]);
+      if (s == q || !is_scan[s] || pf_from[s] >= 0) continue;
+      if (next - scan_k < 128 + 2 * P.total_cells() + 16) break;   // (as the slots)
+      pfr[q].x = next;
+      for (uint32_t j = 1; j <= scan_k; j++) pfr[q].v.push_back("v" + std::to_string(next - j));
+      next -= scan_k + 1;
+      pf_to[q] = int(s);
+      pf_from[s] = int(q);
+      inval.push_back(pfr[q].x);
+    }
+  }
+  h.l(".p2align 6");
+  h.l("Ltin:");
+  h.l("s_mov_b64 exec, s[96:97]");
+  for (uint32_t r : inval) h.l("v_mov_b32 v%u, -1", r);
+  h.l("s_mov_b64 s[76:77], s[96:97]");
+  h.l("s_mov_b64 s[78:79], 0");
+  for (const auto &r : runs) {
+    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", r.pc, VPC);
+    h.l("s_andn2_b64 s[76:77], s[76:77], vcc");
+  }
+  // TPC for the next trip: the pc of every lane in the runs, -1 outside
+  h.l("Ltp:");
+  h.l("s_mov_b64 exec, s[96:97]");
+  h.l("v_mov_b32 %s, %s", TPC, VPC);
+  h.l("s_mov_b64 exec, s[76:77]");
+  h.l("v_mov_b32 %s, -1", TPC);
+  h.l("s_mov_b64 exec, s[96:97]");
+  // ---- the trip (EXEC = ALL between the runs)
   h.l("Ltrip:");
   for (uint32_t k = 0; k < nr; k++) {
     if (!split[k]) continue;
@@ -2718,6 +2769,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       h.l("s_cbranch_scc1 LtF%u", k);
       h.l("LtFr%u:", k);
     }
+    if (pf_from[k] >= 0) {   // the lanes its prefetching scan moved here this trip: LtS
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, VPC);
+      h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
+      h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
+      h.l("s_andn2_b64 s[74:75], s[74:75], vcc");
+      h.l("s_cbranch_scc1 LtS%u", k);
+      h.l("LtSr%u:", k);
+    }
   }
   if (hybrid) {
     // ---- every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL)
@@ -2747,9 +2806,12 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     const JitRun &r = runs[k];
     trip_cost = std::max(trip_cost, r.cnt);
     chained += (fwd_ok[k] ? 2 : 1) * (r.cnt + 64);   // (+ a taken branch's correction)
-    if (is_scan[k])
-      trip_cost = std::max<uint32_t>(trip_cost, scan_k * uint32_t(std::max<int32_t>(
-                                                    0, int32_t(r.cnt) + int16_t(P.code[r.pc + 2].w2 >> 16))) + r.cnt);
+    if (is_scan[k]) {
+      const uint32_t sc = scan_k * uint32_t(std::max<int32_t>(
+                                       0, int32_t(r.cnt) + int16_t(P.code[r.pc + 2].w2 >> 16))) + r.cnt;
+      trip_cost = std::max<uint32_t>(trip_cost, sc);
+      if (pf_from[k] >= 0) chained += sc + 64;   // (LtS: a whole window in the same trip)
+    }
   }
   if (chain) trip_cost = std::max(trip_cost, chained + (uint32_t)kTripScan * 64u);
   h.l("s_sub_u32 s64, s64, 0x%x", trip_cost);
@@ -2794,30 +2856,43 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
-    uint32_t done = 0;
-    // st 0: stage A, 1: stage B, 2: the whole run for the lanes the load cache serves (LtF)
-    for (int st = 0; st < 3; st++) {
+    uint32_t done = 0, done_a = 0;
+    // st 0: stage A, 1: stage B, 2: the whole run for the lanes the load cache serves (LtF),
+    // 3: stage B for the lanes whose window a prefetching scan loaded this trip (LtS)
+    static const char *const stage_name[4] = {"LtA", "LtB", "LtF", "LtS"};
+    for (int st = 0; st < 4; st++) {
       if (st == 0 && !split[k]) continue;
       if (st == 2 && !fwd_ok[k]) continue;
+      if (st == 3 && pf_from[k] < 0) continue;
+      const int sb = st == 3 ? 1 : st;   // (the stage the code is)
       Em e;
       e.trip = true;
-      e.inval = slot_regs;
+      e.inval = inval;
       if (st == 2) e.fwd = fwd[k];
       if (!nob.empty()) e.nanobs = &nob;
       if (ret_pf_on && ret_prefetch_run(P, r)) {   // (POST_CALL in stage A: RET reads v113 in B)
         e.ret_pf = true;
-        e.ret_pf_done = st == 1 && split[k] > 0;
+        e.ret_pf_done = sb == 1 && split[k] > 0;
       }
       e.g = glog;
       e.fb = P.global_cells;
       e.prog = &P;
       e.run = (hybrid ? 8 * nr : 0) + k + uint32_t(st) * nr;   // (labels apart from the SIMT runs')
-      e.done = st == 2 ? 0 : done;
-      const std::string L = (st == 2 ? "LtF" : st ? "LtB" : "LtA") + std::to_string(k);
+      e.done = st == 2 ? 0 : st == 3 ? done_a : done;
+      const std::string L = stage_name[st] + std::to_string(k);
       e.stage_end = L + "e";
       e.l(".p2align 2");
       e.l("%s:", L.c_str());
       e.l("s_mov_b64 exec, s[74:75]");
+      if (st == 0 && pf_to[k] >= 0) trip_scan_prefetch(e, scans[size_t(pf_to[k])], scan_k, pfr[k], L);
+      if (st == 3) {   // the lanes still at the prefetched x: the window as if loaded in stage A
+        const ScanPrefetch &pf = pfr[size_t(pf_from[k])];
+        e.l("v_cmp_eq_u32_e32 vcc, v%u, %s", pf.x, e.v(scans[k].x));
+        e.l("s_and_b64 exec, exec, vcc");
+        e.l("s_cbranch_execz %s", e.stage_end.c_str());
+        for (uint32_t j = 0; j < scan_k; j++) e.l("v_mov_b32 v%u, %s", 108 + j, pf.v[j].c_str());
+        e.l("v_mov_b32 v112, 1");
+      }
       if (st == 2) {   // the lanes whose every cached word is at its load's address
         for (const auto &f : fwd[k]) {
           const DInstr &I = P.code[f.first];
@@ -2828,9 +2903,9 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         }
         e.l("s_cbranch_execz %s", e.stage_end.c_str());
       }
-      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, st, in_region(r.pc + 3), L, slot_of[k]);
+      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, sb, in_region(r.pc + 3), L, slot_of[k]);
       const size_t at = e.o.size();
-      const uint32_t i0 = st == 1 ? split[k] : 0, i1 = st == 0 ? split[k] : nbody;
+      const uint32_t i0 = sb == 1 ? split[k] : 0, i1 = st == 0 ? split[k] : nbody;
       for (uint32_t i = i0; i < i1; i++) {
         const DInstr &I = P.code[r.pc + i];
         e.pc = r.pc + i;
@@ -2839,6 +2914,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         e.done += (I.w0 >> 16) & 0xFFu;
       }
       if (st < 2) done = e.done;
+      if (st == 0) done_a = e.done;
       if (st >= 1) {
         // (loads in flight land first: the transfer reads cells -- a branch's operands, a
         // call's spill, a return's results)
@@ -2933,7 +3009,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       std::string code = sched_on ? e.o.substr(0, at) + schedule(e.o.substr(at)) : e.o;
       code += e.stage_end + ":\n";
       code += "s_mov_b64 exec, s[96:97]\n";
-      code += "s_branch " + std::string(st == 2 ? "LtFr" : st ? "LtBr" : "LtAr") + std::to_string(k) + "\n";
+      code += "s_branch " + std::string(stage_name[st]) + "r" + std::to_string(k) + "\n";
       code += e.tail;
       (st ? oob : ooa) += code;
     }
