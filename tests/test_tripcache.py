@@ -1,9 +1,11 @@
-"""Trip mode's two same-trip shortcuts (jit.cpp trip_source), against the oracle:
+"""Trip mode's same-trip shortcuts (jit.cpp trip_source), against the oracle:
 
 - the load cache: a scan that ends leaves the word it ended on (and its address) in VGPRs;
   a later run whose loads are all at such addresses runs in the same trip (LtF);
 - the successor-window prefetch: a scan that falls into another scan loads the second
-  scan's window too; lanes that leave the first scan run the second in the same trip (LtS).
+  scan's window too; lanes that leave the first scan run the second in the same trip (LtS);
+- br_table threading: a jump onto a run that is one br_table (a state machine's dispatch)
+  takes the table itself, so a state whose successor lies ahead runs in the same trip.
 
 Both are only right while no store of the lane has touched the cached words: the module
 below stores into the prefetched window (run X, which also jumps past the first scan
@@ -72,6 +74,50 @@ SCANS_WAT = r"""
 """
 
 
+# a br_table state machine (C4's shape) whose states jump back to the dispatch with the
+# next state set to a constant (in range, and past the table: its default entry) or computed
+MACHINE_WAT = r"""
+(module
+  (memory 1)
+  (func (export "run") (param $seed i32) (param $n i32) (result i32)
+    (local $x i32) (local $state i32) (local $k i32) (local $acc i32)
+    (local.set $x (i32.or (i32.mul (local.get $seed) (i32.const 2654435761)) (i32.const 1)))
+    (block $done
+      (loop $machine
+        (block $s3
+          (block $s2
+            (block $s1
+              (block $s0
+                (br_table $s0 $s1 $s2 $s3 (local.get $state)))
+              ;; 0: step the generator; computed next state (0..5: 4 and 5 take the default)
+              (br_if $done (i32.ge_u (local.get $k) (local.get $n)))
+              (local.set $k (i32.add (local.get $k) (i32.const 1)))
+              (local.set $x (i32.xor (local.get $x) (i32.shl (local.get $x) (i32.const 13))))
+              (local.set $x (i32.xor (local.get $x) (i32.shr_u (local.get $x) (i32.const 17))))
+              (local.set $x (i32.xor (local.get $x) (i32.shl (local.get $x) (i32.const 5))))
+              (local.set $state (i32.rem_u (local.get $x) (i32.const 6)))
+              (br $machine))
+            ;; 1: constant next state 0
+            (local.set $acc (i32.add (local.get $acc) (local.get $x)))
+            (local.set $state (i32.const 0))
+            (br $machine))
+          ;; 2: constant next state past the table (the default: 3)
+          (local.set $acc (i32.xor (local.get $acc) (i32.mul (local.get $x) (i32.const 3))))
+          (local.set $state (i32.const 9))
+          (br $machine))
+        ;; 3 (and the default): a store, then state 1 or 0 by a parity
+        (i32.store (i32.and (local.get $x) (i32.const 1020)) (local.get $acc))
+        (local.set $state (i32.and (local.get $acc) (i32.const 1)))
+        (br $machine)))
+    (i32.add (local.get $acc) (i32.load (i32.const 64))))
+)
+"""
+
+
+def machine_wasm():
+    return assemble(MACHINE_WAT)
+
+
 def scans_wasm():
     return assemble(SCANS_WAT)
 
@@ -122,6 +168,43 @@ def test_gpu_shortcuts_exact(built, monkeypatch, pf, fwd):
     from wasmedge_amd import batch
     wasm = scans_wasm()
     rs = rows()
+    m = O.Module(wasm)
+    ref = [m.run("run", r) for r in rs]
+    ctx = batch.BatchContext(wasm, len(rs))
+    try:
+        assert ctx.compiled_runs() > 0
+        rets, st, cnt = ctx.execute("run", batch.make_values(rs, [I32, I32]), 1)
+        h = ctx.memory_hash()
+        ints = batch.ret_ints(rets)
+    finally:
+        ctx.close()
+    got = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rs))]
+    assert compare(ref, got, st, cnt, h, [I32], exact=True) == []
+
+
+def test_machine_threads_its_dispatch(built, tmp_path, monkeypatch):
+    """the state runs' jumps take the br_table themselves: a state with a computed next
+    state carries a copy of the table's compare chain (v_min_u32 clamps its index), one
+    with a constant next state jumps straight on; WB_BRT_THREAD=0 leaves the dispatch run's
+    chain alone"""
+    for wasm, copies in ((W.collatz_wasm(), 1), (machine_wasm(), 2)):
+        on = _trip_dump(wasm, tmp_path, monkeypatch).count("v_min_u32")
+        monkeypatch.setenv("WB_BRT_THREAD", "0")
+        off = _trip_dump(wasm, tmp_path, monkeypatch).count("v_min_u32")
+        monkeypatch.delenv("WB_BRT_THREAD")
+        assert on - off == copies
+    m = O.Module(machine_wasm())
+    assert {m.run("run", r)[0] for r in rows()[:64]} == {0}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thread", ["1", "0"])
+def test_gpu_machine_exact(built, monkeypatch, thread):
+    monkeypatch.setenv("WB_TRIP", "1")
+    monkeypatch.setenv("WB_BRT_THREAD", thread)
+    from wasmedge_amd import batch
+    wasm = machine_wasm()
+    rs = [[s, n] for s in range(512) for n in (0, 1, 7, 40, 300)]
     m = O.Module(wasm)
     ref = [m.run("run", r) for r in rs]
     ctx = batch.BatchContext(wasm, len(rs))

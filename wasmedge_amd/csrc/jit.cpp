@@ -2659,6 +2659,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   const bool nob_on = !(getenv("WB_NANOBS") && getenv("WB_NANOBS")[0] == '0');
   const std::vector<uint8_t> nob = nob_on ? nan_observable(P) : std::vector<uint8_t>();
   const bool ret_pf_on = !(getenv("WB_RET_PF") && getenv("WB_RET_PF")[0] == '0');
+  const bool brt_on = !(getenv("WB_BRT_THREAD") && getenv("WB_BRT_THREAD")[0] == '0');
   for (uint32_t k = 0; k < nr && split_on; k++) {
     const JitRun &r = runs[k];
     const uint16_t lop = op_of(P.code[r.pc + r.len - 1]);
@@ -2927,6 +2928,24 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         e.group = nullptr;
         auto out_if = [&](const char *m) { e.l("s_or_b64 s[76:77], s[76:77], %s", m); };
         auto add_cnt = [&](int64_t c) { if (c) e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(c), VCNT); };
+        // the run at pc when it is one br_table (a JMP onto it takes the table: WB_BRT_THREAD)
+        auto brt_thread = [&](uint32_t pc) -> int {
+          if (!brt_on || !start.count(pc)) return -1;
+          const size_t q = start[pc];
+          return runs[q].len == 1 && op_of(P.code[pc]) == OP_BR_TABLE ? int(q) : -1;
+        };
+        // the lanes a br_table sends out of the runs (Y0 = their targets)
+        auto br_table_outs = [&](const DInstr &B) {
+          std::vector<uint32_t> seen;
+          for (uint32_t q = 0; q <= (B.w1 >> 16); q++) {
+            const uint32_t t = P.brtab[2 * (B.w3 + q)];
+            if (in_region(t) || std::find(seen.begin(), seen.end(), t) != seen.end()) continue;
+            seen.push_back(t);
+            e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", t, Y0);
+            e.l("s_and_b64 s[68:69], vcc, exec");
+            out_if("s[68:69]");
+          }
+        };
         if (is_branch_op(lop) && lop != OP_JMP) {
           const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
           branch_cond(e, last);   // vcc = taken
@@ -2941,6 +2960,36 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           add_cnt(r.cnt);
           if (!in_region(tgt)) { e.l("s_and_b64 s[68:69], vcc, exec"); out_if("s[68:69]"); }
           if (!in_region(fall)) { e.l("s_andn2_b64 s[68:69], exec, vcc"); out_if("s[68:69]"); }
+        } else if (lop == OP_JMP && brt_thread(tgt) >= 0) {
+          // a jump onto a run that is one br_table (C4's `br $machine` back to its state
+          // dispatch): the table's choice made here, so that a lane whose entry lies ahead
+          // in the run order goes on in this trip; a state set to a constant in this run
+          // picks its entry at compile time. Counts: this run's, the jump's taken
+          // correction, the br_table run's and its entry's correction.
+          const DInstr &B = P.code[tgt];
+          const uint32_t ba = B.w1 & 0xFFFFu, nb = B.w1 >> 16;
+          add_cnt(int64_t(r.cnt) + int16_t(last.w2 >> 16) + runs[size_t(brt_thread(tgt))].cnt);
+          int64_t kc = -1;   // the state cell's constant, if this run sets it last
+          for (uint32_t i = nbody; i-- > 0;) {
+            const DInstr &I = P.code[r.pc + i];
+            std::vector<uint32_t> w;
+            written(I, &w);
+            if (std::find(w.begin(), w.end(), ba) == w.end()) continue;
+            if (op_of(I) == OP_CONST32 && (I.w2 & 0xFFFFu) == ba) kc = I.w3;
+            break;
+          }
+          if (kc >= 0) {
+            const uint32_t q = std::min<uint32_t>(uint32_t(kc), nb);
+            const uint32_t t = P.brtab[2 * (B.w3 + q)];
+            e.l("v_mov_b32 %s, 0x%x", VPC, t);
+            add_cnt(int32_t(P.brtab[2 * (B.w3 + q) + 1]));
+            if (!in_region(t)) out_if("exec");
+          } else {
+            emit_br_table(e, B);
+            e.l("v_mov_b32 %s, %s", VPC, Y0);
+            e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, Y1);
+            br_table_outs(B);
+          }
         } else if (lop == OP_JMP) {
           e.l("v_mov_b32 %s, 0x%x", VPC, tgt);
           add_cnt(int64_t(r.cnt) + int16_t(last.w2 >> 16));
@@ -2950,15 +2999,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           e.l("v_mov_b32 %s, %s", VPC, Y0);
           e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, Y1);
           add_cnt(r.cnt);
-          std::vector<uint32_t> seen;
-          for (uint32_t q = 0; q <= (last.w1 >> 16); q++) {
-            const uint32_t t = P.brtab[2 * (last.w3 + q)];
-            if (in_region(t) || std::find(seen.begin(), seen.end(), t) != seen.end()) continue;
-            seen.push_back(t);
-            e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", t, Y0);
-            e.l("s_and_b64 s[68:69], vcc, exec");
-            out_if("s[68:69]");
-          }
+          br_table_outs(last);
         } else if (lop == OP_CALL) {
           std::vector<uint8_t> dead;
           if (start.count(tgt)) dead = dead_zeros(P, runs[start[tgt]]);
