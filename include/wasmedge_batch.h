@@ -153,6 +153,17 @@ typedef struct WasmEdge_BatchConfigure {
   const int32_t *Devices;
   uint32_t DeviceCount;
   uint32_t Partition;
+  /* The MultiMemories proposal (WasmEdge_ConfigureAddProposal(Conf,
+   * WasmEdge_Proposal_MultiMemories), include/common/enum.inc:555; off by default,
+   * configure.h:176-182): 0 = off, a second memory fails BatchCreate with MultiMemories
+   * (0x51, validator.cpp:107-113). On: several memories (defined or imported) and memory
+   * indices in loads, stores, memory.size/grow/fill/copy/init and data segments, read as
+   * the reference reads them (a memarg's index after its offset, instruction.cpp:144-156).
+   * Memory 0 keeps every execution path; instructions on the other memories run in the
+   * per-lane step, on memories reserved whole per instance (their initial size, or up to
+   * their limit as far as min(4 GiB, free/8) per batch goes when the module grows them; a
+   * grow past that returns -1). WasmEdge_BatchGetMemory / the memory hash cover memory 0. */
+  uint32_t MultiMemories;
 } WasmEdge_BatchConfigure;
 
 #define WASMEDGE_BATCH_PARTITION_BLOCKS 0u
@@ -170,24 +181,26 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchPlacement(uint32_t NumInstances
  * reference's wasmedge.h included first). It carries over what the reference's
  * WasmEdge_ConfigureContext decides for the interpreter path: the page limit
  * (WasmEdge_ConfigureGetMaxMemoryPage, wasmedge.h:560; RuntimeConfigure::MaxMemPage,
- * configure.h:112-123) and the TailCall proposal (WasmEdge_ConfigureHasProposal,
- * wasmedge.h:495; off by default, configure.h:176-182). The proposals on by default
- * (SIMD, bulk memory, reference types, multi-value, sign extension, saturating
- * conversions, mutable globals) are always on in the batched path; MultiMemories is
- * refused at WasmEdge_BatchCreate. Statistics: instruction counts are always reported;
+ * configure.h:112-123) and the TailCall and MultiMemories proposals
+ * (WasmEdge_ConfigureHasProposal, wasmedge.h:495; off by default, configure.h:176-182).
+ * The proposals on by default (SIMD, bulk memory, reference types, multi-value, sign
+ * extension, saturating conversions, mutable globals) are always on in the batched path.
+ * Statistics: instruction counts are always reported;
  * cost metering is set through CostLimit / CostTable (the reference keeps those on its
  * StatisticsContext). Fields this does not set keep the caller's values; a NULL Conf
- * leaves the reference defaults (MaxMemoryPage 0 = 65536, TailCall off). */
+ * leaves the reference defaults (MaxMemoryPage 0 = 65536, TailCall and MultiMemories off). */
 static inline void WasmEdge_BatchConfigureFromContext(const WasmEdge_ConfigureContext *Conf,
                                                       WasmEdge_BatchConfigure *Out) {
   if (!Out) return;
   if (!Conf) {
     Out->MaxMemoryPage = 0;
     Out->TailCall = 0;
+    Out->MultiMemories = 0;
     return;
   }
   Out->MaxMemoryPage = WasmEdge_ConfigureGetMaxMemoryPage(Conf);
   Out->TailCall = WasmEdge_ConfigureHasProposal(Conf, WasmEdge_Proposal_TailCall) ? 1u : 0u;
+  Out->MultiMemories = WasmEdge_ConfigureHasProposal(Conf, WasmEdge_Proposal_MultiMemories) ? 1u : 0u;
 }
 #endif
 

@@ -39,6 +39,8 @@ def lib():
         L.om_set_cost_limit.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.om_set_tail_call.restype = None
         L.om_set_tail_call.argtypes = [ctypes.c_int]
+        L.om_set_multi_memory.restype = None
+        L.om_set_multi_memory.argtypes = [ctypes.c_int]
         L.om_set_metering.restype = None
         L.om_set_metering.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
         L.om_cost_sum.restype = ctypes.c_uint64
@@ -109,15 +111,18 @@ def _split(v):
 class Module:
     """A loaded + validated module in the oracle (one per wasm binary)."""
 
-    def __init__(self, wasm, page_limit=65536, tail_call=False):
-        """tail_call: the TailCall proposal (return_call / return_call_indirect) is on."""
+    def __init__(self, wasm, page_limit=65536, tail_call=False, multi_memory=False):
+        """tail_call: the TailCall proposal (return_call / return_call_indirect) is on;
+        multi_memory: the MultiMemories proposal."""
         L = lib()
         err = ctypes.c_int(0)
         L.om_set_tail_call(1 if tail_call else 0)
+        L.om_set_multi_memory(1 if multi_memory else 0)
         try:
             self._h = L.om_load(wasm, len(wasm), page_limit, ctypes.byref(err))
         finally:
             L.om_set_tail_call(0)
+            L.om_set_multi_memory(0)
         if not self._h:
             raise OracleError(err.value)
         self.wasm = wasm

@@ -19,6 +19,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -39,6 +40,7 @@ enum { E_OK = 0, E_TERMINATED = 0x01, E_COST_LIMIT = 0x03, E_FUNC_NOT_FOUND = 0x
 
 #define REF_NULL UINT64_MAX        /* null reference in a slot */
 #define PAGE 65536u
+#define OM_MAX_XMEM 7              /* memories past the first (MultiMemories) */
 
 typedef struct {
   uint16_t op;
@@ -52,6 +54,7 @@ typedef struct {
   int32_t pc_off;
   uint32_t lt_start, lt_n;          /* br_table label list (pool) */
   uint32_t mem_off;
+  uint8_t mem, mem2;                /* memory index (MultiMemories; memory.copy: dst, src) */
   Val num;                          /* const immediate / v128 / shuffle mask */
 } Instr;
 
@@ -76,7 +79,7 @@ typedef struct {
   uint32_t table; uint32_t off_start, off_len; uint32_t n;
   uint32_t *items_start, *items_len; /* each item is a const expr range */
 } Elem;
-typedef struct { int mode; uint32_t off_start, off_len; uint8_t *bytes; uint32_t len; } Data;
+typedef struct { int mode; uint32_t off_start, off_len; uint8_t *bytes; uint32_t len; uint32_t mem; } Data;
 
 struct OMod {
   uint32_t ntypes; FType *types;
@@ -85,6 +88,8 @@ struct OMod {
   Label *labels; uint32_t nlabels, caplabels;
   uint32_t ntables; TableT *tables;
   int has_mem; uint32_t mem_min, mem_max; int mem_has_max;
+  /* memories 1..nxmem (the MultiMemories proposal): limits of memory k at [k - 1] */
+  uint32_t nxmem; uint32_t xmin[OM_MAX_XMEM], xmax[OM_MAX_XMEM]; int xhas_max[OM_MAX_XMEM];
   uint32_t nglobals; GlobalT *globals;
   uint32_t nexports; Export *exports;
   int64_t start;
@@ -98,6 +103,8 @@ typedef struct { uint32_t size; uint64_t *refs; uint32_t max; int has_max; } Tab
 struct OInst {
   OMod *m;
   uint8_t *mem; uint32_t pages;
+  /* memories 1..nxmem; sel = the memory now in mem/pages (xmem_exec swaps, 0 otherwise) */
+  uint8_t *xmem[OM_MAX_XMEM]; uint32_t xpages[OM_MAX_XMEM]; uint32_t sel;
   Val *globals;
   TableI *tables;
   int *elem_dropped, *data_dropped;
@@ -172,6 +179,26 @@ static uint32_t push_label(OMod *m) {
   return m->nlabels++;
 }
 
+/* The MultiMemories proposal (configure.h:176-182: off by default); TEST INFRASTRUCTURE
+ * knob mirroring WasmEdge_BatchConfigure::MultiMemories for modules loaded from now on. */
+static int g_multi_memory;
+void om_set_multi_memory(int on) { g_multi_memory = on != 0; }
+
+/* a memory index immediate (instruction.cpp:374-389): a u32 with MultiMemories, else a
+ * zero byte; past 255 (no module has that many memories) it is unknown anyway */
+static uint8_t rd_memidx(Rd *r, int *bad) {
+  if (!g_multi_memory) { if (rd_u8(r) != 0) *bad = 1; return 0; }
+  uint32_t x = rd_u32(r);
+  return x > 255 ? 255 : (uint8_t)x;
+}
+/* memarg (instruction.cpp:144-156): align, offset, then -- with MultiMemories and align
+ * >= 64 -- the memory index */
+static void rd_memarg(Rd *r, Instr *in) {
+  uint32_t al = rd_u32(r);
+  in->mem_off = rd_u32(r);
+  if (g_multi_memory && al >= 64) { uint32_t x = rd_u32(r); in->mem = x > 255 ? 255 : (uint8_t)x; }
+}
+
 /* Immediates of one instruction (lib/loader/ast/instruction.cpp loadInstruction). */
 static int load_immediates(OMod *m, Rd *r, uint32_t ii) {
   Instr *in = &m->code[ii];
@@ -203,7 +230,7 @@ static int load_immediates(OMod *m, Rd *r, uint32_t ii) {
                if (n != 1) return E_TYPECHECK; break; }
   case 0x20: case 0x21: case 0x22: case 0x23: case 0x24: case 0x25: case 0x26:
     in->idx = rd_u32(r); break;
-  case 0x3F: case 0x40: if (rd_u8(r) != 0) return E_MALFORMED; break;
+  case 0x3F: case 0x40: { int bad = 0; in->mem = rd_memidx(r, &bad); if (bad) return E_MALFORMED; break; }
   case 0x41: in->num.lo = (uint32_t)(int32_t)rd_sleb(r, 32); break;
   case 0x42: in->num.lo = (uint64_t)rd_sleb(r, 64); break;
   case 0x43: { uint32_t v = 0; for (int k = 0; k < 4; k++) v |= (uint32_t)rd_u8(r) << (8 * k);
@@ -211,10 +238,22 @@ static int load_immediates(OMod *m, Rd *r, uint32_t ii) {
   case 0x44: { uint64_t v = 0; for (int k = 0; k < 8; k++) v |= (uint64_t)rd_u8(r) << (8 * k);
                in->num.lo = v; break; }
   case 0xD0: in->idx = rd_u8(r); break;
-  case 0xFC08: in->idx = rd_u32(r); if (rd_u8(r) != 0) return E_MALFORMED; break;
+  case 0xFC08: {
+    int bad = 0;
+    in->idx = rd_u32(r);
+    in->mem = rd_memidx(r, &bad);
+    if (bad) return E_MALFORMED;
+    break;
+  }
   case 0xFC09: in->idx = rd_u32(r); break;
-  case 0xFC0A: if (rd_u8(r) || rd_u8(r)) return E_MALFORMED; break;
-  case 0xFC0B: if (rd_u8(r) != 0) return E_MALFORMED; break;
+  case 0xFC0A: {
+    int bad = 0;
+    in->mem = rd_memidx(r, &bad);
+    in->mem2 = rd_memidx(r, &bad);
+    if (bad) return E_MALFORMED;
+    break;
+  }
+  case 0xFC0B: { int bad = 0; in->mem = rd_memidx(r, &bad); if (bad) return E_MALFORMED; break; }
   case 0xFC0C: in->idx2 = rd_u32(r); in->idx = rd_u32(r); break;   /* elem, table */
   case 0xFC0D: in->idx = rd_u32(r); break;
   case 0xFC0E: in->idx = rd_u32(r); in->idx2 = rd_u32(r); break;   /* dst, src */
@@ -229,9 +268,9 @@ static int load_immediates(OMod *m, Rd *r, uint32_t ii) {
   default:
     if ((op >= 0x28 && op <= 0x3E) || (op >= 0xFD00 && op <= 0xFD0B) || op == 0xFD5C ||
         op == 0xFD5D) {
-      rd_u32(r); in->mem_off = rd_u32(r);
+      rd_memarg(r, in);
     } else if (op >= 0xFD54 && op <= 0xFD5B) {
-      rd_u32(r); in->mem_off = rd_u32(r); in->lane = rd_u8(r);
+      rd_memarg(r, in); in->lane = rd_u8(r);
     } else if (op >= 0xFD15 && op <= 0xFD22) {
       in->lane = rd_u8(r);
     }
@@ -452,6 +491,14 @@ static uint8_t sigc(char ch) {
                 case 'd': return T_F64; default: return T_V128; }
 }
 
+/* a memory index of an instruction: unknown memory (InvalidMemoryIdx, formchecker.cpp:
+ * 245-252) -- TypeCheckFailed without MultiMemories, as for a module without memory */
+static int mem_idx_err(const OMod *m, uint32_t k) {
+  const uint32_t nm = (m->has_mem ? 1u : 0u) + m->nxmem;
+  if (k < nm) return 0;
+  return g_multi_memory && nm ? 0x47 : E_TYPECHECK;
+}
+
 static int check_func(OMod *m, uint32_t fi) {
   Func *F = &m->funcs[fi];
   FType *ft = &m->types[F->type];
@@ -599,16 +646,19 @@ static int check_func(OMod *m, uint32_t fi) {
       else { ck_pop_t(&c, t); ck_pop_t(&c, T_I32); }
       break;
     }
-    case 0x3F: if (!m->has_mem) c.err = E_TYPECHECK; ck_push(&c, T_I32); break;
-    case 0x40: if (!m->has_mem) c.err = E_TYPECHECK; ck_pop_t(&c, T_I32); ck_push(&c, T_I32); break;
+    case 0x3F: if ((c.err = mem_idx_err(m, in->mem))) break; ck_push(&c, T_I32); break;
+    case 0x40: if ((c.err = mem_idx_err(m, in->mem))) break; ck_pop_t(&c, T_I32); ck_push(&c, T_I32); break;
     case 0x41: ck_push(&c, T_I32); break;
     case 0x42: ck_push(&c, T_I64); break;
     case 0x43: ck_push(&c, T_F32); break;
     case 0x44: ck_push(&c, T_F64); break;
-    case 0xFC08: if (!m->has_mem || in->idx >= m->ndatas) c.err = E_TYPECHECK;
+    case 0xFC08: if ((c.err = mem_idx_err(m, in->mem))) break;   /* (formchecker.cpp:812-824) */
+      if (in->idx >= m->ndatas) c.err = g_multi_memory ? 0x4A : E_TYPECHECK;
       ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); break;
     case 0xFC09: if (in->idx >= m->ndatas) c.err = E_TYPECHECK; break;
-    case 0xFC0A: case 0xFC0B: if (!m->has_mem) c.err = E_TYPECHECK;
+    case 0xFC0A: case 0xFC0B:   /* copy: the source memory first (formchecker.cpp:826-834) */
+      if (op == 0xFC0A && (c.err = mem_idx_err(m, in->mem2))) break;
+      if ((c.err = mem_idx_err(m, in->mem))) break;
       ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); break;
     case 0xFC0C: if (in->idx >= m->ntables || in->idx2 >= m->nelems) c.err = E_TYPECHECK;
       ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); ck_pop_t(&c, T_I32); break;
@@ -625,7 +675,7 @@ static int check_func(OMod *m, uint32_t fi) {
       if (!s) { c.err = E_ILLEGAL_OPCODE; break; }
       if ((op >= 0x28 && op <= 0x3E) || (op >= 0xFD00 && op <= 0xFD0B) ||
           (op >= 0xFD54 && op <= 0xFD5D)) {
-        if (!m->has_mem) { c.err = E_TYPECHECK; break; }
+        if ((c.err = mem_idx_err(m, in->mem))) break;
       }
       const char *colon = strchr(s, ':');
       int np = (int)(colon - s);
@@ -695,9 +745,15 @@ static int import_entity(OMod *m, Rd *s, uint8_t kind, const char *mod, const ch
     TableT *t = &m->tables[m->ntables++];
     t->reftype = p->type; t->min = p->min; t->max = p->max; t->has_max = p->has_max;
   } else if (kind == 2) {
-    if (m->has_mem) return 0x51;
+    if (m->has_mem && !g_multi_memory) return 0x51;   /* (validator.cpp:107-113) */
     if (!limits_ok(p, mn, hm, mx)) return 0x61;
-    m->has_mem = 1; m->mem_min = p->min; m->mem_max = p->max; m->mem_has_max = p->has_max;
+    if (m->has_mem) {
+      if (m->nxmem >= OM_MAX_XMEM) return 0x51;
+      m->xmin[m->nxmem] = p->min; m->xmax[m->nxmem] = p->max; m->xhas_max[m->nxmem] = p->has_max;
+      m->nxmem++;
+    } else {
+      m->has_mem = 1; m->mem_min = p->min; m->mem_max = p->max; m->mem_has_max = p->has_max;
+    }
   } else {
     if (p->type != ty || p->mut != mut) return 0x61;
     m->globals = realloc(m->globals, sizeof(GlobalT) * (m->nglobals + 2));
@@ -783,8 +839,18 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
     }
     case 5: {
       uint32_t n = rd_u32(&s);
-      if (n > 1 || (n && m->has_mem)) { *err = 0x51; break; }
-      if (n) { m->has_mem = 1; load_limits(&s, &m->mem_min, &m->mem_max, &m->mem_has_max); }
+      if (!g_multi_memory && (n > 1 || (n && m->has_mem))) { *err = 0x51; break; }
+      for (uint32_t k = 0; k < n && !*err; k++) {
+        if (!m->has_mem) {
+          m->has_mem = 1;
+          *err = load_limits(&s, &m->mem_min, &m->mem_max, &m->mem_has_max);
+        } else if (m->nxmem >= OM_MAX_XMEM) {
+          *err = 0x51;
+        } else {
+          *err = load_limits(&s, &m->xmin[m->nxmem], &m->xmax[m->nxmem], &m->xhas_max[m->nxmem]);
+          m->nxmem++;
+        }
+      }
       break;
     }
     case 6: {                       /* after any imported globals */
@@ -885,7 +951,7 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
         Data *d = &m->datas[k];
         uint32_t flags = rd_u32(&s);
         d->mode = (flags & 1) ? 1 : 0;
-        if (flags == 2) rd_u32(&s);
+        if (flags == 2) d->mem = rd_u32(&s);   /* (segment.cpp:316-323) */
         if (!(flags & 1)) *err = load_const_expr(m, &s, &d->off_start, &d->off_len);
         d->len = rd_u32(&s);
         d->bytes = malloc(d->len + 1);
@@ -903,6 +969,8 @@ OMod *om_load(const uint8_t *wasm, uint32_t len, uint32_t page_limit, int *err) 
   free(func_types);
   if (!*err && m->nfuncs - m->nimported != nfunc_decl) *err = E_MALFORMED;
   for (uint32_t f = m->nimported; f < m->nfuncs && !*err; f++) *err = check_func(m, f);
+  for (uint32_t k = 0; k < m->ndatas && !*err; k++)   /* an active segment's memory */
+    if (m->datas[k].mode == 0) *err = mem_idx_err(m, m->datas[k].mem);
   if (*err) { om_free(m); return NULL; }
   return m;
 }

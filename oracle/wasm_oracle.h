@@ -74,6 +74,7 @@ void om_clear_imports(void);
 /* The TailCall proposal (return_call / return_call_indirect) for modules loaded from now
  * on; off by default (configure.h:176-182), when the loader rejects them (IllegalOpCode). */
 void om_set_tail_call(int on);
+void om_set_multi_memory(int on);   /* the MultiMemories proposal for modules loaded from now on */
 void om_add_import(const char *mod, const char *name, uint32_t kind, uint32_t type, uint32_t mut,
                    uint32_t min, uint32_t max, int has_max, uint64_t lo, uint64_t hi);
 

@@ -59,13 +59,15 @@ def from_cells(cells, types):
 
 
 def emu_run(wasm, func, arg_rows, ptypes, rtypes, max_pages=0, gs_depth=0, max_steps=0,
-            host=None, cost_limit=0, cost_table=None, costs_out=None, tail_call=False):
+            host=None, cost_limit=0, cost_table=None, costs_out=None, tail_call=False,
+            multi_memory=False):
     """host: a wb_emu_host_t ctypes callback serving imports inline (hostfuncs.emu_host);
     cost_limit: gas limit (0 = none) with cost_table (list by OpCode, None = unit costs);
-    costs_out: a list that receives each instance's gas total; tail_call: the TailCall
-    proposal."""
+    costs_out: a list that receives each instance's gas total; tail_call / multi_memory: the
+    TailCall / MultiMemories proposals."""
     E = emu_lib()
     E.wb_emu_set_tail_call(1 if tail_call else 0)
+    E.wb_emu_set_multi_memory(1 if multi_memory else 0)
     E.wb_emu_set_host(host)
     E.wb_emu_set_cost_limit(cost_limit)
     if cost_table is None:

@@ -61,7 +61,8 @@ class _Conf(ctypes.Structure):
                 ("CostTableLen", ctypes.c_uint32), ("MemoryGranule", ctypes.c_uint32),
                 ("TailCall", ctypes.c_uint32), ("MemoryReservePages", ctypes.c_uint32),
                 ("MemoryPoolBytes", ctypes.c_uint64), ("Devices", ctypes.POINTER(ctypes.c_int32)),
-                ("DeviceCount", ctypes.c_uint32), ("Partition", ctypes.c_uint32)]
+                ("DeviceCount", ctypes.c_uint32), ("Partition", ctypes.c_uint32),
+                ("MultiMemories", ctypes.c_uint32)]
 
 PARTITION_BLOCKS, PARTITION_INTERLEAVE = 0, 1
 
@@ -242,7 +243,7 @@ class BatchContext:
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
                  memory_granule=0, imports=None, tail_call=False, memory_reserve_pages=0,
-                 memory_pool_bytes=0, devices=None, partition=PARTITION_BLOCKS):
+                 memory_pool_bytes=0, devices=None, partition=PARTITION_BLOCKS, multi_memory=False):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
         metering is on when cost_limit > 0. max_memory_page 0 = the reference's default
         page limit (65536); memory_reserve_pages / memory_pool_bytes: the device layout of
@@ -256,6 +257,7 @@ class BatchContext:
                      host_threads, tab.ctypes.data if tab is not None and len(tab) else None,
                      len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0,
                      memory_reserve_pages, memory_pool_bytes)
+        conf.MultiMemories = 1 if multi_memory else 0
         if devices is not None and len(devices) == 1:
             conf.DeviceOrdinal = devices[0]
         if devices is not None and len(devices) > 1:

@@ -104,7 +104,7 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
 uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   uint8_t ec = 0;
   std::string err = wb::load_program(wasm, len, C->prog, &ec, C->conf.CostLimit != 0, &C->imports,
-                                     C->conf.TailCall != 0);
+                                     C->conf.TailCall != 0, C->conf.MultiMemories != 0);
   if (!err.empty()) return C->fail(ec ? ec : kRuntimeError, err);
   const wb::Program &P = C->prog;
   // gas tables (statistics.h:32: unit costs unless the caller set a table)
@@ -197,8 +197,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     doff.push_back(uint32_t(pool.size()));
     dlen.push_back(uint32_t(d.bytes.size()));
     pool.insert(pool.end(), d.bytes.begin(), d.bytes.end());
-    if (d.active) {
-      dropped[k >> 5] |= 1u << (k & 31);   // active segments are dropped after init
+    if (d.active) dropped[k >> 5] |= 1u << (k & 31);   // active segments are dropped after init
+    if (d.active && !d.mem) {   // (memory 0's image; the others' below)
       uint64_t end = uint64_t(d.offset) + d.bytes.size();
       if (img.size() * 4 < end) img.resize((end + 3) / 4, 0);
       for (size_t b = 0; b < d.bytes.size(); b++) {
@@ -209,6 +209,47 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   }
   C->image_words = uint32_t(img.size());
   C->init_dropped = dropped[0];
+  // memories past the first (MultiMemories): every lane's are reserved whole -- the
+  // initial size, or with a memory.grow on it up to its page limit as far as a budget of
+  // min(4 GiB, an eighth of the free device memory) goes -- back to back, in 4-byte words
+  // interleaved over a wave's lanes; only the per-lane step addresses them (KParams::xmem).
+  // A grow past the reservation returns -1 (the allocation failing, allocator.cpp:101-129).
+  std::vector<uint32_t> ximg;
+  if (!P.xmems.empty()) {
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const uint64_t budget = std::min<uint64_t>(uint64_t(4) << 30, free_b / 8);
+    const uint64_t per_lane = budget / (uint64_t(C->nwaves) * 64 * 65536 * P.xmems.size());
+    uint64_t words = 0;
+    for (size_t k = 0; k < P.xmems.size(); k++) {
+      const auto &xm = P.xmems[k];
+      uint32_t lim = xm.has_max ? std::min<uint32_t>(xm.max, 65536) : 65536;
+      if (C->conf.MaxMemoryPage) lim = std::min(lim, C->conf.MaxMemoryPage);
+      if (xm.min > lim) return C->fail(kMemoryOutOfBounds, "initial memory pages exceed MaxMemoryPage");
+      bool grows = false;
+      for (const auto &I : P.code)
+        grows |= (I.w0 & 0xFFFFu) == OP_XMEM_GROW && (I.w1 >> 16) == k + 1;
+      const uint32_t res = grows ? uint32_t(std::max<uint64_t>(xm.min, std::min<uint64_t>(lim, per_lane))) : xm.min;
+      C->xinfo_h.push_back(uint32_t(words));
+      C->xinfo_h.push_back(res);
+      words += uint64_t(res) << 14;
+      if (words > 0xFFFFFFFFull) return C->fail(kRuntimeError, "memories past the first exceed 16 GiB per instance");
+    }
+    C->xwords = uint32_t(words);
+    ximg.assign(C->xwords, 0u);
+    for (const auto &d : P.datas) {
+      if (!d.active || !d.mem) continue;
+      const uint64_t b0 = uint64_t(C->xinfo_h[2 * (d.mem - 1)]) * 4 + d.offset;
+      for (size_t b = 0; b < d.bytes.size(); b++) {
+        const uint64_t a = b0 + b;
+        ximg[a >> 2] = (ximg[a >> 2] & ~(0xFFu << (8 * (a & 3)))) | (uint32_t(d.bytes[b]) << (8 * (a & 3)));
+      }
+    }
+    C->xpages0.assign(P.xmems.size() * size_t(C->nwaves) * 64, 0u);
+    for (size_t k = 0; k < P.xmems.size(); k++)
+      std::fill(C->xpages0.begin() + k * size_t(C->nwaves) * 64, C->xpages0.begin() + (k + 1) * size_t(C->nwaves) * 64,
+                P.xmems[k].min);
+  }
   std::vector<DFunc> fv;
   for (const auto &f : P.funcs)
     fv.push_back(DFunc{f.imported ? 0xFFFFFFFFu : f.entry_pc, P.type_canon[f.type]});
@@ -279,7 +320,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
             (!C->conf.CostLimit || (C->cost_off.upload(C->cost_off_h, s) &&
                                     C->cost_pool.upload(C->cost_pool_h, s))) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
-            C->data_off.upload(doff, s) && C->data_len.upload(dlen, s);
+            C->data_off.upload(doff, s) && C->data_len.upload(dlen, s) &&
+            (P.xmems.empty() || (C->ximage.upload(ximg, s) && C->xinfo.upload(C->xinfo_h, s)));
   if (!ok) return C->fail(kRuntimeError, "device allocation/upload of the module failed");
   size_t nw = C->nwaves;
   C->ls_slots = LS_GLOBALS + uint32_t(ls_init.size());
@@ -307,6 +349,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->lstate.alloc(nw * size_t(C->ls_slots) * 64) || !C->status.alloc(C->n + 1) ||
       !C->ltab.alloc(nw * size_t(P.tab_words) * 64) ||
       !C->counts.alloc(C->n + 1) || !C->hashes.alloc(C->n + 1) ||
+      (!P.xmems.empty() && (!C->xmem.alloc(nw * 64 * size_t(C->xwords) + 64) ||
+                            !C->xpages.alloc(C->xpages0.size()))) ||
       (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
       ((P.n_imported || C->grow_host || C->gs_grow) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
@@ -418,6 +462,10 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
   k.gs_grow = C->gs_grow ? 1u : 0u;
+  if (!P.xmems.empty()) {
+    k.xmem = C->xmem.ptr; k.xpages = C->xpages.ptr; k.xinfo = C->xinfo.ptr;
+    k.xwords = C->xwords; k.xstride = C->nwaves * 64; k.n_xmem = uint32_t(P.xmems.size());
+  }
   k.init_dropped = C->init_dropped;
   k.ls_slots = C->ls_slots;
   k.is_start = is_start ? 1u : 0u;
@@ -447,7 +495,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   if (C->cap_threads != wpb * 64 || C->cap_lds != wave_lds * wpb + 256) {
     C->cap_threads = wpb * 64;
     C->cap_lds = wave_lds * wpb + 256;
-    C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, k.grow_host, C->cap_threads, C->cap_lds);
+    C->cap_blocks = wb_exec_capacity(vf, k.hframe != nullptr, k.grow_host || k.n_xmem, C->cap_threads, C->cap_lds);
   }
   const char *pe = getenv("WB_PERSIST");
   if (const char *lp = getenv("WB_LPT")) C->lpt = lp[0] != '0';
@@ -669,6 +717,14 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
       !C->hip_ok(wb_launch_mem_init(C->ltab.ptr, C->tab_image.ptr, P.tab_words, P.tab_words,
                                     P.tab_words, C->nwaves, nullptr, 0, 1u, 0u, 0u, nullptr, 0, 0, 0,
                                     C->stream), "table init"))
+    return R(kRuntimeError);
+  // memories past the first: zeros + their active data segments, initial sizes
+  if (!P.xmems.empty() &&
+      ((C->xwords && !C->hip_ok(wb_launch_mem_init(C->xmem.ptr, C->ximage.ptr, C->xwords, C->xwords,
+                                                    C->xwords, C->nwaves, nullptr, 0, 1u, 0u, 0u, nullptr,
+                                                    0, 0, 0, C->stream), "memory init")) ||
+       !C->hip_ok(hipMemcpyAsync(C->xpages.ptr, C->xpages0.data(), C->xpages0.size() * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, C->stream), "memory sizes")))
     return R(kRuntimeError);
   // gas: instantiation's constant expressions are priced first (module.cpp order); one
   // past the limit fails the instantiation like the reference's VM::instantiate

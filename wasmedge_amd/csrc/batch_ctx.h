@@ -129,6 +129,12 @@ struct WasmEdge_BatchContext {
   DevBuf<uint8_t> data_pool;
   // instance state
   DevBuf<uint32_t> mem, gstack, lstate, params, results, ltab;
+  // memories past the first (MultiMemories, KParams::xmem): their device words, every
+  // lane's initial image (zeros + active data segments), sizes; at every Reset from
+  // ximage / xpages0
+  DevBuf<uint32_t> xmem, ximage, xpages, xinfo;
+  std::vector<uint32_t> xpages0, xinfo_h;   // xinfo: base word, page limit per memory
+  uint32_t xwords = 0;
   // host-import yield path (only allocated when the module imports functions)
   DevBuf<uint32_t> fsave, hcall, hbuf;
   uint32_t hb_cells = 0;

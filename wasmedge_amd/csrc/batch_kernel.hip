@@ -374,6 +374,12 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   // only [0, hwm) of each lane (plus the image), the rest is still the zero it was given
   uint32_t hwm = LS(LS_HWM);
 #define WB_MARK(ea, n) (hwm = max(hwm, (uint32_t)min((uint64_t)(ea) + (uint64_t)(n), 0xFFFFFFFFull)))
+  // memories past the first (MultiMemories, KParams::xmem): 4-byte words interleaved over
+  // the wave's lanes; only the per-lane step (dbc_step.inc XLD ... XMEM_COPY) reaches them
+#define XMEM(k) GMem{p.xmem + ((size_t)(inst >> 6) * p.xwords + p.xinfo[2u * ((k) - 1u)]) * 64u + (inst & 63u), 0u}
+#define XPAGES(k) p.xpages[(size_t)((k) - 1u) * p.xstride + inst]
+#define XLIMIT(k) p.xinfo[2u * ((k) - 1u) + 1u]
+#define XGROW(k, cur, n) (XPAGES(k) = (cur) + (n))
   uint64_t count = 0;
   // the running gas total (metered runs): kept in the instance state between launches
   uint64_t cost = (uint64_t)LS(LS_COST) | ((uint64_t)LS(LS_COST + 1) << 32);
@@ -616,7 +622,9 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         if (VF && p.simt && (w0 & DBC_HOT) && !first) goto k_leave;
         first = false;
         switch (op) {
+#define WB_XMEM_ON 0
 #include "dbc_step.inc"
+#undef WB_XMEM_ON
         }
       k_next:
         sc += cnt8;
@@ -729,9 +737,13 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         status = 0x03u;
         goto s_done;
       }
-      if (!PG || !__ballot(pages >= p.rpages)) {
+      // (memories past the first live only in the paged copy: a module with them runs the
+      // PG kernels and takes that copy always)
+      if (!PG || (!__ballot(pages >= p.rpages) && !p.n_xmem)) {
         switch (op) {
+#define WB_XMEM_ON 0
 #include "dbc_step.inc"
+#undef WB_XMEM_ON
         }
       } else {
         // a lane of this group has grown past the reserved layout: the step's accesses go
@@ -743,7 +755,9 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
                            lane << p.mlog};
         const GMemP &mem = mem_pg;
         switch (op) {
+#define WB_XMEM_ON 1
 #include "dbc_step.inc"
+#undef WB_XMEM_ON
         }
       }
     s_next:
@@ -1189,7 +1203,7 @@ static void exec_attrs() {
 extern "C" hipError_t wb_launch_exec(const KParams *p, uint32_t blocks, uint32_t threads,
                                      size_t lds_bytes, int vframe, hipStream_t s) {
   exec_attrs();
-  const void *k = exec_kernel(vframe, p->hframe != nullptr, p->grow_host != 0);
+  const void *k = exec_kernel(vframe, p->hframe != nullptr, p->grow_host != 0 || p->n_xmem != 0);
   void *args[] = {const_cast<KParams *>(p)};
   return hipLaunchKernel(k, dim3(blocks), dim3(threads), args, lds_bytes, s);
 }

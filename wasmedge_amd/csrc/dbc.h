@@ -148,6 +148,14 @@ struct DInstr {
   X(V_BINX) X(V_UNX)                                                                   \
   /* a = address cell, b = vector cell, c = dst, d = lane | log2(bytes) << 8, imm = off */ \
   X(V_LDLANE) X(V_STLANE)                                                              \
+  /* memories past the first (MultiMemories; the per-lane step only), k = memory index:  */ \
+  /*   XLD: a = address, b = k, c = dst, d = the memory-0 load op, imm = offset          */ \
+  /*   XST: a = address, b = value, c = k, d = the memory-0 store op, imm = offset       */ \
+  /*   XLANE: as V_LDLANE / V_STLANE, d = lane | log2(bytes) << 4 | load << 6 | k << 8   */ \
+  /*   XMEM_SIZE: b = k, c = dst; XMEM_GROW: a = pages, b = k, c = dst                    */ \
+  /*   XMEM_FILL: a, b, c as MEM_FILL, imm = k; XMEM_INIT: as MEM_INIT, d = k            */ \
+  /*   XMEM_COPY: as MEM_COPY, imm = dst memory | src memory << 16 (one of them > 0)    */ \
+  X(XLD) X(XST) X(XLANE) X(XMEM_SIZE) X(XMEM_GROW) X(XMEM_FILL) X(XMEM_COPY) X(XMEM_INIT)  \
   X(DBC_NUM_OPS)
 
 enum DOp : uint16_t {

@@ -4,6 +4,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include "dbc.h"
 
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
@@ -473,6 +474,66 @@ template <class M> WB_HD uint8_t mbyte(M m, uint32_t a) {
 }
 template <class M> WB_HD void mbyte_set(M m, uint32_t a, uint8_t v) {
   reinterpret_cast<uint8_t *>(mw(m, a >> 2))[a & 3u] = v;
+}
+
+// A memory-0 load op as XLD carries it (memories past the first): bytes read, sign
+// extension, a 64-bit cell pair, a v128 result (memory.ipp:12-38, 70-220)
+struct LdShape { uint32_t n; bool sx, w64, v; };
+WB_HD __attribute__((always_inline)) LdShape ld_shape(uint32_t op) {
+  switch (op) {
+    case OP_LD8S32: return {1, true, false, false};
+    case OP_LD8U32: return {1, false, false, false};
+    case OP_LD16S32: return {2, true, false, false};
+    case OP_LD16U32: return {2, false, false, false};
+    case OP_LD32: return {4, false, false, false};
+    case OP_LD8S64: return {1, true, true, false};
+    case OP_LD8U64: return {1, false, true, false};
+    case OP_LD16S64: return {2, true, true, false};
+    case OP_LD16U64: return {2, false, true, false};
+    case OP_LD32S64: return {4, true, true, false};
+    case OP_LD32U64: return {4, false, true, false};
+    case OP_LD64: return {8, false, true, false};
+    case OP_LD128: return {16, false, false, true};
+    case OP_V_LD8SPLAT: return {1, false, false, true};
+    case OP_V_LD16SPLAT: return {2, false, false, true};
+    case OP_V_LD32SPLAT: case OP_V_LD32ZERO: return {4, false, false, true};
+    default: return {8, false, false, true};   // the 64-bit extending, splat and zero forms
+  }
+}
+// the v128 a load form makes of its bytes (x: the first 8, hi: bytes 8..15 of LD128)
+WB_HD __attribute__((always_inline)) void v128_of_load(uint32_t op, uint64_t x, uint64_t hi, uint32_t o[4]) {
+  o[0] = o[1] = o[2] = o[3] = 0;
+  switch (op) {
+    case OP_LD128:
+      o[0] = (uint32_t)x; o[1] = (uint32_t)(x >> 32); o[2] = (uint32_t)hi; o[3] = (uint32_t)(hi >> 32);
+      break;
+    case OP_V_LD8X8S: case OP_V_LD8X8U:
+      for (int k = 0; k < 4; k++) {
+        uint32_t b0 = (x >> (16 * k)) & 0xFF, b1 = (x >> (16 * k + 8)) & 0xFF;
+        if (op == OP_V_LD8X8S) { b0 = (uint32_t)(int32_t)(int8_t)b0 & 0xFFFF; b1 = (uint32_t)(int32_t)(int8_t)b1 & 0xFFFF; }
+        o[k] = b0 | (b1 << 16);
+      }
+      break;
+    case OP_V_LD16X4S: case OP_V_LD16X4U:
+      for (int k = 0; k < 4; k++) {
+        const uint32_t h = (x >> (16 * k)) & 0xFFFF;
+        o[k] = op == OP_V_LD16X4S ? (uint32_t)(int32_t)(int16_t)h : h;
+      }
+      break;
+    case OP_V_LD32X2S: case OP_V_LD32X2U:
+      for (int k = 0; k < 2; k++) {
+        const uint32_t v = (uint32_t)(x >> (32 * k));
+        o[2 * k] = v;
+        o[2 * k + 1] = op == OP_V_LD32X2S ? (((int32_t)v < 0) ? 0xFFFFFFFFu : 0u) : 0u;
+      }
+      break;
+    case OP_V_LD8SPLAT: o[0] = o[1] = o[2] = o[3] = ((uint32_t)x & 0xFF) * 0x01010101u; break;
+    case OP_V_LD16SPLAT: { const uint32_t h = (uint32_t)x & 0xFFFF; o[0] = o[1] = o[2] = o[3] = h | (h << 16); break; }
+    case OP_V_LD32SPLAT: o[0] = o[1] = o[2] = o[3] = (uint32_t)x; break;
+    case OP_V_LD64SPLAT: o[0] = o[2] = (uint32_t)x; o[1] = o[3] = (uint32_t)(x >> 32); break;
+    case OP_V_LD32ZERO: o[0] = (uint32_t)x; break;
+    default: o[0] = (uint32_t)x; o[1] = (uint32_t)(x >> 32); break;   // LD64ZERO
+  }
 }
 
 WB_HD uint32_t clz32(uint32_t x) { return x ? __builtin_clz(x) : 32; }

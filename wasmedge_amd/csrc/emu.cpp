@@ -29,6 +29,7 @@ typedef int (*wb_emu_host_t)(uint32_t inst, uint32_t func, const uint32_t *args,
 static wb_emu_host_t g_host = nullptr;
 static uint64_t g_cost_limit = ~0ull;   // gas limit (0 = none)
 static bool g_tail_call = false;      // TailCall proposal (wb_emu_set_tail_call)
+static bool g_multi_memory = false;   // MultiMemories proposal (wb_emu_set_multi_memory)
 static std::vector<uint64_t> g_cost_tab;   // cost per OpCode (empty: the unit table)
 static std::vector<uint64_t> g_costs;      // per instance: its gas total after the last run
 static std::vector<wb::HostImport> g_imports;   // provided tables / memories / globals
@@ -69,6 +70,8 @@ __attribute__((visibility("default"))) uint32_t wb_emu_num_ops() { return OP_DBC
 __attribute__((visibility("default"))) void wb_emu_set_host(wb_emu_host_t h) { g_host = h; }
 // the TailCall proposal for modules loaded from now on (WasmEdge_BatchConfigure::TailCall)
 __attribute__((visibility("default"))) void wb_emu_set_tail_call(int on) { g_tail_call = on != 0; }
+// ... and the MultiMemories proposal (WasmEdge_BatchConfigure::MultiMemories)
+__attribute__((visibility("default"))) void wb_emu_set_multi_memory(int on) { g_multi_memory = on != 0; }
 __attribute__((visibility("default"))) void wb_emu_set_cost_limit(uint64_t l) { g_cost_limit = l ? l : ~0ull; }
 // WasmEdge_StatisticsSetCostTable (statistics.h:59-66): `len` entries, the rest 0;
 // tab = NULL and len = 0: back to the default unit table
@@ -118,7 +121,8 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     uint32_t max_pages, uint32_t gs_depth, uint64_t max_steps) {
   wb::Program P;
   uint8_t ec = 0;
-  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull, &g_imports, g_tail_call);
+  g_err = wb::load_program(wasm, len, P, &ec, g_cost_limit != ~0ull, &g_imports, g_tail_call,
+                           g_multi_memory);
   if (!g_err.empty()) return ec ? ec : 2;
   int f = wb::find_export(P, func);
   if (f < 0) { g_err = "function not found"; return 0x05; }
@@ -189,7 +193,23 @@ __attribute__((visibility("default"))) int wb_emu_execute(
     memv.assign(size_t(P.mem_min) << 14, 0u);   // (memory.grow resizes it)
     uint8_t *mb = reinterpret_cast<uint8_t *>(memv.data());
     for (const auto &d : P.datas)
-      if (d.active && !d.bytes.empty()) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
+      if (d.active && !d.mem && !d.bytes.empty()) memcpy(mb + d.offset, d.bytes.data(), d.bytes.size());
+    // memories past the first (MultiMemories): their own vectors, limits as memory 0's
+    std::vector<std::vector<uint32_t>> xmemv(P.xmems.size());
+    std::vector<uint32_t> xpg(P.xmems.size()), xlim(P.xmems.size());
+    for (size_t k = 0; k < P.xmems.size(); k++) {
+      xpg[k] = P.xmems[k].min;
+      xlim[k] = std::min<uint32_t>(65536, P.xmems[k].has_max ? P.xmems[k].max : 65536);
+      if (max_pages) xlim[k] = std::min(xlim[k], max_pages);
+      xmemv[k].assign(size_t(xpg[k]) << 14, 0u);
+    }
+    for (const auto &d : P.datas)
+      if (d.active && d.mem && !d.bytes.empty())
+        memcpy(reinterpret_cast<uint8_t *>(xmemv[d.mem - 1].data()) + d.offset, d.bytes.data(), d.bytes.size());
+#define XMEM(k) xmemv[(k) - 1u].data()
+#define XPAGES(k) xpg[(k) - 1u]
+#define XLIMIT(k) xlim[(k) - 1u]
+#define XGROW(k, cur, n) do { xmemv[(k) - 1u].resize(size_t((cur) + (n)) << 14, 0u); xpg[(k) - 1u] = (cur) + (n); } while (0)
     uint32_t *fr = frame.data(), *gs = gstack.data(), *mem = memv.data();
 #define CELL(x) fr[(uint32_t)(x)]
 #define R32(x) CELL(x)
@@ -255,7 +275,9 @@ __attribute__((visibility("default"))) int wb_emu_execute(
           goto e_done;
         }
         switch (op) {
+#define WB_XMEM_ON 1
 #include "dbc_step.inc"
+#undef WB_XMEM_ON
         }
       e_next:
         if (metered && (status == WB_STATUS_RUNNING || status == WB_STATUS_OK) &&

@@ -336,6 +336,7 @@ class Lowerer {
       case OP_V_LD16X4U: case OP_V_LD32X2S: case OP_V_LD32X2U: case OP_V_LD8SPLAT:
       case OP_V_LD16SPLAT: case OP_V_LD32SPLAT: case OP_V_LD64SPLAT: case OP_V_LD32ZERO:
       case OP_V_LD64ZERO: case OP_V_LDLANE: case OP_V_STLANE:
+      case OP_XLD: case OP_XST: case OP_XLANE: case OP_XMEM_FILL: case OP_XMEM_COPY: case OP_XMEM_INIT:
         return true;
       default:
         return op >= OP_BR_EQ && op <= OP_BR_GE_U_I;
@@ -603,6 +604,25 @@ class Lowerer {
   void do_simple(const SimpleOp &s);
   void do_load(uint16_t dop, uint8_t rtype, Reader &r);
   void do_store(uint16_t dop, uint8_t vtype, Reader &r);
+  // MultiMemories (instruction.cpp:144-156, 374-389; formchecker.cpp:245-252)
+  uint32_t nmems() const { return (P.has_mem ? 1u : 0u) + uint32_t(P.xmems.size()); }
+  void check_mem(uint32_t k) {
+    if (k >= nmems()) fail(P.multi_memory && nmems() ? 0x47 : E_TYPECHECK, "unknown memory");
+  }
+  // a memory-index immediate: a u32 with the proposal, else a zero byte
+  uint32_t memidx(Reader &r) {
+    if (P.multi_memory) return r.u32();
+    if (r.u8() != 0) fail(E_TYPECHECK, "unknown memory");
+    return 0;
+  }
+  // a memarg: align, offset, then (the proposal, align >= 64) the memory index
+  uint32_t memarg(Reader &r, uint32_t *off) {
+    const uint32_t al = r.u32();
+    *off = r.u32();
+    const uint32_t k = P.multi_memory && al >= 64 ? r.u32() : 0;
+    check_mem(k);
+    return k;
+  }
   void do_call(uint32_t callee);
 };
 
@@ -715,27 +735,27 @@ bool Lowerer::try_fuse_branch(const Entry &cond, bool branch_if_true, Ctrl &f) {
 }
 
 void Lowerer::do_load(uint16_t dop, uint8_t rtype, Reader &r) {
-  r.u32();
-  uint32_t off = r.u32();
-  if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
+  uint32_t off;
+  const uint32_t k = memarg(r, &off);
   Entry a = pop_t(I32);
-  if (a.var) P.divergent_mem = true;
+  if (a.var && !k) P.divergent_mem = true;
   if (!live()) { push_cell(rtype); return; }
   uint32_t ac = src(a);
-  emit(dop, ac, 0, a.cell, 0, off);
+  if (k) emit(OP_XLD, ac, k, a.cell, dop, off);   // (memory k: the per-lane step)
+  else emit(dop, ac, 0, a.cell, 0, off);
   push_cell(rtype, last_emit);
 }
 
 void Lowerer::do_store(uint16_t dop, uint8_t vtype, Reader &r) {
-  r.u32();
-  uint32_t off = r.u32();
-  if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
+  uint32_t off;
+  const uint32_t k = memarg(r, &off);
   Entry v = pop_t(vtype);
   Entry a = pop_t(I32);
-  if (a.var) P.divergent_mem = true;
+  if (a.var && !k) P.divergent_mem = true;
   if (!live()) return;
   uint32_t ac = src(a), vc = src(v);
-  emit(dop, ac, vc, 0, 0, off);
+  if (k) emit(OP_XST, ac, vc, k, dop, off);
+  else emit(dop, ac, vc, 0, 0, off);
 }
 
 void Lowerer::do_call(uint32_t callee) {
@@ -1225,17 +1245,25 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
       case 0x3D: do_store(OP_ST16, I64, r); break;
       case 0x3E: do_store(OP_ST32, I64, r); break;
       case 0x3F: {  // memory.size (memoryInstr.cpp:9-15)
-        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
-        if (live()) { emit(OP_MEM_SIZE, 0, 0, top_cell()); push_cell(I32, last_emit); }
-        else push_cell(I32);
+        const uint32_t k = memidx(r);
+        check_mem(k);
+        if (live()) {
+          if (k) emit(OP_XMEM_SIZE, 0, k, top_cell());
+          else emit(OP_MEM_SIZE, 0, 0, top_cell());
+          push_cell(I32, last_emit);
+        } else {
+          push_cell(I32);
+        }
         break;
       }
       case 0x40: {  // memory.grow (memoryInstr.cpp:17-31)
-        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        const uint32_t k = memidx(r);
+        check_mem(k);
         Entry n = pop_t(I32);
         if (!live()) { push_cell(I32); break; }
         uint32_t a = src(n);
-        emit(OP_MEM_GROW, a, 0, n.cell);
+        if (k) emit(OP_XMEM_GROW, a, k, n.cell);
+        else emit(OP_MEM_GROW, a, 0, n.cell);
         push_cell(I32, last_emit);
         break;
       }
@@ -1278,11 +1306,14 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
                    uint32_t k[4] = {f, 0, 0, 0}; push_const(FUNCREF, k); break; }
       case 0xFC08: {  // memory.init (memoryInstr.cpp:33-49)
         uint32_t di = r.u32();
-        if (r.u8() != 0 || !P.has_mem || di >= P.datas.size()) fail(E_TYPECHECK, "unknown data");
+        const uint32_t k = memidx(r);
+        check_mem(k);   // (the memory first, formchecker.cpp:812-824)
+        if (di >= P.datas.size()) fail(P.multi_memory ? 0x4A : E_TYPECHECK, "unknown data");
         Entry n = pop_t(I32), s = pop_t(I32), d = pop_t(I32);
         if (!live()) break;
         uint32_t dc = src(d), sc = src(s), nc = src(n);
-        emit(OP_MEM_INIT, dc, sc, nc, 0, di);
+        if (k) emit(OP_XMEM_INIT, dc, sc, nc, k, di);
+        else emit(OP_MEM_INIT, dc, sc, nc, 0, di);
         break;
       }
       case 0xFC09: {
@@ -1292,12 +1323,15 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
         break;
       }
       case 0xFC0A: case 0xFC0B: {  // memory.copy / memory.fill (memoryInstr.cpp:59-101)
-        if (op == 0xFC0A) { r.u8(); }
-        if (r.u8() != 0 || !P.has_mem) fail(E_TYPECHECK, "unknown memory");
+        const uint32_t k = memidx(r), k2 = op == 0xFC0A ? memidx(r) : 0;
+        if (op == 0xFC0A) check_mem(k2);   // (copy: the source first, formchecker.cpp:826-834)
+        check_mem(k);
         Entry n = pop_t(I32), s = pop_t(I32), d = pop_t(I32);
         if (!live()) break;
         uint32_t dc = src(d), sc = src(s), nc = src(n);
-        emit(op == 0xFC0A ? OP_MEM_COPY : OP_MEM_FILL, dc, sc, nc);
+        if (op == 0xFC0A && (k || k2)) emit(OP_XMEM_COPY, dc, sc, nc, 0, k | (k2 << 16));
+        else if (op == 0xFC0B && k) emit(OP_XMEM_FILL, dc, sc, nc, 0, k);
+        else emit(op == 0xFC0A ? OP_MEM_COPY : OP_MEM_FILL, dc, sc, nc);
         break;
       }
       case 0xFC10: {  // table.size: a constant for the shared immutable table
@@ -1383,15 +1417,15 @@ void Lowerer::lower_function(uint32_t fi, std::vector<CallFix> &cf) {
       case 0xFD58: case 0xFD59: case 0xFD5A: case 0xFD5B: {   // v128.storeN_lane
         const bool ld = op <= 0xFD57;
         const uint32_t lg = (op - 0xFD54) & 3;                 // log2 of the lane bytes
-        r.u32();
-        uint32_t off = r.u32();
+        uint32_t off;
+        const uint32_t k = memarg(r, &off);
         uint8_t lane = r.u8();
-        if (!P.has_mem) fail(E_TYPECHECK, "unknown memory");
         if (lane >= (16u >> lg)) fail(E_TYPECHECK, "invalid lane index");
         Entry v = pop_t(V128), a = pop_t(I32);
         if (!live()) { if (ld) push_cell(V128); break; }
         uint32_t ac = src(a), vc = src(v);
-        emit(ld ? OP_V_LDLANE : OP_V_STLANE, ac, vc, ld ? a.cell : 0, lane | (lg << 8), off);
+        if (k) emit(OP_XLANE, ac, vc, ld ? a.cell : 0, lane | (lg << 4) | (ld ? 64u : 0u) | (k << 8), off);
+        else emit(ld ? OP_V_LDLANE : OP_V_STLANE, ac, vc, ld ? a.cell : 0, lane | (lg << 8), off);
         if (ld) push_cell(V128, last_emit);
         break;
       }
@@ -1683,11 +1717,16 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
               P.tables.push_back(t);
               P.ntables = uint32_t(P.tables.size());
             } else if (kind == 2) {
-              if (P.has_mem) throw Err{0x51, "multiple memories"};
+              if (P.has_mem && !P.multi_memory) throw Err{0x51, "multiple memories"};
               if (!limits_match(*h, mn, fl & 1, mx))
                 throw Err{0x61, "incompatible import type " + mod + "." + nm};
               if (h->min > 65536 || (h->has_max && h->max > 65536))
                 throw Err{0x53, "memory size must be at most 65536 pages (4GiB)"};
+              if (P.has_mem) {   // (a further memory: MultiMemories)
+                if (P.xmems.size() >= kMaxXMem) throw Err{E_UNSUPPORTED, "more than 8 memories"};
+                P.xmems.push_back(Program::MemLimits{h->min, h->has_max ? h->max : 65536u, h->has_max});
+                continue;
+              }
               P.has_mem = true;
               P.mem_min = h->min;
               P.mem_has_max = h->has_max;
@@ -1739,14 +1778,23 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
       }
       case 5: {
         uint32_t n = s.u32();
-        if (n > 1 || (n && P.has_mem)) throw Err{0x51, "multiple memories"};
-        if (n) {
+        if (!P.multi_memory && (n > 1 || (n && P.has_mem))) throw Err{0x51, "multiple memories"};
+        for (uint32_t k = 0; k < n; k++) {
           uint8_t fl = s.u8();
-          P.has_mem = true;
-          P.mem_min = s.u32();
-          if (fl & 1) { P.mem_has_max = true; P.mem_max = s.u32(); }
-          if (P.mem_min > 65536 || (P.mem_has_max && P.mem_max > 65536))
+          Program::MemLimits ml;
+          ml.min = s.u32();
+          if (fl & 1) { ml.has_max = true; ml.max = s.u32(); }
+          if (ml.min > 65536 || (ml.has_max && ml.max > 65536))
             throw Err{0x53, "memory size must be at most 65536 pages (4GiB)"};
+          if (P.has_mem) {   // (a further memory: MultiMemories)
+            if (P.xmems.size() >= kMaxXMem) throw Err{E_UNSUPPORTED, "more than 8 memories"};
+            P.xmems.push_back(ml);
+            continue;
+          }
+          P.has_mem = true;
+          P.mem_min = ml.min;
+          P.mem_has_max = ml.has_max;
+          if (ml.has_max) P.mem_max = ml.max;
         }
         break;
       }
@@ -1840,7 +1888,7 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
           uint32_t flags = s.u32();
           DataSeg d;
           d.active = !(flags & 1);
-          if (flags == 2) s.u32();
+          if (flags == 2) d.mem = s.u32();   // (segment.cpp:316-323)
           if (d.active) d.offset = eval_const(s, P, gvals, &P.init_ops).k[0];
           uint32_t m = s.u32();
           if (uint64_t(s.end - s.p) < m) throw Err{E_MALFORMED, "length out of bounds"};
@@ -1896,9 +1944,14 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
     if (e.func >= P.ntables) throw Err{E_TYPECHECK, "unknown table"};
   for (auto &e : P.global_exports)
     if (e.func >= P.global_types.size()) throw Err{E_TYPECHECK, "unknown global"};
-  for (auto &d : P.datas)
-    if (d.active && uint64_t(d.offset) + d.bytes.size() > uint64_t(P.mem_min) * 65536)
+  for (auto &d : P.datas) {
+    if (!d.active) continue;
+    const uint32_t nm = (P.has_mem ? 1u : 0u) + uint32_t(P.xmems.size());
+    if (d.mem >= nm) throw Err{uint8_t(P.multi_memory && nm ? 0x47 : E_TYPECHECK), "unknown memory"};
+    const uint32_t mn = d.mem ? P.xmems[d.mem - 1].min : P.mem_min;
+    if (uint64_t(d.offset) + d.bytes.size() > uint64_t(mn) * 65536)
       throw Err{0x63, "data segment does not fit"};
+  }
   if (P.start_func >= 0) {   // validator.cpp: the start function has type [] -> []
     if (uint64_t(P.start_func) >= P.funcs.size()) throw Err{E_TYPECHECK, "unknown function"};
     const FuncType &st = P.types[P.funcs[P.start_func].type];
@@ -2008,11 +2061,13 @@ uint64_t build_cost_pool(const Program &P, const uint64_t *tab, uint64_t limit,
 }
 
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
-                         bool exact_globals, const std::vector<HostImport> *imports, bool tail_call) {
+                         bool exact_globals, const std::vector<HostImport> *imports, bool tail_call,
+                         bool multi_memory) {
   try {
     out = Program();
     out.exact_globals = exact_globals;
     out.tail_call = tail_call;
+    out.multi_memory = multi_memory;
     parse_and_lower(wasm, len, out, imports);
     *errcode = 0;
     return "";

@@ -27,6 +27,7 @@ struct FuncType {
 
 struct DataSeg {
   bool active = true;
+  uint32_t mem = 0;                   // the memory an active segment initialises
   uint32_t offset = 0;
   std::vector<uint8_t> bytes;
 };
@@ -47,6 +48,8 @@ struct ElemSeg {
 // Per-lane table capacity beyond `min` when the table has no (or a larger) max: the
 // device analogue of the memory page budget (table.grow past it returns -1).
 constexpr uint32_t kTableGrowLimit = 4096;
+// memories past the first a module may have (MultiMemories)
+constexpr uint32_t kMaxXMem = 7;
 
 struct ExportFunc {
   std::string name;
@@ -74,6 +77,10 @@ struct Program {
   bool has_mem = false;
   uint32_t mem_min = 0, mem_max = 65536;
   bool mem_has_max = false;
+  // memories 1.. (the MultiMemories proposal; every memory instruction on them runs in the
+  // per-lane step, batch_kernel.hip "extra memories"): limits as memory 0's
+  struct MemLimits { uint32_t min = 0, max = 65536; bool has_max = false; };
+  std::vector<MemLimits> xmems;
   std::vector<DataSeg> datas;
   std::vector<uint8_t> global_types;
   std::vector<uint8_t> global_mut;
@@ -120,6 +127,10 @@ struct Program {
   // the TailCall proposal (return_call / return_call_indirect) is enabled; off, they fail
   // to load with IllegalOpCode like the reference's default (loader/ast/instruction.cpp:903-907)
   bool tail_call = false;
+  // the MultiMemories proposal: several memories and memory indices in memory
+  // instructions (instruction.cpp:144-156, 374-389); off, a second memory fails with
+  // MultiMemories (0x51, validator.cpp:107-113)
+  bool multi_memory = false;
   // some load/store address depends on per-instance data (a parameter, a loaded value, a
   // global): the batch then interleaves memory in 128-byte granules (batch_api.cpp)
   bool divergent_mem = false;
@@ -144,7 +155,8 @@ struct HostImport {
 // IncompatibleImportType 0x61).
 std::string load_program(const uint8_t *wasm, size_t len, Program &out, uint8_t *errcode,
                          bool exact_globals = false,
-                         const std::vector<HostImport> *imports = nullptr, bool tail_call = false);
+                         const std::vector<HostImport> *imports = nullptr, bool tail_call = false,
+                         bool multi_memory = false);
 
 int find_export(const Program &p, const std::string &name);
 

@@ -96,6 +96,15 @@ struct KParams {
                                 // what the core leaves to it
   uint32_t gs_grow;             // 1: a call past gs_depth parks for the host to grow the call
                                 // stack (WB_STACK_CALL) instead of trapping 0xB0
+  // memories 1..n_xmem (MultiMemories; only the per-lane step addresses them): each lane's
+  // xwords words hold them back to back, memory k at word xinfo[2(k - 1)], 4-byte words
+  // interleaved over the wave's 64 lanes ([wave][word][64]); xpages[(k - 1) * xstride +
+  // lane] = memory k's size, xinfo[2(k - 1) + 1] = its page limit (the reservation). (A
+  // device table, not arrays in KParams: indexing those would move KParams off SGPRs.)
+  uint32_t *xmem;
+  uint32_t *xpages;
+  const uint32_t *xinfo;
+  uint32_t xwords, xstride, n_xmem;
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the

@@ -566,6 +566,12 @@ class Assembler:
         def tok(k):
             return toks[k] if k < len(toks) else None
 
+        def memref(k, digits=True):   # token k names a memory ($name or index), else None
+            t = tok(k)
+            if isinstance(t, str) and t in self.mem_names:
+                return self.mem_names[t]
+            return int(t) if digits and isinstance(t, str) and t.isdigit() else None
+
         if base_kind == O.NONE:
             pass
         elif base_kind == O.LABEL:
@@ -603,6 +609,9 @@ class Assembler:
             used = 1
         elif base_kind == O.MEM or base_kind == O.MEMLANE:
             off, align = 0, nat_align
+            mi = memref(used, base_kind == O.MEM)   # (MultiMemories: the memory before the memarg)
+            if mi is not None:
+                used += 1
             while tok(used) is not None and isinstance(tok(used), str) and "=" in tok(used):
                 k, v = tok(used).split("=")
                 if k == "offset":
@@ -610,7 +619,10 @@ class Assembler:
                 elif k == "align":
                     align = int(math.log2(int(v, 0)))
                 used += 1
-            code += uleb(align) + uleb(off)
+            if mi:   # the reference's memarg order: align | 64, offset, memory index
+                code += uleb(align | 64) + uleb(off) + uleb(mi)   # (instruction.cpp:144-156)
+            else:
+                code += uleb(align) + uleb(off)
             if base_kind == O.MEMLANE:
                 code.append(int(toks[used]))
                 used += 1
@@ -627,9 +639,14 @@ class Assembler:
             code += struct.pack("<Q", _float_bits(toks[0], 64))
             used = 1
         elif base_kind == O.MEMIDX:
-            code.append(0)
+            mi = memref(0)
+            code += uleb(mi or 0)
+            used = 1 if mi is not None else 0
         elif base_kind == O.MEMMEM:
-            code += b"\x00\x00"
+            a, b = memref(0), memref(1)
+            if a is not None and b is not None:
+                used = 2
+            code += uleb(a or 0) + uleb(b or 0) if used else b"\x00\x00"
         elif base_kind == O.TABLE:
             t = 0
             if tok(0) is not None and isinstance(tok(0), str) and \
@@ -671,10 +688,11 @@ class Assembler:
             code += bytes(int(t) for t in toks[:16])
             used = 16
         elif base_kind == O.DATA:
-            code += uleb(self._resolve(toks[0], self.data_names))
-            used = 1
+            mi = memref(0) if not kind & 0x100 and tok(1) is not None and not isinstance(tok(1), list) else None
+            code += uleb(self._resolve(toks[1 if mi is not None else 0], self.data_names))
+            used = 2 if mi is not None else 1
             if not kind & 0x100:
-                code.append(0)
+                code += uleb(mi or 0)
         elif base_kind == O.ELEM:
             if kind & 0x100:
                 code += uleb(self._resolve(toks[0], self.elem_names))
@@ -780,7 +798,9 @@ class Assembler:
             segs = []
             for d in self.datas:
                 rest = list(d)
+                mi = 0
                 if rest and isinstance(rest[0], list) and rest[0][0] == "memory":
+                    mi = self._resolve(rest[0][1], self.mem_names)
                     rest = rest[1:]
                 if rest and isinstance(rest[0], list):
                     off = rest[0]
@@ -789,7 +809,8 @@ class Assembler:
                     else:
                         off = [off]
                     data = b"".join(_strbytes(s) for s in rest[1:])
-                    segs.append(b"\x00" + self._const_expr(off) + uleb(len(data)) + data)
+                    head = b"\x02" + uleb(mi) if mi else b"\x00"   # (segment.cpp:316-323)
+                    segs.append(head + self._const_expr(off) + uleb(len(data)) + data)
                 else:
                     data = b"".join(_strbytes(s) for s in rest)
                     segs.append(b"\x01" + uleb(len(data)) + data)
