@@ -171,6 +171,8 @@ def test_gpu_multi_memory_exact(built, name):
     ctx = batch.BatchContext(wasm, len(rs), multi_memory=True)
     try:
         for rep in range(2):
+            if rep:
+                ctx.reset()   # (Execute keeps instance state: the second run starts over)
             rets, st, cnt = ctx.execute("run", batch.make_values(rs, [I32, I32]), 1)
             h = ctx.memory_hash()
             ints = batch.ret_ints(rets)

@@ -8,7 +8,7 @@ step() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-250)"
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
-step tests 900 python -u -m pytest tests/test_multimem.py tests/test_memgrow.py tests/test_layout.py tests/test_hostcall.py tests/test_deepstack.py -m gpu -v --timeout 300 --timeout-method thread
+step tests 900 python -u -m pytest tests/test_multimem.py -m gpu -v --timeout 300 --timeout-method thread
 step c2 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
 step c1 300 python bench.py --workload c1 --steps 2 --warmup 2 --no-cpu-baseline
 echo all done
