@@ -247,13 +247,6 @@ struct Em {
   // RET's return record together with the restored cells (one LDS wait instead of two):
   // ret_pf asks POST_CALL to issue it into v113, ret_pf_done tells RET it is there
   bool ret_pf = false, ret_pf_done = false;
-  // The leaf-call cache (jit_source, WB_LCC=0 turns it off): v255 = the return record of
-  // the lane's top frame as its compiled CALL pushed it, v254 / v253 = that call's spilled
-  // cells (at most 2); -2 = the frame was popped by a compiled RET and v254.. still hold the
-  // spills its POST_CALL restores; -1 = nothing. LDS always holds the truth (the CALL
-  // writes through); the cache only spares the RET's and the POST_CALL's LDS round trips
-  // for a callee that made no call. Any entry from the core (Lce stubs) invalidates it.
-  bool lcc = false;
   const std::vector<uint8_t> *nanobs = nullptr;   // nan_observable(), per pc
   bool nan_needed() const { return !(nanobs && pc < nanobs->size() && !(*nanobs)[pc]); }
   void nan_fix(const std::vector<NanItem> &items, int w) {
@@ -902,26 +895,6 @@ bool emit(Em &e, const DInstr &I) {
       e.stack_ok = !e.trip;
       for (uint32_t k = r; k-- > 0;)
         if (L != fb) e.l("v_mov_b32 %s, %s", e.v(L + k), e.v(fb + k));
-      // the leaf-call cache (Em::lcc): after a callee that made no call, the spills from
-      // v254.. (every lane's cache at -2), else from LDS
-      const bool lfast = e.lcc && L > fb && L - fb <= 2;
-      const std::string lid = std::to_string(e.run) + "_" + std::to_string(e.pc);
-      if (lfast) {
-        e.l("v_cmp_eq_u32_e32 vcc, -2, v255");
-        e.l("s_and_b64 vcc, vcc, exec");
-        e.l("s_cmp_eq_u64 vcc, exec");
-        e.l("s_cbranch_scc0 Lpcs%s", lid.c_str());
-        e.l("v_subrev_u32_e32 v102, %u, v102", L - fb);
-        for (uint32_t k = 0; k < L - fb; k++) e.l("v_mov_b32 %s, v%u", e.v(fb + k), 254 - k);
-        if (e.ret_pf) {
-          e.l("v_lshl_add_u32 %s, v102, 8, v103", X0);
-          e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X0);
-          e.l("ds_read_b32 v113, %s", X1);
-          e.l("s_waitcnt lgkmcnt(0)");
-        }
-        e.l("s_branch Lpcd%s", lid.c_str());
-        e.l("Lpcs%s:", lid.c_str());
-      }
       if (L > fb) {
         e.l("v_subrev_u32_e32 v102, %u, v102", L - fb);
         e.l("v_lshl_add_u32 %s, v102, 8, v103", X0);
@@ -933,8 +906,6 @@ bool emit(Em &e, const DInstr &I) {
         }
         e.l("s_waitcnt lgkmcnt(0)");
       }
-      if (lfast) e.l("Lpcd%s:", lid.c_str());
-      if (e.lcc) e.l("v_mov_b32 v255, -1");
       return true;
     }
     case OP_TAIL_CALL:   // the last instruction of a run (emit_tail_call)
@@ -1583,14 +1554,6 @@ void emit_call(Em &e, const DInstr &I, uint32_t pc, const std::vector<uint8_t> *
   for (uint32_t k = 0; k < n; k++) e.l("ds_write_b32 %s, %s offset:%u", X1, e.v(fb + k), k * 256u);
   e.l("v_mov_b32 %s, 0x%x", Y1, ((pc + 1) & 0xFFFFFu) | (L << 20));
   e.l("ds_write_b32 %s, %s offset:%u", X1, Y1, n * 256u);
-  if (e.lcc) {   // (the leaf-call cache: this call's record and spills)
-    if (n <= 2) {
-      e.l("v_mov_b32 v255, %s", Y1);
-      for (uint32_t k = 0; k < n; k++) e.l("v_mov_b32 v%u, %s", 254 - k, e.v(fb + k));
-    } else {
-      e.l("v_mov_b32 v255, -1");
-    }
-  }
   e.l("v_add_u32_e32 v102, %u, v102", n + 1);
   for (uint32_t k = 0; k < nargs; k++)
     if (L != fb) e.l("v_mov_b32 %s, %s", e.v(fb + k), e.v(L + k));
@@ -1631,29 +1594,12 @@ std::string emit_ret(Em &e, const DInstr &I, const std::string &split,
     e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
     e.l("v_cndmask_b32_e64 %s, v113, -1, vcc", Y1);
   } else {
-    // the leaf-call cache (Em::lcc): every lane's record in v255, no LDS round trip (the
-    // CALL that wrote it checked the LDS bound)
-    const std::string id = std::to_string(e.run) + "_" + std::to_string(e.pc);
-    if (e.lcc) {
-      e.l("v_cmp_gt_u32_e32 vcc, -2, v255");
-      e.l("s_and_b64 vcc, vcc, exec");
-      e.l("s_cmp_eq_u64 vcc, exec");
-      e.l("s_cbranch_scc0 Lrcs%s", id.c_str());
-      e.l("v_mov_b32 %s, v255", Y1);
-      e.l("s_branch Lrcg%s", id.c_str());
-      e.l("Lrcs%s:", id.c_str());
-    }
     e.l("v_lshl_add_u32 %s, v102, 8, v103", X1);
     e.l("v_subrev_u32_e32 %s, 0x100, %s", X1, X1);
     e.l("ds_read_b32 %s, %s", Y1, X1);
     e.l("v_cmp_lt_u32_e32 vcc, s93, v102");
     e.l("s_waitcnt lgkmcnt(0)");
     e.l("v_cndmask_b32_e64 %s, %s, -1, vcc", Y1, Y1);
-    if (e.lcc) {   // a cached frame is popped: its spills stay for the POST_CALL (-2)
-      e.l("Lrcg%s:", id.c_str());
-      e.l("v_cmp_gt_u32_e32 vcc, -2, v255");
-      e.l("v_cndmask_b32_e64 v255, -1, -2, vcc");
-    }
   }
   if (!known.empty()) {
     if (known.size() > 1) e.l("v_mov_b32 %s, 0x%x", X0, known[1].first);
@@ -3424,29 +3370,17 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
     if (post >= 0) inl_target[size_t(post)] = 1;
   }
   const bool ret_pf_on = !(getenv("WB_RET_PF") && getenv("WB_RET_PF")[0] == '0');
-  // the leaf-call cache (Em::lcc): modules whose compiled runs call, without trips (their
-  // slots live in v247..v255), with v253..v255 above every cell an inlined callee may use;
-  // not metered (WB_LCC=0 turns it off)
-  bool runs_call = false;
-  for (const auto &r : runs) runs_call |= op_of(P.code[r.pc + r.len - 1]) == OP_CALL;
-  const bool lcc_on = runs_call && !cost && !hybrid && 128 + 2 * P.total_cells() + 16 <= 253 &&
-                      !(getenv("WB_LCC") && getenv("WB_LCC")[0] == '0');
   for (size_t jb = 0; jb < jobs.size(); jb++) {
     const size_t k = jobs[jb].first;
     const int var = jobs[jb].second;
     const JitRun &r = runs[k];
     Em e;
     e.ret_pf = ret_pf_on && !cost && !inl_target[k] && ret_prefetch_run(P, r);
-    e.lcc = lcc_on;
     e.g = glog;
     e.run = uint32_t(k + size_t(var) * 2 * runs.size());   // (stub labels apart)
     const std::string K = std::to_string(k) + (var == 1 ? "c" : var == 2 ? "p" : "");
     if (!nob.empty()) e.nanobs = &nob;
     e.l(".p2align 6");
-    if (lcc_on && var == 0) {   // entered from the core (Ltab): the leaf-call cache is stale
-      e.l("Lce%s:", K.c_str());
-      e.l("v_mov_b32 v255, -1");
-    }
     e.l("Lb%s:", K.c_str());
     const DInstr &last = P.code[r.pc + r.len - 1];
     const uint16_t lop = op_of(last);
@@ -4126,8 +4060,7 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
   if (hybrid) body += trip_source(P, runs, glog, true);
   body = resolve_jumps(body);
   body += ".p2align 3\nLtab:\n";
-  for (size_t k = 0; k < runs.size(); k++)
-    body += std::string(".quad ") + (lcc_on ? "Lce" : "Lb") + std::to_string(k) + " - Ltab\n";
+  for (size_t k = 0; k < runs.size(); k++) body += ".quad Lb" + std::to_string(k) + " - Ltab\n";
   body += "Lend:\n";
   std::string src =
       "// generated by jit.cpp: compiled runs of the V-frame threaded core\n"
