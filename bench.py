@@ -483,6 +483,10 @@ def main():
     elapsed, ksum = ph.timed(args.steps)
     instrs_per_step, traps, ctx, n = ph.instrs_per_step, ph.traps, ph.ctx, ph.n
     total_instrs = dist.sum(instrs_per_step) * args.steps
+    # checksum of checksums over every instance's final linear memory (hash kernel, after
+    # the timed region; before the fresh-input steps, which leave other instances' states)
+    rets, st, cnt = ctx.results(1)
+    hashes = ctx.memory_hash()
     fresh = None
     if args.vary_args == "on":
         fi, fs, fk = ph.fresh(args.steps)
@@ -494,10 +498,6 @@ def main():
                          "the arguments and is not reused; SetArgs before each step's clock, "
                          "the clock covers Reset + Run as for `value`"
                          % ("262144" if args.workload == "c5" else "2^30")}
-    # checksum of checksums over every instance's final linear memory (hash kernel, after
-    # the timed region)
-    rets, st, cnt = ctx.results(1)
-    hashes = ctx.memory_hash()
     checksum = int(hashes.sum(dtype=np.uint64))
     gpu = {"counts": cnt, "hashes": hashes, "status": st, "ret": rets["lo"][:, 0],
            "ret32": args.workload not in ("c5", "mt")}
