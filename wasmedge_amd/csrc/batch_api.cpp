@@ -134,6 +134,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       !C->hip_ok(hipMalloc(&C->stop, 4), "interrupt flag"))
     return kRuntimeError;
   (void)hipMemset(C->stop, 0, 4);
+  // a lane parked for the host (KParams::parked): a host-mapped word, so a Run with no
+  // parked lane skips the service round's status copy (262 KB at 256K instances)
+  if (hipHostMalloc(reinterpret_cast<void **>(&C->parked_h), 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void **>(&C->parked_d), C->parked_h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    if (C->parked_h) (void)hipHostFree(C->parked_h);
+    C->parked_h = C->parked_d = nullptr;   // (then every Run takes the service round)
+  }
   (void)hipEventCreate(&C->ev0);
   (void)hipEventCreate(&C->ev1);
   hipStream_t s = C->stream;
@@ -462,6 +470,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
   k.gs_grow = C->gs_grow ? 1u : 0u;
+  k.parked = C->parked_d;
   if (!P.xmems.empty()) {
     k.xmem = C->xmem.ptr; k.xpages = C->xpages.ptr; k.xinfo = C->xinfo.ptr;
     k.xwords = C->xwords; k.xstride = C->nwaves * 64; k.n_xmem = uint32_t(P.xmems.size());
@@ -566,9 +575,12 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
   // (the flag is cleared only after an Interrupt: one stream operation less per run)
   if (C->stop_dirty.exchange(false) &&
       !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
+  if (C->parked_h) *C->parked_h = 0u;   // (the previous launch has ended: launch_once syncs)
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
   if (e || !(C->prog.n_imported || C->grow_host || C->gs_grow)) return e;
   for (;;) {
+    if (C->parked_h && !__atomic_load_n(C->parked_h, __ATOMIC_ACQUIRE)) return 0;   // none parked
+    if (C->parked_h) *C->parked_h = 0u;
     // every round resumes the lanes the host serviced; lanes it ended keep its code
     const int64_t k = service_host_calls(C);
     if (k < 0) return kRuntimeError;
@@ -1188,6 +1200,7 @@ void WasmEdge_BatchDelete(WasmEdge_BatchContext *C) {
   }
   if (C->ev_order) (void)hipEventDestroy(C->ev_order);
   if (C->stop) (void)hipFree(C->stop);
+  if (C->parked_h) (void)hipHostFree(C->parked_h);
   if (C->stats) (void)hipFree(C->stats);
   if (C->ev0) (void)hipEventDestroy(C->ev0);
   if (C->ev1) (void)hipEventDestroy(C->ev1);

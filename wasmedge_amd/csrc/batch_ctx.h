@@ -72,6 +72,7 @@ struct WasmEdge_BatchContext {
   hipStream_t stream = nullptr;
   hipStream_t ctl_stream = nullptr;  // interrupt requests, while `stream` runs a kernel
   uint32_t *stop = nullptr;          // uncached device word polled by the kernel
+  uint32_t *parked_h = nullptr, *parked_d = nullptr;   // host-mapped: a lane parked (KParams::parked)
   std::atomic<bool> stop_dirty{false};   // an Interrupt set *stop since the last clear
   uint64_t *stats = nullptr;         // WB_STATS builds: per-wave counters (WB_STATS_OUT)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -818,6 +818,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
     p.status[inst] = (uint8_t)status;
     p.counts[inst] = count;
     if (status == WB_ERR_HOST_CALL && fs) {   // park: the host loop takes over
+      if (p.parked) *p.parked = 1u;
       LS(LS_RPC) = pc;
       LS(LS_GSP) = gsp;
       LS(LS_HBASE) = ybase;

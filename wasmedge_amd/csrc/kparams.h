@@ -103,6 +103,8 @@ struct KParams {
   // device table, not arrays in KParams: indexing those would move KParams off SGPRs.)
   uint32_t *xmem;
   uint32_t *xpages;
+  uint32_t *parked;             // host-mapped word: 1 when a lane parked for the host (the host
+                                // then runs its service round; 0 = none parked, no round)
   const uint32_t *xinfo;
   uint32_t xwords, xstride, n_xmem;
 };
