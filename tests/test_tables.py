@@ -70,8 +70,8 @@ TABLES = assemble(r"""
 )
 """)
 
-# a table that grows to its max, then refuses (-1); the whole table refilled. (A table
-# with no max grows on the device up to min + kTableGrowLimit = 4096 slots, DESIGN.md.)
+# a table that grows to its max, then refuses (-1); the whole table refilled. (Past its
+# first min + kTableGrowLimit slots a table widens at run time: WIDE below.)
 GROW = assemble(r"""
 (module
   (table $t 1 3000 funcref)
@@ -146,3 +146,57 @@ def test_gpu_table_grow(built):
     ref = _oracle(GROW, "grow", GROW_ARGS)
     got, st, cnt, h = _gpu_rounds(GROW, "grow", [GROW_ARGS])[0]
     assert compare(ref, got, st, cnt, h, [I32]) == []
+
+
+# Tables widen past their first per-lane capacity (min + kTableGrowLimit): a table.grow
+# past it parks the lane, the host relays every lane's tables out wider (hostcall.cpp
+# widen_tables) and the grow runs again -- as the reference's Refs vector grows (table.h:
+# 59-72) up to the table's max. One big grow per lane, three more of 1500 each, an
+# externref table up to its max (past it: -1); the entries written before a relayout
+# survive it (call_indirect through slot 0 and through the big grow's last slot).
+WIDE = assemble(r"""
+(module
+  (type $v (func (result i32)))
+  (table $t 2 funcref)
+  (table $u 1 20000 externref)
+  (func $g (type $v) (i32.const 5))
+  (func $h (type $v) (i32.const 9))
+  (elem declare func $g)
+  (elem (table $t) (i32.const 0) func $h)
+  (func (export "widen") (param $x i32) (result i32)
+    (local $a i32) (local $k i32) (local $s i32) (local $r i32)
+    (local.set $a (table.grow $t (ref.func $g) (i32.mul (local.get $x) (i32.const 997))))
+    (loop $l
+      (local.set $s (i32.add (local.get $s) (table.grow $t (ref.null func) (i32.const 1500))))
+      (local.set $k (i32.add (local.get $k) (i32.const 1)))
+      (br_if $l (i32.lt_u (local.get $k) (i32.const 3))))
+    (local.set $s (i32.add (local.get $s)
+      (table.grow $u (ref.null extern) (i32.mul (local.get $x) (i32.const 311)))))
+    (local.set $r (i32.add (i32.add (local.get $a) (local.get $s))
+      (i32.add (i32.mul (table.size $t) (i32.const 7)) (i32.mul (table.size $u) (i32.const 3)))))
+    (local.set $r (i32.add (local.get $r)
+      (i32.mul (call_indirect $t (type $v) (i32.const 0)) (i32.const 100))))
+    (if (local.get $x)
+      (then (local.set $r (i32.add (local.get $r)
+        (i32.mul (call_indirect $t (type $v) (i32.add (local.get $a) (i32.const 1))) (i32.const 1000))))))
+    (i32.add (local.get $r)
+      (i32.mul (ref.is_null (table.get $t (i32.sub (table.size $t) (i32.const 1)))) (i32.const 10000))))
+)
+""")
+WIDE_ROUNDS = [[[x] for x in range(130)], [[(7 * x + 3) % 130] for x in range(130)]]
+
+
+def test_table_widen_emulator(built):
+    ref = _oracle_rounds(WIDE, "widen", WIDE_ROUNDS[:1])[0]
+    assert max(r[1][0] for r in ref if r[0] == 0) > 4096 * 7   # (past the first capacity)
+    rets, st, cnt, h = emu_run(WIDE, "widen", WIDE_ROUNDS[0], [I32], [I32])
+    assert compare(ref, rets, st, cnt, h, [I32]) == []
+
+
+@pytest.mark.gpu
+def test_gpu_table_widen(built):
+    """Two invocations on the same 130 instances: the second grows the widened tables
+    again (and widens them further), entries and sizes carried over."""
+    ref = _oracle_rounds(WIDE, "widen", WIDE_ROUNDS)
+    for r, (got, st, cnt, h) in enumerate(_gpu_rounds(WIDE, "widen", WIDE_ROUNDS)):
+        assert compare(ref[r], got, st, cnt, h, [I32]) == [], "round %d" % r

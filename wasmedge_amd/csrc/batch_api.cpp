@@ -195,6 +195,16 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
   const char *sge = getenv("WB_STACK_GROW");
   C->gs_grow = !C->conf.CallStackCells && !(sge && sge[0] == '0');
+  // per-lane tables widen past their first capacity up to table_widen_limit (WB_TABLE_WIDEN=0
+  // keeps the first capacity: test aid)
+  std::vector<uint32_t> tlim;
+  const char *twe = getenv("WB_TABLE_WIDEN");
+  if (P.mut_tables && !(twe && twe[0] == '0'))
+    for (uint32_t t = 0; t < P.ntables; t++) {
+      tlim.push_back(wb::table_widen_limit(P.tables[t]));
+      C->tg_grow |= tlim.back() > P.tabinfo[2 * t + 1];
+    }
+  if (!C->tg_grow) tlim.clear();
   // module image: active data segments over the initial pages
   std::vector<uint32_t> img;
   std::vector<uint8_t> pool;
@@ -324,7 +334,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
             C->global_init.upload(ls_init, s) && C->image.upload(img, s) &&
             C->tab_image.upload(P.tab_image, s) && C->tabinfo.upload(P.tabinfo, s) &&
             C->elem_pool.upload(P.elem_pool, s) && C->elem_off.upload(P.elem_off, s) &&
-            C->elem_len.upload(P.elem_len, s) &&
+            C->elem_len.upload(P.elem_len, s) && (!C->tg_grow || C->tlimit.upload(tlim, s)) &&
             (!C->conf.CostLimit || (C->cost_off.upload(C->cost_off_h, s) &&
                                     C->cost_pool.upload(C->cost_pool_h, s))) &&
             C->funcs.upload(fv, s) && C->data_pool.upload(pool, s) &&
@@ -360,7 +370,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       (!P.xmems.empty() && (!C->xmem.alloc(nw * 64 * size_t(C->xwords) + 64) ||
                             !C->xpages.alloc(C->xpages0.size()))) ||
       (C->frame_hbm && !C->hframe.alloc(nw * size_t(P.total_cells()) * 64)) ||
-      ((P.n_imported || C->grow_host || C->gs_grow) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
+      ((P.n_imported || C->grow_host || C->gs_grow || C->tg_grow) && (!C->fsave.alloc(nw * size_t(P.total_cells() + C->gs_lds) * 64) ||
                         !C->hcall.alloc(C->n) || !C->hbuf.alloc(size_t(C->n) * C->hb_cells))))
     return C->fail(kRuntimeError, "device allocation of instance state failed (" +
                                       std::to_string(nw * size_t(C->mem_words) * 256 >> 20) +
@@ -470,6 +480,8 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   k.gs_depth = C->gs_depth;
   k.gs_lds = C->gs_lds;
   k.gs_grow = C->gs_grow ? 1u : 0u;
+  k.tg_grow = C->tg_grow ? 1u : 0u;
+  k.tlimit = C->tlimit.ptr;
   k.parked = C->parked_d;
   if (!P.xmems.empty()) {
     k.xmem = C->xmem.ptr; k.xpages = C->xpages.ptr; k.xinfo = C->xinfo.ptr;
@@ -577,7 +589,7 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
       !C->hip_ok(hipMemsetAsync(C->stop, 0, 4, C->stream), "interrupt flag")) return kRuntimeError;
   if (C->parked_h) *C->parked_h = 0u;   // (the previous launch has ended: launch_once syncs)
   uint8_t e = launch_once(C, entry_pc, is_start, false, KernelSeconds);
-  if (e || !(C->prog.n_imported || C->grow_host || C->gs_grow)) return e;
+  if (e || !(C->prog.n_imported || C->grow_host || C->gs_grow || C->tg_grow)) return e;
   for (;;) {
     if (C->parked_h && !__atomic_load_n(C->parked_h, __ATOMIC_ACQUIRE)) return 0;   // none parked
     if (C->parked_h) *C->parked_h = 0u;

@@ -156,6 +156,10 @@ struct WasmEdge_BatchContext {
   // the call stack grows on demand (CallStackCells 0): a call past gs_depth parks, the host
   // doubles the stack (grow_stack) while device memory allows (KParams::gs_grow)
   bool gs_grow = false;
+  // per-lane tables widen on demand: a table.grow past its capacity parks, the host relays
+  // the tables out wider (hostcall.cpp widen_tables; KParams::tg_grow / tlimit)
+  bool tg_grow = false;
+  DevBuf<uint32_t> tlimit;
   // Paged linear memory (DESIGN.md "Linear memory"): `mem_max_pages` is the page limit
   // (65536, the module's max, MaxMemoryPage); pages [0, rpages) of every lane live in the
   // reserved layout at `mem` (mem_words = rpages * 16384 words per lane), page q >= rpages

@@ -355,6 +355,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   uint32_t *const lt = p.ltab ? p.ltab + (size_t)(inst >> 6) * p.tab_words * 64u + (inst & 63u) : nullptr;
 #define TSIZE(t) LS(p.ls_tab + (t))
 #define TENT(t, i) lt[(size_t)(p.tabinfo[2u * (t)] + (i)) << 6]
+#define WB_TWIDEN(t, want) ((void)0)   // (a grow past the capacity parks before the step)
 // dropped element segments: mask words after the table sizes; dropped data segments: the
 // first 32 in `dropped` (LS_DROPPED), the rest in mask words at ls_drop_ext (slow paths only)
 #define ELEM_DROPPED(e) ((LS(p.ls_tab + p.ntables + ((e) >> 5)) >> ((e) & 31u)) & 1u)
@@ -732,6 +733,21 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         add = 0;
         npc = pcs;
         goto s_done;
+      }
+      // a table.grow past its table's per-lane capacity, within the table's widen limit
+      // (KParams::tg_grow; the reference's Refs vector grows up to the max, table.h:59-72):
+      // the lane parks with the request n staged (ybase = its cell) for the host to widen
+      // every lane's table (hostcall.cpp widen_tables) and runs the grow again on resume
+      if (p.tg_grow && op == OP_TABLE_GROW) {
+        const uint64_t want = (uint64_t)TSIZE(D_) + R32(B_);
+        if (want > p.tabinfo[2u * D_ + 1u] && want <= p.tlimit[D_]) {
+          status = WB_ERR_HOST_CALL;
+          ycall = WB_TGROW_CALL | D_;
+          ybase = B_;
+          add = 0;
+          npc = pcs;
+          goto s_done;
+        }
       }
       if (p.cost_off && gas_step(p.cost_pool + coff, 0, cnt8 - post8, p.cost_limit, cost, add)) {
         status = 0x03u;

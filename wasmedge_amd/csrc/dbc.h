@@ -186,3 +186,8 @@ struct DFunc {
 // (KParams::gs_grow): the host grows it and the lane runs the call again (hostcall.cpp
 // grow_stack)
 #define WB_STACK_CALL 0xFFFFFFFDu
+// ... | t when a table.grow would pass table t's per-lane capacity while tables may still
+// widen (KParams::tg_grow; t < 2^24): the host widens every lane's table t and the lane runs
+// the grow again (hostcall.cpp widen_tables)
+#define WB_TGROW_CALL 0xF0000000u
+#define WB_TGROW_MASK 0xFF000000u

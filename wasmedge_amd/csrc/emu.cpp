@@ -168,6 +168,36 @@ __attribute__((visibility("default"))) int wb_emu_execute(
 #define SET_ELEM_DROPPED(e) (edrop[(e) >> 5] |= 1u << ((e) & 31u))
 #define DATA_DROPPED(s) ((dropped[(s) >> 5] >> ((s) & 31u)) & 1u)
 #define SET_DATA_DROPPED(s) (dropped[(s) >> 5] |= 1u << ((s) & 31u))
+  // a table.grow past table t's capacity: the tables widen as the library's host service
+  // does (hostcall.cpp widen_tables: at least double, within table_widen_limit), this
+  // instance's entries and the image later instances start from relaid out together
+  const char *twe = getenv("WB_TABLE_WIDEN");   // (=0: the first capacity stays, as the library's)
+  const bool no_widen = twe && twe[0] == '0';
+  auto twiden = [&](uint32_t t, uint64_t want) {
+    if (no_widen || want > wb::table_widen_limit(P.tables[t])) return;
+    const uint64_t cap = std::min<uint64_t>(wb::table_widen_limit(P.tables[t]),
+                                            std::max<uint64_t>(want, 2ull * P.tabinfo[2 * t + 1]));
+    std::vector<uint32_t> info(P.tabinfo.size());
+    uint64_t words = 0;
+    for (uint32_t u = 0; u < P.ntables; u++) {
+      info[2 * u] = uint32_t(words);
+      info[2 * u + 1] = u == t ? uint32_t(cap) : P.tabinfo[2 * u + 1];
+      words += info[2 * u + 1];
+    }
+    std::vector<uint32_t> nl(words, 0xFFFFFFFFu), ni(words, 0xFFFFFFFFu);
+    for (uint32_t u = 0; u < P.ntables; u++) {
+      const uint32_t f = P.tabinfo[2 * u], c = P.tabinfo[2 * u + 1];
+      std::copy(ltabv.begin() + f, ltabv.begin() + f + c, nl.begin() + info[2 * u]);
+      std::copy(P.tab_image.begin() + f, P.tab_image.begin() + f + c, ni.begin() + info[2 * u]);
+    }
+    ltabv.swap(nl);
+    P.tab_image.swap(ni);
+    P.tabinfo.swap(info);
+    P.tab_words = uint32_t(words);
+    p.tabinfo = P.tabinfo.data();
+    p.tab_words = P.tab_words;
+  };
+#define WB_TWIDEN(t, want) twiden((t), (want))
   std::vector<uint32_t> frame(P.total_cells() + 8), gstack(gs_depth);
   std::vector<uint32_t> memv;
   // gas metering: per DBC prefix sums of its instructions' costs (unit table by default)

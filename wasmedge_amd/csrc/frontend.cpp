@@ -2003,8 +2003,8 @@ void parse_and_lower(const uint8_t *wasm, size_t len, Program &P,
     }
   }
   if (P.mut_tables) {
-    // per-lane table words: each table gets min + kTableGrowLimit slots (bounded by its
-    // max); element segment pool for table.init; active and declarative segments
+    // per-lane table words: each table starts with min + kTableGrowLimit slots (bounded by
+    // its max; a grow past them widens the tables at run time); element segment pool for table.init; active and declarative segments
     // start dropped (elem.cpp)
     P.init_edropped.assign((P.elems.size() + 31) / 32 + (P.elems.empty() ? 1 : 0), 0u);
     for (uint32_t t = 0; t < P.ntables; t++) {

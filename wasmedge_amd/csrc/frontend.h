@@ -45,9 +45,15 @@ struct ElemSeg {
   std::vector<uint32_t> items;        // function index per item, 0xFFFFFFFF = null ref
 };
 
-// Per-lane table capacity beyond `min` when the table has no (or a larger) max: the
-// device analogue of the memory page budget (table.grow past it returns -1).
+// Per-lane table capacity beyond `min` a table starts with when it has no (or a larger)
+// max; a table.grow past it widens every lane's table (hostcall.cpp widen_tables).
 constexpr uint32_t kTableGrowLimit = 4096;
+// The most entries a table can widen to per lane (with its max, if smaller): table.grow
+// past it returns -1, as at the reference's Refs vector failing to grow (table.h:59-72).
+constexpr uint32_t kTableWidenMax = 1u << 24;
+inline uint32_t table_widen_limit(const struct TableInfo &T) {
+  return T.has_max && T.max < kTableWidenMax ? T.max : kTableWidenMax;
+}
 // memories past the first a module may have (MultiMemories)
 constexpr uint32_t kMaxXMem = 7;
 

@@ -398,6 +398,102 @@ bool grow_stack(WasmEdge_BatchContext *C, uint64_t need) {
   return true;
 }
 
+// Every lane's per-lane tables relaid out wider, between launches: table t to at least
+// need[t] entries (at least double, within table_widen_limit), the others as they were.
+// [wave][tab_words][64] copied table by table into a new buffer whose new slots are null;
+// the image Reset starts from and tabinfo follow. False (nothing changed) when 3/4 of the
+// device memory left does not hold the new tables.
+static bool widen_tables(WasmEdge_BatchContext *C, const std::vector<uint64_t> &need) {
+  wb::Program &P = C->prog;
+  std::vector<uint32_t> info(P.tabinfo.size());
+  uint64_t words = 0;
+  for (uint32_t t = 0; t < P.ntables; t++) {
+    uint64_t cap = P.tabinfo[2 * t + 1];
+    if (need[t] > cap)
+      cap = std::min<uint64_t>(wb::table_widen_limit(P.tables[t]), std::max<uint64_t>(need[t], 2 * cap));
+    info[2 * t] = uint32_t(words);
+    info[2 * t + 1] = uint32_t(cap);
+    words += cap;
+  }
+  size_t free_b = 0, total_b = 0;
+  (void)hipMemGetInfo(&free_b, &total_b);
+  const uint64_t nw = C->nwaves, bytes = nw * words * 256;
+  if (words >= (1ull << 28) || bytes > uint64_t(free_b) / 4 * 3) return false;
+  uint32_t *nt = nullptr;
+  if (hipMalloc(&nt, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  bool ok = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(nt), 0xFFFFFFFFu, nw * words * 64, C->stream) == hipSuccess;
+  for (uint32_t t = 0; ok && t < P.ntables; t++) {
+    const uint64_t f = P.tabinfo[2 * t], c = P.tabinfo[2 * t + 1], nf = info[2 * t];
+    if (!c) continue;
+    // (one 2D copy per table: rows = waves, each the table's c x 64 words of that wave)
+    ok = hipMemcpy2DAsync(nt + nf * 64, words * 256, C->ltab.ptr + f * 64, uint64_t(P.tab_words) * 256,
+                          c * 256, nw, hipMemcpyDeviceToDevice, C->stream) == hipSuccess;
+  }
+  ok = ok && hipStreamSynchronize(C->stream) == hipSuccess;
+  if (!ok) {
+    (void)hipFree(nt);
+    (void)hipGetLastError();
+    return false;
+  }
+  std::vector<uint32_t> img(words, 0xFFFFFFFFu);
+  for (uint32_t t = 0; t < P.ntables; t++)
+    std::copy(P.tab_image.begin() + P.tabinfo[2 * t], P.tab_image.begin() + P.tabinfo[2 * t] + P.tabinfo[2 * t + 1],
+              img.begin() + info[2 * t]);
+  (void)hipFree(C->ltab.ptr);
+  C->ltab.ptr = nt;
+  C->ltab.n = nw * words * 64;
+  P.tab_image.swap(img);
+  P.tabinfo.swap(info);
+  P.tab_words = uint32_t(words);
+  return C->tab_image.upload(P.tab_image, C->stream) && C->tabinfo.upload(P.tabinfo, C->stream) &&
+         hipStreamSynchronize(C->stream) == hipSuccess;
+}
+
+// Lanes parked at a table.grow past their table's capacity (WB_TGROW_CALL | t; the request
+// n in their staged cell): every table asked for widens to the largest size a lane asks
+// (widen_tables), and every such lane runs its grow again -- or, with no device memory left
+// for it, the tables stop widening and the grow returns -1 as at a fixed capacity.
+static bool serve_table_grows(WasmEdge_BatchContext *C, const std::vector<uint32_t> &parked,
+                              std::vector<uint32_t> &hcall, const std::vector<uint32_t> &hbuf,
+                              int64_t *resumed) {
+  const wb::Program &P = C->prog;
+  const uint32_t nw = C->nwaves, hb = C->hb_cells;
+  std::vector<uint8_t> asked(P.ntables, 0);
+  bool any = false;
+  for (uint32_t i : parked)
+    if ((hcall[i] & WB_TGROW_MASK) == WB_TGROW_CALL) {
+      asked[hcall[i] & ~WB_TGROW_MASK] = 1;
+      any = true;
+    }
+  if (!any) return true;
+  // table sizes of the tables asked for: one 256-byte row per wave each
+  const size_t row = 64 * sizeof(uint32_t), pitch = size_t(C->ls_slots) * row;
+  std::vector<std::vector<uint32_t>> size(P.ntables);
+  for (uint32_t t = 0; t < P.ntables; t++) {
+    if (!asked[t]) continue;
+    size[t].assign(size_t(nw) * 64, 0);
+    if (!C->hip_ok(hipMemcpy2D(size[t].data(), row, C->lstate.ptr + size_t(LS_GLOBALS + P.global_cells + t) * 64,
+                               pitch, row, nw, hipMemcpyDeviceToHost), "table sizes"))
+      return false;
+  }
+  std::vector<uint64_t> need(P.ntables, 0);
+  for (uint32_t i : parked)
+    if ((hcall[i] & WB_TGROW_MASK) == WB_TGROW_CALL) {
+      const uint32_t t = hcall[i] & ~WB_TGROW_MASK;
+      need[t] = std::max<uint64_t>(need[t], uint64_t(size[t][i]) + hbuf[size_t(i) * hb]);
+    }
+  if (!widen_tables(C, need)) C->tg_grow = false;
+  for (uint32_t i : parked)
+    if ((hcall[i] & WB_TGROW_MASK) == WB_TGROW_CALL) {
+      hcall[i] = 0;   // (no result cells: the grow runs again)
+      ++*resumed;
+    }
+  return true;
+}
+
 // Lanes parked at a memory.grow past their wave's rows (WB_GROW_CALL; the request n in
 // their staged result cell): per wave, rows for the largest request (plus a quarter of what
 // the wave holds, so that a lane growing page by page parks rarely), then each lane's grow
@@ -507,7 +603,8 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
   int64_t grown = 0;
   std::vector<uint8_t> hcall_grow(parked.size(), 0);
   for (size_t j = 0; j < parked.size(); j++)
-    hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL || hcall[parked[j]] == WB_STACK_CALL;
+    hcall_grow[j] = hcall[parked[j]] == WB_GROW_CALL || hcall[parked[j]] == WB_STACK_CALL ||
+                    (hcall[parked[j]] & WB_TGROW_MASK) == WB_TGROW_CALL;
   if (C->grow_host) {
     serve_grows(C, parked, hcall, hbuf, pages, &pages_dirty, &grown);
     if (!pool_upload(C)) return -1;
@@ -534,6 +631,8 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
         }
     }
   }
+  // table.grow past a table's capacity (WB_TGROW_CALL | t)
+  if (C->tg_grow && !serve_table_grows(C, parked, hcall, hbuf, &grown)) return -1;
   RoundCache rc;
   rc.C = C;
   rc.w0 = waves.front().first;

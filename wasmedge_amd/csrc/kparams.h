@@ -107,6 +107,11 @@ struct KParams {
                                 // then runs its service round; 0 = none parked, no round)
   const uint32_t *xinfo;
   uint32_t xwords, xstride, n_xmem;
+  // 1: a table.grow past its table's capacity (tabinfo), within tlimit[t] (frontend.h
+  // table_widen_limit), parks for the host to widen the tables (WB_TGROW_CALL | t) instead
+  // of returning -1
+  uint32_t tg_grow;
+  const uint32_t *tlimit;
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
