@@ -237,7 +237,8 @@ typedef struct WasmEdge_BatchImport {
   enum WasmEdge_ValType Type;   /* table: FuncRef / ExternRef; global: its value type */
   uint32_t Mutable;             /* global: 1 = var */
   WasmEdge_Value Value;         /* global: its initial value (a funcref is a function
-                                   index of the module, null 0xFFFFFFFF) */
+                                   index of the module, an externref any 64-bit value,
+                                   null 0xFFFFFFFF) */
 } WasmEdge_BatchImport;
 
 /* WasmEdge_BatchCreate with the module's table / memory / global imports provided. */
@@ -419,9 +420,11 @@ WASMEDGE_BATCH_API WasmEdge_Result WasmEdge_BatchSetMemory(WasmEdge_BatchContext
  * WasmEdge_StoreFindTable/FindGlobal + WasmEdge_TableInstanceGetData/SetData/GetSize,
  * lib/api/wasmedge.cpp:2099-2139, and WasmEdge_GlobalInstanceGetValue/SetValue,
  * :2273-2295). Inst = WASMEDGE_BATCH_ALL_INSTANCES writes every instance. Reference
- * values are 32-bit on the device: a funcref is the module's function index, an
- * externref a host-chosen handle (a host function receives it in its argument), null is
- * 0xFFFFFFFF. TableGetData/SetData: TableOutOfBounds (0x87) past the instance's table
+ * values: a funcref is the module's function index; an externref is any 64-bit host value
+ * (a pointer, as WasmEdge_ValueGenExternRef makes, wasmedge.h:254,318), given back
+ * unchanged wherever it leaves the batch (results, host-function arguments, table and
+ * global reads); null is 0xFFFFFFFF for both. (On the device refs are 32-bit: a value
+ * from 2^31 up is carried as a handle the context interns.) TableGetData/SetData: TableOutOfBounds (0x87) past the instance's table
  * size, RefTypeMismatch (0x8E) for a value of the wrong reference type. GlobalSetValue
  * ignores a constant global or a value of another type, as the reference does. An
  * unknown export name gives FuncNotFound (0x05). Writes persist until BatchReset. */

@@ -197,3 +197,69 @@ def test_gpu_externref_stl_reference_answers(built):
         assert [int(r[0]) for r in batch.ret_ints(rets)] == [40 + 50 + 60 + 70 + 80] * n
     finally:
         ctx.close()
+
+
+# ---- 64-bit externref values: the reference's externrefs are host pointers
+# (WasmEdge_ValueGenExternRef(void*), wasmedge.h:254,318; ExternrefTest.cpp passes &AddClass).
+# Values from 2^31 up cross the boundary unchanged -- arguments, results, host-function
+# arguments and results, table and global reads and writes -- while the device carries a
+# 32-bit handle the context interns (batch_ctx.h xref_in / xref_out).
+def _keep_wasm():
+    from wasmedge_amd.wat import assemble
+    return assemble(r"""
+(module
+  (import "env" "echo" (func $echo (param externref) (result externref)))
+  (table $t 4 externref)
+  (global $g (mut externref) (ref.null extern))
+  (export "t" (table $t))
+  (export "g" (global $g))
+  (func (export "keep") (param $a externref) (param $b externref) (result externref)
+    (table.set $t (i32.const 1) (local.get $a))
+    (global.set $g (local.get $b))
+    (call $echo (table.get $t (i32.const 1))))
+  (func (export "peek") (result externref) (table.get $t (i32.const 2)))
+)
+""")
+
+
+def _ptr(i, k):
+    """A pointer-like 64-bit value, distinct per (lane, k)."""
+    return 0x00007F3A5C000000 + (i * 4 + k) * 48
+
+
+@pytest.mark.gpu
+def test_gpu_externref_64bit_values(built):
+    from wasmedge_amd import batch
+    n = 130
+    seen = {}
+
+    def echo(mem, a):
+        seen[mem.instance] = a[0]
+        return 0, [a[0]]
+
+    ctx = batch.BatchContext(_keep_wasm(), n, device=0)
+    try:
+        ctx.add_host_function("env", "echo", echo, 1, 1)
+        rows = [[_ptr(i, 0), NULL if i % 5 == 3 else _ptr(i, 1)] for i in range(n)]
+        rets, st, cnt = ctx.execute("keep", batch.make_values(rows, [EXTERNREF, EXTERNREF]), 1)
+        assert (st == 0).all()
+        assert [int(r[0]) for r in batch.ret_ints(rets)] == [r[0] for r in rows]
+        assert seen == {i: rows[i][0] for i in range(n)}        # the host saw the pointer
+        for i in (0, 3, 64, 129):
+            assert ctx.table_get("t", i, 1) == (rows[i][0], EXTERNREF)
+            assert ctx.global_get("g", i) == (rows[i][1], EXTERNREF)
+            assert ctx.table_get("t", i, 0) == (NULL, EXTERNREF)
+        # written by the host through the API, read back by the module and the API
+        for i in range(n):
+            ctx.table_set("t", i, 2, _ptr(i, 2), EXTERNREF)
+        ctx.global_set("g", 7, _ptr(7, 3), EXTERNREF)
+        rets, st, cnt = ctx.execute("peek", batch.make_values([[]] * n, []), 1)
+        assert (st == 0).all()
+        assert [int(r[0]) for r in batch.ret_ints(rets)] == [_ptr(i, 2) for i in range(n)]
+        assert ctx.global_get("g", 7) == (_ptr(7, 3), EXTERNREF)
+        # small values stay their own device refs (the handles the tests above use)
+        rets, st, cnt = ctx.execute("keep", batch.make_values([[5, 6]] * n, [EXTERNREF, EXTERNREF]), 1)
+        assert [int(r[0]) for r in batch.ret_ints(rets)] == [5] * n
+        assert ctx.global_get("g", 0) == (6, EXTERNREF)
+    finally:
+        ctx.close()

@@ -217,7 +217,7 @@ def make_values(rows, types):
         for k, t in enumerate(types):
             col = arr[:, k].astype(np.uint64) if arr.dtype.kind == "u" else \
                 arr[:, k].astype(np.int64).view(np.uint64)
-            if t in (I32, F32, FUNCREF, EXTERNREF):
+            if t in (I32, F32, FUNCREF):   # (an externref is any 64-bit host value)
                 col = col & np.uint64(0xFFFFFFFF)
             out["lo"][:, k] = col
             out["type"][:, k] = t
@@ -227,9 +227,9 @@ def make_values(rows, types):
     for i, r in enumerate(rows):
         for k, t in enumerate(types):
             v = int(r[k]) & ((1 << 128) - 1)
-            if t in (I32, F32, FUNCREF, EXTERNREF):
+            if t in (I32, F32, FUNCREF):
                 v &= 0xFFFFFFFF
-            elif t in (I64, F64):
+            elif t in (I64, F64, EXTERNREF):
                 v &= (1 << 64) - 1
             out["lo"][i, k] = v & 0xFFFFFFFFFFFFFFFF
             out["hi"][i, k] = v >> 64

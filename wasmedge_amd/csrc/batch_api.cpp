@@ -640,7 +640,9 @@ WasmEdge_BatchContext *WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfi
     h.min = I.Min;
     h.max = I.Max;
     h.has_max = I.HasMax != 0;
-    for (uint32_t q = 0; q < 4; q++) h.value[q] = uint32_t(I.Value.Value >> (32 * q));
+    const uint128_t iv = I.Kind == WASMEDGE_BATCH_IMPORT_GLOBAL && I.Type == WasmEdge_ValType_ExternRef
+                             ? uint128_t(C->xref_in(I.Value.Value)) : I.Value.Value;
+    for (uint32_t q = 0; q < 4; q++) h.value[q] = uint32_t(iv >> (32 * q));
     C->imports.push_back(h);
   }
   uint8_t e = setup(C, WasmBuf, WasmLen);
@@ -675,7 +677,7 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
       const WasmEdge_Value &v = Params[size_t(i) * ParamLen + k];
       if (uint8_t(v.Type) != t.params[k])
         return R(C->fail(kFuncSigMismatch, "parameter type mismatch"));
-      uint128_t x = v.Value;
+      const uint128_t x = t.params[k] == wb::EXTERNREF ? uint128_t(C->xref_in(v.Value)) : v.Value;
       for (uint32_t q = 0; q < cells_of_value(t.params[k]); q++)
         cells[size_t(i) * pc + at++] = uint32_t(x >> (32 * q));
     }
@@ -836,7 +838,7 @@ WasmEdge_Result WasmEdge_BatchResults(WasmEdge_BatchContext *C, WasmEdge_Value *
           v |= uint128_t(cells[size_t(i) * rc + at++]) << (32 * q);
         if (k < ReturnLen) {
           WasmEdge_Value &out = Returns[size_t(i) * ReturnLen + k];
-          out.Value = st[i] == 0 ? v : 0;
+          out.Value = st[i] != 0 ? 0 : ty == wb::EXTERNREF ? C->xref_out(uint32_t(v)) : v;
           out.Type = static_cast<enum WasmEdge_ValType>(ty);
         }
       }
@@ -1020,7 +1022,7 @@ WasmEdge_Result WasmEdge_BatchTableGetData(WasmEdge_BatchContext *C, const WasmE
   uint32_t v = 0;
   if (!get_lane(C, C->ltab.ptr, P.tab_words, P.tabinfo[2 * t] + Offset, Inst, &v))
     return R(kRuntimeError);
-  Data->Value = v;
+  Data->Value = P.tables[t].type == wb::EXTERNREF ? C->xref_out(v) : uint128_t(v);
   Data->Type = static_cast<enum WasmEdge_ValType>(P.tables[t].type);
   return R(0);
 }
@@ -1040,7 +1042,7 @@ WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmE
   const int t = find_named(P.table_exports, TableName);
   if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
   if (uint32_t(Data.Type) != P.tables[t].type) return R(kRefTypeMismatch);
-  const uint32_t v = uint32_t(Data.Value);
+  const uint32_t v = P.tables[t].type == wb::EXTERNREF ? C->xref_in(Data.Value) : uint32_t(Data.Value);
   if (P.tables[t].type == wb::FUNCREF && v != 0xFFFFFFFFu && v >= P.funcs.size())
     return R(C->fail(kRuntimeError, "funcref is not a function index of the module"));
   if (Inst == WASMEDGE_BATCH_ALL_INSTANCES) {
@@ -1083,6 +1085,7 @@ WasmEdge_Result WasmEdge_BatchGlobalGetValue(WasmEdge_BatchContext *C, const Was
     v |= uint128_t(w) << (32 * q);
   }
   if ((t == wb::FUNCREF || t == wb::EXTERNREF) && uint32_t(v) == 0xFFFFFFFFu) v = 0xFFFFFFFFu;
+  if (t == wb::EXTERNREF) v = C->xref_out(uint32_t(v));
   Value->Value = v;
   Value->Type = static_cast<enum WasmEdge_ValType>(t);
   return R(0);
@@ -1107,9 +1110,10 @@ WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchContext *C, const Was
   // wasmedge.cpp:2286-2295: a constant global or a value of another type is ignored
   const uint8_t t = P.global_types[g];
   if (!P.global_mut[g] || uint32_t(Value.Type) != t) return R(0);
+  const uint128_t x = t == wb::EXTERNREF ? uint128_t(C->xref_in(Value.Value)) : Value.Value;
   for (uint32_t q = 0; q < wb::cells_of(t); q++)
     if (!put_lane(C, C->lstate.ptr, C->ls_slots, LS_GLOBALS + P.global_cell[g] + q, Inst,
-                  uint32_t(Value.Value >> (32 * q))))
+                  uint32_t(x >> (32 * q))))
       return R(kRuntimeError);
   return R(0);
 }

@@ -213,6 +213,30 @@ struct WasmEdge_BatchContext {
   // the batch-wide instance id of this context's lane `local`
   uint32_t gid(uint32_t local) const;
 
+  // externref values at the boundary (the reference's are host pointers, wasmedge.h:254,318)
+  // and the 32-bit refs the device carries: null is 0xFFFFFFFF both sides, a value below
+  // 2^31 is its own device ref, a wider one (a pointer) is interned as 0x80000000 + its
+  // index here, for the context's life, and given back as the same 64-bit value
+  std::vector<uint64_t> xref_vals;
+  std::unordered_map<uint64_t, uint32_t> xref_ids;
+  std::mutex xref_mu;   // (host functions may run on several threads)
+  uint32_t xref_in(uint128_t v) {
+    const uint64_t x = uint64_t(v);
+    if (x < 0x80000000ull || x == 0xFFFFFFFFull) return uint32_t(x);
+    std::lock_guard<std::mutex> g(xref_mu);
+    auto it = xref_ids.find(x);
+    if (it != xref_ids.end()) return it->second;
+    if (xref_vals.size() >= 0x7FFFFFFFull) return 0xFFFFFFFFu;   // (2^31 - 1 distinct values)
+    const uint32_t h = 0x80000000u + uint32_t(xref_vals.size());
+    xref_vals.push_back(x);
+    xref_ids.emplace(x, h);
+    return h;
+  }
+  uint128_t xref_out(uint32_t h) {
+    if (h < 0x80000000u || h == 0xFFFFFFFFu) return h;
+    std::lock_guard<std::mutex> g(xref_mu);
+    return h - 0x80000000u < xref_vals.size() ? xref_vals[h - 0x80000000u] : h;
+  }
   uint8_t fail(uint8_t code, const std::string &m) {
     last_error = m;
     return code;

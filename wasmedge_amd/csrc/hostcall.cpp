@@ -675,7 +675,7 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
         for (size_t q = 0; q < t.params.size(); q++) {
           uint128_t v = 0;
           for (uint32_t c = 0; c < wb::cells_of(t.params[q]); c++) v |= uint128_t(cells[at++]) << (32 * c);
-          args[q].Value = v;
+          args[q].Value = t.params[q] == wb::EXTERNREF ? C->xref_out(uint32_t(v)) : v;
           args[q].Type = static_cast<enum WasmEdge_ValType>(t.params[q]);
         }
         for (size_t q = 0; q < t.results.size(); q++)
@@ -688,8 +688,10 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
           continue;
         }
         at = 0;
-        for (size_t q = 0; q < t.results.size(); q++)
-          for (uint32_t c = 0; c < wb::cells_of(t.results[q]); c++) cells[at++] = uint32_t(rets[q].Value >> (32 * c));
+        for (size_t q = 0; q < t.results.size(); q++) {
+          const uint128_t v = t.results[q] == wb::EXTERNREF ? uint128_t(C->xref_in(rets[q].Value)) : rets[q].Value;
+          for (uint32_t c = 0; c < wb::cells_of(t.results[q]); c++) cells[at++] = uint32_t(v >> (32 * c));
+        }
         hcall[i] = at;
         mine++;
       }
