@@ -455,7 +455,9 @@ def main():
     if args.steps is None:
         args.steps = 20 if args.workload == "c2" else 3
     if args.warmup is None:
-        args.warmup = 2 if args.workload == "c2" else 1
+        # (modules whose addresses may differ per instance run the layout trial over their
+        # first three runs -- warm-up, 128-byte granules, 4-byte words: untimed)
+        args.warmup = 2 if args.workload == "c2" else 3 if args.workload in ("c3", "c3grow", "mt") else 1
     if args.instances is None:
         args.instances = default_instances(args.workload)
     if args.vary_args == "auto":
