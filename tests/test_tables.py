@@ -200,3 +200,38 @@ def test_gpu_table_widen(built):
     ref = _oracle_rounds(WIDE, "widen", WIDE_ROUNDS)
     for r, (got, st, cnt, h) in enumerate(_gpu_rounds(WIDE, "widen", WIDE_ROUNDS)):
         assert compare(ref[r], got, st, cnt, h, [I32]) == [], "round %d" % r
+
+
+# Metered: the grow that widens the tables is counted and priced once (the lane parks before
+# the step and runs it again), so the limit lands on the same instruction as the oracle's
+# whether or not a widening happens there (engine.cpp:1616-1630).
+WIDE_LIMITS = list(range(1, 24)) + [40, 1000, 10 ** 6]
+
+
+def _oracle_metered(wasm, func, rows, limit):
+    m = O.Module(wasm)
+    return [O.Instance(m, cost_limit=limit).invoke(func, r) for r in rows]
+
+
+def test_table_widen_metered_emulator(built):
+    rows = [[x] for x in (0, 1, 5, 50, 129)]
+    for limit in WIDE_LIMITS:
+        ref = _oracle_metered(WIDE, "widen", rows, limit)
+        rets, st, cnt, h = emu_run(WIDE, "widen", rows, [I32], [I32], cost_limit=limit)
+        assert compare(ref, rets, st, cnt, h, [I32]) == [], limit
+
+
+@pytest.mark.gpu
+def test_gpu_table_widen_metered(built):
+    from wasmedge_amd import batch
+    rows = [[x] for x in range(0, 130, 3)]
+    for limit in WIDE_LIMITS:
+        ref = _oracle_metered(WIDE, "widen", rows, limit)
+        ctx = batch.BatchContext(WIDE, len(rows), device=0, cost_limit=limit)
+        try:
+            rets, st, cnt = ctx.execute("widen", batch.make_values(rows, [I32]), 1)
+            ints = batch.ret_ints(rets)
+            got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == [], limit
+        finally:
+            ctx.close()
