@@ -226,6 +226,11 @@ def test_gpu_table_widen_metered(built):
     from wasmedge_amd import batch
     rows = [[x] for x in range(0, 130, 3)]
     for limit in WIDE_LIMITS:
+        if O.Instance(O.Module(WIDE), cost_limit=limit).error:   # instantiation runs out of gas
+            with pytest.raises(batch.WasmEdgeError) as e:
+                batch.BatchContext(WIDE, len(rows), device=0, cost_limit=limit)
+            assert e.value.code == 0x03
+            continue
         ref = _oracle_metered(WIDE, "widen", rows, limit)
         ctx = batch.BatchContext(WIDE, len(rows), device=0, cost_limit=limit)
         try:
