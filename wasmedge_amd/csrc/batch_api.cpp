@@ -684,8 +684,12 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
   }
   uint32_t rc = 0;
   for (uint8_t ty : t.results) rc += cells_of_value(ty);
-  if (!C->params.alloc(cells.size()) ||
-      !C->results.alloc(size_t(C->n) * (rc ? rc : 1)))
+  // (the buffers stay when their sizes do: a caller passing new arguments every run pays no
+  // device allocation, and the kernel reads the same pages)
+  const size_t rn = size_t(C->n) * (rc ? rc : 1);
+  if ((C->params.n != cells.size() || !C->params.ptr) && !C->params.alloc(cells.size()))
+    return R(C->fail(kRuntimeError, "device allocation failed"));
+  if ((C->results.n != rn || !C->results.ptr) && !C->results.alloc(rn))
     return R(C->fail(kRuntimeError, "device allocation failed"));
   if (!C->hip_ok(hipMemcpyAsync(C->params.ptr, cells.data(), cells.size() * 4,
                                 hipMemcpyHostToDevice, C->stream), "params upload"))
