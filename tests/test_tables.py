@@ -240,3 +240,21 @@ def test_gpu_table_widen_metered(built):
             assert compare(ref, got, st, cnt, ctx.memory_hash(), [I32]) == [], limit
         finally:
             ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("part", [0, 1])
+def test_gpu_table_widen_two_shards(built, part):
+    """Two shards on one device (multi.cpp): each shard widens its own lanes' tables in its
+    own service round; every lane still matches the oracle, over two runs."""
+    from wasmedge_amd import batch
+    ref = _oracle_rounds(WIDE, "widen", WIDE_ROUNDS)
+    ctx = batch.BatchContext(WIDE, len(WIDE_ROUNDS[0]), devices=[0, 0], partition=part)
+    try:
+        for r, rows in enumerate(WIDE_ROUNDS):
+            rets, st, cnt = ctx.execute("widen", batch.make_values(rows, [I32]), 1)
+            ints = batch.ret_ints(rets)
+            got = [[int(x) for x in ints[i]] if st[i] == 0 else [] for i in range(len(rows))]
+            assert compare(ref[r], got, st, cnt, ctx.memory_hash(), [I32]) == [], "round %d" % r
+    finally:
+        ctx.close()
