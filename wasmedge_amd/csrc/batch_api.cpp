@@ -544,10 +544,25 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
                          ? C->wave_order.ptr : nullptr;
     }
   }
+  // a Reset left to this launch (WasmEdge_BatchReset): each wave does its part first
+  const bool rf = C->reset_deferred && !resume && !is_start;
+  if (rf) {
+    k.rf_on = 1;
+    k.rf_image = C->image.ptr;
+    k.rf_image_words = C->image_words;
+    k.rf_init_words = C->mem_words;
+    k.rf_global_init = C->global_init.ptr;
+    k.rf_init_pages = P.mem_min;
+    k.rf_init_dropped = C->init_dropped;
+    k.rf_init_cost = C->init_cost;
+  } else if (C->reset_deferred && !wbh_reset_now(C)) {
+    return kRuntimeError;
+  }
   (void)hipEventRecord(C->ev0, C->stream);
   // +1 cell row: the threaded core reads operand cells k and k+1 (ds_read2_b32)
   if (!C->hip_ok(wb_launch_exec(&k, blocks, wpb * 64, wave_lds * wpb + 256, vf, C->stream), "launch"))
     return kRuntimeError;
+  if (rf) C->reset_deferred = false;
   (void)hipEventRecord(C->ev1, C->stream);
   // the next launch of this function takes the longest waves first (sorted on the device,
   // after the timed kernel, on a stream of its own so that it overlaps the next Reset; the
@@ -603,6 +618,19 @@ uint8_t launch_exec(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start,
 }
 
 }  // namespace
+
+// (batch_ctx.h) the Reset a launch was to fold in, as wb_mem_init_kernel's write-mark path
+bool wbh_reset_now(WasmEdge_BatchContext *C) {
+  C->reset_deferred = false;
+  const wb::Program &P = C->prog;
+  if (!C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, C->mem_words, C->mem_words,
+                                    C->nwaves, C->lstate.ptr, C->ls_slots, 0u, C->mlog, 1u,
+                                    C->global_init.ptr, P.mem_min, C->init_dropped, C->init_cost,
+                                    C->stream), "mem init"))
+    return false;
+  C->reset_pending = true;
+  return true;
+}
 
 extern "C" {
 
@@ -735,7 +763,18 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   if (!pool_reset(C)) return R(kRuntimeError);
   // after a run the memory kernel's write-mark path resets the instance state as well
   const bool fused = P.has_mem && !C->mem_fresh && init_words;
-  if (P.has_mem &&
+  // ... or, when that kernel is all this Reset launches (4-byte granules, no per-lane
+  // tables, no memories past the first, no start function, no timing asked), the next
+  // interpreter launch does it wave by wave (batch_kernel.hip fused_reset): one kernel and
+  // one launch gap less per Reset + Run. A host accessor before that launch does it first
+  // (settle). WB_FUSED_RESET=0 keeps the separate kernel.
+  const char *fre = getenv("WB_FUSED_RESET");
+  C->reset_deferred = false;
+  const bool defer = fused && C->mlog == 0 && !P.mut_tables && P.xmems.empty() && P.start_func < 0 &&
+                     !KernelSeconds && !(C->conf.CostLimit && C->init_exceeded) && !(fre && fre[0] == '0');
+  if (defer) {
+    C->reset_deferred = true;
+  } else if (P.has_mem &&
       !C->hip_ok(wb_launch_mem_init(C->mem.ptr, C->image.ptr, C->image_words, init_words,
                                     C->mem_words, C->nwaves, C->lstate.ptr, C->ls_slots,
                                     C->mem_fresh ? 1u : 0u, C->mlog, fused ? 1u : 0u, C->global_init.ptr, P.mem_min,

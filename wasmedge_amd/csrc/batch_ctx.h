@@ -56,6 +56,10 @@ struct DevBuf {
 
 namespace wbh { struct WaveView; }
 
+// a Reset left to the next launch (batch_kernel.hip fused_reset) done now, as its own
+// kernel: for a host accessor or any device work that reads instance state first
+bool wbh_reset_now(WasmEdge_BatchContext *C);
+
 struct WasmEdge_BatchMemoryContext {   // one instance's linear memory, for host functions
   WasmEdge_BatchContext *ctx;
   uint32_t inst;
@@ -200,6 +204,8 @@ struct WasmEdge_BatchContext {
   // so NOT ordered before the host accessors' synchronous null-stream copies): every host
   // accessor settles first.
   bool reset_pending = false;
+  // ... or not even queued: the next launch of the interpreter does it (fused_reset)
+  bool reset_deferred = false;
 
   // Multi-device contexts (WasmEdge_BatchConfigure::Devices, multi.cpp): the parent holds
   // one shard context per entry of Devices (nullptr: no instances there) and routes every
@@ -248,6 +254,7 @@ struct WasmEdge_BatchContext {
   }
   // wait for queued Reset kernels before a host copy touches instance state
   bool settle() {
+    if (reset_deferred && !wbh_reset_now(this)) return false;
     if (!reset_pending) return true;
     reset_pending = false;
     return hip_ok(hipStreamSynchronize(stream), "reset kernels");

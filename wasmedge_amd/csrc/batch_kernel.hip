@@ -880,6 +880,46 @@ __device__ __forceinline__ uint32_t next_wave(const KParams &p, uint32_t &turn) 
   return p.wave_order ? __builtin_amdgcn_readfirstlane(p.wave_order[w]) : w;
 }
 
+// Instance state at instantiation (instantiate/module.cpp: memory of `min` pages, active
+// data segments dropped, globals from their initialisers, no failure yet): LS slot `slot`.
+struct StateInit {
+  const uint32_t *global_init;
+  uint32_t init_pages, init_dropped;
+  uint64_t init_cost;
+  uint32_t on;   // (mem init) reset the state too
+};
+__device__ __forceinline__ uint32_t state_word(uint32_t slot, const StateInit &st) {
+  if (slot == LS_PAGES) return st.init_pages;
+  if (slot == LS_DROPPED) return st.init_dropped;
+  if (slot == LS_RPC) return 0xFFFFFFFFu;
+  if (slot == LS_COST) return (uint32_t)st.init_cost;
+  if (slot == LS_COST + 1) return (uint32_t)(st.init_cost >> 32);
+  if (slot >= LS_GLOBALS) return st.global_init[slot - LS_GLOBALS];
+  return 0;
+}
+
+// A Reset folded into the launch (KParams::rf_on; batch_api.cpp WasmEdge_BatchReset, 4-byte
+// granules only): before its wave runs, each lane rewrites its own memory words below the
+// wave's write mark (or the image) and its instance state -- wb_mem_init_kernel's
+// write-mark path for one wave, with no kernel of its own. Every lane writes only its own
+// column, so its later loads see the words in program order.
+__device__ __forceinline__ void fused_reset(const KParams &p, uint32_t wave, uint32_t lane) {
+  uint32_t *const lw = p.lstate + (size_t)wave * p.ls_slots * 64u + lane;
+  uint32_t m = lw[(size_t)LS_HWM << 6];
+  for (uint32_t o = 32; o; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, 64));
+  const uint64_t hw = ((uint64_t)m + 3u) / 4u;
+  uint32_t rows = (uint32_t)(hw < p.rf_init_words ? hw : p.rf_init_words);
+  if (rows < p.rf_image_words && p.rf_image_words <= p.rf_init_words) rows = p.rf_image_words;
+  uint32_t *const wm = p.mem + (size_t)wave * p.mem_words * 64u + lane;
+  for (uint32_t w = 0; w < rows; w++) wm[(size_t)w << 6] = w < p.rf_image_words ? p.rf_image[w] : 0u;
+  // (state_word's words, from the kernel arguments: no StateInit on the stack)
+  for (uint32_t slot = 0; slot < p.ls_slots; slot++)
+    lw[(size_t)slot << 6] = slot == LS_PAGES ? p.rf_init_pages : slot == LS_DROPPED ? p.rf_init_dropped
+                          : slot == LS_RPC ? 0xFFFFFFFFu : slot == LS_COST ? (uint32_t)p.rf_init_cost
+                          : slot == LS_COST + 1 ? (uint32_t)(p.rf_init_cost >> 32)
+                          : slot >= LS_GLOBALS ? p.rf_global_init[slot - LS_GLOBALS] : 0u;
+}
+
 template <bool VF, bool PG>
 __device__ __forceinline__ void exec_body(const KParams &p) {
   extern __shared__ uint32_t lds[];
@@ -890,6 +930,7 @@ __device__ __forceinline__ void exec_body(const KParams &p) {
   uint32_t turn = 0;
   for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
+    if (p.rf_on && wave < ((p.n + 63u) >> 6)) fused_reset(p, wave, lane);   // (batch waves only)
     const uint64_t ws = p.wave_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
     interp<VF, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
                GMem{p.mem + (size_t)wave * p.mem_words * 64u + (lane << p.mlog), p.mlog},
@@ -915,6 +956,7 @@ __device__ __forceinline__ void exec_hbm_body(const KParams &p) {
   uint32_t turn = 0;
   for (uint32_t wave; (wave = next_wave(p, turn)) != 0xFFFFFFFFu;) {
     const uint32_t inst = wave * 64u + lane;
+    if (p.rf_on && wave < ((p.n + 63u) >> 6)) fused_reset(p, wave, lane);   // (batch waves only)
     const uint64_t ws = p.wave_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
     HbmFrame F{p.hframe + (size_t)wave * p.total_cells * 64u + lane};
     interp<false, PG>(p, F, inst, p.gstack + (size_t)wave * p.gs_depth * 64u + lane,
@@ -951,24 +993,6 @@ extern "C" __global__ void __launch_bounds__(256, 2) wb_exec_vf_pg_kernel(const 
 // `init_words` = the rows this covers: the whole reserved layout (rpages), so that pages a
 // lane grows into later read zero without memory.grow writing them; pool rows are zeroed
 // by the host (batch_api.cpp pool_reset).
-// Instance state at instantiation (instantiate/module.cpp: memory of `min` pages, active
-// data segments dropped, globals from their initialisers, no failure yet): LS slot `slot`.
-struct StateInit {
-  const uint32_t *global_init;
-  uint32_t init_pages, init_dropped;
-  uint64_t init_cost;
-  uint32_t on;   // (mem init) reset the state too
-};
-__device__ __forceinline__ uint32_t state_word(uint32_t slot, const StateInit &st) {
-  if (slot == LS_PAGES) return st.init_pages;
-  if (slot == LS_DROPPED) return st.init_dropped;
-  if (slot == LS_RPC) return 0xFFFFFFFFu;
-  if (slot == LS_COST) return (uint32_t)st.init_cost;
-  if (slot == LS_COST + 1) return (uint32_t)(st.init_cost >> 32);
-  if (slot >= LS_GLOBALS) return st.global_init[slot - LS_GLOBALS];
-  return 0;
-}
-
 // (write-mark path) with st.on set, the wave's instance state is reset too, after
 // its mark was read: one launch per Reset instead of two
 extern "C" __global__ void __launch_bounds__(256)

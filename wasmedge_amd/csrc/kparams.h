@@ -112,6 +112,11 @@ struct KParams {
   // of returning -1
   uint32_t tg_grow;
   const uint32_t *tlimit;
+  // a Reset folded into this launch (batch_kernel.hip fused_reset): the memory image, the
+  // rows a Reset covers, and the instance state's initial words (StateInit)
+  uint32_t rf_on, rf_image_words, rf_init_words, rf_init_pages, rf_init_dropped;
+  const uint32_t *rf_image, *rf_global_init;
+  uint64_t rf_init_cost;
 };
 
 // Per-lane instance state that persists across invocations until the next Reset (the
