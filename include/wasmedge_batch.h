@@ -164,6 +164,17 @@ typedef struct WasmEdge_BatchConfigure {
    * their limit as far as min(4 GiB, free/8) per batch goes when the module grows them; a
    * grow past that returns -1). WasmEdge_BatchGetMemory / the memory hash cover memory 0. */
   uint32_t MultiMemories;
+  /* Pages reserved per instance for each memory past the first that the module grows
+   * (0 = chosen as above: the page limit as far as min(4 GiB, free/8) for the whole batch
+   * goes -- with tens of thousands of instances that can be few or none, and then
+   * memory.grow on it returns -1 where the reference's would succeed). Clamped to [initial
+   * size, limit]; BatchCreate fails with RuntimeError when the batch does not fit.
+   * WasmEdge_BatchGetExtraMemoryPages reports the reservation in use. */
+  uint32_t ExtraMemoryReservePages;
+  /* Cap on the device memory the call stack may grow to when CallStackCells is 0 (bytes;
+   * 0 = an eighth of the device's memory). Past it a call ends the instance with 0xB0.
+   * Each BatchReset returns the stack to its first depth. */
+  uint64_t CallStackMaxBytes;
 } WasmEdge_BatchConfigure;
 
 #define WASMEDGE_BATCH_PARTITION_BLOCKS 0u
@@ -352,15 +363,33 @@ WasmEdge_BatchMemorySetData(WasmEdge_BatchMemoryContext *MemCxt, const uint8_t *
  * Binds the module's imports args_get, args_sizes_get, environ_get, environ_sizes_get,
  * fd_write, proc_exit and sched_yield (those with the WASI signature) to host functions
  * inside the library, as WasmEdge_ImportObjectCreateWASI / InitWASI would
- * (include/api/wasmedge/wasmedge.h:2719-2754, lib/host/wasi/wasifunc.cpp). Args/Envs are
- * shared by every instance. fd_write to fd 1 / 2 is captured per instance (fd 0 gives
- * NOTCAPABLE, other fds BADF: no preopened directories); proc_exit records the exit code
+ * (include/api/wasmedge/wasmedge.h:2719-2754, lib/host/wasi/wasifunc.cpp), plus
+ * fd_prestat_get and fd_prestat_dir_name. Args/Envs are shared by every instance unless an
+ * instance has its own args (WasmEdge_BatchWASISetInstanceArgs). fd_write to fd 1 / 2 is
+ * captured per instance (fd 0 gives NOTCAPABLE, other fds BADF); proc_exit records the exit code
  * and ends the instance with Terminated (0x01). Calling it again re-initialises the
  * environment and clears the captured output and exit codes. Other WASI imports stay
  * unbound (0xB1 when reached) unless registered with WasmEdge_BatchAddHostFunction. */
 WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchInitWASI(WasmEdge_BatchContext *Cxt, const char *const *Args, const uint32_t ArgLen,
                        const char *const *Envs, const uint32_t EnvLen);
+/* The same with preopened directories, as WasmEdge_ImportObjectInitWASI's Preopens
+ * (wasmedge.h:2739-2742): "guest:host" or one path for both; they become fds 3, 4, ... in
+ * the order given (environ.cpp:54-93), named by VINode::canonicalGuest. fd_prestat_get /
+ * fd_prestat_dir_name report them (wasifunc.cpp:724-766; stdio fds give INVAL, others
+ * BADF). */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *Cxt, const char *const *Args,
+                                   const uint32_t ArgLen, const char *const *Envs,
+                                   const uint32_t EnvLen, const char *const *Preopens,
+                                   const uint32_t PreopenLen);
+/* Instance Inst's own command line (args_get / args_sizes_get), in place of the shared Args:
+ * the reference builds one Environ per VM (environ.cpp:95-98), so N instances with their
+ * own arguments are N VMs with their own WASI modules. Call after WasmEdge_BatchInitWASI
+ * (which clears every instance's own args). */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchWASISetInstanceArgs(WasmEdge_BatchContext *Cxt, uint32_t Inst,
+                                  const char *const *Args, const uint32_t ArgLen);
 /* proc_exit code of instance Inst (0 if it never called it; WasmEdge_ImportObjectWASIGetExitCode,
  * wasmedge.h:2754). */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchWASIGetExitCode(const WasmEdge_BatchContext *Cxt,
@@ -402,6 +431,10 @@ WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchC
  * memory, and MemoryPoolBytes past the initial layout). Layout only: results never depend
  * on it. */
 WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetReservedPages(const WasmEdge_BatchContext *Cxt);
+/* Pages every instance has reserved for memory MemIdx >= 1 (MultiMemories): memory.grow on
+ * it returns -1 past them (0 for an index the module does not have). */
+WASMEDGE_BATCH_API uint32_t WasmEdge_BatchGetExtraMemoryPages(const WasmEdge_BatchContext *Cxt,
+                                                              uint32_t MemIdx);
 
 /* Hash of every instance's final linear memory 0 (definition in DESIGN.md; the oracle
  * computes the same function). Hashes: [NumInstances]. */

@@ -83,6 +83,10 @@ def lib():
         cpp = ctypes.POINTER(ctypes.c_char_p)
         L.om_set_wasi.restype = None
         L.om_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
+        L.om_set_wasi_preopens.restype = None
+        L.om_set_wasi_preopens.argtypes = [cpp, ctypes.c_uint32]
+        L.om_set_instance_args.restype = None
+        L.om_set_instance_args.argtypes = [ctypes.c_void_p, cpp, ctypes.c_uint32]
         L.om_wasi_exit_code.restype = ctypes.c_uint32
         L.om_wasi_exit_code.argtypes = [ctypes.c_void_p]
         L.om_wasi_output.restype = ctypes.c_uint64
@@ -260,6 +264,11 @@ class Instance:
     def wasi_exit_code(self):
         return lib().om_wasi_exit_code(self._h)
 
+    def set_args(self, args):
+        """This instance's own WASI command line (one Environ per VM)."""
+        a = (ctypes.c_char_p * max(len(args), 1))(*[x.encode() for x in args])
+        lib().om_set_instance_args(self._h, a, len(args))
+
     def table_set(self, tab, off, ref):
         """Write one table entry (ref: function index / externref handle, None = null);
         returns the ErrCode (0x87 out of bounds)."""
@@ -276,12 +285,14 @@ def set_lazy_imports(on):
     lib().om_set_lazy_imports(1 if on else 0)
 
 
-def set_wasi(on, args=(), envs=()):
+def set_wasi(on, args=(), envs=(), preopens=()):
     """Bind the WASI subset (wasi_snapshot_preview1) for later instantiations, with these
-    args/envs shared by every instance (the batched path's WasmEdge_BatchInitWASI)."""
+    args/envs shared by every instance (the batched path's WasmEdge_BatchInitWASI) and
+    these preopened directories (fds 3, 4, ...)."""
     def arr(v):
         return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
     lib().om_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
+    lib().om_set_wasi_preopens(arr(list(preopens)), len(preopens))
 
 
 def set_imports(imports):

@@ -126,6 +126,7 @@ struct OInst {
   /* WASI subset (wasifunc.cpp): captured fd 1 / fd 2 bytes and the proc_exit code */
   uint8_t *wasi_out[2]; uint64_t wasi_len[2], wasi_cap[2];
   uint32_t wasi_exit;
+  char **own_args; uint32_t own_nargs; int has_own_args;   /* this VM's own command line */
 };
 
 /* ------------------------------------------------------------------ reader */

@@ -64,6 +64,10 @@ void om_set_lazy_imports(int on);
  * by every instance). Per instance: captured fd 1/2 bytes and the proc_exit code. */
 void om_set_wasi(int on, const char *const *args, uint32_t nargs, const char *const *envs,
                  uint32_t nenvs);
+/* fd_prestat_get / fd_prestat_dir_name: preopened directories ("guest:host" or one path)
+ * as fds 3, 4, ... for later instantiations; an instance's own args (one Environ per VM). */
+void om_set_wasi_preopens(const char *const *dirs, uint32_t n);
+void om_set_instance_args(OInst *i, const char *const *args, uint32_t n);
 uint32_t om_wasi_exit_code(const OInst *i);
 uint64_t om_wasi_output(const OInst *i, uint32_t fd, const uint8_t **data);
 

@@ -12,6 +12,8 @@ answers):
                     (answers in test/externref/ExternrefTest.cpp:308-356)
   externref_stl.wasm    test/externref/externrefTestData/stl.wasm (:372-465)
   rust_add.wasm     tools/wasmedge/examples/add.wasm (compiled Rust/WASI; add 2 2 -> 4)
+  hello.wasm        tools/wasmedge/examples/hello.wasm (compiled Rust/WASI command;
+                    README.md:5-15 runs it as `wasmedge hello.wasm 1 2 3`)
   executor_interrupt.wasm  bytes of test/executor/ExecutorTest.cpp:122-126 (endless
                     loop in _start; cancel -> Interrupted, :127-145)
 """
@@ -48,6 +50,8 @@ def main():
                 os.path.join(OUT, "externref_stl.wasm"))
     shutil.copy(os.path.join(REF, "tools/wasmedge/examples/add.wasm"),
                 os.path.join(OUT, "rust_add.wasm"))
+    shutil.copy(os.path.join(REF, "tools/wasmedge/examples/hello.wasm"),
+                os.path.join(OUT, "hello.wasm"))
     src = open(os.path.join(REF, "test/executor/ExecutorTest.cpp")).read()
     m = re.search(r"std::array<WasmEdge::Byte, 46> Wasm\{(.*?)\};", src, re.S)
     data = bytes(int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]{2}", m.group(1)))

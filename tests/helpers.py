@@ -28,6 +28,8 @@ def emu_lib():
         E.wb_emu_get_costs.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         cpp = ctypes.POINTER(ctypes.c_char_p)
         E.wb_emu_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
+        E.wb_emu_set_wasi_preopens.argtypes = [cpp, ctypes.c_uint32]
+        E.wb_emu_set_instance_args.argtypes = [ctypes.c_uint32, cpp, ctypes.c_uint32]
         E.wb_emu_wasi_output.restype = ctypes.c_uint32
         E.wb_emu_wasi_output.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         E.wb_emu_wasi_exit_code.restype = ctypes.c_uint32
@@ -111,11 +113,17 @@ def emu_set_imports(imports):
                             0 if mx is None else 1, ctypes.cast(cells, ctypes.c_void_p))
 
 
-def emu_set_wasi(on, args=(), envs=()):
-    """The emulator's copy of the library's WASI subset (wasi_impl.h)."""
+def emu_set_wasi(on, args=(), envs=(), preopens=(), instance_args=None):
+    """The emulator's copy of the library's WASI subset (wasi_impl.h); instance_args:
+    {instance: its own args} for the next run."""
     def arr(v):
         return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
-    emu_lib().wb_emu_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
+    E = emu_lib()
+    E.wb_emu_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
+    E.wb_emu_set_wasi_preopens(arr(list(preopens)), len(preopens))
+    E.wb_emu_clear_instance_args()
+    for i, a in (instance_args or {}).items():
+        E.wb_emu_set_instance_args(i, arr(list(a)), len(a))
 
 
 def emu_wasi_output(inst, fd):

@@ -62,7 +62,8 @@ class _Conf(ctypes.Structure):
                 ("TailCall", ctypes.c_uint32), ("MemoryReservePages", ctypes.c_uint32),
                 ("MemoryPoolBytes", ctypes.c_uint64), ("Devices", ctypes.POINTER(ctypes.c_int32)),
                 ("DeviceCount", ctypes.c_uint32), ("Partition", ctypes.c_uint32),
-                ("MultiMemories", ctypes.c_uint32)]
+                ("MultiMemories", ctypes.c_uint32), ("ExtraMemoryReservePages", ctypes.c_uint32),
+                ("CallStackMaxBytes", ctypes.c_uint64)]
 
 PARTITION_BLOCKS, PARTITION_INTERLEAVE = 0, 1
 
@@ -191,6 +192,10 @@ def lib():
         L.WasmEdge_BatchGetTotalCosts.argtypes = [vp, vp]
         L.WasmEdge_BatchInitWASI.restype = _Result
         L.WasmEdge_BatchInitWASI.argtypes = [vp, cpp, u32, cpp, u32]
+        L.WasmEdge_BatchInitWASIWithPreopens.restype = _Result
+        L.WasmEdge_BatchInitWASIWithPreopens.argtypes = [vp, cpp, u32, cpp, u32, cpp, u32]
+        L.WasmEdge_BatchWASISetInstanceArgs.restype = _Result
+        L.WasmEdge_BatchWASISetInstanceArgs.argtypes = [vp, u32, cpp, u32]
         L.WasmEdge_BatchWASIGetExitCode.restype = u32
         L.WasmEdge_BatchWASIGetExitCode.argtypes = [vp, u32]
         L.WasmEdge_BatchWASIGetOutput.restype = u32
@@ -201,6 +206,8 @@ def lib():
         L.WasmEdge_BatchGetMemoryGranule.argtypes = [vp]
         L.WasmEdge_BatchGetReservedPages.restype = u32
         L.WasmEdge_BatchGetReservedPages.argtypes = [vp]
+        L.WasmEdge_BatchGetExtraMemoryPages.restype = u32
+        L.WasmEdge_BatchGetExtraMemoryPages.argtypes = [vp, u32]
         L.WasmEdge_BatchGetEngine.restype = ctypes.c_char_p
         L.WasmEdge_BatchGetEngine.argtypes = [vp]
         _lib = L
@@ -243,7 +250,8 @@ class BatchContext:
     def __init__(self, wasm, n, max_memory_page=0, call_stack_cells=0, max_steps=0,
                  time_limit=0.0, device=-1, cost_limit=0, host_threads=0, cost_table=None,
                  memory_granule=0, imports=None, tail_call=False, memory_reserve_pages=0,
-                 memory_pool_bytes=0, devices=None, partition=PARTITION_BLOCKS, multi_memory=False):
+                 memory_pool_bytes=0, devices=None, partition=PARTITION_BLOCKS, multi_memory=False,
+                 extra_memory_reserve_pages=0, call_stack_max_bytes=0):
         """cost_table: gas cost per OpCode (list; missing entries 0), None = unit costs;
         metering is on when cost_limit > 0. max_memory_page 0 = the reference's default
         page limit (65536); memory_reserve_pages / memory_pool_bytes: the device layout of
@@ -258,6 +266,8 @@ class BatchContext:
                      len(tab) if tab is not None else 0, memory_granule, 1 if tail_call else 0,
                      memory_reserve_pages, memory_pool_bytes)
         conf.MultiMemories = 1 if multi_memory else 0
+        conf.ExtraMemoryReservePages = extra_memory_reserve_pages
+        conf.CallStackMaxBytes = call_stack_max_bytes
         if devices is not None and len(devices) == 1:
             conf.DeviceOrdinal = devices[0]
         if devices is not None and len(devices) > 1:
@@ -377,6 +387,10 @@ class BatchContext:
         (WasmEdge_BatchGetReservedPages)."""
         return lib().WasmEdge_BatchGetReservedPages(self._h)
 
+    def extra_memory_pages(self, mem):
+        """Pages reserved per instance for memory `mem` >= 1 (WasmEdge_BatchGetExtraMemoryPages)."""
+        return lib().WasmEdge_BatchGetExtraMemoryPages(self._h, mem)
+
     def engine(self):
         """The execution engine the context runs, e.g. "compiled-runs+simt/vgpr-frames"
         (WasmEdge_BatchGetEngine)."""
@@ -444,13 +458,16 @@ class BatchContext:
                                                                 self._name(name), cb, None, cost))
 
 
-    # built-in WASI subset (WasmEdge_BatchInitWASI): args/envs shared by every instance
-    def init_wasi(self, args=(), envs=()):
-        def arr(v):
-            a = (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
-            return a
-        a, e = arr(list(args)), arr(list(envs))
-        self._check(lib().WasmEdge_BatchInitWASI(self._h, a, len(args), e, len(envs)))
+    # built-in WASI subset (WasmEdge_BatchInitWASIWithPreopens): args/envs shared by every
+    # instance, preopened directories as fds 3, 4, ...
+    def init_wasi(self, args=(), envs=(), preopens=()):
+        a, e, p = _cstrs(args), _cstrs(envs), _cstrs(preopens)
+        self._check(lib().WasmEdge_BatchInitWASIWithPreopens(self._h, a, len(args), e, len(envs),
+                                                             p, len(preopens)))
+
+    def set_instance_args(self, inst, args):
+        """Instance `inst`'s own command line (WasmEdge_BatchWASISetInstanceArgs)."""
+        self._check(lib().WasmEdge_BatchWASISetInstanceArgs(self._h, inst, _cstrs(args), len(args)))
 
     def wasi_exit_code(self, inst):
         return lib().WasmEdge_BatchWASIGetExitCode(self._h, inst)
@@ -460,6 +477,11 @@ class BatchContext:
         buf = ctypes.create_string_buffer(max(n, 1))
         lib().WasmEdge_BatchWASIGetOutput(self._h, inst, fd, buf, n)
         return buf.raw[:n]
+
+
+def _cstrs(v):
+    v = list(v)
+    return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
 
 
 def ret_ints(rets):

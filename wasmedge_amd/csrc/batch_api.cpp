@@ -195,6 +195,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   C->gs_depth = C->conf.CallStackCells ? C->conf.CallStackCells : 4096;
   const char *sge = getenv("WB_STACK_GROW");
   C->gs_grow = !C->conf.CallStackCells && !(sge && sge[0] == '0');
+  C->gs_grow0 = C->gs_grow;
+  C->gs_depth0 = C->gs_depth;
   // per-lane tables widen past their first capacity up to table_widen_limit (WB_TABLE_WIDEN=0
   // keeps the first capacity: test aid)
   std::vector<uint32_t> tlim;
@@ -247,7 +249,8 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       bool grows = false;
       for (const auto &I : P.code)
         grows |= (I.w0 & 0xFFFFu) == OP_XMEM_GROW && (I.w1 >> 16) == k + 1;
-      const uint32_t res = grows ? uint32_t(std::max<uint64_t>(xm.min, std::min<uint64_t>(lim, per_lane))) : xm.min;
+      const uint64_t want = C->conf.ExtraMemoryReservePages ? C->conf.ExtraMemoryReservePages : per_lane;
+      const uint32_t res = grows ? uint32_t(std::max<uint64_t>(xm.min, std::min<uint64_t>(lim, want))) : xm.min;
       C->xinfo_h.push_back(uint32_t(words));
       C->xinfo_h.push_back(res);
       words += uint64_t(res) << 14;
@@ -668,8 +671,14 @@ WasmEdge_BatchContext *WasmEdge_BatchCreateWithImports(const WasmEdge_BatchConfi
     h.min = I.Min;
     h.max = I.Max;
     h.has_max = I.HasMax != 0;
+    bool full = false;
     const uint128_t iv = I.Kind == WASMEDGE_BATCH_IMPORT_GLOBAL && I.Type == WasmEdge_ValType_ExternRef
-                             ? uint128_t(C->xref_in(I.Value.Value)) : I.Value.Value;
+                             ? uint128_t(C->xref_in(I.Value.Value, &full)) : I.Value.Value;
+    if (full) {
+      if (Res) *Res = R(kRuntimeError);
+      delete C;
+      return nullptr;
+    }
     for (uint32_t q = 0; q < 4; q++) h.value[q] = uint32_t(iv >> (32 * q));
     C->imports.push_back(h);
   }
@@ -705,7 +714,9 @@ WasmEdge_Result WasmEdge_BatchSetArgs(WasmEdge_BatchContext *C, const WasmEdge_S
       const WasmEdge_Value &v = Params[size_t(i) * ParamLen + k];
       if (uint8_t(v.Type) != t.params[k])
         return R(C->fail(kFuncSigMismatch, "parameter type mismatch"));
-      const uint128_t x = t.params[k] == wb::EXTERNREF ? uint128_t(C->xref_in(v.Value)) : v.Value;
+      bool full = false;
+      const uint128_t x = t.params[k] == wb::EXTERNREF ? uint128_t(C->xref_in(v.Value, &full)) : v.Value;
+      if (full) return R(C->fail(kRuntimeError, "externref intern table full (2^31 - 1 values)"));
       for (uint32_t q = 0; q < cells_of_value(t.params[k]); q++)
         cells[size_t(i) * pc + at++] = uint32_t(x >> (32 * q));
     }
@@ -757,6 +768,8 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
     for (uint32_t i = 0; i < C->n; i++) reached = std::max(reached, pages[i]);
     if (!grow_layout(C, reached, reached, false)) return R(kRuntimeError);
   }
+  // the call stack's growth is given back (hostcall.cpp shrink_stack)
+  if (!shrink_stack(C)) return R(kRuntimeError);
   // the whole reserved layout: pages a lane grows into within it must read zero
   const uint32_t init_words = C->mem_words;
   (void)hipEventRecord(C->ev0, C->stream);
@@ -950,6 +963,12 @@ uint32_t WasmEdge_BatchGetReservedPages(const WasmEdge_BatchContext *C) {
   return C ? C->rpages : 0;
 }
 
+uint32_t WasmEdge_BatchGetExtraMemoryPages(const WasmEdge_BatchContext *C, uint32_t MemIdx) {
+  if (C && !C->shards.empty()) return WasmEdge_BatchGetExtraMemoryPages(wbm::first(C), MemIdx);
+  if (!C || MemIdx == 0 || size_t(MemIdx) * 2 > C->xinfo_h.size()) return 0;
+  return C->xinfo_h[2 * (MemIdx - 1) + 1];
+}
+
 uint32_t WasmEdge_BatchGetMemoryGranule(const WasmEdge_BatchContext *C) {
   if (C && !C->shards.empty()) return WasmEdge_BatchGetMemoryGranule(wbm::first(C));
   return C ? 4u << C->mlog : 0;
@@ -1085,7 +1104,9 @@ WasmEdge_Result WasmEdge_BatchTableSetData(WasmEdge_BatchContext *C, const WasmE
   const int t = find_named(P.table_exports, TableName);
   if (t < 0) return R(C->fail(kFuncNotFound, "table export not found"));
   if (uint32_t(Data.Type) != P.tables[t].type) return R(kRefTypeMismatch);
-  const uint32_t v = P.tables[t].type == wb::EXTERNREF ? C->xref_in(Data.Value) : uint32_t(Data.Value);
+  bool full = false;
+  const uint32_t v = P.tables[t].type == wb::EXTERNREF ? C->xref_in(Data.Value, &full) : uint32_t(Data.Value);
+  if (full) return R(C->fail(kRuntimeError, "externref intern table full (2^31 - 1 values)"));
   if (P.tables[t].type == wb::FUNCREF && v != 0xFFFFFFFFu && v >= P.funcs.size())
     return R(C->fail(kRuntimeError, "funcref is not a function index of the module"));
   if (Inst == WASMEDGE_BATCH_ALL_INSTANCES) {
@@ -1153,7 +1174,9 @@ WasmEdge_Result WasmEdge_BatchGlobalSetValue(WasmEdge_BatchContext *C, const Was
   // wasmedge.cpp:2286-2295: a constant global or a value of another type is ignored
   const uint8_t t = P.global_types[g];
   if (!P.global_mut[g] || uint32_t(Value.Type) != t) return R(0);
-  const uint128_t x = t == wb::EXTERNREF ? uint128_t(C->xref_in(Value.Value)) : Value.Value;
+  bool full = false;
+  const uint128_t x = t == wb::EXTERNREF ? uint128_t(C->xref_in(Value.Value, &full)) : Value.Value;
+  if (full) return R(C->fail(kRuntimeError, "externref intern table full (2^31 - 1 values)"));
   for (uint32_t q = 0; q < wb::cells_of(t); q++)
     if (!put_lane(C, C->lstate.ptr, C->ls_slots, LS_GLOBALS + P.global_cell[g] + q, Inst,
                   uint32_t(x >> (32 * q))))

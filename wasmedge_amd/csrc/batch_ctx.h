@@ -159,7 +159,8 @@ struct WasmEdge_BatchContext {
   uint32_t mem_max_pages = 0, mem_words = 0, gs_depth = 0, ls_slots = 0, gs_lds = 0;
   // the call stack grows on demand (CallStackCells 0): a call past gs_depth parks, the host
   // doubles the stack (grow_stack) while device memory allows (KParams::gs_grow)
-  bool gs_grow = false;
+  bool gs_grow = false, gs_grow0 = false;
+  uint32_t gs_depth0 = 0;                 // (the depth BatchReset returns the stack to)
   // per-lane tables widen on demand: a table.grow past its capacity parks, the host relays
   // the tables out wider (hostcall.cpp widen_tables; KParams::tg_grow / tlimit)
   bool tg_grow = false;
@@ -226,13 +227,18 @@ struct WasmEdge_BatchContext {
   std::vector<uint64_t> xref_vals;
   std::unordered_map<uint64_t, uint32_t> xref_ids;
   std::mutex xref_mu;   // (host functions may run on several threads)
-  uint32_t xref_in(uint128_t v) {
+  // *full is set when a wide value finds the intern table full: the call that passed it
+  // fails (RuntimeError; a host function's result: HostFuncFailed) instead of passing null
+  uint32_t xref_in(uint128_t v, bool *full) {
     const uint64_t x = uint64_t(v);
     if (x < 0x80000000ull || x == 0xFFFFFFFFull) return uint32_t(x);
     std::lock_guard<std::mutex> g(xref_mu);
     auto it = xref_ids.find(x);
     if (it != xref_ids.end()) return it->second;
-    if (xref_vals.size() >= 0x7FFFFFFFull) return 0xFFFFFFFFu;   // (2^31 - 1 distinct values)
+    if (xref_vals.size() >= 0x7FFFFFFFull) {   // (2^31 - 1 distinct values)
+      *full = true;
+      return 0xFFFFFFFFu;
+    }
     const uint32_t h = 0x80000000u + uint32_t(xref_vals.size());
     xref_vals.push_back(x);
     xref_ids.emplace(x, h);
@@ -349,6 +355,7 @@ bool pool_reset(WasmEdge_BatchContext *C);
 // launches, its contents copied); false: no device memory for it (the caller then stops
 // growing it: calls past it trap 0xB0 as with a fixed CallStackCells)
 bool grow_stack(WasmEdge_BatchContext *C, uint64_t need);
+bool shrink_stack(WasmEdge_BatchContext *C);
 // grow the reserved layout to at least `need` pages per instance (up to `want`), within the
 // device memory and MemoryPoolBytes; live: keep the instances' memory (pool rows move into
 // the layout), else the next Reset rewrites it (mem_fresh). false only on a device error;

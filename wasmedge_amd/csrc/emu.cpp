@@ -103,6 +103,27 @@ __attribute__((visibility("default"))) void wb_emu_set_wasi(int on, const char *
   g_wasi_env.args.assign(args, args + nargs);
   g_wasi_env.envs.assign(envs, envs + nenvs);
 }
+// preopen guest names (fds 3, 4, ...) and per-instance command lines for the next
+// wb_emu_execute (an instance without its own args uses the shared ones)
+static std::vector<std::vector<std::string>> g_wasi_inst_args;
+static std::vector<bool> g_wasi_inst_own;
+__attribute__((visibility("default"))) void wb_emu_set_wasi_preopens(const char *const *dirs, uint32_t n) {
+  g_wasi_env.preopens.clear();
+  for (uint32_t k = 0; k < n; k++) {
+    const std::string d = dirs[k];
+    const size_t colon = d.find(':');
+    g_wasi_env.preopens.push_back(wbw::canonical_guest(colon == std::string::npos ? d : d.substr(0, colon)));
+  }
+}
+__attribute__((visibility("default"))) void wb_emu_set_instance_args(uint32_t inst, const char *const *args, uint32_t n) {
+  if (inst >= g_wasi_inst_args.size()) { g_wasi_inst_args.resize(inst + 1); g_wasi_inst_own.resize(inst + 1, false); }
+  g_wasi_inst_args[inst].assign(args, args + n);
+  g_wasi_inst_own[inst] = true;
+}
+__attribute__((visibility("default"))) void wb_emu_clear_instance_args() {
+  g_wasi_inst_args.clear();
+  g_wasi_inst_own.clear();
+}
 __attribute__((visibility("default"))) uint32_t wb_emu_wasi_output(uint32_t inst, uint32_t fd, uint8_t *buf, uint32_t len) {
   if (inst >= g_wasi_lanes.size() || (fd != 1 && fd != 2)) return 0;
   const std::string &o = g_wasi_lanes[inst].out[fd - 1];
@@ -214,6 +235,8 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   // imports served by the WASI subset (wasi_impl.h), per function index
   std::vector<int> wasi_fn(P.funcs.size(), -1);
   g_wasi_lanes.assign(g_wasi ? n : 0, wbw::Lane{});
+  for (uint32_t k = 0; g_wasi && k < n && k < g_wasi_inst_own.size(); k++)
+    if (g_wasi_inst_own[k]) { g_wasi_lanes[k].own_args = true; g_wasi_lanes[k].args = g_wasi_inst_args[k]; }
   for (uint32_t f = 0; g_wasi && f < P.n_imported; f++)
     if (P.funcs[f].import_module == "wasi_snapshot_preview1")
       wasi_fn[f] = wbw::lookup(P.funcs[f].import_name, P.types[P.funcs[f].type].params,
@@ -326,7 +349,9 @@ __attribute__((visibility("default"))) int wb_emu_execute(
           if (wfn >= 0) {
             EmuMem em;
             em.mb = mb; em.bytes = uint64_t(pages) << 16; em.has = P.has_mem;
-            e = wbw::call(wfn, g_wasi_env, g_wasi_lanes[inst], em, &fr[ybase], &rets[0]);
+            uint32_t wa[wbw::kMaxArgs] = {0};
+            for (uint32_t k = 0; k < ht.params.size() && k < wbw::kMaxArgs; k++) wa[k] = fr[ybase + k];
+            e = wbw::call(wfn, g_wasi_env, g_wasi_lanes[inst], em, wa, &rets[0]);
           } else {
             e = g_host(inst, ycall, &fr[ybase], rets, mb, uint64_t(pages) << 16);
           }

@@ -290,19 +290,31 @@ bool grow_layout(WasmEdge_BatchContext *C, uint32_t need, uint32_t want, bool li
   if (cap < need) return true;
   const uint32_t target = uint32_t(std::min<uint64_t>(want, cap));
   const size_t old_words = C->mem_words, new_words = size_t(target) << 14;
-  if (!live) {   // (the next Reset writes every page: drop the old layout first)
-    for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
-    C->pool_chunks.clear();
-    C->pool_free.clear();
-    C->pool_bytes = 0;
-    if (!C->mem.alloc(size_t(C->nwaves) * new_words * 64 + 64)) {
-      (void)hipGetLastError();   // (no room after all: the layout it had)
-      if (!C->mem.alloc(size_t(C->nwaves) * old_words * 64 + 64))
-        return C->hip_ok(hipErrorOutOfMemory, "memory layout");
-      C->pool_used = true;   // (its pool rows went with it: pool_reset restarts the table)
-      C->mem_fresh = true;
-      return true;
+  if (!live) {   // (the next Reset writes every page: nothing is copied)
+    // the new layout is allocated before the old one goes, so a failure leaves the context
+    // with the layout it had (never without one); the pool rows go first only when the
+    // new layout does not fit beside them
+    const size_t bytes = (size_t(C->nwaves) * new_words * 64 + 64) * 4;
+    uint32_t *nm = nullptr;
+    auto drop_pool = [&] {
+      for (const auto &ch : C->pool_chunks) (void)hipFree(ch.first);
+      C->pool_chunks.clear();
+      C->pool_free.clear();
+      C->pool_bytes = 0;
+    };
+    if (hipMalloc(&nm, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      drop_pool();
+      if (hipMalloc(&nm, bytes) != hipSuccess) {
+        (void)hipGetLastError();   // (no room after all: the layout it had)
+        C->pool_used = true;   // (its pool rows went: pool_reset restarts the table)
+        return true;
+      }
     }
+    drop_pool();
+    (void)hipFree(C->mem.ptr);
+    C->mem.ptr = nm;
+    C->mem.n = size_t(C->nwaves) * new_words * 64 + 64;
     C->mem_fresh = true;
   } else {
     uint32_t *nm = nullptr;
@@ -368,14 +380,20 @@ bool grow_layout(WasmEdge_BatchContext *C, uint32_t need, uint32_t want, bool li
 
 // The call stack's HBM part doubled (at least), between launches: [wave][slot][64] at the
 // old depth copied into the new one (one 2D copy while its pitch allows), the old freed.
-// Bounded by 3/4 of the device memory left; false when that does not hold `need` cells.
+// Bounded by CallStackMaxBytes (0: an eighth of the device's memory) and by 3/4 of the
+// device memory left, so a runaway recursion cannot take the device from the context's
+// own memory growth or from other contexts; false when that does not hold `need` cells.
+// BatchReset gives the growth back (shrink_stack).
 bool grow_stack(WasmEdge_BatchContext *C, uint64_t need) {
   const uint64_t old_d = C->gs_depth;
   uint64_t d = std::max<uint64_t>(old_d * 2, need);
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
   const uint64_t per_cell = uint64_t(C->nwaves) * 256;   // one cell of every lane
-  const uint64_t cap = std::min<uint64_t>(uint64_t(free_b) / 4 * 3 / per_cell, 0x7FFFFFFFull / 256);
+  const uint64_t share = C->conf.CallStackMaxBytes ? C->conf.CallStackMaxBytes : uint64_t(total_b) / 8;
+  const uint64_t held = old_d * per_cell;                // (freed once the copy is made)
+  uint64_t cap = std::min<uint64_t>(uint64_t(free_b) / 4 * 3 / per_cell, 0x7FFFFFFFull / 256);
+  cap = std::min<uint64_t>(cap, std::max<uint64_t>(share, held) / per_cell);
   d = std::min(d, cap);
   if (d <= old_d || d < need) return false;
   uint32_t *ns = nullptr;
@@ -395,6 +413,25 @@ bool grow_stack(WasmEdge_BatchContext *C, uint64_t need) {
   C->gstack.ptr = ns;
   C->gstack.n = size_t(C->nwaves) * d * 64;
   C->gs_depth = uint32_t(d);
+  return true;
+}
+
+// At BatchReset: the call stack back to its first depth and growth re-armed (a stack that
+// once hit its bound grows again for the next run). Between launches; the stack's contents
+// are dead after a Reset.
+bool shrink_stack(WasmEdge_BatchContext *C) {
+  C->gs_grow = C->gs_grow0;
+  if (C->gs_depth <= C->gs_depth0) return true;
+  uint32_t *ns = nullptr;
+  if (!C->hip_ok(hipStreamSynchronize(C->stream), "call stack")) return false;
+  if (hipMalloc(&ns, size_t(C->nwaves) * C->gs_depth0 * 256) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;   // (keeps the deeper stack it has)
+  }
+  (void)hipFree(C->gstack.ptr);
+  C->gstack.ptr = ns;
+  C->gstack.n = size_t(C->nwaves) * C->gs_depth0 * 64;
+  C->gs_depth = C->gs_depth0;
   return true;
 }
 
@@ -688,9 +725,15 @@ int64_t service_host_calls(WasmEdge_BatchContext *C) {
           continue;
         }
         at = 0;
+        bool full = false;
         for (size_t q = 0; q < t.results.size(); q++) {
-          const uint128_t v = t.results[q] == wb::EXTERNREF ? uint128_t(C->xref_in(rets[q].Value)) : rets[q].Value;
+          const uint128_t v = t.results[q] == wb::EXTERNREF ? uint128_t(C->xref_in(rets[q].Value, &full)) : rets[q].Value;
           for (uint32_t c = 0; c < wb::cells_of(t.results[q]); c++) cells[at++] = uint32_t(v >> (32 * c));
+        }
+        if (full) {   // (the intern table is full: the host function's result cannot pass)
+          st[i] = 0x8D;   // HostFuncFailed
+          hcall[i] = 0xFFFFFFFFu;
+          continue;
         }
         hcall[i] = at;
         mine++;

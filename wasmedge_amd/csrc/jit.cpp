@@ -2895,10 +2895,19 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         e.l("v_mov_b32 v112, 1");
       }
       if (st == 2) {   // the lanes whose every cached word is at its load's address
+        // (the effective address is 33 bits: a lane whose x + offset carries, or lands on
+        // 0xFFFFFFFF -- the invalid slots' mark, never a 4-byte load in bounds -- takes
+        // the plain path, which traps it)
         for (const auto &f : fwd[k]) {
           const DInstr &I = P.code[f.first];
-          if (I.w3) e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, I.w3, e.v(I.w1 & 0xFFFFu));
-          else e.l("v_mov_b32 %s, %s", Y0, e.v(I.w1 & 0xFFFFu));
+          if (I.w3) {
+            e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", Y0, I.w3, e.v(I.w1 & 0xFFFFu));
+            e.l("s_andn2_b64 exec, exec, vcc");
+          } else {
+            e.l("v_mov_b32 %s, %s", Y0, e.v(I.w1 & 0xFFFFu));
+          }
+          e.l("v_cmp_ne_u32_e32 vcc, -1, %s", Y0);
+          e.l("s_and_b64 exec, exec, vcc");
           e.l("v_cmp_eq_u32_e32 vcc, v%u, %s", f.second.first, Y0);
           e.l("s_and_b64 exec, exec, vcc");
         }

@@ -31,10 +31,10 @@ WasmEdge_Result wasi_trampoline(void *Data, WasmEdge_BatchMemoryContext *M,
   const auto *slot = static_cast<const WasmEdge_BatchContext::WasiSlot *>(Data);
   WasmEdge_BatchContext *C = slot->ctx;
   const uint32_t inst = M->inst;   // (this context's own lane index: its WASI state)
-  uint32_t a[4] = {0, 0, 0, 0}, ret = 0;
+  uint32_t a[wbw::kMaxArgs] = {0}, ret = 0;
   const size_t f = size_t(slot - C->wasi_slots.data());   // the import's function index
   const wb::FuncType &t = C->prog.types[C->prog.funcs[f].type];
-  for (size_t k = 0; k < t.params.size() && k < 4; k++) a[k] = uint32_t(Params[k].Value);
+  for (size_t k = 0; k < t.params.size() && k < wbw::kMaxArgs; k++) a[k] = uint32_t(Params[k].Value);
   CtxMem mem(M);
   const uint8_t e = wbw::call(slot->fn, C->wasi_env, C->wasi_lanes[inst], mem, a, &ret);
   if (e) return R(e);
@@ -49,13 +49,30 @@ extern "C" {
 WasmEdge_Result WasmEdge_BatchInitWASI(WasmEdge_BatchContext *C, const char *const *Args,
                                        const uint32_t ArgLen, const char *const *Envs,
                                        const uint32_t EnvLen) {
+  return WasmEdge_BatchInitWASIWithPreopens(C, Args, ArgLen, Envs, EnvLen, nullptr, 0);
+}
+
+WasmEdge_Result WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *C, const char *const *Args,
+                                                   const uint32_t ArgLen, const char *const *Envs,
+                                                   const uint32_t EnvLen,
+                                                   const char *const *Preopens,
+                                                   const uint32_t PreopenLen) {
   if (!C) return R(kWrongVMWorkflow);
   if (!C->shards.empty())
-    return wbm::all(C, [&](WasmEdge_BatchContext *s) { return WasmEdge_BatchInitWASI(s, Args, ArgLen, Envs, EnvLen); });
+    return wbm::all(C, [&](WasmEdge_BatchContext *s) {
+      return WasmEdge_BatchInitWASIWithPreopens(s, Args, ArgLen, Envs, EnvLen, Preopens, PreopenLen);
+    });
   C->wasi_env.args.clear();
   C->wasi_env.envs.clear();
+  C->wasi_env.preopens.clear();
   for (uint32_t k = 0; k < ArgLen; k++) C->wasi_env.args.emplace_back(Args && Args[k] ? Args[k] : "");
   for (uint32_t k = 0; k < EnvLen; k++) C->wasi_env.envs.emplace_back(Envs && Envs[k] ? Envs[k] : "");
+  // "guest:host" or one path for both (environ.cpp:57-66); the fds follow the list's order
+  for (uint32_t k = 0; k < PreopenLen; k++) {
+    const std::string d = Preopens && Preopens[k] ? Preopens[k] : "";
+    const size_t colon = d.find(':');
+    C->wasi_env.preopens.push_back(wbw::canonical_guest(colon == std::string::npos ? d : d.substr(0, colon)));
+  }
   C->wasi_lanes.assign(C->n, wbw::Lane{});
   const wb::Program &P = C->prog;
   C->wasi_slots.assign(P.funcs.size(), WasmEdge_BatchContext::WasiSlot{C, -1});
@@ -67,6 +84,21 @@ WasmEdge_Result WasmEdge_BatchInitWASI(WasmEdge_BatchContext *C, const char *con
     C->wasi_slots[f].fn = fn;
     C->hosts[f] = WasmEdge_BatchContext::HostFn{wasi_trampoline, &C->wasi_slots[f]};
   }
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchWASISetInstanceArgs(WasmEdge_BatchContext *C, uint32_t Inst,
+                                                  const char *const *Args, const uint32_t ArgLen) {
+  WasmEdge_BatchContext *s;
+  uint32_t l;
+  if (C && !C->shards.empty())
+    return wbm::route(C, Inst, &s, &l) ? WasmEdge_BatchWASISetInstanceArgs(s, l, Args, ArgLen)
+                                       : R(kWrongVMWorkflow);
+  if (!C || Inst >= C->wasi_lanes.size()) return R(kWrongVMWorkflow);
+  wbw::Lane &L = C->wasi_lanes[Inst];
+  L.own_args = true;
+  L.args.clear();
+  for (uint32_t k = 0; k < ArgLen; k++) L.args.emplace_back(Args && Args[k] ? Args[k] : "");
   return R(0);
 }
 

@@ -11,6 +11,13 @@
 //                                  vinode.h:337-343), other fds BADF (no preopens here)
 //   proc_exit                      wasifunc.cpp:1550-1554 (exit code, then Terminated)
 //   sched_yield                    wasifunc.cpp:1571-1576
+//   fd_prestat_get                 wasifunc.cpp:746-766, environ.h:385-399: BADF for an fd
+//                                  with no node, INVAL for the stdio nodes (no name), else
+//                                  tag DIR + the preopen's name length
+//   fd_prestat_dir_name            wasifunc.cpp:724-744, environ.h:406-420: the name's
+//                                  first min(name, len) bytes
+// Args may be given per instance (WasmEdge_BatchWASISetInstanceArgs); the reference builds
+// one Environ per VM, so per-instance args are per-VM args.
 // Every pointer is bounds-checked like MemoryInstance::getPointer (memory.h:226-233:
 // Offset + sizeof(T) * Count <= size, the product in 32 bits) before anything is written.
 #pragma once
@@ -24,21 +31,52 @@ namespace wbw {
 enum : uint32_t {                       // thirdparty/wasi/api.hpp
   ERRNO_SUCCESS = 0, ERRNO_BADF = 8, ERRNO_FAULT = 21, ERRNO_INVAL = 28, ERRNO_NOTCAPABLE = 76
 };
+constexpr uint8_t kPreopenTypeDir = 0;  // __WASI_PREOPENTYPE_DIR
 constexpr uint32_t kIOVMax = 1024;      // include/host/wasi/environ.h:33
+constexpr uint32_t kMaxArgs = 4;        // operands of the widest function in the subset
 constexpr uint8_t kTerminated = 0x01;   // ErrCode::Terminated (enum.inc)
 
 enum Fn { ARGS_GET, ARGS_SIZES_GET, ENVIRON_GET, ENVIRON_SIZES_GET, FD_WRITE, PROC_EXIT,
-          SCHED_YIELD, NUM_FNS };
+          SCHED_YIELD, FD_PRESTAT_GET, FD_PRESTAT_DIR_NAME, NUM_FNS };
 
-// configuration shared by every instance (WasmEdge_ImportObjectCreateWASI's Args/Envs)
+// configuration shared by every instance (WasmEdge_ImportObjectCreateWASI's Args/Envs/
+// Preopens): preopens are the guest names of fds 3, 4, ... (environ.cpp:54-93)
 struct Env {
-  std::vector<std::string> args, envs;
+  std::vector<std::string> args, envs, preopens;
 };
-// per-instance WASI state: captured stdout/stderr and the proc_exit code
+// per-instance WASI state: captured stdout/stderr, the proc_exit code and, when the
+// instance has args of its own, those args
 struct Lane {
   std::string out[2];
   uint32_t exit_code = 0;
+  bool own_args = false;
+  std::vector<std::string> args;
 };
+
+// VINode::canonicalGuest (lib/host/wasi/vinode.cpp:54-97), the name a preopen binds under:
+// leading slashes dropped, "." kept only as the first part, ".." pops, "" -> "/"
+inline std::string canonical_guest(const std::string &path) {
+  std::vector<std::string> parts;
+  size_t i = 0;
+  while (i < path.size() && path[i] == '/') i++;
+  while (i < path.size()) {
+    size_t j = path.find('/', i);
+    if (j == std::string::npos) j = path.size();
+    const std::string part = path.substr(i, j - i);
+    while (j < path.size() && path[j] == '/') j++;
+    if (part == "..") {
+      if (!parts.empty()) parts.pop_back();
+    } else if (part[0] != '.' || parts.size() != 1) {
+      parts.push_back(part);
+    }
+    i = j;
+  }
+  if (parts.empty()) parts.push_back("");
+  std::string r;
+  for (const auto &p : parts) r += p + "/";
+  r.pop_back();
+  return r.empty() ? std::string("/") : r;
+}
 
 // one instance's linear memory
 struct MemIO {
@@ -61,7 +99,9 @@ inline int lookup(const std::string &name, const std::vector<uint8_t> &params,
                           {"environ_sizes_get", ENVIRON_SIZES_GET, 2, 1},
                           {"fd_write", FD_WRITE, 4, 1},
                           {"proc_exit", PROC_EXIT, 1, 0},
-                          {"sched_yield", SCHED_YIELD, 0, 1}};
+                          {"sched_yield", SCHED_YIELD, 0, 1},
+                          {"fd_prestat_get", FD_PRESTAT_GET, 2, 1},
+                          {"fd_prestat_dir_name", FD_PRESTAT_DIR_NAME, 3, 1}};
   for (const S &s : tab) {
     if (name != s.n) continue;
     if (params.size() != s.np || results.size() != s.nr) return -1;
@@ -150,17 +190,52 @@ inline uint32_t fd_write(MemIO &m, Lane &lane, int32_t fd, uint32_t iovs, uint32
   return ERRNO_SUCCESS;
 }
 
+// the node behind fd: -1 none, 0..2 stdio, 3.. preopen k - 3 (Environ::getNodeOrNull)
+inline int node_of(const Env &env, int32_t fd) {
+  if (fd < 0) return -1;
+  if (fd <= 2) return fd;
+  return uint64_t(fd) - 3 < env.preopens.size() ? fd : -1;
+}
+
+// __wasi_prestat_t {u8 tag; u32 pr_name_len} (8 bytes; the 3 padding bytes untouched)
+inline uint32_t fd_prestat_get(MemIO &m, const Env &env, int32_t fd, uint32_t ptr) {
+  if (!m.present()) return ERRNO_FAULT;
+  if (!in_bounds(m, ptr, 8, 1)) return ERRNO_FAULT;
+  const int n = node_of(env, fd);
+  if (n < 0) return ERRNO_BADF;
+  if (n <= 2) return ERRNO_INVAL;                       // stdio nodes have no name
+  const std::string &name = env.preopens[n - 3];
+  const uint8_t tag = kPreopenTypeDir;
+  m.write(ptr, 1, &tag);
+  put_u32(m, ptr + 4, uint32_t(name.size()));
+  return ERRNO_SUCCESS;
+}
+
+inline uint32_t fd_prestat_dir_name(MemIO &m, const Env &env, int32_t fd, uint32_t buf, uint32_t len) {
+  if (!m.present()) return ERRNO_FAULT;
+  if (!in_bounds(m, buf, 1, len)) return ERRNO_FAULT;
+  const int n = node_of(env, fd);
+  if (n < 0) return ERRNO_BADF;
+  if (n <= 2) return ERRNO_INVAL;
+  const std::string &name = env.preopens[n - 3];
+  const uint32_t k = uint32_t(name.size()) < len ? uint32_t(name.size()) : len;
+  if (k) m.write(buf, k, reinterpret_cast<const uint8_t *>(name.data()));
+  return ERRNO_SUCCESS;
+}
+
 // Run WASI function `f` for one instance. args: i32 operands; *ret: the errno result.
 // Returns 0, or the ErrCode that ends the instance (Terminated for proc_exit).
 inline uint8_t call(int f, const Env &env, Lane &lane, MemIO &m, const uint32_t *a, uint32_t *ret) {
   switch (f) {
-  case ARGS_GET: *ret = list_get(m, env.args, a[0], a[1]); return 0;
-  case ARGS_SIZES_GET: *ret = list_sizes(m, env.args, a[0], a[1]); return 0;
+  case ARGS_GET: *ret = list_get(m, lane.own_args ? lane.args : env.args, a[0], a[1]); return 0;
+  case ARGS_SIZES_GET: *ret = list_sizes(m, lane.own_args ? lane.args : env.args, a[0], a[1]); return 0;
   case ENVIRON_GET: *ret = list_get(m, env.envs, a[0], a[1]); return 0;
   case ENVIRON_SIZES_GET: *ret = list_sizes(m, env.envs, a[0], a[1]); return 0;
   case FD_WRITE: *ret = fd_write(m, lane, int32_t(a[0]), a[1], a[2], a[3]); return 0;
   case PROC_EXIT: lane.exit_code = a[0]; return kTerminated;
   case SCHED_YIELD: *ret = ERRNO_SUCCESS; return 0;
+  case FD_PRESTAT_GET: *ret = fd_prestat_get(m, env, int32_t(a[0]), a[1]); return 0;
+  case FD_PRESTAT_DIR_NAME: *ret = fd_prestat_dir_name(m, env, int32_t(a[0]), a[1], a[2]); return 0;
   }
   return 0x8D;   // HostFuncFailed
 }
