@@ -9,9 +9,13 @@ to completion.  Instruction counts are the reference's Statistics counts
 
 Workload at N=1 (configs[1]): C2 -- 64K instances of the BLAKE3 compression loop
 (wasmedge_amd/workloads.py), per-instance input.  Multi-GPU: one process per GPU
-(torch.distributed.run), each rank runs its own 64K-instance shard (instance ids
-[rank*64K, (rank+1)*64K)), no data-path collective -> "scaling": "weak"; a CPU-side
-(gloo) barrier + max-over-ranks brackets the timed region.
+(torch.distributed.run), no data-path collective; a CPU-side (gloo) barrier +
+max-over-ranks brackets the timed region.  The default is STRONG scaling, the metric's
+configuration: the job's 64K instances (C5: 256K) split into contiguous id blocks over the
+ranks ("scaling": "strong"); --scaling weak gives every rank 64K of its own.  At N > 1 the
+line carries `expected_speedup` with its basis: 64K instances are 1024 waves, one per SIMD
+of ONE GPU, so splitting them over more GPUs leaves SIMDs idle without shortening any
+wave -- about 1x (C5's 4096 waves: up to 4x).
 
 Prints ONE JSON line on rank 0.
 """
@@ -145,6 +149,28 @@ def shard_ids(rank, n, world=1, scaling="weak"):
         lo, hi = rank * n // world, (rank + 1) * n // world
         return np.arange(lo, hi, dtype=np.int64)
     return np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+
+
+SIMDS_PER_GPU = 256 * 4   # MI355X: 256 CUs x 4 SIMDs
+
+
+def expected_speedup(total_instances, n_gpus, scaling):
+    """What N GPUs can give over one on this job (reported, never measured here): a wave of
+    64 instances runs on one SIMD, and its run time does not shrink when other SIMDs are
+    idle (profiles/r02e_strong_scaling_c2.json: per-rank step time at 64K/N instances
+    13.25 / 13.21 / 13.15 / 13.15 ms for N = 1/2/4/8 on one GPU). Strong scaling therefore
+    speeds up only while one GPU holds more waves than SIMDs: min(N, waves / SIMDs), at
+    least 1. Weak scaling: N (every GPU runs a whole job of its own)."""
+    waves = -(-int(total_instances) // 64)
+    if scaling == "weak":
+        return {"value": float(n_gpus), "basis": "weak scaling: every GPU runs its own %d "
+                "instances; instances are independent (no collective)" % (total_instances // n_gpus)}
+    v = max(1.0, min(float(n_gpus), waves / SIMDS_PER_GPU))
+    return {"value": v,
+            "basis": "strong scaling: %d instances = %d waves of 64 against %d SIMDs per GPU; a "
+                     "wave runs on one SIMD and its time does not shrink when other SIMDs idle, "
+                     "so N GPUs give min(N, waves / SIMDs) = %.2fx (at least 1)"
+                     % (total_instances, waves, SIMDS_PER_GPU, v)}
 
 
 def _free_port():
@@ -564,6 +590,8 @@ def main():
     ph.close()
     # the metric's configuration at N > 1 is the fixed total (strong); the weak-scaling
     # figure (every rank --instances of its own) rides along as an extra key
+    if n_gpus > 1:
+        out["expected_speedup"] = expected_speedup(out["config"]["instances"], n_gpus, args.scaling)
     if n_gpus > 1 and args.scaling == "strong" and not args.no_weak:
         wids = shard_ids(dist.rank, args.instances, dist.world, "weak") if not devices else \
             np.arange(args.instances * len(devices), dtype=np.int64)
@@ -653,9 +681,12 @@ def dry_run(args, dist):
     hi = dist.max(float(ids[-1]))
     dist.barrier()
     if dist.rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": dist.world, "scaling": args.scaling,
-                          "instances": int(total), "first_id": int(lo), "last_id": int(hi),
-                          "max_over_ranks": t}), flush=True)
+        line = {"dry_run": True, "n_gpus": dist.world, "scaling": args.scaling,
+                "instances": int(total), "first_id": int(lo), "last_id": int(hi),
+                "max_over_ranks": t}
+        if dist.world > 1:
+            line["expected_speedup"] = expected_speedup(int(total), dist.world, args.scaling)
+        print(json.dumps(line), flush=True)
     if dist.td:
         dist.td.destroy_process_group()
     return 0

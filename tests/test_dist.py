@@ -72,8 +72,10 @@ def test_bench_launcher_default_is_the_metric_config():
     job's 64K instances split over the GPUs (strong scaling)."""
     rc, lines = _run_bench("--gpus", "2", "--dry-run")
     assert rc == 0 and len(lines) == 1
+    exp = lines[0].pop("expected_speedup")
     assert lines[0] == {"dry_run": True, "n_gpus": 2, "scaling": "strong", "instances": 65536,
                         "first_id": 0, "last_id": 65535, "max_over_ranks": 2.0}
+    assert exp["value"] == 1.0 and "1024 waves" in exp["basis"]
     rc, lines = _run_bench("--gpus", "2", "--dry-run", "--workload", "c5")
     assert rc == 0 and lines[0]["instances"] == 262144
 
@@ -83,6 +85,7 @@ def test_bench_launcher_spawns_ranks_weak():
     own launcher (no torchrun); the ranks rendezvous on 127.0.0.1, shard by id and reduce."""
     rc, lines = _run_bench("--gpus", "2", "--dry-run", "--scaling", "weak", "--instances", "65536")
     assert rc == 0 and len(lines) == 1
+    assert lines[0].pop("expected_speedup")["value"] == 2.0
     assert lines[0] == {"dry_run": True, "n_gpus": 2, "scaling": "weak", "instances": 131072,
                         "first_id": 0, "last_id": 131071, "max_over_ranks": 2.0}
 
@@ -106,3 +109,17 @@ def test_strong_shards_cover_the_job():
         ids = [bench.shard_ids(r, 65536, world, "strong") for r in range(world)]
         assert sum(len(x) for x in ids) == 65536
         assert all(int(a[-1]) + 1 == int(b[0]) for a, b in zip(ids, ids[1:]))
+
+
+def test_bench_expected_speedup_at_8_gpus():
+    """an N > 1 line states the speed-up its configuration can give, with
+    the basis -- ~1x at 64K instances (1024 waves = one per SIMD of one GPU), up to 4x for
+    C5's 256K, N under weak scaling."""
+    import bench
+    rc, lines = _run_bench("--gpus", "8", "--dry-run")
+    assert rc == 0 and lines[0]["n_gpus"] == 8
+    assert lines[0]["expected_speedup"]["value"] == 1.0
+    rc, lines = _run_bench("--gpus", "8", "--dry-run", "--workload", "c5")
+    assert rc == 0 and lines[0]["expected_speedup"]["value"] == 4.0
+    assert bench.expected_speedup(65536, 8, "weak")["value"] == 8.0
+    assert bench.expected_speedup(262144, 2, "strong")["value"] == 2.0
