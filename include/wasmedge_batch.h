@@ -375,9 +375,14 @@ WasmEdge_BatchInitWASI(WasmEdge_BatchContext *Cxt, const char *const *Args, cons
                        const char *const *Envs, const uint32_t EnvLen);
 /* The same with preopened directories, as WasmEdge_ImportObjectInitWASI's Preopens
  * (wasmedge.h:2739-2742): "guest:host" or one path for both; they become fds 3, 4, ... in
- * the order given (environ.cpp:54-93), named by VINode::canonicalGuest. fd_prestat_get /
- * fd_prestat_dir_name report them (wasifunc.cpp:724-766; stdio fds give INVAL, others
- * BADF). */
+ * the order given (environ.cpp:54-93), named by VINode::canonicalGuest, with the
+ * reference's rights, and behave as a read-only mount (N instances share the host
+ * directory): path_open, fd_read, fd_seek, fd_tell, fd_close, fd_fdstat_get,
+ * fd_filestat_get, path_filestat_get, fd_prestat_get / _dir_name work on them, an open that
+ * would create, truncate or write fails with ROFS. A file is read whole when an instance
+ * first opens it. Also bound: clock_time_get, clock_res_get, random_get,
+ * fd_fdstat_set_flags (wasmedge_amd/csrc/wasi_impl.h lists each with its reference
+ * lines). */
 WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *Cxt, const char *const *Args,
                                    const uint32_t ArgLen, const char *const *Envs,
@@ -387,6 +392,13 @@ WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *Cxt, const char *const
  * the reference builds one Environ per VM (environ.cpp:95-98), so N instances with their
  * own arguments are N VMs with their own WASI modules. Call after WasmEdge_BatchInitWASI
  * (which clears every instance's own args). */
+/* Reproducible WASI: instance i's new fd numbers and random_get bytes come from a
+ * generator seeded by (Seed, i) -- the reference draws both from std::random_device
+ * (environ.h:834-850, 1096-1108), and so does this library by default -- and every clock
+ * reads ClockNs, advancing 1 us per call of the instance (clock_res_get: 1 ns). Call after
+ * the InitWASI call it applies to; it also resets the instances' fd tables. */
+WASMEDGE_BATCH_API WasmEdge_Result
+WasmEdge_BatchWASISetDeterministic(WasmEdge_BatchContext *Cxt, uint64_t Seed, uint64_t ClockNs);
 WASMEDGE_BATCH_API WasmEdge_Result
 WasmEdge_BatchWASISetInstanceArgs(WasmEdge_BatchContext *Cxt, uint32_t Inst,
                                   const char *const *Args, const uint32_t ArgLen);

@@ -85,6 +85,10 @@ def lib():
         L.om_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
         L.om_set_wasi_preopens.restype = None
         L.om_set_wasi_preopens.argtypes = [cpp, ctypes.c_uint32]
+        L.om_set_wasi_deterministic.restype = None
+        L.om_set_wasi_deterministic.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+        L.om_wasi_set_lane.restype = None
+        L.om_wasi_set_lane.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.om_set_instance_args.restype = None
         L.om_set_instance_args.argtypes = [ctypes.c_void_p, cpp, ctypes.c_uint32]
         L.om_wasi_exit_code.restype = ctypes.c_uint32
@@ -264,6 +268,16 @@ class Instance:
     def wasi_exit_code(self):
         return lib().om_wasi_exit_code(self._h)
 
+    def memory(self, off, n):
+        """n bytes of linear memory 0 from off."""
+        L = lib()
+        assert off + n <= L.om_mem_pages(self._h) * 65536
+        return ctypes.string_at(L.om_mem_data(self._h) + off, n)
+
+    def set_lane(self, lane):
+        """The instance id its WASI generator is keyed on (fd numbers, random_get)."""
+        lib().om_wasi_set_lane(self._h, lane)
+
     def set_args(self, args):
         """This instance's own WASI command line (one Environ per VM)."""
         a = (ctypes.c_char_p * max(len(args), 1))(*[x.encode() for x in args])
@@ -285,14 +299,17 @@ def set_lazy_imports(on):
     lib().om_set_lazy_imports(1 if on else 0)
 
 
-def set_wasi(on, args=(), envs=(), preopens=()):
+def set_wasi(on, args=(), envs=(), preopens=(), deterministic=None):
     """Bind the WASI subset (wasi_snapshot_preview1) for later instantiations, with these
     args/envs shared by every instance (the batched path's WasmEdge_BatchInitWASI) and
-    these preopened directories (fds 3, 4, ...)."""
+    these preopened directories (fds 3, 4, ...); deterministic: (seed, clock_ns) as
+    WasmEdge_BatchWASISetDeterministic."""
     def arr(v):
         return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
     lib().om_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
     lib().om_set_wasi_preopens(arr(list(preopens)), len(preopens))
+    seed, clock = deterministic or (0, 0)
+    lib().om_set_wasi_deterministic(1 if deterministic else 0, seed, clock)
 
 
 def set_imports(imports):

@@ -127,6 +127,9 @@ struct OInst {
   uint8_t *wasi_out[2]; uint64_t wasi_len[2], wasi_cap[2];
   uint32_t wasi_exit;
   char **own_args; uint32_t own_nargs; int has_own_args;   /* this VM's own command line */
+  /* WASI fd table (Environ::FdMap; wasi_fs.inc), the lane's generator and clock calls */
+  struct WFd *wfd; uint32_t nwfd, capwfd; int wfd_init;
+  uint64_t wrng, wclock; uint32_t wasi_lane;
 };
 
 /* ------------------------------------------------------------------ reader */

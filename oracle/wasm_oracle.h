@@ -68,6 +68,10 @@ void om_set_wasi(int on, const char *const *args, uint32_t nargs, const char *co
  * as fds 3, 4, ... for later instantiations; an instance's own args (one Environ per VM). */
 void om_set_wasi_preopens(const char *const *dirs, uint32_t n);
 void om_set_instance_args(OInst *i, const char *const *args, uint32_t n);
+/* WASI file/clock/random subset (wasi_fs.inc): reproducible fds, random_get and clocks
+ * (seed, clock_ns), and the instance id an instance's generator is keyed on */
+void om_set_wasi_deterministic(int on, uint64_t seed, uint64_t clock_ns);
+void om_wasi_set_lane(OInst *i, uint32_t lane);
 uint32_t om_wasi_exit_code(const OInst *i);
 uint64_t om_wasi_output(const OInst *i, uint32_t fd, const uint8_t **data);
 

@@ -14,6 +14,8 @@ answers):
   rust_add.wasm     tools/wasmedge/examples/add.wasm (compiled Rust/WASI; add 2 2 -> 4)
   hello.wasm        tools/wasmedge/examples/hello.wasm (compiled Rust/WASI command;
                     README.md:5-15 runs it as `wasmedge hello.wasm 1 2 3`)
+  qjs.wasm          tools/wasmedge/examples/js/qjs.wasm (QuickJS, a WASI command;
+                    js/README.md:9-14 runs `wasmedge --dir .:. qjs.wasm hello.js 1 2 3`)
   executor_interrupt.wasm  bytes of test/executor/ExecutorTest.cpp:122-126 (endless
                     loop in _start; cancel -> Interrupted, :127-145)
 """
@@ -52,6 +54,8 @@ def main():
                 os.path.join(OUT, "rust_add.wasm"))
     shutil.copy(os.path.join(REF, "tools/wasmedge/examples/hello.wasm"),
                 os.path.join(OUT, "hello.wasm"))
+    shutil.copy(os.path.join(REF, "tools/wasmedge/examples/js/qjs.wasm"),
+                os.path.join(OUT, "qjs.wasm"))
     src = open(os.path.join(REF, "test/executor/ExecutorTest.cpp")).read()
     m = re.search(r"std::array<WasmEdge::Byte, 46> Wasm\{(.*?)\};", src, re.S)
     data = bytes(int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]{2}", m.group(1)))

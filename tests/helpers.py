@@ -30,6 +30,7 @@ def emu_lib():
         E.wb_emu_set_wasi.argtypes = [ctypes.c_int, cpp, ctypes.c_uint32, cpp, ctypes.c_uint32]
         E.wb_emu_set_wasi_preopens.argtypes = [cpp, ctypes.c_uint32]
         E.wb_emu_set_instance_args.argtypes = [ctypes.c_uint32, cpp, ctypes.c_uint32]
+        E.wb_emu_set_wasi_deterministic.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         E.wb_emu_wasi_output.restype = ctypes.c_uint32
         E.wb_emu_wasi_output.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         E.wb_emu_wasi_exit_code.restype = ctypes.c_uint32
@@ -113,15 +114,17 @@ def emu_set_imports(imports):
                             0 if mx is None else 1, ctypes.cast(cells, ctypes.c_void_p))
 
 
-def emu_set_wasi(on, args=(), envs=(), preopens=(), instance_args=None):
+def emu_set_wasi(on, args=(), envs=(), preopens=(), instance_args=None, deterministic=None):
     """The emulator's copy of the library's WASI subset (wasi_impl.h); instance_args:
-    {instance: its own args} for the next run."""
+    {instance: its own args} for the next run; deterministic: (seed, clock_ns)."""
     def arr(v):
         return (ctypes.c_char_p * max(len(v), 1))(*[x.encode() for x in v])
     E = emu_lib()
     E.wb_emu_set_wasi(1 if on else 0, arr(list(args)), len(args), arr(list(envs)), len(envs))
     E.wb_emu_set_wasi_preopens(arr(list(preopens)), len(preopens))
     E.wb_emu_clear_instance_args()
+    seed, clock = deterministic or (0, 0)
+    E.wb_emu_set_wasi_deterministic(1 if deterministic else 0, seed, clock)
     for i, a in (instance_args or {}).items():
         E.wb_emu_set_instance_args(i, arr(list(a)), len(a))
 

@@ -194,6 +194,8 @@ def lib():
         L.WasmEdge_BatchInitWASI.argtypes = [vp, cpp, u32, cpp, u32]
         L.WasmEdge_BatchInitWASIWithPreopens.restype = _Result
         L.WasmEdge_BatchInitWASIWithPreopens.argtypes = [vp, cpp, u32, cpp, u32, cpp, u32]
+        L.WasmEdge_BatchWASISetDeterministic.restype = _Result
+        L.WasmEdge_BatchWASISetDeterministic.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.WasmEdge_BatchWASISetInstanceArgs.restype = _Result
         L.WasmEdge_BatchWASISetInstanceArgs.argtypes = [vp, u32, cpp, u32]
         L.WasmEdge_BatchWASIGetExitCode.restype = u32
@@ -464,6 +466,10 @@ class BatchContext:
         a, e, p = _cstrs(args), _cstrs(envs), _cstrs(preopens)
         self._check(lib().WasmEdge_BatchInitWASIWithPreopens(self._h, a, len(args), e, len(envs),
                                                              p, len(preopens)))
+
+    def wasi_deterministic(self, seed, clock_ns):
+        """Reproducible fd numbers / random_get / clocks (WasmEdge_BatchWASISetDeterministic)."""
+        self._check(lib().WasmEdge_BatchWASISetDeterministic(self._h, seed, clock_ns))
 
     def set_instance_args(self, inst, args):
         """Instance `inst`'s own command line (WasmEdge_BatchWASISetInstanceArgs)."""

@@ -109,11 +109,14 @@ static std::vector<std::vector<std::string>> g_wasi_inst_args;
 static std::vector<bool> g_wasi_inst_own;
 __attribute__((visibility("default"))) void wb_emu_set_wasi_preopens(const char *const *dirs, uint32_t n) {
   g_wasi_env.preopens.clear();
-  for (uint32_t k = 0; k < n; k++) {
-    const std::string d = dirs[k];
-    const size_t colon = d.find(':');
-    g_wasi_env.preopens.push_back(wbw::canonical_guest(colon == std::string::npos ? d : d.substr(0, colon)));
-  }
+  g_wasi_env.host.clear();
+  for (uint32_t k = 0; k < n; k++) wbw::add_preopen(g_wasi_env, dirs[k]);
+}
+// reproducible fd numbers / random_get / clocks (WasmEdge_BatchWASISetDeterministic)
+__attribute__((visibility("default"))) void wb_emu_set_wasi_deterministic(int on, uint64_t seed, uint64_t clock_ns) {
+  g_wasi_env.seed = seed;
+  g_wasi_env.fixed_clock = on != 0;
+  g_wasi_env.clock_ns = clock_ns;
 }
 __attribute__((visibility("default"))) void wb_emu_set_instance_args(uint32_t inst, const char *const *args, uint32_t n) {
   if (inst >= g_wasi_inst_args.size()) { g_wasi_inst_args.resize(inst + 1); g_wasi_inst_own.resize(inst + 1, false); }
@@ -235,6 +238,7 @@ __attribute__((visibility("default"))) int wb_emu_execute(
   // imports served by the WASI subset (wasi_impl.h), per function index
   std::vector<int> wasi_fn(P.funcs.size(), -1);
   g_wasi_lanes.assign(g_wasi ? n : 0, wbw::Lane{});
+  for (uint32_t k = 0; k < g_wasi_lanes.size(); k++) g_wasi_lanes[k].index = k;
   for (uint32_t k = 0; g_wasi && k < n && k < g_wasi_inst_own.size(); k++)
     if (g_wasi_inst_own[k]) { g_wasi_lanes[k].own_args = true; g_wasi_lanes[k].args = g_wasi_inst_args[k]; }
   for (uint32_t f = 0; g_wasi && f < P.n_imported; f++)
@@ -349,8 +353,8 @@ __attribute__((visibility("default"))) int wb_emu_execute(
           if (wfn >= 0) {
             EmuMem em;
             em.mb = mb; em.bytes = uint64_t(pages) << 16; em.has = P.has_mem;
-            uint32_t wa[wbw::kMaxArgs] = {0};
-            for (uint32_t k = 0; k < ht.params.size() && k < wbw::kMaxArgs; k++) wa[k] = fr[ybase + k];
+            uint64_t wa[wbw::kMaxArgs] = {0};
+            wbw::args_of_cells(ht.params, &fr[ybase], wa);
             e = wbw::call(wfn, g_wasi_env, g_wasi_lanes[inst], em, wa, &rets[0]);
           } else {
             e = g_host(inst, ycall, &fr[ybase], rets, mb, uint64_t(pages) << 16);

@@ -31,10 +31,12 @@ WasmEdge_Result wasi_trampoline(void *Data, WasmEdge_BatchMemoryContext *M,
   const auto *slot = static_cast<const WasmEdge_BatchContext::WasiSlot *>(Data);
   WasmEdge_BatchContext *C = slot->ctx;
   const uint32_t inst = M->inst;   // (this context's own lane index: its WASI state)
-  uint32_t a[wbw::kMaxArgs] = {0}, ret = 0;
+  uint64_t a[wbw::kMaxArgs] = {0};
+  uint32_t ret = 0;
   const size_t f = size_t(slot - C->wasi_slots.data());   // the import's function index
   const wb::FuncType &t = C->prog.types[C->prog.funcs[f].type];
-  for (size_t k = 0; k < t.params.size() && k < wbw::kMaxArgs; k++) a[k] = uint32_t(Params[k].Value);
+  for (size_t k = 0; k < t.params.size() && k < wbw::kMaxArgs; k++)
+    a[k] = t.params[k] == 0x7E ? uint64_t(Params[k].Value) : uint64_t(uint32_t(Params[k].Value));
   CtxMem mem(M);
   const uint8_t e = wbw::call(slot->fn, C->wasi_env, C->wasi_lanes[inst], mem, a, &ret);
   if (e) return R(e);
@@ -58,22 +60,34 @@ WasmEdge_Result WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *C, con
                                                    const char *const *Preopens,
                                                    const uint32_t PreopenLen) {
   if (!C) return R(kWrongVMWorkflow);
-  if (!C->shards.empty())
-    return wbm::all(C, [&](WasmEdge_BatchContext *s) {
+  if (!C->shards.empty()) {
+    const uint64_t seed = wbw::host_seed();
+    const WasmEdge_Result r = wbm::all(C, [&](WasmEdge_BatchContext *s) {
       return WasmEdge_BatchInitWASIWithPreopens(s, Args, ArgLen, Envs, EnvLen, Preopens, PreopenLen);
     });
+    if (r.Code) return r;
+    // (one seed, and every lane's generator keyed on its id in the whole batch)
+    for (uint32_t i = 0; i < C->n; i++) {
+      WasmEdge_BatchContext *s;
+      uint32_t l;
+      if (!wbm::route(C, i, &s, &l)) continue;
+      s->wasi_env.seed = seed;
+      s->wasi_lanes[l].index = i;
+    }
+    return r;
+  }
   C->wasi_env.args.clear();
   C->wasi_env.envs.clear();
   C->wasi_env.preopens.clear();
+  C->wasi_env.host.clear();
+  C->wasi_env.fixed_clock = false;
+  C->wasi_env.seed = wbw::host_seed();
   for (uint32_t k = 0; k < ArgLen; k++) C->wasi_env.args.emplace_back(Args && Args[k] ? Args[k] : "");
   for (uint32_t k = 0; k < EnvLen; k++) C->wasi_env.envs.emplace_back(Envs && Envs[k] ? Envs[k] : "");
   // "guest:host" or one path for both (environ.cpp:57-66); the fds follow the list's order
-  for (uint32_t k = 0; k < PreopenLen; k++) {
-    const std::string d = Preopens && Preopens[k] ? Preopens[k] : "";
-    const size_t colon = d.find(':');
-    C->wasi_env.preopens.push_back(wbw::canonical_guest(colon == std::string::npos ? d : d.substr(0, colon)));
-  }
+  for (uint32_t k = 0; k < PreopenLen; k++) wbw::add_preopen(C->wasi_env, Preopens && Preopens[k] ? Preopens[k] : "");
   C->wasi_lanes.assign(C->n, wbw::Lane{});
+  for (uint32_t i = 0; i < C->n; i++) C->wasi_lanes[i].index = i;
   const wb::Program &P = C->prog;
   C->wasi_slots.assign(P.funcs.size(), WasmEdge_BatchContext::WasiSlot{C, -1});
   for (uint32_t f = 0; f < P.n_imported; f++) {
@@ -83,6 +97,22 @@ WasmEdge_Result WasmEdge_BatchInitWASIWithPreopens(WasmEdge_BatchContext *C, con
     if (fn < 0) continue;
     C->wasi_slots[f].fn = fn;
     C->hosts[f] = WasmEdge_BatchContext::HostFn{wasi_trampoline, &C->wasi_slots[f]};
+  }
+  return R(0);
+}
+
+WasmEdge_Result WasmEdge_BatchWASISetDeterministic(WasmEdge_BatchContext *C, uint64_t Seed,
+                                                   uint64_t ClockNs) {
+  if (!C) return R(kWrongVMWorkflow);
+  if (!C->shards.empty())
+    return wbm::all(C, [&](WasmEdge_BatchContext *s) { return WasmEdge_BatchWASISetDeterministic(s, Seed, ClockNs); });
+  C->wasi_env.seed = Seed;
+  C->wasi_env.fixed_clock = true;
+  C->wasi_env.clock_ns = ClockNs;
+  for (auto &L : C->wasi_lanes) {   // (the lanes' tables and generators start over)
+    L.fs_ready = false;
+    L.fds.clear();
+    L.clock_calls = 0;
   }
   return R(0);
 }
