@@ -2012,6 +2012,7 @@ std::string simt_sched(bool hybrid, bool depth) {
 // runs kTripScan iterations per trip in trip mode (trip_scan_stage): every lane's next
 // loads go out together, then each lane's exit iteration is found in order.
 constexpr uint32_t kTripScan = 4;   // trip mode: scan iterations per trip (trip_scan_stage)
+constexpr uint32_t kTripBatch = 4;  // trip mode: lane-test compares issued together (trip_source)
 struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
 
 bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
@@ -2722,6 +2723,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   }
   h.l(".p2align 6");
   h.l("Ltin:");
+  h.l("s_waitcnt lgkmcnt(0)");   // (a handler's bank-B prefetch must land: the batches use s[86:91])
   h.l("s_mov_b64 exec, s[96:97]");
   for (uint32_t r : inval) h.l("v_mov_b32 v%u, -1", r);
   h.l("s_mov_b64 s[76:77], s[96:97]");
@@ -2739,12 +2741,47 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_mov_b64 exec, s[96:97]");
   // ---- the trip (EXEC = ALL between the runs)
   h.l("Ltrip:");
-  for (uint32_t k = 0; k < nr; k++) {
-    if (!split[k]) continue;
-    h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
-    h.l("s_and_b64 s[74:75], vcc, exec");
-    h.l("s_cbranch_scc1 LtA%u", k);
-    h.l("LtAr%u:", k);
+  // Batched lane tests (WB_TRIP_BATCH=0 turns them off): a run's test is a VALU compare
+  // whose mask a scalar branch reads, and that VALU -> SALU -> branch chain costs ~48
+  // cycles against ~20 for the branch alone (tools/ubench/lat.hip). So the compares of up
+  // to kTripBatch consecutive tests go out back to back into their own masks (s[80:81],
+  // s[86:91]: free between the runs; the trips start after every SMEM load has landed),
+  // and the tests then read them. A stage-A run moves no other run's lanes (it only takes
+  // its own out of TPC), so its batch stays valid; a stage-B run may move lanes onto later
+  // runs (VPC), so it recomputes the rest of its batch before it returns (stage end), and a
+  // run with its own LtF / LtS tests ends a batch.
+  const bool batch_on = !(getenv("WB_TRIP_BATCH") && getenv("WB_TRIP_BATCH")[0] == '0');
+  // dst = (v == pc) per lane; VOP3 takes no literal, so a pc past the inline constants goes
+  // through s68 / s69 (alternating: the compare has read one before the next is written)
+  auto vcmp64 = [](Em &x, const char *dst, uint32_t pc, const char *v, uint32_t j) {
+    if (pc <= 64) {
+      x.l("v_cmp_eq_u32_e64 %s, %u, %s", dst, pc, v);
+    } else {
+      x.l("s_mov_b32 s%u, 0x%x", 68 + (j & 1), pc);
+      x.l("v_cmp_eq_u32_e64 %s, s%u, %s", dst, 68 + (j & 1), v);
+    }
+  };
+  static const char *const PREG[kTripBatch] = {"s[80:81]", "s[86:87]", "s[88:89]", "s[90:91]"};
+  const uint32_t G = batch_on ? kTripBatch : 1;
+  {
+    std::vector<uint32_t> a;
+    for (uint32_t k = 0; k < nr; k++)
+      if (split[k]) a.push_back(k);
+    for (size_t b = 0; b < a.size(); b += G) {
+      const size_t e = std::min(a.size(), b + G);
+      if (batch_on)
+        for (size_t j = b; j < e; j++) vcmp64(h, PREG[j - b], runs[a[j]].pc, TPC, uint32_t(j - b));
+      for (size_t j = b; j < e; j++) {
+        if (batch_on) {
+          h.l("s_and_b64 s[74:75], %s, exec", PREG[j - b]);
+        } else {
+          h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[a[j]].pc, TPC);
+          h.l("s_and_b64 s[74:75], vcc, exec");
+        }
+        h.l("s_cbranch_scc1 LtA%u", a[j]);
+        h.l("LtAr%u:", a[j]);
+      }
+    }
   }
   h.l("s_waitcnt vmcnt(0)");
   // Forward chaining (WB_TRIP_CHAIN=0 turns it off): a run without a stage A takes every
@@ -2752,8 +2789,25 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // run of this trip moved there -- except the lanes waiting outside the trips (escapes
   // included). A run with a stage A takes only the lanes that began the trip there.
   const bool chain = !(getenv("WB_TRIP_CHAIN") && getenv("WB_TRIP_CHAIN")[0] == '0');
+  // stage-B batches: run k's test reads PREG[k - bfirst[k]]; a stage-B run k recomputes
+  // the masks of runs k+1 .. blast[k] (trip_source's stage code, below)
+  std::vector<uint32_t> bfirst(nr, 0), blast(nr, 0);
+  for (uint32_t k = 0; k < nr;) {
+    uint32_t e = k;
+    while (e + 1 < nr && e + 1 - k < G && !fwd_ok[e] && pf_from[e] < 0) e++;
+    for (uint32_t j = k; j <= e; j++) { bfirst[j] = k; blast[j] = e; }
+    k = e + 1;
+  }
+  auto b_cmp = [&](Em &x, uint32_t k) {   // run k's test mask into its batch register
+    vcmp64(x, PREG[k - bfirst[k]], runs[k].pc, chain && !split[k] ? VPC : TPC, k - bfirst[k]);
+  };
   for (uint32_t k = 0; k < nr; k++) {
-    if (chain && !split[k]) {
+    if (batch_on && bfirst[k] == k)
+      for (uint32_t j = k; j <= blast[k]; j++) b_cmp(h, j);
+    if (batch_on) {
+      if (chain && !split[k]) h.l("s_andn2_b64 s[74:75], %s, s[76:77]", PREG[k - bfirst[k]]);
+      else h.l("s_and_b64 s[74:75], %s, exec", PREG[k - bfirst[k]]);
+    } else if (chain && !split[k]) {
       h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, VPC);
       h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
     } else {
@@ -3059,6 +3113,11 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       std::string code = sched_on ? e.o.substr(0, at) + schedule(e.o.substr(at)) : e.o;
       code += e.stage_end + ":\n";
       code += "s_mov_b64 exec, s[96:97]\n";
+      if (st == 1 && batch_on) {   // (this run may have moved lanes: the rest of its batch)
+        Em rb;
+        for (uint32_t j = k + 1; j <= blast[k]; j++) b_cmp(rb, j);
+        code += rb.o;
+      }
       code += "s_branch " + std::string(stage_name[st]) + "r" + std::to_string(k) + "\n";
       code += e.tail;
       (st ? oob : ooa) += code;
