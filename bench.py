@@ -563,6 +563,9 @@ def main():
                         "granule": ctx.memory_granule()}, **extra),
         "memory_checksum": "%016x" % checksum,
         "kernel_instr_per_s": total_instrs / (dist.max(kernel_avg) * args.steps),
+        # the interpreter kernel's mean duration per step, HIP events on the library's stream
+        # (the rooflines' time basis); ms_per_step adds the Reset and the launch gaps
+        "kernel_ms": 1e3 * dist.max(kernel_avg),
     }
     if fresh:
         out["fresh_input"] = fresh
@@ -620,9 +623,29 @@ def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_inst
              "frac": None,
              "basis": "256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md); one "
                       "wave issues VALU at most every 4 cycles"}
+    # one time basis, named: `achieved` / `frac` use this run's HIP-event kernel time; the
+    # profile's traced kernel time (rocprofv3 kernel trace of the same command, another run)
+    # gives `frac_traced`, and the profile also records the HIP-event time its own bench run
+    # measured, so the two clocks can be compared in the same process
+    timing = {"time_basis": "kernel_ms: this run's HIP-event kernel time on the library's stream",
+              "kernel_ms": 1e3 * kernel_max}
+    if prof.get("kernel_avg_ns"):
+        timing["traced_kernel_ms"] = prof["kernel_avg_ns"] / 1e6
+        if prof.get("bench_kernel_ms"):
+            timing["traced_run_hip_event_kernel_ms"] = prof["bench_kernel_ms"]
+        if timing["traced_kernel_ms"] > out["ms_per_step"]:
+            timing["note"] = ("the traced kernel (%.4g ms, rocprofv3 kernel trace of another run%s) is "
+                              "longer than this line's step (%.4g ms): the trace pass runs under the "
+                              "profiler on another box; frac uses this run's own kernel time"
+                              % (timing["traced_kernel_ms"],
+                                 ", whose own HIP events read %.4g ms" % prof["bench_kernel_ms"]
+                                 if prof.get("bench_kernel_ms") else "", out["ms_per_step"]))
     if prof.get("valu_insts_per_launch"):
         valu = prof["valu_insts_per_launch"] * 64.0 / kernel_max
         wps = prof.get("waves_per_simd")
+        issue.update(timing)
+        if prof.get("kernel_avg_ns"):
+            issue["frac_traced"] = prof["valu_insts_per_launch"] * 64.0 / (prof["kernel_avg_ns"] * 1e-9) / VALU_PEAK
         issue.update({
             "achieved": valu, "frac": valu / VALU_PEAK,
             "single_wave_ceiling": min(1.0, 0.5 * wps) if wps else None,
@@ -642,7 +665,7 @@ def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_inst
         achieved = bytes_launch / kernel_max / 1e9
         out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                           "traffic": traffic,
+                           "traffic": traffic, **timing,
                            "note": "algorithmic = linear-memory bytes of the wasm loads and "
                                    "stores (%.4f B per wasm instr%s); traffic = HBM bytes per "
                                    "launch, FETCH_SIZE x 2 (MI355X_MICROARCH.md 'HBM') + "
@@ -653,6 +676,8 @@ def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_inst
             out["roofline"]["algorithmic_store_bytes"] = stb * instrs_per_step
         if prof.get("write_bytes") and c3_split:
             out["roofline"]["write_over_store_bytes"] = prof["write_bytes"] / (c3_split[1] * instrs_per_step)
+        if prof.get("kernel_avg_ns"):
+            out["roofline"]["frac_traced"] = bytes_launch / (prof["kernel_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS
         out["issue_roofline"] = issue
     else:
         out["roofline"] = dict(issue)

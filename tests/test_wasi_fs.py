@@ -183,7 +183,7 @@ def tree(tmp_path_factory):
     return str(d)
 
 
-def _oracle(tree, rows):
+def _oracle(tree, rows, mems=None):
     O.set_wasi(True, ["fs.wasm"], [], preopens=[".:" + tree], deterministic=(SEED, CLOCK))
     try:
         m = O.Module(FS)
@@ -192,6 +192,8 @@ def _oracle(tree, rows):
             inst = O.Instance(m)
             inst.set_lane(i)
             out.append(inst.invoke("run", r))
+            if mems is not None:
+                mems.append(inst.memory(0, 8192))
         return out
     finally:
         O.set_wasi(False)
@@ -236,7 +238,8 @@ def test_emulator_fs_matches_oracle(built, tree):
 def test_gpu_fs_matches_oracle(built, tree):
     from wasmedge_amd import batch
     rows = ROWS * 3
-    ref = _oracle(tree, rows)
+    mems = []
+    ref = _oracle(tree, rows, mems)
     ctx = batch.BatchContext(FS, len(rows), device=0, host_threads=8)
     try:
         ctx.init_wasi(["fs.wasm"], [], preopens=[".:" + tree])
@@ -244,6 +247,14 @@ def test_gpu_fs_matches_oracle(built, tree):
         rets, st, cnt = ctx.execute("run", batch.make_values(rows, [I32]), 1)
         ints = batch.ret_ints(rets)
         vals = [[int(ints[i][0])] if st[i] == 0 else [] for i in range(len(rows))]
-        assert compare(ref, vals, st, cnt, ctx.memory_hash(), [I32]) == []
+        bad = compare(ref, vals, st, cnt, ctx.memory_hash(), [I32])
+        # (on a mismatch: the first lane's differing words, oracle vs GPU)
+        words = []
+        if bad:
+            i = bad[0][0]
+            g = ctx.memory(i, 0, 8192)
+            words = [(k, mems[i][k:k + 4].hex(), g[k:k + 4].hex()) for k in range(0, 8192, 4)
+                     if mems[i][k:k + 4] != g[k:k + 4]][:16]
+        assert bad == [], (len(bad), words)
     finally:
         ctx.close()

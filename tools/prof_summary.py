@@ -113,7 +113,10 @@ def main():
            "wave_quad_cycles_per_launch": wc,
            "wait_any_frac": g("SQ_WAIT_ANY") / wc, "active_any_frac": g("SQ_ACTIVE_INST_ANY") / wc,
            "active_valu_frac": g("SQ_ACTIVE_INST_VALU") / wc,
-           "bench_ms_per_step": line["ms_per_step"]}
+           "bench_ms_per_step": line["ms_per_step"],
+           # the HIP-event kernel time the traced run's own bench line measured (same
+           # process, same launches as the trace): the two clocks side by side
+           "bench_kernel_ms": line.get("kernel_ms")}
     # mean resident waves per SIMD over the kernel: wave cycles / (kernel cycles x SIMDs)
     if gui:
         out["waves_per_simd"] = 4.0 * wc / (gui / XCDS) / SIMDS
@@ -136,8 +139,10 @@ def main():
         if k.startswith("wb_"):
             lines.append("| %s | %s | %.6g |" % (k, c, v))
     lines += ["", "## Derived (interpreter kernel `%s`)" % K, "",
-              "* average duration (kernel trace): %.3f ms; bench ms per step in the trace "
-              "pass %.3f" % (avg_ns / 1e6, line["ms_per_step"]),
+              "* average duration (kernel trace): %.3f ms; the same run's HIP-event kernel time "
+              "%s ms; bench ms per step in the trace pass %.3f" % (
+                  avg_ns / 1e6, "%.3f" % line["kernel_ms"] if line.get("kernel_ms") else "n/a",
+                  line["ms_per_step"]),
               "* FETCH_SIZE correction: x%.1f (the guide); check: wb_mem_hash_kernel streams a "
               "known %d B = FETCH_SIZE x %s" % (fetch_factor, hash_bytes,
                                                 "%.4f" % fetch_check if fetch_check else "n/a"),

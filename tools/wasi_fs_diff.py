@@ -21,6 +21,11 @@ def tree():
     (d / "sub" / "inner.txt").write_bytes(b"inner")
     os.symlink("hi.txt", d / "link")
     os.symlink("sub", d / "dlink")
+    if os.environ.get("PIN"):   # (the test fixture's pinned times)
+        now = time.time()
+        for p in (d / "hi.txt", d / "sub" / "inner.txt"):
+            os.utime(p, (now + 3600, now))
+        os.utime(d / "sub", (now + 3600, now))
     return str(d)
 
 
@@ -32,7 +37,7 @@ def lst(d):
 d = tree()
 print("fs", os.popen("stat -f -c %T " + d).read().strip(), os.popen("findmnt -T " + d + " -o OPTIONS -n").read().strip())
 print("before", lst(d))
-rows = [[s] for s in range(5)] * 3
+rows = [[s] for s in range(5)] * int(os.environ.get("REP", "3"))
 O.set_wasi(True, ["fs.wasm"], [], preopens=[".:" + d], deterministic=(T.SEED, T.CLOCK))
 m = O.Module(T.FS)
 om = []
@@ -42,7 +47,7 @@ for i, r in enumerate(rows):
     res = inst.invoke("run", r)
     om.append((res, inst.memory(0, 65536)))
 print("after oracle", lst(d))
-ctx = batch.BatchContext(T.FS, len(rows), device=0)
+ctx = batch.BatchContext(T.FS, len(rows), device=0, host_threads=int(os.environ.get("HT", "0")))
 ctx.init_wasi(["fs.wasm"], [], preopens=[".:" + d])
 ctx.wasi_deterministic(T.SEED, T.CLOCK)
 rets, st, cnt = ctx.execute("run", batch.make_values(rows, [batch.I32]), 1)
