@@ -176,10 +176,15 @@ def tree(tmp_path_factory):
     (d / "sub" / "inner.txt").write_bytes(b"inner")
     os.symlink("hi.txt", d / "link")
     os.symlink("sub", d / "dlink")
+    # access times after the modification and change times, so that no read (relatime)
+    # changes what a later stat reports -- the symbolic links too: readlink would otherwise
+    # update a link's atime while it still equals its mtime, which on the coarse file clock
+    # can last past the first read
     now = time.time()
-    for p in (d / "hi.txt", d / "sub" / "inner.txt"):
+    for p in (d / "hi.txt", d / "sub" / "inner.txt", d / "sub"):
         os.utime(p, (now + 3600, now))
-    os.utime(d / "sub", (now + 3600, now))
+    for p in (d / "link", d / "dlink"):
+        os.utime(p, (now + 3600, now), follow_symlinks=False)
     return str(d)
 
 
