@@ -69,7 +69,9 @@ def lane_args(n, seed=11):
     return out
 
 
-def oracle_rows(args, jsdir):
+def oracle_rows(args, jsdir, lanes=None):
+    """The oracle's rows for these command lines; lanes: each one's instance id (its WASI
+    generator key; default 0, 1, ...)."""
     O.set_lazy_imports(True)
     O.set_wasi(True, ["qjs.wasm"], ["HOME=/"], preopens=[".:" + jsdir], deterministic=(SEED, CLOCK))
     try:
@@ -77,7 +79,7 @@ def oracle_rows(args, jsdir):
         rows = []
         for i, a in enumerate(args):
             inst = O.Instance(m)
-            inst.set_lane(i)
+            inst.set_lane(lanes[i] if lanes is not None else i)
             inst.set_args(a)
             res = inst.invoke("_start", [])
             rows.append((res, inst.wasi_output(1), inst.wasi_output(2), inst.wasi_exit_code()))
@@ -120,8 +122,8 @@ def test_emulator_matches_oracle(built, jsdir):
 @pytest.mark.gpu
 def test_gpu_quickjs_512_lanes(built, jsdir, monkeypatch):
     """512 instances of QuickJS (8 waves), each with its own command line, on the threaded
-    core (WB_JIT=0: the 64,000 compiled runs of this module take a minute of hiprtc at
-    BatchCreate, see test_quickjs_runs_assemble), host calls served on 16 threads."""
+    core (WB_JIT=0: the 64,000 compiled runs of this module take about a minute of hiprtc
+    at BatchCreate; tools/qjs_gpu.py runs them at scale), host calls on 16 threads."""
     from wasmedge_amd import batch
     monkeypatch.setenv("WB_JIT", "0")
     args = lane_args(512)

@@ -2013,6 +2013,7 @@ std::string simt_sched(bool hybrid, bool depth) {
 // loads go out together, then each lane's exit iteration is found in order.
 constexpr uint32_t kTripScan = 4;   // trip mode: scan iterations per trip (trip_scan_stage)
 constexpr uint32_t kTripBatch = 4;  // trip mode: lane-test compares issued together (trip_source)
+constexpr uint32_t kTripGuard = 4;  // trip mode: a function's runs share one range test from this many
 struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
 
 bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
@@ -2791,17 +2792,50 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   const bool chain = !(getenv("WB_TRIP_CHAIN") && getenv("WB_TRIP_CHAIN")[0] == '0');
   // stage-B batches: run k's test reads PREG[k - bfirst[k]]; a stage-B run k recomputes
   // the masks of runs k+1 .. blast[k] (trip_source's stage code, below)
+  // Function guards (WB_TRIP_GUARD=0 turns them off): the runs of one function are
+  // consecutive in the chain, and while no lane's VPC or TPC lies in their pc range none of
+  // their tests can take lanes -- C3's `sort` (fill and checksum loops) while every lane
+  // sorts. A block of at least kTripGuard runs is skipped after one range test (the batch
+  // registers, s68 / s69; computed where the block starts, after the runs before it moved
+  // their lanes), and batches never cross a block.
+  const bool guard_on = batch_on && !(getenv("WB_TRIP_GUARD") && getenv("WB_TRIP_GUARD")[0] == '0');
+  std::vector<int64_t> fn_of(nr);
+  for (uint32_t k = 0; k < nr; k++) fn_of[k] = func_of(runs[k].pc);
+  std::vector<uint32_t> gend(nr, 0xFFFFFFFFu);   // block start -> its last run (guarded blocks)
+  for (uint32_t k = 0; k < nr && guard_on;) {
+    uint32_t e = k;
+    while (e + 1 < nr && fn_of[e + 1] == fn_of[k]) e++;
+    if (e + 1 - k >= kTripGuard) gend[k] = e;
+    k = e + 1;
+  }
   std::vector<uint32_t> bfirst(nr, 0), blast(nr, 0);
   for (uint32_t k = 0; k < nr;) {
     uint32_t e = k;
-    while (e + 1 < nr && e + 1 - k < G && !fwd_ok[e] && pf_from[e] < 0) e++;
+    while (e + 1 < nr && e + 1 - k < G && !fwd_ok[e] && pf_from[e] < 0 &&
+           !(guard_on && fn_of[e + 1] != fn_of[e]))
+      e++;
     for (uint32_t j = k; j <= e; j++) { bfirst[j] = k; blast[j] = e; }
     k = e + 1;
   }
   auto b_cmp = [&](Em &x, uint32_t k) {   // run k's test mask into its batch register
     vcmp64(x, PREG[k - bfirst[k]], runs[k].pc, chain && !split[k] ? VPC : TPC, k - bfirst[k]);
   };
+  std::vector<uint32_t> gopen;   // guarded blocks whose skip label is still to be placed
   for (uint32_t k = 0; k < nr; k++) {
+    if (gend[k] != 0xFFFFFFFFu) {   // lo <= VPC <= hi or lo <= TPC <= hi, else past the block
+      const uint32_t lo = runs[k].pc, hi = runs[gend[k]].pc;
+      h.l("s_mov_b32 s68, 0x%x", lo);
+      h.l("s_mov_b32 s69, 0x%x", hi + 1);
+      h.l("v_cmp_le_u32_e64 s[80:81], s68, %s", VPC);
+      h.l("v_cmp_gt_u32_e64 s[86:87], s69, %s", VPC);
+      h.l("v_cmp_le_u32_e64 s[88:89], s68, %s", TPC);
+      h.l("v_cmp_gt_u32_e64 s[90:91], s69, %s", TPC);
+      h.l("s_and_b64 s[80:81], s[80:81], s[86:87]");
+      h.l("s_and_b64 s[88:89], s[88:89], s[90:91]");
+      h.l("s_or_b64 s[80:81], s[80:81], s[88:89]");
+      h.l("s_cbranch_scc0 Lg%u", k);
+      gopen.push_back(k);
+    }
     if (batch_on && bfirst[k] == k)
       for (uint32_t j = k; j <= blast[k]; j++) b_cmp(h, j);
     if (batch_on) {
@@ -2832,6 +2866,10 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       h.l("s_cbranch_scc1 LtS%u", k);
       h.l("LtSr%u:", k);
     }
+    if (!gopen.empty() && gend[gopen.back()] == k) {
+      h.l("Lg%u:", gopen.back());
+      gopen.pop_back();
+    }
   }
   if (hybrid) {
     // ---- every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL)
@@ -2845,11 +2883,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     h.l("Ltnc:");
   }
   // ---- after the trip: go on while more lanes are in the runs than outside them
+  // (one branch: none in the runs implies more outside than in, since ALL is not empty)
   h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
-  h.l("s_cmp_eq_u64 s[80:81], 0");
-  h.l("s_cbranch_scc1 Ltx");
-  h.l("s_cmp_eq_u64 s[76:77], 0");
-  h.l("s_cbranch_scc1 Ltbud");
   h.l("s_bcnt1_i32_b64 s68, s[80:81]");
   h.l("s_bcnt1_i32_b64 s69, s[76:77]");
   h.l("s_cmp_gt_u32 s69, s68");
