@@ -73,6 +73,14 @@ def workload(name, args):
         return (workloads.qsort_grow_wasm(), "sort", lambda ids: np.stack([ids, np.full_like(ids, el)], 1),
                 [I32, I32], "C3 quicksort of %d i32 per instance, memory grown from 1 page by "
                             "memory.grow (no declared max)" % el, {"elements": el})
+    if name == "c3x":
+        # not a BASELINE config: C3's quicksort with its array on memory 1 (MultiMemories),
+        # instruction for instruction C3's program on a memory past the first (VERDICT r5
+        # item 8: the compiled XLD / XST against C3's memory-0 accesses)
+        el = args.elements
+        return (workloads.qsort_x_wasm(), "sort", lambda ids: np.stack([ids, np.full_like(ids, el)], 1),
+                [I32, I32], "C3 quicksort of %d i32 per instance on memory 1 (MultiMemories)" % el,
+                {"elements": el})
     if name == "c4":
         return (workloads.collatz_wasm(), "collatz",
                 lambda ids: np.stack([ids, np.full_like(ids, 10000)], 1), [I32, I32],
@@ -221,7 +229,8 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, tail_call=False):
+def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, tail_call=False,
+                 multi_memory=False):
     """The oracle (C restatement of the reference interpreter, oracle/) timed on the
     box's host cores over a bounded sample of the same workload: chunks of instances
     (ids 0, 1, 2, ...), first on ONE thread for about budget_s / 4 seconds, then on
@@ -232,7 +241,7 @@ def cpu_baseline(wasm, func, build_rows, ptypes, budget_s, threads, gpu, what, t
     into (load, store) bytes per wasm instruction."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
-    m = oracle_py.Module(wasm, tail_call=tail_call)
+    m = oracle_py.Module(wasm, tail_call=tail_call, multi_memory=multi_memory)
     n_max = len(gpu["counts"])
     # chunks of about a quarter of a phase at the oracle's ~2e8 instr/s per thread
     t_inst = float(gpu["counts"].mean()) / 2e8
@@ -297,7 +306,7 @@ def load_profile(workload, config):
 def elapsed_hint(args):
     """Long steps (full-size C3) report progress on stderr so a run is never silent for
     minutes; short ones stay quiet inside the timed region."""
-    return args.workload in ("c3", "c3grow") and args.elements >= 65536
+    return args.workload in ("c3", "c3grow", "c3x") and args.elements >= 65536
 
 
 # The job's instance count per workload when --instances is not given: the metric's "64K
@@ -346,6 +355,8 @@ class Phase:
         kw = {"max_memory_page": 17} if args.workload == "c3" else {}
         if args.workload == "tail":
             kw["tail_call"] = True
+        if args.workload == "c3x":
+            kw["multi_memory"] = True
         if args.cost_limit:
             kw["cost_limit"] = args.cost_limit
         if devices:
@@ -468,7 +479,7 @@ def main():
                     help="instances (default 65536; 262144 for c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3grow", "c4", "c5", "mt", "tail"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3grow", "c3x", "c4", "c5", "mt", "tail"])
     ap.add_argument("--mt-n", type=int, default=100000, help="mt19937 draws per instance")
     ap.add_argument("--elements", type=int, default=262144, help="C3 i32 per instance")
     ap.add_argument("--vary-args", default="auto", choices=["auto", "on", "off"],
@@ -483,7 +494,7 @@ def main():
     if args.warmup is None:
         # (modules whose addresses may differ per instance run the layout trial over their
         # first three runs -- warm-up, 128-byte granules, 4-byte words: untimed)
-        args.warmup = 2 if args.workload == "c2" else 3 if args.workload in ("c3", "c3grow", "mt") else 1
+        args.warmup = 2 if args.workload == "c2" else 3 if args.workload in ("c3", "c3grow", "c3x", "mt") else 1
     if args.instances is None:
         args.instances = default_instances(args.workload)
     if args.vary_args == "auto":
@@ -579,8 +590,9 @@ def main():
         threads = host_cores()
         out["cpu_baseline"], bpi, c3_split = cpu_baseline(wasm, func, build_rows, ptypes, args.cpu_seconds,
                                                           threads, gpu, args.workload.upper(),
-                                                          tail_call=args.workload == "tail")
-        if args.workload in ("c3", "c3grow"):
+                                                          tail_call=args.workload == "tail",
+                                                          multi_memory=args.workload == "c3x")
+        if args.workload in ("c3", "c3grow", "c3x"):
             # qsort's bytes per instruction is stable across instances
             c3_bytes_per_instr, c3_bpi_src = bpi, " on the oracle sample"
     if args.workload != "c2":
@@ -656,7 +668,7 @@ def rooflines(out, args, prof, instrs_per_step, kernel_max, n, c3_bytes_per_inst
                       "SQ_WAVE_CYCLES per launch)" % prof.get("source")})
     else:
         issue["note"] = "no PMC summary for this configuration (tools/prof_bench.sh)"
-    if args.workload in ("c3", "c3grow"):
+    if args.workload in ("c3", "c3grow", "c3x"):
         # HBM-bound config: algorithmic bytes = the linear-memory bytes of the wasm loads and
         # stores, per wasm instruction as the oracle counts them on the CPU-baseline sample
         # (or the committed figure when the baseline leg is skipped) x this launch's count

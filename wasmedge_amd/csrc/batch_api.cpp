@@ -80,7 +80,7 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
     std::vector<uint64_t> addr;
     const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
     const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
-                                           want_trip);
+                                           want_trip, &C->xinfo_h);
     const std::string err = src.empty() ? std::string("compiled runs: no source")
                                         : wb::jit_load(src, runs.size(), C->device, &addr);
     if (err.empty()) {
@@ -316,7 +316,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
   // whose lanes part ways inside their loops (wb::trips_pay); WB_TRIP=0 / 1 forces it off /
   // on (A/B measurement aid). SIMT contexts only.
   const char *tre = getenv("WB_TRIP");
-  bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem || wb::trips_pay(P));
+  bool want_trip = want_simt && (tre ? tre[0] == '1' : P.divergent_mem || P.divergent_xmem || wb::trips_pay(P));
   C->want_simt = want_simt;
   C->want_trip = want_trip;
   C->jit_on = C->threaded && C->vframe && !(jte && jte[0] == '0');

@@ -194,7 +194,8 @@ struct HbmFrame {
 // left in s[74:75] and, for every lane in ALL, its pc (v92) and the wasm instructions it
 // retired (v93): in SIMT mode (KParams::simt) the compiled runs schedule the lanes among
 // themselves (jit.cpp Lsched), otherwise ALL = the group = EXEC throughout. The caller's
-// EXEC (`ex`) is restored at the end.
+// EXEC (`ex`) is restored at the end. s[98:99] = the wave's block of the memories past the
+// first (KParams::xmem; the compiled XLD / XST, jit.cpp emit_xmem), 0 without them.
 #define TC_RUN_VF_ASM(...) \
   asm volatile( \
       "s_mov_b32 s60, %[clo]\n\t" \
@@ -223,6 +224,8 @@ struct HbmFrame {
       "v_mov_b32 v97, %[ghi]\n\t" \
       "s_mov_b32 s94, %[vsync]\n\t" \
       "s_mov_b32 s95, %[low]\n\t" \
+      "s_mov_b32 s98, %[xlo]\n\t" \
+      "s_mov_b32 s99, %[xhi]\n\t" \
       "s_mov_b64 exec, s[96:97]\n\t" \
       "s_getpc_b64 s[66:67]\n" \
       "Ltc_ret_%=:\n\t" \
@@ -253,10 +256,11 @@ struct HbmFrame {
       : [clo] "s"(clo), [chi] "s"(chi), [pc] "s"(pc), [oth] "s"(oth), [lim] "s"(lim), [fr] "v"(fr), \
         [pages] "v"(pages), [mlo] "v"(mlo), [mhi] "v"(mhi), [stk] "v"(stk), [msh] "s"(msh), \
         [slds] "s"(slds), [vsync] "s"(vsync), [low] "s"(lw), [llo] "s"(llo), [lhi] "s"(lhi), \
-        [all] "s"(all), [grp] "s"(grp), [ex] "s"(ex) \
+        [all] "s"(all), [grp] "s"(grp), [ex] "s"(ex), [xlo] "s"(xlo), [xhi] "s"(xhi) \
       : "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
         "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
         "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", \
+        "s98", "s99", \
         "v92", "v93", "v94", "v98", "v95", "v96", "v97", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
         "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", \
         "v124", "v125", "v126", "v127", "vcc", "scc", "memory", ##__VA_ARGS__);
@@ -284,7 +288,7 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
                                            uint32_t vsync, uint64_t &gas, uint64_t gas_limit,
                                            uint32_t *ncnt, uint32_t *reason, uint32_t lim,
                                            SimtOut *so = nullptr, uint64_t all = 0, uint64_t grp = 0,
-                                           uint32_t vpc = 0) {
+                                           uint32_t vpc = 0, uint64_t xbase = 0) {
   uint32_t npc, cnt, why;
   // metered contexts: the lane's gas total in v[96:97] and the limit in v[94:95] for the
   // compiled runs (jit.cpp), which price themselves; handlers never touch them
@@ -305,6 +309,8 @@ __device__ __forceinline__ uint32_t tc_run(const void *tcode, uint32_t pc, uint3
     // (the caller's EXEC; without SIMT the core runs exactly it: ALL = the group = EXEC)
     const uint64_t ex = __builtin_amdgcn_read_exec();
     if (!so) all = grp = ex;
+    const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xbase);
+    const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xbase >> 32));
     uint32_t noth, nlow, vcnt;
     uint64_t ngrp;
     TC_RUN_VF_ASM(TC_VREGS);
@@ -431,6 +437,8 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   const uint32_t lane = __lane_id();
   const uint32_t fr_lds = F.lds_addr();   // this lane's cell 0, LDS byte address
   const uint32_t stk_lds = (uint32_t)(uintptr_t)stk;   // its call-stack slot 0
+  // the wave's block of the memories past the first (XMEM below; the compiled XLD / XST)
+  const uint64_t xbase = p.n_xmem ? (uint64_t)(uintptr_t)(p.xmem + (size_t)(inst >> 6) * p.xwords * 64u) : 0;
 
   for (;;) {
     // ---- schedule: which group of lanes (same pc) runs next; `other` = the lowest pc
@@ -501,7 +509,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
         uint32_t ncnt, why;
         const uint32_t gpc = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm,
                                         stk_lds, S_lds, (TC_VF_CELLS - p.total_cells) * 8u, cost, ~0ull,
-                                        &ncnt, &why, core_lim, &so, runmask, act, pc);
+                                        &ncnt, &why, core_lim, &so, runmask, act, pc, xbase);
         WB_STAT_ADD(ST_CYC_TC, WB_NOW() - tt0);
         if (status == WB_STATUS_RUNNING) {
           pc = so.vpc;
@@ -576,7 +584,7 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
           scost = 0;
           pcs = tc_run<VF>(p.tcode, pcs, other, low, fr_lds, pages, mem.p, mem.g, gsp, hwm, stk_lds, S_lds,
                             (TC_VF_CELLS - p.total_cells) * 8u, cost,
-                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why, core_lim);
+                            p.cost_off ? p.cost_limit : ~0ull, &ncnt, &why, core_lim, nullptr, 0, 0, 0, xbase);
           // (sign-extended: a core call that only takes a jump whose count correction is
           // negative -- a `br` out of blocks, cnt 1 + tcnt -2 -- retires -1 instructions)
           asc += (uint64_t)(int64_t)(int32_t)ncnt;

@@ -738,10 +738,10 @@ void Lowerer::do_load(uint16_t dop, uint8_t rtype, Reader &r) {
   uint32_t off;
   const uint32_t k = memarg(r, &off);
   Entry a = pop_t(I32);
-  if (a.var && !k) P.divergent_mem = true;
+  if (a.var) (k ? P.divergent_xmem : P.divergent_mem) = true;
   if (!live()) { push_cell(rtype); return; }
   uint32_t ac = src(a);
-  if (k) emit(OP_XLD, ac, k, a.cell, dop, off);   // (memory k: the per-lane step)
+  if (k) emit(OP_XLD, ac, k, a.cell, dop, off);   // (memory k: compiled runs, else the per-lane step)
   else emit(dop, ac, 0, a.cell, 0, off);
   push_cell(rtype, last_emit);
 }
@@ -751,7 +751,7 @@ void Lowerer::do_store(uint16_t dop, uint8_t vtype, Reader &r) {
   const uint32_t k = memarg(r, &off);
   Entry v = pop_t(vtype);
   Entry a = pop_t(I32);
-  if (a.var && !k) P.divergent_mem = true;
+  if (a.var) (k ? P.divergent_xmem : P.divergent_mem) = true;
   if (!live()) return;
   uint32_t ac = src(a), vc = src(v);
   if (k) emit(OP_XST, ac, vc, k, dop, off);

@@ -140,6 +140,9 @@ struct Program {
   // some load/store address depends on per-instance data (a parameter, a loaded value, a
   // global): the batch then interleaves memory in 128-byte granules (batch_api.cpp)
   bool divergent_mem = false;
+  // the same for a memory past the first (its layout is fixed; only the trip-mode choice
+  // reads it)
+  bool divergent_xmem = false;
 };
 
 // A table, memory or global import the embedder provides (WasmEdge_BatchImport). Every

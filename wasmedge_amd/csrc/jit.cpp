@@ -59,6 +59,20 @@ uint32_t mem_bytes(uint16_t op) {
   }
 }
 
+// Memories past the first (MultiMemories; frontend.cpp do_load / do_store): XLD a, k -> c
+// and XST a, b -> memory c carry the memory-0 op in D. xmop = that op (0 for anything else).
+bool load_wide_op(uint16_t op) {
+  return op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
+         op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
+}
+uint16_t xmop(const DInstr &I) {
+  const uint16_t op = uint16_t(I.w0 & 0x7FFFu);
+  return op == OP_XLD || op == OP_XST ? uint16_t(I.w2 >> 16) : uint16_t(0);
+}
+// The word offsets of the extra memories in a lane's block (batch_ctx.h xinfo_h: memory k
+// at word xinfo[2 (k - 1)]), for the jit_source call that is compiling (null in dry runs)
+thread_local const std::vector<uint32_t> *g_xinfo = nullptr;
+
 // compare ops: VOPC suffix (32-bit form; the 64-bit form appends "64" to the type)
 const char *cmp_kind(uint16_t k) {   // k: 0 EQ, 1 NE, 2 LT_S, 3 LT_U, 4 GT_S, 5 GT_U, 6 LE_S, 7 LE_U, 8 GE_S, 9 GE_U
   static const char *const n[] = {"eq_u", "ne_u", "lt_i", "lt_u", "gt_i", "gt_u", "le_i", "le_u", "ge_i", "ge_u"};
@@ -564,6 +578,119 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const 
     e.nvm++;
   }
   for (uint32_t r : e.inval) e.l("v_mov_b32 v%u, -1", r);   // (trip load cache: stale now)
+  return true;
+}
+
+// ---------------------------------------------------------------- extra memories
+// XLD / XST on memory k >= 1 (dbc_step.inc OP_XLD / OP_XST; memory.ipp:12-68 on the
+// instance getMemInstByIdx names, helper.cpp:206-215). Memory k of every lane lies in
+// KParams::xmem as 4-byte words interleaved over the wave's 64 lanes (batch_kernel.hip
+// XMEM): the core holds the wave's block in s[98:99], so the lane's word w of memory k is
+// at s[98:99] + (xinfo[2 (k - 1)] + w) * 256 + lane * 4 -- the word interleave of memory 0.
+// The check is the memory-0 group check on one access with the module's declared minimum
+// as the bound: every lane's memory k has at least that many pages (the size starts there
+// and only grows), so an access past it -- in bounds on a grown memory or not -- and a
+// misaligned one leave before the instruction and the C++ step executes it exactly.
+// No write mark: Reset rewrites the extra memories whole.
+// RP = the lane's word 0 of memory k: s[98:99] + xinfo[2 (k - 1)] * 256 + lane * 4
+void xmem_lane_base(Em &e, uint32_t k) {
+  const uint64_t woff = g_xinfo && size_t(2 * (k - 1)) < g_xinfo->size() ? (*g_xinfo)[2 * (k - 1)] : 0;
+  e.l("v_mbcnt_lo_u32_b32 %s, -1, 0", W0);
+  e.l("v_mbcnt_hi_u32_b32 %s, -1, %s", W0, W0);
+  e.l("v_lshlrev_b32_e32 %s, 2, %s", W0, W0);
+  if (woff) {
+    e.l("s_add_u32 s68, s98, 0x%x", uint32_t(woff << 8));
+    e.l("s_addc_u32 s69, s99, 0x%x", uint32_t(woff >> 24));
+    e.l("v_lshl_add_u64 %s, %s, 0, s[68:69]", RP, WP);
+  } else {
+    e.l("v_lshl_add_u64 %s, %s, 0, s[98:99]", RP, WP);
+  }
+}
+
+bool emit_xmem(Em &e, const DInstr &I) {
+  const uint16_t op = op_of(I), mop = xmop(I);
+  const bool st = op == OP_XST;
+  const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, imm = I.w3;
+  const uint32_t k = st ? c : b, n = mem_bytes(mop);
+  if (!n || is_store_op(mop) != st || !e.prog || k == 0 || k > e.prog->xmems.size()) return false;
+  if (uint64_t(imm) + n - 1 > 0xFFFFFFFFull) return false;
+  const uint32_t minp = e.prog->xmems[k - 1].min;
+  const bool wide = load_wide_op(mop);
+  if (st) e.drain();   // (a store never overtakes a load of this run)
+  else e.sync({a, c, wide || n >= 8 ? c + 1 : c, n == 16 ? c + 2 : c, n == 16 ? c + 3 : c});
+  // bounds: the last byte a + imm + n - 1 must not carry and must lie below minp pages
+  e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, imm + n - 1, e.v(a));
+  e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
+  e.l("s_mov_b32 s68, 0x%x", minp);
+  e.l("v_cmp_le_u32_e64 %s, s68, %s", T2, X1);
+  e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  const uint32_t m = n >= 4 ? 3 : n - 1;   // (as jit_groups: 4-byte alignment for 8 and 16)
+  if (m) {
+    if (imm & m) {
+      e.l("v_add_u32_e32 %s, %u, %s", Y0, imm & m, e.v(a));
+      e.l("v_and_b32_e32 %s, %u, %s", Y0, m, Y0);
+    } else {
+      e.l("v_and_b32_e32 %s, %u, %s", Y0, m, e.v(a));
+    }
+    e.l("v_cmp_ne_u32_e32 vcc, 0, %s", Y0);
+    e.l("s_or_b64 %s, %s, vcc", T2, T2);
+  }
+  e.leave_if_t2();
+  if (!st && mop == OP_LD32) {
+    const auto f = e.fwd.find(e.pc);
+    if (f != e.fwd.end()) {   // (trip load cache: these lanes' word is in the value VGPR)
+      e.l("v_mov_b32 %s, v%u", e.v(c), f->second.second);
+      return true;
+    }
+  }
+  xmem_lane_base(e, k);
+  // XP = the access's first word (n >= 4: aligned, words at +256 each) or byte
+  uint32_t off = 0;
+  if (n >= 4) {
+    e.l("v_mov_b32 %s, %s", W0, e.v(a));
+    e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
+    const uint64_t kk = uint64_t(imm) * 64u;
+    if (kk + 256 * (n / 4 - 1) <= 4095) {
+      off = uint32_t(kk);
+    } else {
+      e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(kk), X0);
+      e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(kk >> 32), X1);
+    }
+  } else {
+    std::string ea = e.V(a);
+    if (imm) { e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, imm, e.v(a)); ea = Y0; }
+    e.l("v_lshrrev_b32_e32 %s, 2, %s", W0, ea.c_str());
+    e.l("v_lshlrev_b64 %s, 8, %s", XP, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
+    e.l("v_and_b32_e32 %s, 3, %s", W0, ea.c_str());
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  }
+  auto at = [&](uint32_t q) { return std::string(XP) + ", off offset:" + std::to_string(off + 256 * q); };
+  if (st) {
+    const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
+    for (uint32_t q = 0; q < std::max(1u, n / 4); q++) {
+      const std::string ad = at(q);
+      const size_t k1 = ad.find(", off");
+      e.l("%s %s, %s%s", ins, ad.substr(0, k1).c_str(), e.v(b + q), ad.substr(k1).c_str());
+      e.nvm++;
+    }
+    for (uint32_t r : e.inval) e.l("v_mov_b32 v%u, -1", r);   // (trip load cache: stale now)
+    return true;
+  }
+  const char *ins = n == 1 ? (mop == OP_LD8S32 || mop == OP_LD8S64 ? "global_load_sbyte" : "global_load_ubyte")
+                    : n == 2 ? (mop == OP_LD16S32 || mop == OP_LD16S64 ? "global_load_sshort" : "global_load_ushort")
+                             : "global_load_dword";
+  for (uint32_t q = 0; q < std::max(1u, n / 4); q++) {
+    e.l("%s %s, %s", ins, e.v(c + q), at(q).c_str());
+    e.loaded(c + q);
+  }
+  if (mop == OP_LD8U64 || mop == OP_LD16U64 || mop == OP_LD32U64) {
+    e.l("v_mov_b32 %s, 0", e.v(c + 1));
+  } else if (wide && mop != OP_LD64) {   // sign extension needs the loaded word
+    e.sync({c});
+    e.l("v_ashrrev_i32_e32 %s, 31, %s", e.v(c + 1), e.v(c));
+  }
   return true;
 }
 
@@ -1130,6 +1257,7 @@ bool emit(Em &e, const DInstr &I) {
     if (is_store_op(op)) return emit_store(e, op, a, b, imm);
     return emit_load(e, op, a, c, imm);
   }
+  if (op == OP_XLD || op == OP_XST) return emit_xmem(e, I);
   return false;
 }
 
@@ -1348,7 +1476,7 @@ void written(const DInstr &I, std::vector<uint32_t> *out) {
   const uint16_t op = op_of(I);
   const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
   out->clear();
-  if (is_store_op(op) || op == OP_NOP_CNT) return;
+  if (is_store_op(op) || op == OP_NOP_CNT || op == OP_XST) return;
   if (op == OP_ZERO_LOCALS) {
     for (uint32_t k = 0; k < b; k++) out->push_back(a + k);
     return;
@@ -1368,6 +1496,7 @@ std::vector<MemGroup> jit_groups(const Program &P, const JitRun &r, std::vector<
   for (uint32_t i = 0; i < r.len; i++) {
     const DInstr &I = P.code[r.pc + i];
     const uint16_t op = op_of(I);
+    if (xmop(I)) open = -1;   // (an extra memory's access computes its address in the temps)
     if (const uint32_t n = mem_bytes(op)) {
       const uint32_t a = I.w1 & 0xFFFFu, imm = I.w3;
       if (open < 0 || G[size_t(open)].base != a) {
@@ -1406,10 +1535,7 @@ struct LoadBatch {
   std::vector<uint32_t> order;   // issue order (body indices)
 };
 
-bool load_wide(uint16_t op) {
-  return op == OP_LD8S64 || op == OP_LD8U64 || op == OP_LD16S64 || op == OP_LD16U64 ||
-         op == OP_LD32S64 || op == OP_LD32U64 || op == OP_LD64;
-}
+bool load_wide(uint16_t op) { return load_wide_op(op); }
 uint32_t load_cells(uint16_t op) { return op == OP_LD128 ? 4u : load_wide(op) ? 2u : 1u; }
 
 // an operand field naming the cell (or the cell below it: a 64-bit operand's high word);
@@ -2014,7 +2140,9 @@ std::string simt_sched(bool hybrid, bool depth) {
 constexpr uint32_t kTripScan = 4;   // trip mode: scan iterations per trip (trip_scan_stage)
 constexpr uint32_t kTripBatch = 4;  // trip mode: lane-test compares issued together (trip_source)
 constexpr uint32_t kTripGuard = 4;  // trip mode: a function's runs share one range test from this many
-struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; };
+// (mem: the memory the load reads -- 0, or k >= 1 for an XLD of a 32-bit word, whose
+// window is checked against minp, memory k's declared minimum: emit_xmem)
+struct ScanLoop { uint32_t x, y, off; int32_t d; bool y_first; uint32_t mem = 0, minp = 0; };
 
 bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
   if (r.len != 3) return false;
@@ -2023,7 +2151,9 @@ bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
   if ((o0 != OP_I32_ADD_I && o0 != OP_I32_SUB_I) || (i0.w1 & 0xFFFFu) != (i0.w2 & 0xFFFFu)) return false;
   if (i0.w3 == 0 || i0.w3 % 4 || i0.w3 > 64) return false;
   const uint32_t x = i0.w1 & 0xFFFFu;
-  if (o1 != OP_LD32 || (i1.w1 & 0xFFFFu) != x || (i1.w2 & 0xFFFFu) == x) return false;
+  const bool xl = o1 == OP_XLD && xmop(i1) == OP_LD32;   // (memory k >= 1: k in the b field)
+  if ((o1 != OP_LD32 && !xl) || (i1.w1 & 0xFFFFu) != x || (i1.w2 & 0xFFFFu) == x) return false;
+  if (xl && ((i1.w1 >> 16) == 0 || (i1.w1 >> 16) > P.xmems.size())) return false;
   const uint32_t y = i1.w2 & 0xFFFFu;
   if (!is_branch_op(o2) || o2 == OP_JMP || o2 == OP_BR_IF || o2 == OP_BR_UNLESS || i2.w3 != r.pc) return false;
   const uint32_t a = i2.w1 & 0xFFFFu, b = i2.w1 >> 16;
@@ -2040,6 +2170,10 @@ bool scan_loop_of(const Program &P, const JitRun &r, ScanLoop *sl) {
   }
   if (uint64_t(i1.w3) + 64u * 2 * kTripScan + 4 > 0xFFFFFFFFull) return false;   // (the window, with room)
   *sl = ScanLoop{x, y, i1.w3, o0 == OP_I32_ADD_I ? int32_t(i0.w3) : -int32_t(i0.w3), y_first};
+  if (xl) {
+    sl->mem = i1.w1 >> 16;
+    sl->minp = P.xmems[sl->mem - 1].min;
+  }
   return true;
 }
 
@@ -2442,10 +2576,10 @@ uint32_t trip_split(const Program &P, const JitRun &r, uint32_t nbody) {
   for (uint32_t i = 0; i < nbody; i++) {
     const DInstr &I = P.code[r.pc + i];
     const uint16_t op = op_of(I);
-    if (names_any(I, loaded) || (op == OP_POST_CALL && i) || is_store_op(op)) break;
-    if (mem_bytes(op)) {
+    if (names_any(I, loaded) || (op == OP_POST_CALL && i) || is_store_op(op) || op == OP_XST) break;
+    if (mem_bytes(op) || op == OP_XLD) {
       const uint32_t c = I.w2 & 0xFFFFu;
-      for (uint32_t k = 0; k < load_cells(op); k++) loaded[c + k] = 1;
+      for (uint32_t k = 0; k < load_cells(op == OP_XLD ? xmop(I) : op); k++) loaded[c + k] = 1;
       any = true;
     }
     s = i + 1;
@@ -2468,7 +2602,12 @@ void scan_window_fails(Em &e, const ScanLoop &sl, uint32_t U) {
   const uint32_t up = sl.off + (sl.d > 0 ? uint32_t(sl.d) * U : 0u) + 3u;
   e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, up, e.v(sl.x));
   e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
-  e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+  if (sl.mem) {
+    e.l("s_mov_b32 s68, 0x%x", sl.minp);
+    e.l("v_cmp_le_u32_e64 %s, s68, %s", T2, X1);
+  } else {
+    e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
+  }
   e.l("s_or_b64 %s, %s, vcc", T2, T2);
   e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, sl.off, e.v(sl.x));
   if (sl.d < 0) {
@@ -2482,9 +2621,14 @@ void scan_window_fails(Em &e, const ScanLoop &sl, uint32_t U) {
 
 // the scan window's U words into dst[0..U-1] (the window checked)
 void scan_window_loads(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<std::string> &dst) {
+  if (sl.mem) xmem_lane_base(e, sl.mem);   // (RP: the lane's word 0 of memory k)
   for (uint32_t j = 1; j <= U; j++) {
     e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(sl.x));
-    if (e.g == 0) {
+    if (sl.mem) {   // (the word interleave of the extra memories)
+      e.l("v_mov_b32 %s, %s", W0, Y0);
+      e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
+    } else if (e.g == 0) {
       e.l("v_mov_b32 %s, %s", W0, Y0);
       e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
       e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
@@ -2689,11 +2833,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     for (uint32_t i = 0; i < split[k] && ok; i++) {
       const DInstr &I = P.code[runs[k].pc + i];
       const uint16_t op = op_of(I);
-      if (!mem_bytes(op)) continue;
+      if (!mem_bytes(op) && !xmop(I)) continue;
       ok = false;
-      if (op != OP_LD32) break;
+      const bool xl = op == OP_XLD && xmop(I) == OP_LD32;
+      if (op != OP_LD32 && !xl) break;
+      const uint32_t mk = xl ? (I.w1 >> 16) : 0;   // (the cache holds its scan's memory's words)
       for (uint32_t q = 0; q < nr; q++)
-        if (is_scan[q] && slot_of[q].first >= 0 && scans[q].x == (I.w1 & 0xFFFFu) && scans[q].off == I.w3) {
+        if (is_scan[q] && slot_of[q].first >= 0 && scans[q].mem == mk && scans[q].x == (I.w1 & 0xFFFFu) &&
+            scans[q].off == I.w3) {
           fwd[k][runs[k].pc + i] = {uint32_t(slot_of[q].first), uint32_t(slot_of[q].second)};
           ok = any = true;
           break;
@@ -3356,8 +3503,14 @@ bool recursive(const Program &P) {
 }
 
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost, bool simt, bool trip) {
+                       const JitCost *cost, bool simt, bool trip, const std::vector<uint32_t> *xinfo) {
   if (cost) simt = false;
+  // (extra memories: their accesses compile only against the context's word offsets)
+  if (!P.xmems.empty() && (!xinfo || xinfo->size() < 2 * P.xmems.size())) return "";
+  struct XinfoScope {
+    explicit XinfoScope(const std::vector<uint32_t> *x) { g_xinfo = x; }
+    ~XinfoScope() { g_xinfo = nullptr; }
+  } xscope(xinfo);
   // trip mode beside SIMT scheduling (hybrid, the default) or alone (WB_HYBRID=0)
   const bool trips = trip && simt && runs.size() <= kTripMaxRuns;
   const bool hybrid = trips && !(getenv("WB_HYBRID") && getenv("WB_HYBRID")[0] == '0');
@@ -4319,9 +4472,17 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
                                                                    char *err, uint32_t errlen) {
   wb::Program P;
   uint8_t ec = 0;
-  std::string e = wb::load_program(wasm, len, P, &ec);
+  std::string e = wb::load_program(wasm, len, P, &ec, false, nullptr, true, true);
   std::vector<wb::JitRun> runs;
   if (e.empty() && P.total_cells() > TC_VF_CELLS) e = "frame too large for V frames";
+  // extra memories laid out at their minimum sizes (batch_api.cpp reserves more for grown ones)
+  std::vector<uint32_t> xinfo;
+  uint64_t words = 0;
+  for (const auto &xm : P.xmems) {
+    xinfo.push_back(uint32_t(words));
+    xinfo.push_back(xm.min);
+    words += uint64_t(xm.min) << 14;
+  }
   if (e.empty()) {
     std::vector<DInstr> code = P.code;
     code.push_back(DInstr{0, 0, 0, 0});
@@ -4360,7 +4521,7 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       if (simt) runs = wb::jit_runs(P, tc, true, simt == 2);
       if (runs.empty()) continue;
       std::vector<char> obj;
-      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2);
+      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2, &xinfo);
       if (const char *dump = getenv(simt == 2 ? "WB_JIT_DUMP_TRIP" : simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
         if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
       e = src.empty() ? "no source" : wb::jit_compile(src, &obj);
@@ -4379,7 +4540,7 @@ extern "C" __attribute__((visibility("default"))) int wb_trip_choice(const uint8
   wb::Program P;
   uint8_t ec = 0;
   if (!wb::load_program(wasm, len, P, &ec).empty()) return -1;
-  return P.divergent_mem || wb::trips_pay(P) ? 1 : 0;
+  return P.divergent_mem || P.divergent_xmem || wb::trips_pay(P) ? 1 : 0;
 }
 
 // TEST hook (tests/test_depth_pick.py, CPU): whether the module counts as recursive for the

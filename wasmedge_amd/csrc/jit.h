@@ -60,8 +60,13 @@ constexpr size_t kTripMaxRuns = 96;
 // trip: (with simt, not with cost) trip mode instead of per-group runs: every lane of the
 // wave at a run start runs that run in each trip, all of them together (jit.cpp "Trip
 // mode"); for modules whose lanes part ways on loaded data.
+// xinfo: (modules with memories past the first) the context's xinfo_h -- memory k's word
+// offset in a lane's block at [2 (k - 1)] -- for the compiled XLD / XST (jit.cpp
+// emit_xmem, which address the wave's block through s[98:99], set by the kernel at every
+// core call); without it such a module gets no source.
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost = nullptr, bool simt = false, bool trip = false);
+                       const JitCost *cost = nullptr, bool simt = false, bool trip = false,
+                       const std::vector<uint32_t> *xinfo = nullptr);
 
 // Whether trip mode pays for a module whose memory addresses do not depend on per-instance
 // data (Program::divergent_mem picks it for those): lanes part ways inside a loop on every

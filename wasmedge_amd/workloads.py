@@ -243,6 +243,24 @@ def qsort_grow_wasm():
     return assemble(qsort_grow_wat())
 
 
+def qsort_x_wat(pages=17):
+    """C3's quicksort with its array on memory 1 (the MultiMemories proposal): memory 0 is
+    a one-page memory nothing touches, and every load and store names memory 1 -- the same
+    program, instruction for instruction, on a memory past the first (the
+    compiled XLD / XST against C3's memory-0 accesses)."""
+    src = qsort_wat(pages)
+    old = '  (memory (export "memory") %d)' % pages
+    assert old in src
+    src = src.replace(old, "  (memory $m0 1)\n  (memory $m1 %d)" % pages)
+    for op in ("i32.load", "i32.store"):
+        src = src.replace("(%s " % op, "(%s $m1 " % op)
+    return src
+
+
+def qsort_x_wasm(pages=17):
+    return assemble(qsort_x_wat(pages))
+
+
 # ---------------------------------------------------------------------------- C4
 def collatz_wat():
     return r"""
