@@ -79,6 +79,12 @@ XJ_WAT = r"""
           (i32.wrap_i64 (i64.shr_s (i64.load16_s $m1 (i32.and (local.get $x) (i32.const 0xfffe))) (i64.const 48)))))
         (local.set $acc (i32.add (local.get $acc)
           (i32.wrap_i64 (i64.load8_u $m2 (i32.and (local.get $x) (i32.const 0x1ffff))))))
+        ;; 8 and 16 bytes at 4 mod 8 / 4 mod 16 (across granules of 8 or 16 bytes)
+        (local.set $acc (i32.xor (local.get $acc)
+          (i32.wrap_i64 (i64.shr_u (i64.load $m2 offset=4 (i32.and (local.get $x) (i32.const 0xfff0))) (i64.const 16)))))
+        (local.set $acc (i32.add (local.get $acc)
+          (i32x4.extract_lane 2 (v128.load $m1 offset=4 (i32.and (i32.shr_u (local.get $x) (i32.const 2)) (i32.const 0xffe0))))))
+        (i64.store $m1 offset=12 (i32.and (i32.shr_u (local.get $x) (i32.const 6)) (i32.const 0xfff0)) (i64.extend_i32_u (local.get $acc)))
         ;; a misaligned word (lanes leave to the per-lane step) every 4th trip
         (if (i32.eqz (i32.and (local.get $k) (i32.const 3)))
           (then (local.set $acc (i32.add (local.get $acc)
@@ -175,10 +181,14 @@ def _gpu_rows(wasm, func, rs, env, monkeypatch, reps=2):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"WB_TRIP": "0"}, {"WB_TRIP": "1"}, {"WB_JIT": "0"}],
-                         ids=["default", "simt", "trip", "core"])
+@pytest.mark.parametrize("env", [{}, {"WB_TRIP": "0"}, {"WB_TRIP": "1"}, {"WB_JIT": "0"},
+                                 {"WB_XGRAN": "4"}, {"WB_XGRAN": "8"}, {"WB_XGRAN": "16"},
+                                 {"WB_XGRAN": "4", "WB_JIT": "0"}],
+                         ids=["default", "simt", "trip", "core", "gran4", "gran8", "gran16", "gran4-core"])
 def test_gpu_extra_memory_accesses(built, monkeypatch, env):
-    """bit-exact against the oracle on every engine, twice around a Reset"""
+    """bit-exact against the oracle on every engine and granule of the extra memories
+    (the default for this module's data-dependent addresses: 128 bytes), twice around a
+    Reset"""
     wasm = xj_wasm()
     rs = rows()
     ref = [O.Module(wasm, multi_memory=True).run("run", r) for r in rs]
@@ -247,3 +257,18 @@ def test_gpu_c3_on_memory_1(built, monkeypatch):
         ctx.close()
     assert (st0 == 0).all() and (cnt0 == cnt).all()
     assert [int(ints0[i][0]) & 0xFFFFFFFF for i in range(len(rs))] == [r[0] & 0xFFFFFFFF for r in rets]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gran", ["4", "16", "128"])
+def test_gpu_bulk_ops_by_granule(built, monkeypatch, gran):
+    """tests/test_multimem.py's module (size / grow / fill / init / copy within and across
+    memories, v128 and lane forms, an active data segment on memory 1, traps on memories
+    1 and 2) with the extra memories in granules of 4, 16 and 128 bytes"""
+    from test_multimem import mm_wasm, rows as mm_rows
+    wasm = mm_wasm()
+    rs = mm_rows()
+    ref = [O.Module(wasm, multi_memory=True).run("run", r) for r in rs]
+    out, _ = _gpu_rows(wasm, "run", rs, {"WB_XGRAN": gran}, monkeypatch)
+    for rets, st, cnt, h in out:
+        assert compare(ref, rets, st, cnt, h, [I32], exact=True) == []

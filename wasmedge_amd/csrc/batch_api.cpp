@@ -80,7 +80,7 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
     std::vector<uint64_t> addr;
     const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
     const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
-                                           want_trip, &C->xinfo_h);
+                                           want_trip, &C->xinfo_h, C->xlog);
     const std::string err = src.empty() ? std::string("compiled runs: no source")
                                         : wb::jit_load(src, runs.size(), C->device, &addr);
     if (err.empty()) {
@@ -257,6 +257,14 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
       if (words > 0xFFFFFFFFull) return C->fail(kRuntimeError, "memories past the first exceed 16 GiB per instance");
     }
     C->xwords = uint32_t(words);
+    // their granule, fixed here (no layout trial: memory 0's picks its own): 128 bytes when
+    // some access to them depends on per-instance data (Program::divergent_xmem: a lane's
+    // nearby words then share a cache line, as memory 0's default), else 4 (lanes' words
+    // side by side, coalesced where they move together). WB_XGRAN=<bytes> forces one (A/B).
+    const char *xge = getenv("WB_XGRAN");
+    const uint32_t xgb = xge ? uint32_t(atoi(xge)) : P.divergent_xmem ? 128u : 4u;
+    C->xlog = 0;
+    while (C->xlog < 5 && (4u << C->xlog) < xgb) C->xlog++;
     ximg.assign(C->xwords, 0u);
     for (const auto &d : P.datas) {
       if (!d.active || !d.mem) continue;
@@ -489,6 +497,7 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
   if (!P.xmems.empty()) {
     k.xmem = C->xmem.ptr; k.xpages = C->xpages.ptr; k.xinfo = C->xinfo.ptr;
     k.xwords = C->xwords; k.xstride = C->nwaves * 64; k.n_xmem = uint32_t(P.xmems.size());
+    k.xlog = C->xlog;
   }
   k.init_dropped = C->init_dropped;
   k.ls_slots = C->ls_slots;
@@ -803,7 +812,7 @@ WasmEdge_Result WasmEdge_BatchReset(WasmEdge_BatchContext *C, double *KernelSeco
   // memories past the first: zeros + their active data segments, initial sizes
   if (!P.xmems.empty() &&
       ((C->xwords && !C->hip_ok(wb_launch_mem_init(C->xmem.ptr, C->ximage.ptr, C->xwords, C->xwords,
-                                                    C->xwords, C->nwaves, nullptr, 0, 1u, 0u, 0u, nullptr,
+                                                    C->xwords, C->nwaves, nullptr, 0, 1u, C->xlog, 0u, nullptr,
                                                     0, 0, 0, C->stream), "memory init")) ||
        !C->hip_ok(hipMemcpyAsync(C->xpages.ptr, C->xpages0.data(), C->xpages0.size() * sizeof(uint32_t),
                                  hipMemcpyHostToDevice, C->stream), "memory sizes")))

@@ -140,6 +140,8 @@ struct WasmEdge_BatchContext {
   DevBuf<uint32_t> xmem, ximage, xpages, xinfo;
   std::vector<uint32_t> xpages0, xinfo_h;   // xinfo: base word, page limit per memory
   uint32_t xwords = 0;
+  // their granule: 4 << xlog bytes (KParams::xlog; batch_api.cpp setup)
+  uint32_t xlog = 0;
   // host-import yield path (only allocated when the module imports functions)
   DevBuf<uint32_t> fsave, hcall, hbuf;
   uint32_t hb_cells = 0;

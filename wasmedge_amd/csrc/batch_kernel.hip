@@ -381,9 +381,11 @@ __device__ __forceinline__ void interp(const KParams &p, Frame &F, const uint32_
   // only [0, hwm) of each lane (plus the image), the rest is still the zero it was given
   uint32_t hwm = LS(LS_HWM);
 #define WB_MARK(ea, n) (hwm = max(hwm, (uint32_t)min((uint64_t)(ea) + (uint64_t)(n), 0xFFFFFFFFull)))
-  // memories past the first (MultiMemories, KParams::xmem): 4-byte words interleaved over
-  // the wave's lanes; only the per-lane step (dbc_step.inc XLD ... XMEM_COPY) reaches them
-#define XMEM(k) GMem{p.xmem + ((size_t)(inst >> 6) * p.xwords + p.xinfo[2u * ((k) - 1u)]) * 64u + (inst & 63u), 0u}
+  // memories past the first (MultiMemories, KParams::xmem): granules of 4 << xlog bytes
+  // interleaved over the wave's lanes; the per-lane step (dbc_step.inc XLD ... XMEM_COPY)
+  // and the compiled XLD / XST (jit.cpp emit_xmem) reach them
+#define XMEM(k) GMem{p.xmem + ((size_t)(inst >> 6) * p.xwords + p.xinfo[2u * ((k) - 1u)]) * 64u + \
+                     ((inst & 63u) << p.xlog), p.xlog}
 #define XPAGES(k) p.xpages[(size_t)((k) - 1u) * p.xstride + inst]
 #define XLIMIT(k) p.xinfo[2u * ((k) - 1u) + 1u]
 #define XGROW(k, cur, n) (XPAGES(k) = (cur) + (n))

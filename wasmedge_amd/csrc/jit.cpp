@@ -72,6 +72,7 @@ uint16_t xmop(const DInstr &I) {
 // The word offsets of the extra memories in a lane's block (batch_ctx.h xinfo_h: memory k
 // at word xinfo[2 (k - 1)]), for the jit_source call that is compiling (null in dry runs)
 thread_local const std::vector<uint32_t> *g_xinfo = nullptr;
+thread_local uint32_t g_xlog = 0;   // (their granule: 4 << g_xlog bytes, KParams::xlog)
 
 // compare ops: VOPC suffix (32-bit form; the 64-bit form appends "64" to the type)
 const char *cmp_kind(uint16_t k) {   // k: 0 EQ, 1 NE, 2 LT_S, 3 LT_U, 4 GT_S, 5 GT_U, 6 LE_S, 7 LE_U, 8 GE_S, 9 GE_U
@@ -592,12 +593,12 @@ bool emit_store(Em &e, uint16_t op, uint32_t a, uint32_t b, uint32_t imm, const 
 // and only grows), so an access past it -- in bounds on a grown memory or not -- and a
 // misaligned one leave before the instruction and the C++ step executes it exactly.
 // No write mark: Reset rewrites the extra memories whole.
-// RP = the lane's word 0 of memory k: s[98:99] + xinfo[2 (k - 1)] * 256 + lane * 4
+// RP = the lane's granule 0 of memory k: s[98:99] + xinfo[2 (k - 1)] * 256 + lane * (4 << g)
 void xmem_lane_base(Em &e, uint32_t k) {
   const uint64_t woff = g_xinfo && size_t(2 * (k - 1)) < g_xinfo->size() ? (*g_xinfo)[2 * (k - 1)] : 0;
   e.l("v_mbcnt_lo_u32_b32 %s, -1, 0", W0);
   e.l("v_mbcnt_hi_u32_b32 %s, -1, %s", W0, W0);
-  e.l("v_lshlrev_b32_e32 %s, 2, %s", W0, W0);
+  e.l("v_lshlrev_b32_e32 %s, %u, %s", W0, 2 + g_xlog, W0);
   if (woff) {
     e.l("s_add_u32 s68, s98, 0x%x", uint32_t(woff << 8));
     e.l("s_addc_u32 s69, s99, 0x%x", uint32_t(woff >> 24));
@@ -644,9 +645,23 @@ bool emit_xmem(Em &e, const DInstr &I) {
     }
   }
   xmem_lane_base(e, k);
-  // XP = the access's first word (n >= 4: aligned, words at +256 each) or byte
-  uint32_t off = 0;
-  if (n >= 4) {
+  const uint32_t nw = n >= 4 ? n / 4 : 1;   // words (or the one sub-word access)
+  std::string adr[4];                       // each one's "vaddr, off[ offset:k]"
+  if (g_xlog) {   // granules of 4 << g bytes: each word's granule address in a pair of its own
+    static const char *const PR[4] = {"v[118:119]", "v[126:127]", "v[108:109]", "v[110:111]"};
+    const uint32_t g = g_xlog;
+    for (uint32_t q = 0; q < nw; q++) {
+      std::string ea = e.V(a);
+      if (imm + 4 * q) { e.l("v_add_u32_e32 %s, 0x%x, %s", Y1, imm + 4 * q, e.v(a)); ea = Y1; }
+      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + g, ea.c_str());
+      e.l("v_lshlrev_b64 %s, %u, %s", PR[q], 8 + g, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", PR[q], PR[q], RP);
+      e.l("v_bfe_u32 %s, %s, 0, %u", W0, ea.c_str(), 2 + g);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", PR[q], WP, PR[q]);
+      adr[q] = std::string(PR[q]) + ", off";
+    }
+  } else if (n >= 4) {   // the word interleave: XP = the first word, the others at +256 each
+    uint32_t off = 0;
     e.l("v_mov_b32 %s, %s", W0, e.v(a));
     e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
     e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
@@ -657,7 +672,8 @@ bool emit_xmem(Em &e, const DInstr &I) {
       e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, uint32_t(kk), X0);
       e.l("v_addc_co_u32_e32 %s, vcc, 0x%x, %s, vcc", X1, uint32_t(kk >> 32), X1);
     }
-  } else {
+    for (uint32_t q = 0; q < nw; q++) adr[q] = std::string(XP) + ", off offset:" + std::to_string(off + 256 * q);
+  } else {               // the word interleave, a byte or a half: XP = its byte
     std::string ea = e.V(a);
     if (imm) { e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, imm, e.v(a)); ea = Y0; }
     e.l("v_lshrrev_b32_e32 %s, 2, %s", W0, ea.c_str());
@@ -665,8 +681,9 @@ bool emit_xmem(Em &e, const DInstr &I) {
     e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
     e.l("v_and_b32_e32 %s, 3, %s", W0, ea.c_str());
     e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+    adr[0] = std::string(XP) + ", off";
   }
-  auto at = [&](uint32_t q) { return std::string(XP) + ", off offset:" + std::to_string(off + 256 * q); };
+  auto at = [&](uint32_t q) { return adr[q]; };
   if (st) {
     const char *ins = n == 1 ? "global_store_byte" : n == 2 ? "global_store_short" : "global_store_dword";
     for (uint32_t q = 0; q < std::max(1u, n / 4); q++) {
@@ -2624,10 +2641,16 @@ void scan_window_loads(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<
   if (sl.mem) xmem_lane_base(e, sl.mem);   // (RP: the lane's word 0 of memory k)
   for (uint32_t j = 1; j <= U; j++) {
     e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(sl.x));
-    if (sl.mem) {   // (the word interleave of the extra memories)
+    if (sl.mem && !g_xlog) {   // (an extra memory in the word interleave)
       e.l("v_mov_b32 %s, %s", W0, Y0);
       e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
       e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
+    } else if (sl.mem) {       // (an extra memory in granules of 4 << g_xlog bytes)
+      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + g_xlog, Y0);
+      e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + g_xlog, WP);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, RP);
+      e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + g_xlog);
+      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
     } else if (e.g == 0) {
       e.l("v_mov_b32 %s, %s", W0, Y0);
       e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
@@ -3503,14 +3526,15 @@ bool recursive(const Program &P) {
 }
 
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
-                       const JitCost *cost, bool simt, bool trip, const std::vector<uint32_t> *xinfo) {
+                       const JitCost *cost, bool simt, bool trip, const std::vector<uint32_t> *xinfo,
+                       uint32_t xlog) {
   if (cost) simt = false;
   // (extra memories: their accesses compile only against the context's word offsets)
   if (!P.xmems.empty() && (!xinfo || xinfo->size() < 2 * P.xmems.size())) return "";
   struct XinfoScope {
-    explicit XinfoScope(const std::vector<uint32_t> *x) { g_xinfo = x; }
-    ~XinfoScope() { g_xinfo = nullptr; }
-  } xscope(xinfo);
+    XinfoScope(const std::vector<uint32_t> *x, uint32_t lg) { g_xinfo = x; g_xlog = lg; }
+    ~XinfoScope() { g_xinfo = nullptr; g_xlog = 0; }
+  } xscope(xinfo, xlog);
   // trip mode beside SIMT scheduling (hybrid, the default) or alone (WB_HYBRID=0)
   const bool trips = trip && simt && runs.size() <= kTripMaxRuns;
   const bool hybrid = trips && !(getenv("WB_HYBRID") && getenv("WB_HYBRID")[0] == '0');
@@ -4521,7 +4545,8 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       if (simt) runs = wb::jit_runs(P, tc, true, simt == 2);
       if (runs.empty()) continue;
       std::vector<char> obj;
-      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2, &xinfo);
+      const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2, &xinfo,
+                                             P.divergent_xmem ? 5u : 0u);
       if (const char *dump = getenv(simt == 2 ? "WB_JIT_DUMP_TRIP" : simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
         if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
       e = src.empty() ? "no source" : wb::jit_compile(src, &obj);

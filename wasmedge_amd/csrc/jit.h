@@ -63,10 +63,10 @@ constexpr size_t kTripMaxRuns = 96;
 // xinfo: (modules with memories past the first) the context's xinfo_h -- memory k's word
 // offset in a lane's block at [2 (k - 1)] -- for the compiled XLD / XST (jit.cpp
 // emit_xmem, which address the wave's block through s[98:99], set by the kernel at every
-// core call); without it such a module gets no source.
+// core call); without it such a module gets no source. xlog: their granule (KParams::xlog).
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost = nullptr, bool simt = false, bool trip = false,
-                       const std::vector<uint32_t> *xinfo = nullptr);
+                       const std::vector<uint32_t> *xinfo = nullptr, uint32_t xlog = 0);
 
 // Whether trip mode pays for a module whose memory addresses do not depend on per-instance
 // data (Program::divergent_mem picks it for those): lanes part ways inside a loop on every

@@ -96,17 +96,18 @@ struct KParams {
                                 // what the core leaves to it
   uint32_t gs_grow;             // 1: a call past gs_depth parks for the host to grow the call
                                 // stack (WB_STACK_CALL) instead of trapping 0xB0
-  // memories 1..n_xmem (MultiMemories; only the per-lane step addresses them): each lane's
-  // xwords words hold them back to back, memory k at word xinfo[2(k - 1)], 4-byte words
-  // interleaved over the wave's 64 lanes ([wave][word][64]); xpages[(k - 1) * xstride +
-  // lane] = memory k's size, xinfo[2(k - 1) + 1] = its page limit (the reservation). (A
-  // device table, not arrays in KParams: indexing those would move KParams off SGPRs.)
+  // memories 1..n_xmem (MultiMemories): each lane's xwords words hold them back to back,
+  // memory k at word xinfo[2(k - 1)], interleaved over the wave's 64 lanes in granules of
+  // 4 << xlog bytes as memory 0 is (GMem: [wave][word >> xlog][64][2^xlog]); xpages[(k - 1)
+  // * xstride + lane] = memory k's size, xinfo[2(k - 1) + 1] = its page limit (the
+  // reservation). (A device table, not arrays in KParams: indexing those would move KParams
+  // off SGPRs.)
   uint32_t *xmem;
   uint32_t *xpages;
   uint32_t *parked;             // host-mapped word: 1 when a lane parked for the host (the host
                                 // then runs its service round; 0 = none parked, no round)
   const uint32_t *xinfo;
-  uint32_t xwords, xstride, n_xmem;
+  uint32_t xwords, xstride, n_xmem, xlog;
   // 1: a table.grow past its table's capacity (tabinfo), within tlimit[t] (frontend.h
   // table_widen_limit), parks for the host to widen the tables (WB_TGROW_CALL | t) instead
   // of returning -1
