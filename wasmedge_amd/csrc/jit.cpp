@@ -2962,49 +2962,76 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   const bool chain = !(getenv("WB_TRIP_CHAIN") && getenv("WB_TRIP_CHAIN")[0] == '0');
   // stage-B batches: run k's test reads PREG[k - bfirst[k]]; a stage-B run k recomputes
   // the masks of runs k+1 .. blast[k] (trip_source's stage code, below)
-  // Function guards (WB_TRIP_GUARD=0 turns them off): the runs of one function are
-  // consecutive in the chain, and while no lane's VPC or TPC lies in their pc range none of
-  // their tests can take lanes -- C3's `sort` (fill and checksum loops) while every lane
-  // sorts. A block of at least kTripGuard runs is skipped after one range test (the batch
-  // registers, s68 / s69; computed where the block starts, after the runs before it moved
-  // their lanes), and batches never cross a block.
+  // Guards (WB_TRIP_GUARD=0 turns them off): a block of consecutive runs is skipped after
+  // one range test while no lane's VPC lies in its pc range (none of its tests could take
+  // lanes then). The blocks: (1) the runs of one function -- C3's `sort` (fill and checksum
+  // loops) while every lane sorts -- unless they are every run of the trips (a lane is
+  // always in them then: C4's one function); (2) within those, a stretch of runs outside
+  // every loop (no backward branch spans them: entries, exits, the trap tails after C4's
+  // state machine), cold while the lanes loop. A block needs at least kTripGuard runs; the
+  // test uses the batch registers and s68 / s69 where the block starts (after the runs
+  // before it moved their lanes), blocks nest, and batches never cross a block's edge.
+  // (VPC alone decides: a lane that a stage-B test takes by its TPC began the trip at that
+  // run's pc and is still there -- a stage-A run moves none of its lanes but the ones that
+  // leave, which take TPC -1, and no other run's test takes it.)
   const bool guard_on = batch_on && !(getenv("WB_TRIP_GUARD") && getenv("WB_TRIP_GUARD")[0] == '0');
   std::vector<int64_t> fn_of(nr);
   for (uint32_t k = 0; k < nr; k++) fn_of[k] = func_of(runs[k].pc);
-  std::vector<uint32_t> gend(nr, 0xFFFFFFFFu);   // block start -> its last run (guarded blocks)
+  std::vector<uint8_t> in_loop(nr, 0);   // some backward branch spans the run's start
+  for (uint32_t pc = 0; pc < P.code.size(); pc++) {
+    const DInstr &I = P.code[pc];
+    const uint16_t o = op_of(I);
+    std::vector<uint32_t> tg;
+    if (is_branch_op(o) || o == OP_BR_IF_MOV1 || o == OP_BR_IF_MOV2) tg.push_back(I.w3);
+    if (o == OP_BR_TABLE)
+      for (uint32_t q = 0; q <= (I.w1 >> 16); q++)
+        if (2 * (size_t(I.w3) + q) < P.brtab.size()) tg.push_back(P.brtab[2 * (size_t(I.w3) + q)]);
+    for (uint32_t t : tg)
+      if (t <= pc)
+        for (uint32_t k = 0; k < nr; k++) in_loop[k] |= runs[k].pc >= t && runs[k].pc <= pc;
+  }
+  std::vector<std::vector<uint32_t>> gblk(nr);   // block start -> the last runs of its blocks (outer first)
+  std::vector<uint8_t> cut(nr + 1, 0);            // a block's edge lies before run k
+  auto add_block = [&](uint32_t k, uint32_t e) {
+    if (e + 1 - k < kTripGuard) return;
+    gblk[k].push_back(e);
+    cut[k] = cut[e + 1] = 1;
+  };
   for (uint32_t k = 0; k < nr && guard_on;) {
     uint32_t e = k;
     while (e + 1 < nr && fn_of[e + 1] == fn_of[k]) e++;
-    if (e + 1 - k >= kTripGuard) gend[k] = e;
+    if (!(k == 0 && e + 1 == nr)) add_block(k, e);
+    for (uint32_t j = k; j <= e;) {   // the function's stretches outside every loop
+      if (in_loop[j]) { j++; continue; }
+      uint32_t f = j;
+      while (f + 1 <= e && !in_loop[f + 1]) f++;
+      if (!(j == k && f == e)) add_block(j, f);   // (not the function's block again)
+      j = f + 1;
+    }
     k = e + 1;
   }
   std::vector<uint32_t> bfirst(nr, 0), blast(nr, 0);
   for (uint32_t k = 0; k < nr;) {
     uint32_t e = k;
-    while (e + 1 < nr && e + 1 - k < G && !fwd_ok[e] && pf_from[e] < 0 &&
-           !(guard_on && fn_of[e + 1] != fn_of[e]))
-      e++;
+    while (e + 1 < nr && e + 1 - k < G && !fwd_ok[e] && pf_from[e] < 0 && !cut[e + 1]) e++;
     for (uint32_t j = k; j <= e; j++) { bfirst[j] = k; blast[j] = e; }
     k = e + 1;
   }
   auto b_cmp = [&](Em &x, uint32_t k) {   // run k's test mask into its batch register
     vcmp64(x, PREG[k - bfirst[k]], runs[k].pc, chain && !split[k] ? VPC : TPC, k - bfirst[k]);
   };
-  std::vector<uint32_t> gopen;   // guarded blocks whose skip label is still to be placed
+  std::vector<std::pair<uint32_t, uint32_t>> gopen;   // (label id, last run) of blocks still open
+  uint32_t nguard = 0;
   for (uint32_t k = 0; k < nr; k++) {
-    if (gend[k] != 0xFFFFFFFFu) {   // lo <= VPC <= hi or lo <= TPC <= hi, else past the block
-      const uint32_t lo = runs[k].pc, hi = runs[gend[k]].pc;
+    for (uint32_t e : gblk[k]) {   // lo <= VPC <= hi, else past the block
+      const uint32_t lo = runs[k].pc, hi = runs[e].pc;
       h.l("s_mov_b32 s68, 0x%x", lo);
       h.l("s_mov_b32 s69, 0x%x", hi + 1);
       h.l("v_cmp_le_u32_e64 s[80:81], s68, %s", VPC);
       h.l("v_cmp_gt_u32_e64 s[86:87], s69, %s", VPC);
-      h.l("v_cmp_le_u32_e64 s[88:89], s68, %s", TPC);
-      h.l("v_cmp_gt_u32_e64 s[90:91], s69, %s", TPC);
       h.l("s_and_b64 s[80:81], s[80:81], s[86:87]");
-      h.l("s_and_b64 s[88:89], s[88:89], s[90:91]");
-      h.l("s_or_b64 s[80:81], s[80:81], s[88:89]");
-      h.l("s_cbranch_scc0 Lg%u", k);
-      gopen.push_back(k);
+      h.l("s_cbranch_scc0 Lg%u", nguard);
+      gopen.push_back({nguard++, e});
     }
     if (batch_on && bfirst[k] == k)
       for (uint32_t j = k; j <= blast[k]; j++) b_cmp(h, j);
@@ -3036,8 +3063,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       h.l("s_cbranch_scc1 LtS%u", k);
       h.l("LtSr%u:", k);
     }
-    if (!gopen.empty() && gend[gopen.back()] == k) {
-      h.l("Lg%u:", gopen.back());
+    while (!gopen.empty() && gopen.back().second == k) {
+      h.l("Lg%u:", gopen.back().first);
       gopen.pop_back();
     }
   }
