@@ -766,7 +766,11 @@ bool emit(Em &e, const DInstr &I) {
     e.sync({a, a + 1, b, b + 1, c});
     const char *x = e.src64(a, A0, A1, AP);
     const char *y;
-    if (ri) {
+    std::string kimm;
+    if (ri && int32_t(imm) >= -16 && int32_t(imm) <= 64) {   // (an inline constant: sign-extended)
+      kimm = std::to_string(int32_t(imm));
+      y = kimm.c_str();
+    } else if (ri) {
       e.l("v_mov_b32 %s, 0x%x", Z0, imm);
       e.l("v_ashrrev_i32_e32 %s, 31, %s", Z1, Z0);
       y = ZP;
@@ -1187,13 +1191,46 @@ bool emit(Em &e, const DInstr &I) {
       e.sync({a, a + 1, b, b + 1, c, c + 1});
       // operands as word registers; the b operand of *_I in Z
       std::string bl = e.V(b), bh = e.V(b + 1);
-      if (ri) {
+      if (ri && op == OP_I64_MUL_I && int32_t(imm) < 0) {   // (the general path below)
         e.l("v_mov_b32 %s, 0x%x", Z0, imm);
         e.l("v_ashrrev_i32_e32 %s, 31, %s", Z1, Z0);
         bl = Z0;
         bh = Z1;
       }
       const std::string al = e.V(a), ah = e.V(a + 1);
+      if (ri && op != OP_I64_MUL_I) {
+        // a 32-bit immediate (its high word 0 or -1): word by word, straight into the cells
+        // unless c overlaps a partly (then through R)
+        const bool neg = int32_t(imm) < 0, direct = c == a || c + 1 < a || c > a + 1;
+        const std::string lo = direct ? e.V(c) : R0, hi = direct ? e.V(c + 1) : R1;
+        if (op == OP_I64_ADD_I) {
+          e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", lo.c_str(), imm, al.c_str());
+          e.l("v_addc_co_u32_e32 %s, vcc, %d, %s, vcc", hi.c_str(), neg ? -1 : 0, ah.c_str());
+        } else if (op == OP_I64_SUB_I) {
+          e.l("v_subrev_co_u32_e32 %s, vcc, 0x%x, %s", lo.c_str(), imm, al.c_str());
+          e.l("v_subbrev_co_u32_e32 %s, vcc, %d, %s, vcc", hi.c_str(), neg ? -1 : 0, ah.c_str());
+        } else {
+          const bool and_ = op == OP_I64_AND_I, or_ = op == OP_I64_OR_I;
+          e.l("%s %s, 0x%x, %s", and_ ? "v_and_b32_e32" : or_ ? "v_or_b32_e32" : "v_xor_b32_e32", lo.c_str(), imm,
+              al.c_str());
+          if ((and_ && !neg) || (or_ && neg)) e.l("v_mov_b32 %s, %d", hi.c_str(), neg ? -1 : 0);
+          else if (!neg || and_ || or_) { if (hi != ah) e.l("v_mov_b32 %s, %s", hi.c_str(), ah.c_str()); }
+          else e.l("v_not_b32_e32 %s, %s", hi.c_str(), ah.c_str());
+        }
+        if (!direct) e.put64(c);
+        return true;
+      }
+      if (op == OP_I64_MUL_I && int32_t(imm) >= 0) {   // (high word 0: no a_lo * b_hi term)
+        const bool inl = imm <= 64;
+        if (!inl) e.l("s_mov_b32 s68, 0x%x", imm);
+        const std::string k = inl ? std::to_string(imm) : std::string("s68");
+        e.l("v_mul_hi_u32 %s, %s, %s", X0, al.c_str(), k.c_str());
+        e.l("v_mul_lo_u32 %s, %s, %s", Y0, ah.c_str(), k.c_str());
+        e.l("v_mul_lo_u32 %s, %s, %s", R0, al.c_str(), k.c_str());
+        e.l("v_add_u32_e32 %s, %s, %s", R1, X0, Y0);
+        e.put64(c);
+        return true;
+      }
       if (op == OP_I64_ADD || op == OP_I64_ADD_I) {
         const char *x = e.src64(a, A0, A1, AP);
         const char *y = ri ? ZP : e.src64(b, B0, B1, BP);
@@ -1774,19 +1811,54 @@ std::string emit_ret(Em &e, const DInstr &I, const std::string &split,
 
 // BR_TABLE (controlInstr.cpp:53-70; dbc_step.inc): index = min(cell a, b) (b = the
 // default's index), entry brtab[imm + index] = (target pc, taken-count correction).
-// Per lane: Y0 = target, Y1 = correction (a compare chain over the entries).
+// Per lane: Y0 = target, Y1 = correction. A table of at most 4 entries whose targets fit a
+// byte and corrections a signed byte (C4's state machine) reads both as byte fields of a
+// constant (v_bfe at 8 * index); larger ones take a compare chain over the entries that
+// differ from the default, with inline constants where they fit.
 void emit_br_table(Em &e, const DInstr &I) {
   const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, imm = I.w3;
   const std::vector<uint32_t> &bt = e.prog->brtab;
+  auto tgt = [&](uint32_t k) { return bt[2 * (imm + k)]; };
+  auto cor = [&](uint32_t k) { return int32_t(bt[2 * (imm + k) + 1]); };
+  bool same_c = true, bytes = b < 4;
+  for (uint32_t k = 0; k <= b; k++) {
+    same_c = same_c && cor(k) == cor(b);
+    bytes = bytes && tgt(k) < 256 && cor(k) >= -128 && cor(k) <= 127;
+  }
   e.l("v_min_u32_e32 %s, 0x%x, %s", X0, b, e.v(a));
-  e.l("v_mov_b32 %s, 0x%x", Y0, bt[2 * (imm + b)]);
-  e.l("v_mov_b32 %s, 0x%x", Y1, bt[2 * (imm + b) + 1]);
+  if (bytes) {
+    uint32_t kt = 0, kc = 0;
+    for (uint32_t k = 0; k <= b; k++) {
+      kt |= tgt(k) << (8 * k);
+      kc |= (uint32_t(cor(k)) & 0xFFu) << (8 * k);
+    }
+    e.l("v_lshlrev_b32_e32 %s, 3, %s", X1, X0);
+    e.l("v_mov_b32 %s, 0x%x", Y0, kt);
+    e.l("v_bfe_u32 %s, %s, %s, 8", Y0, Y0, X1);
+    if (same_c) {
+      e.l("v_mov_b32 %s, 0x%x", Y1, uint32_t(cor(b)));
+    } else {
+      e.l("v_mov_b32 %s, 0x%x", Y1, kc);
+      e.l("v_bfe_i32 %s, %s, %s, 8", Y1, Y1, X1);
+    }
+    return;
+  }
+  auto inl = [](uint32_t v) { return int32_t(v) >= -16 && int32_t(v) <= 64; };
+  auto sel = [&](const char *dst, uint32_t v) {   // dst = vcc ? v : dst
+    if (inl(v)) {
+      e.l("v_cndmask_b32_e64 %s, %s, %d, vcc", dst, dst, int32_t(v));
+    } else {
+      e.l("v_mov_b32 %s, 0x%x", X1, v);
+      e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", dst, dst, X1);
+    }
+  };
+  e.l("v_mov_b32 %s, 0x%x", Y0, tgt(b));
+  e.l("v_mov_b32 %s, 0x%x", Y1, uint32_t(cor(b)));
   for (uint32_t k = 0; k < b; k++) {
+    if (tgt(k) == tgt(b) && cor(k) == cor(b)) continue;
     e.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", k, X0);
-    e.l("v_mov_b32 %s, 0x%x", X1, bt[2 * (imm + k)]);
-    e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", Y0, Y0, X1);
-    e.l("v_mov_b32 %s, 0x%x", X1, bt[2 * (imm + k) + 1]);
-    e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", Y1, Y1, X1);
+    if (tgt(k) != tgt(b)) sel(Y0, tgt(k));
+    if (cor(k) != cor(b)) sel(Y1, uint32_t(cor(k)));
   }
 }
 
@@ -2906,10 +2978,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // TPC for the next trip: the pc of every lane in the runs, -1 outside
   h.l("Ltp:");
   h.l("s_mov_b64 exec, s[96:97]");
-  h.l("v_mov_b32 %s, %s", TPC, VPC);
-  h.l("s_mov_b64 exec, s[76:77]");
-  h.l("v_mov_b32 %s, -1", TPC);
-  h.l("s_mov_b64 exec, s[96:97]");
+  h.l("v_cndmask_b32_e64 %s, %s, -1, s[76:77]", TPC, VPC);
   // ---- the trip (EXEC = ALL between the runs)
   h.l("Ltrip:");
   // Batched lane tests (WB_TRIP_BATCH=0 turns them off): a run's test is a VALU compare
@@ -3075,12 +3144,16 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     h.l("v_readfirstlane_b32 s68, %s", VPC);
     h.l("s_nop 1");
     h.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
-    h.l("s_cbranch_vccnz Ltnc");
+    h.l("s_cbranch_vccnz Ltbud");   // (every lane in the runs: the trips go on)
     long_jump(h, "Lsched", "Ltcq");
     h.l("Ltnc:");
   }
   // ---- after the trip: go on while more lanes are in the runs than outside them
   // (one branch: none in the runs implies more outside than in, since ALL is not empty)
+  if (!hybrid) {
+    h.l("s_cmp_eq_u64 s[76:77], 0");
+    h.l("s_cbranch_scc1 Ltbud");
+  }
   h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
   h.l("s_bcnt1_i32_b64 s68, s[80:81]");
   h.l("s_bcnt1_i32_b64 s69, s[76:77]");
