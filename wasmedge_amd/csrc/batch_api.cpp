@@ -76,7 +76,7 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
   if (!runs.empty()) {
     std::vector<uint8_t> start(P.code.size() + 1, 0);
     for (const auto &r : runs) start[r.pc] = 1;
-    std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start);
+    std::vector<TInstr> tcj = wb::build_threaded(P, codepad, true, &start, &C->xinfo_h, C->xlog);
     std::vector<uint64_t> addr;
     const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
     const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
@@ -308,7 +308,7 @@ uint8_t setup(WasmEdge_BatchContext *C, const uint8_t *wasm, uint32_t len) {
     C->sched = 0;
   const bool vf_fit = C->threaded && P.total_cells() <= TC_VF_CELLS;
   C->vframe = vf_fit && (vfe ? vfe[0] == '1' : true);
-  if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe);
+  if (C->threaded) tcv = wb::build_threaded(P, codepad, C->vframe, nullptr, &C->xinfo_h, C->xlog);
   // compiled runs (jit.h) for the V-frame core; WB_JIT=0 interprets them instead. A
   // compile failure is not fatal (the core interprets) but is kept as the last error.
   const char *jte = getenv("WB_JIT");
@@ -552,7 +552,12 @@ uint8_t launch_once(WasmEdge_BatchContext *C, uint32_t entry_pc, bool is_start, 
       k.wave_ticks = C->wave_ticks.ptr;
       // (only for the same function on the same arguments: waves of other inputs take
       // other times, and an order learned from them is noise -- the fresh-input bench)
-      k.wave_order = C->order_pc == entry_pc && C->order_fp == C->args_fp && C->trial != 1 && C->trial != 3
+      // (WB_ORDER_ANY=1: also on other arguments -- an experiment, the per-slot cost of the
+      // last launch as the guess)
+      const char *oae = getenv("WB_ORDER_ANY");
+      const bool any_args = oae && oae[0] == '1';
+      k.wave_order = C->order_pc == entry_pc && (C->order_fp == C->args_fp || any_args) && C->trial != 1 &&
+                             C->trial != 3
                          ? C->wave_order.ptr : nullptr;
     }
   }

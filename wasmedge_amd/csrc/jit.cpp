@@ -3948,8 +3948,12 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
       if (lim) {
         e.l("s_cmp_gt_u32 s68, 0x%x", tend);
       } else if (taken) {
-        e.l("s_cmp_ge_u32 s95, 0x%x", to * 32u);   // to <= LOW: re-aim OTHER
-        e.l("s_cselect_b32 s63, s95, s63");
+        if (to == 0) {   // (pc 0 <= LOW always)
+          e.l("s_mov_b32 s63, s95");
+        } else {
+          e.l("s_cmp_ge_u32 s95, 0x%x", to * 32u);   // to <= LOW: re-aim OTHER
+          e.l("s_cselect_b32 s63, s95, s63");
+        }
         e.l("s_cmp_lt_u32 s65, s64");
         e.l("s_cselect_b32 s68, s63, 0");
         e.l("s_cmp_gt_u32 s68, 0x%x", tend);
