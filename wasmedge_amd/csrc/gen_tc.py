@@ -875,6 +875,77 @@ def specs():
     add("ST64", ["ST64"], lambda g: mem_check(g, 8) + word2() + [
         "global_store_dword %s, %s, off" % (XP, B[0]),
         "global_store_dword %s, %s, off" % (ZP, B[1])] + mark(8) + g.next())
+    # ---- memories past the first (MultiMemories; XLD / XST with the memory-0 op in D,
+    # jit.cpp emit_xmem). V blob only (the LDS blob leaves them to the C++ step). The
+    # translator (tc.cpp) picks the slot by that op and sets: w1 = the address cell, w2 =
+    # (XLD) memory k's declared minimum in pages / (XST) the value cell, w3 = (XLD) the
+    # result cell / (XST) the minimum, w4 = offset, w5 = memory k's word offset in a lane's
+    # block (xinfo, a multiple of 16384) | the granule log g, w7 = offset + n - 1. Bounds
+    # against the minimum (every lane's memory k has at least that many pages; past it the
+    # C++ step decides), alignment as mem_check; the wave's block is s[98:99] (the kernel
+    # sets it at every core call), the lane's byte ea at block + w5 / 32 * 32 * 256 +
+    # (lane << (2 + g)) + (ea >> (2 + g) << (8 + g)) + (ea & (4 << g) - 1).
+    def xmem_addr(g, n, minp):
+        out = ["v_add_co_u32_e64 %s, %s, %s, %s" % (X[0], T2, A[0], g.x(7)),   # last byte
+               "v_lshrrev_b32_e32 %s, 16, %s" % (X[1], X[0]),
+               "v_cmp_le_u32_e64 vcc, %s, %s" % (minp, X[1]),
+               "s_or_b64 %s, %s, vcc" % (T2, T2)]
+        m = 3 if n >= 4 else n - 1
+        if m:
+            out += ["v_and_b32_e32 %s, %d, %s" % (Y[0], m, X[0]),
+                    "v_cmp_ne_u32_e64 vcc, %d, %s" % (m, Y[0]),
+                    "s_or_b64 %s, %s, vcc" % (T2, T2)]
+        out += ["s_and_b64 %s, %s, exec" % (T2, T2), "s_cbranch_scc1 %s" % g.xh(),
+                "v_add_u32_e64 %s, %s, %s" % (Y[0], A[0], g.x(4)),   # ea
+                "s_and_b32 s68, %s, 31" % g.x(5),                     # g
+                "s_andn2_b32 s69, %s, 31" % g.x(5),                   # word offset
+                "s_lshl_b32 s74, s69, 8", "s_lshr_b32 s75, s69, 24",  # (T2 is free again)
+                "s_add_u32 s74, s74, s98", "s_addc_u32 s75, s75, s99",
+                "s_add_u32 s69, s68, 2",
+                "s_add_u32 s68, s68, 8",
+                "v_mbcnt_lo_u32_b32 %s, -1, 0" % W[0],
+                "v_mbcnt_hi_u32_b32 %s, -1, %s" % (W[0], W[0]),
+                "v_lshlrev_b32_e64 %s, s69, %s" % (W[0], W[0]),
+                "v_lshl_add_u64 %s, %s, 0, s[74:75]" % (ZP, WP)]      # ZP = the lane's granule 0
+        def at(dst, ea):
+            return ["v_lshrrev_b32_e64 %s, s69, %s" % (W[0], ea),
+                    "v_lshlrev_b64 %s, s68, %s" % (dst, WP),
+                    "v_lshl_add_u64 %s, %s, 0, %s" % (dst, dst, ZP),
+                    "v_bfe_u32 %s, %s, 0, s69" % (W[0], ea),
+                    "v_lshl_add_u64 %s, %s, 0, %s" % (dst, WP, dst)]
+        return out + at(XP, Y[0])
+
+    def x_word2(g):   # XP = the second word's address (ea + 4: maybe the next granule), once
+        # the first word's access has gone out (a memory instruction reads XP at issue)
+        return ["v_add_u32_e32 %s, 4, %s" % (Y[1], Y[0]),
+                "v_lshrrev_b32_e64 %s, s69, %s" % (W[0], Y[1]),
+                "v_lshlrev_b64 %s, s68, %s" % (XP, WP),
+                "v_lshl_add_u64 %s, %s, 0, %s" % (XP, XP, ZP),
+                "v_bfe_u32 %s, %s, 0, s69" % (W[0], Y[1]),
+                "v_lshl_add_u64 %s, %s, 0, %s" % (XP, WP, XP)]
+
+    def x_exit(g):
+        return g.exit_here()
+    for nm, (n, ins, width, ext) in LOADS.items():
+        def xbody(g, n=n, ins=ins, width=width, ext=ext):
+            if not g.vf:
+                return x_exit(g)
+            out = xmem_addr(g, n, g.x(2)) + ["%s %s, %s, off" % (ins, R[0], XP), "s_waitcnt vmcnt(0)"]
+            if width == 32:
+                return out + g.w32() + g.next()
+            hi = "v_mov_b32 %s, 0" % R[1] if ext == "zero" else "v_ashrrev_i32_e32 %s, 31, %s" % (R[1], R[0])
+            return out + [hi] + g.w64() + g.next()
+        add("XLD_" + nm, [], xbody)
+    add("XLD_LD64", [], lambda g: x_exit(g) if not g.vf else xmem_addr(g, 8, g.x(2)) + [
+        "global_load_dword %s, %s, off" % (R[0], XP)] + x_word2(g) + [
+        "global_load_dword %s, %s, off" % (R[1], XP),
+        "s_waitcnt vmcnt(0)"] + g.w64() + g.next(), slots=2)
+    for nm, (n, ins) in STORES.items():
+        add("XST_" + nm, [], lambda g, n=n, ins=ins: x_exit(g) if not g.vf else xmem_addr(g, n, g.x(3)) + [
+            "%s %s, %s, off" % (ins, XP, B[0])] + g.next())
+    add("XST_ST64", [], lambda g: x_exit(g) if not g.vf else xmem_addr(g, 8, g.x(3)) + [
+        "global_store_dword %s, %s, off" % (XP, B[0])] + x_word2(g) + [
+        "global_store_dword %s, %s, off" % (XP, B[1])] + g.next(), slots=2)
     # ---- compiled blocks (jit.cpp): a straight-line run of instructions compiled for
     # this module, entered here. Fields: w1/w2 = the block's code address, w5 = (run
     # length - 1) * 32. The block reloads both banks for the instruction after the run

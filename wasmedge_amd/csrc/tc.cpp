@@ -42,8 +42,37 @@ std::vector<uint8_t> jump_targets(const Program &P) {
   return target;
 }
 
+// the V blob's handler of an extra memory's access (XLD / XST with the memory-0 op `mop`)
+static int tc_xslot(uint16_t op, uint16_t mop) {
+  if (op == OP_XLD) {
+    switch (mop) {
+      case OP_LD32: return TC_SLOT_XLD_LD32;
+      case OP_LD8U32: return TC_SLOT_XLD_LD8U32;
+      case OP_LD8S32: return TC_SLOT_XLD_LD8S32;
+      case OP_LD16U32: return TC_SLOT_XLD_LD16U32;
+      case OP_LD16S32: return TC_SLOT_XLD_LD16S32;
+      case OP_LD32U64: return TC_SLOT_XLD_LD32U64;
+      case OP_LD32S64: return TC_SLOT_XLD_LD32S64;
+      case OP_LD8U64: return TC_SLOT_XLD_LD8U64;
+      case OP_LD8S64: return TC_SLOT_XLD_LD8S64;
+      case OP_LD16U64: return TC_SLOT_XLD_LD16U64;
+      case OP_LD16S64: return TC_SLOT_XLD_LD16S64;
+      case OP_LD64: return TC_SLOT_XLD_LD64;
+      default: return 0;
+    }
+  }
+  switch (mop) {
+    case OP_ST8: return TC_SLOT_XST_ST8;
+    case OP_ST16: return TC_SLOT_XST_ST16;
+    case OP_ST32: return TC_SLOT_XST_ST32;
+    case OP_ST64: return TC_SLOT_XST_ST64;
+    default: return 0;
+  }
+}
+
 std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe,
-                                   const std::vector<uint8_t> *run_start) {
+                                   const std::vector<uint8_t> *run_start,
+                                   const std::vector<uint32_t> *xinfo, uint32_t xlog) {
   const uint32_t T = P.total_cells();
   // operand fields: LDS byte offsets (cell * 256) for the LDS-frame blob, cell indices
   // (= VGPR index past v128) for the V-frame blob
@@ -58,6 +87,12 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
     const uint32_t a = I.w1 & 0xFFFFu, b = I.w1 >> 16, c = I.w2 & 0xFFFFu, d = I.w2 >> 16;
     const uint32_t imm = I.w3, cnt = (I.w0 >> 16) & 0xFFu;
     int slot = tc_slot(op);
+    // (memories past the first: V blob, with the context's layout; gen_tc.py xmem_addr)
+    const bool xop = (op == OP_XLD || op == OP_XST) && vframe && xinfo;
+    const uint32_t xk = op == OP_XLD ? b : c;
+    if (xop && xk >= 1 && xk <= P.xmems.size() && size_t(2 * xk) <= xinfo->size() &&
+        ((*xinfo)[2 * (xk - 1)] & 31u) == 0 && xlog < 32)
+      slot = tc_xslot(op, uint16_t(d));
     uint32_t a_eff = a;
     if (op == OP_V_EXTRACT32 || op == OP_V_EXTRACT64) {   // a lane of a v128 = a cell move
       a_eff = a + (op == OP_V_EXTRACT32 ? d : 2 * d);
@@ -89,6 +124,12 @@ std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, 
       const uint64_t last = uint64_t(imm) + n - 1;
       if (last > 0xFFFFFFFFull) continue;
       w[7] = uint32_t(last);
+    } else if (op == OP_XLD || op == OP_XST) {   // (xop: a slot was found above)
+      const uint64_t last = uint64_t(imm) + mem_bytes(uint16_t(d)) - 1;
+      if (last > 0xFFFFFFFFull) continue;
+      w[7] = uint32_t(last);
+      w[5] = (*xinfo)[2 * (xk - 1)] | xlog;       // word offset | granule log
+      w[op == OP_XLD ? 2 : 3] = P.xmems[xk - 1].min;   // (the other field: the value / result cell)
     } else if (op == OP_CONST64) {
       w[7] = I.w1;   // high word
       w[1] = w[2] = 0;

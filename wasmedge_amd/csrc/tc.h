@@ -29,8 +29,12 @@ struct Program;
 // fields for the V-frame blob (frame cells in VGPRs; needs total cells <= TC_VF_CELLS).
 // run_start (optional): pcs where a compiled run will begin (jit.h); no fused tuple
 // handler covers one of them past its first instruction.
+// xinfo / xlog: (memories past the first) the context's word offsets and granule
+// (batch_ctx.h xinfo_h, xlog) for the V blob's XLD / XST handlers; without them those
+// instructions have no handler (the C++ step runs them).
 std::vector<TInstr> build_threaded(const Program &P, std::vector<DInstr> &code, bool vframe,
-                                   const std::vector<uint8_t> *run_start = nullptr);
+                                   const std::vector<uint8_t> *run_start = nullptr,
+                                   const std::vector<uint32_t> *xinfo = nullptr, uint32_t xlog = 0);
 // Jump targets and resume points of P (index pc; size code + 1): branch/br_table/call
 // targets, the instruction after every call, function entries and bodies.
 std::vector<uint8_t> jump_targets(const Program &P);
