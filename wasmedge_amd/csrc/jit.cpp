@@ -405,6 +405,9 @@ struct MemGroup {
   uint32_t maxlast = 0;             // highest offset + n - 1
   uint64_t store_end = 0;           // highest offset + n of a store (0: no store)
   std::vector<std::pair<uint32_t, uint32_t>> aligns;   // distinct (offset & m, m)
+  // (trip load cache, LtF) every access of the group is a 32-bit access at an address a
+  // scan window already checked for these lanes: no bounds / alignment test
+  bool checked = false;
 };
 
 // the group's base pair (word interleave): MEM + a * 64
@@ -418,6 +421,15 @@ void group_base(Em &e, const MemGroup &G) {
 
 void group_check(Em &e, const MemGroup &G) {
   const uint32_t a = G.base;
+  if (G.checked) {   // (the write mark and the base only)
+    if (G.store_end) {
+      e.l("s_mov_b32 s69, 0x%x", uint32_t(G.store_end));
+      e.l("v_add_u32_e64 %s, %s, s69 clamp", Y1, e.v(a));
+      e.l("v_max_u32_e32 %s, %s, %s", HWM, HWM, Y1);
+    }
+    group_base(e, G);
+    return;
+  }
   e.l("v_add_co_u32_e32 %s, vcc, 0x%x, %s", X0, G.maxlast, e.v(a));
   e.l("v_lshrrev_b32_e32 %s, 16, %s", X1, X0);
   e.l("v_cmp_ge_u32_e64 %s, %s, %s", T2, X1, PAGES);
@@ -2784,6 +2796,52 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
   e.l("s_andn2_b64 s[84:85], exec, vcc");        // plain lanes
   e.l("s_and_b64 exec, exec, vcc");
   e.l("s_cbranch_execz %s_sb", L.c_str());
+  if (!(getenv("WB_TRIP_SCANBF") && getenv("WB_TRIP_SCANBF")[0] == '0')) {
+    // Branch-free (WB_TRIP_SCANBF=0: the iteration-by-iteration form below): each lane's
+    // exit iteration E (U + 1: none) and the word it ended on, from the last iteration to
+    // the first; then x += d * min(E, U), the count min(E, U) * (cnt + tcnt) less the
+    // untaken branch's tcnt for the lanes that leave, and those lanes' pc, cache slot and
+    // place outside the trips -- exactly what the iterations one by one retire.
+    const char *E = X0, *Yv = X1, *Em = Y0, *tmp = Y1;
+    e.l("v_mov_b32 %s, %u", E, U + 1);
+    e.l("v_mov_b32 %s, %s", Yv, T[U - 1]);
+    for (uint32_t j = U; j >= 1; j--) {
+      scan_cond(e, br, sl, T[j - 1]);   // vcc = goes round at iteration j
+      e.l("v_cndmask_b32_e64 %s, %u, %s, vcc", E, j, E);
+      if (j < U) e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", Yv, T[j - 1], Yv);
+    }
+    e.l("v_min_u32_e32 %s, %u, %s", Em, U, E);
+    auto k32 = [&](int32_t v, const char *sreg) -> std::string {   // an inline constant or an SGPR
+      if (v >= -16 && v <= 64) return std::to_string(v);
+      e.l("s_mov_b32 %s, 0x%x", sreg, uint32_t(v));
+      return sreg;
+    };
+    const std::string dk = k32(sl.d, "s68");
+    e.l("v_mad_i32_i24 %s, %s, %s, %s", e.v(x), Em, dk.c_str(), e.v(x));
+    e.l("v_mov_b32 %s, %s", e.v(y), Yv);
+    const std::string ck = k32(int32_t(r.cnt) + tcnt, "s69");
+    e.l("v_mad_i32_i24 %s, %s, %s, %s", VCNT, Em, ck.c_str(), VCNT);
+    e.l("v_cmp_lt_u32_e32 vcc, %u, %s", U, E);   // vcc = still going round
+    if (tcnt) {
+      e.l("v_mov_b32 %s, 0x%x", tmp, uint32_t(-tcnt));
+      e.l("v_cndmask_b32_e64 %s, %s, 0, vcc", tmp, tmp);
+      e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, tmp);
+    }
+    e.l("v_cndmask_b32_e32 %s, 0x%x, %s, vcc", VPC, fall, VPC);
+    if (slot.first >= 0) {   // (the load cache: the word that ended the scan, and its address)
+      e.l("v_add_u32_e32 %s, 0x%x, %s", tmp, sl.off, e.v(x));
+      e.l("v_cndmask_b32_e32 v%d, %s, v%d, vcc", slot.first, tmp, slot.first);
+      e.l("v_cndmask_b32_e32 v%d, %s, v%d, vcc", slot.second, Yv, slot.second);
+    }
+    if (!fall_in) {   // (the lanes that leave wait outside the trips)
+      e.l("s_andn2_b64 s[68:69], exec, vcc");
+      e.l("s_or_b64 s[76:77], s[76:77], s[68:69]");
+    }
+    e.l("%s_sb:", L.c_str());
+    e.l("s_mov_b64 exec, s[84:85]");
+    e.l("s_cbranch_execz %s", e.stage_end.c_str());
+    return;
+  }
   e.l("s_mov_b64 s[82:83], exec");
   for (uint32_t j = 1; j <= U; j++) {
     const std::string nx = L + "_n" + std::to_string(j);
@@ -3216,6 +3274,36 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
+    // the load cache's stage (LtF) enters with every lane's cached addresses equal to its
+    // loads' (and the scan windows that set them passed the bounds and alignment test): a
+    // group whose every access is a 32-bit access at such a (cell, offset), with the cell
+    // unwritten since the run's start, needs no test there (WB_TRIP_FWDCHK=0 keeps them)
+    std::vector<MemGroup> groups_f = groups;
+    if (fwd_ok[k] && !(getenv("WB_TRIP_FWDCHK") && getenv("WB_TRIP_FWDCHK")[0] == '0')) {
+      std::vector<std::pair<uint32_t, uint32_t>> ok;   // checked (cell, offset)
+      for (const auto &f : fwd[k]) ok.push_back({P.code[f.first].w1 & 0xFFFFu, P.code[f.first].w3});
+      std::vector<uint8_t> good(groups_f.size(), 1), written_c(TC_VF_CELLS + 8, 0);
+      int cur = -1;
+      std::vector<uint32_t> w;
+      for (uint32_t i = 0; i < r.len; i++) {
+        const DInstr &I = P.code[r.pc + i];
+        const uint16_t op = op_of(I);
+        if (lead[i] >= 0) cur = lead[i];
+        if (const uint32_t n = mem_bytes(op)) {
+          const uint32_t a = I.w1 & 0xFFFFu;
+          const bool hit = std::find(ok.begin(), ok.end(), std::make_pair(a, I.w3)) != ok.end();
+          if (cur < 0 || n != 4 || !hit || a >= written_c.size() || written_c[a]) {
+            if (cur >= 0) good[size_t(cur)] = 0;
+          }
+        } else if (xmop(I)) {
+          cur = -1;
+        }
+        written(I, &w);
+        for (uint32_t x : w)
+          if (x < written_c.size()) written_c[x] = 1;
+      }
+      for (size_t q = 0; q < groups_f.size(); q++) groups_f[q].checked = good[q] != 0;
+    }
     uint32_t done = 0, done_a = 0;
     // st 0: stage A, 1: stage B, 2: the whole run for the lanes the load cache serves (LtF),
     // 3: stage B for the lanes whose window a prefetching scan loaded this trip (LtS)
@@ -3278,7 +3366,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       for (uint32_t i = i0; i < i1; i++) {
         const DInstr &I = P.code[r.pc + i];
         e.pc = r.pc + i;
-        e.group = lead[i] >= 0 ? &groups[size_t(lead[i])] : nullptr;
+        e.group = lead[i] >= 0 ? &(st == 2 ? groups_f : groups)[size_t(lead[i])] : nullptr;
         if (!emit(e, I)) return "";
         e.done += (I.w0 >> 16) & 0xFFu;
       }
