@@ -2721,8 +2721,52 @@ void scan_window_fails(Em &e, const ScanLoop &sl, uint32_t U) {
 }
 
 // the scan window's U words into dst[0..U-1] (the window checked)
+void scan_window_words(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<std::string> &dst);
 void scan_window_loads(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<std::string> &dst) {
   if (sl.mem) xmem_lane_base(e, sl.mem);   // (RP: the lane's word 0 of memory k)
+  // One 16-byte load per lane whose window lies in one granule (granules of 16 bytes or
+  // more, |d| = 4, the destination registers consecutive in address order), the word by
+  // word path for the others (WB_TRIP_X4=0: word by word always)
+  const uint32_t g = sl.mem ? g_xlog : e.g;
+  int r = -1;
+  if (U == 4 && g >= 2 && (sl.d == 4 || sl.d == -4) && !(getenv("WB_TRIP_X4") && getenv("WB_TRIP_X4")[0] == '0')) {
+    int lo = -1;
+    bool ok = true;
+    for (uint32_t q = 0; q < 4 && ok; q++) {   // q-th word in address order
+      const std::string &reg = dst[sl.d > 0 ? q : 3 - q];
+      const int v = reg.size() > 1 && reg[0] == 'v' ? atoi(reg.c_str() + 1) : -1;
+      if (q == 0) lo = v;
+      ok = v >= 0 && v == lo + int(q);
+    }
+    if (ok && !(lo & 1)) r = lo;   // (VGPR tuples start at even registers)
+  }
+  if (r < 0) { scan_window_words(e, sl, U, dst); return; }
+  static thread_local int nx4 = 0;
+  const std::string id = std::to_string(nx4++);
+  const char *base = sl.mem ? RP : MEM;
+  const uint32_t lo_off = uint32_t(int64_t(sl.off) + (sl.d > 0 ? 4 : -16));
+  e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, lo_off, e.v(sl.x));
+  e.l("v_and_b32_e32 %s, 0x%x, %s", Y1, (4u << g) - 1u, Y0);
+  e.l("v_cmp_ge_u32_e32 vcc, 0x%x, %s", (4u << g) - 16u, Y1);   // the window in one granule
+  e.l("s_mov_b64 s[68:69], exec");
+  e.l("s_and_b64 exec, exec, vcc");
+  e.l("s_cbranch_execz Lx4a%s", id.c_str());
+  e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + g, Y0);
+  e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + g, WP);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, base);
+  e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + g);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  e.l("global_load_dwordx4 v[%d:%d], %s, off", r, r + 3, XP);
+  e.l("Lx4a%s:", id.c_str());
+  e.l("s_andn2_b64 exec, s[68:69], vcc");
+  e.l("s_cbranch_execz Lx4b%s", id.c_str());
+  scan_window_words(e, sl, U, dst);
+  e.l("Lx4b%s:", id.c_str());
+  e.l("s_mov_b64 exec, s[68:69]");
+}
+
+// (word by word: RP already set for an extra memory)
+void scan_window_words(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<std::string> &dst) {
   for (uint32_t j = 1; j <= U; j++) {
     e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, uint32_t(int64_t(sl.off) + int64_t(sl.d) * j), e.v(sl.x));
     if (sl.mem && !g_xlog) {   // (an extra memory in the word interleave)
@@ -2771,9 +2815,23 @@ void trip_scan_prefetch(Em &e, const ScanLoop &succ, uint32_t U, const ScanPrefe
   e.l("s_or_b64 exec, exec, s[84:85]");
 }
 
+// the window's j-th word's register (v108..v111, in address order: one 16-byte load fills
+// them, scan_window_loads)
+const char *scan_T(const ScanLoop &sl, uint32_t j) {
+  static const char *const up[kTripScan] = {"v108", "v109", "v110", "v111"};
+  static const char *const down[kTripScan] = {"v111", "v110", "v109", "v108"};
+  return sl.d > 0 ? up[j] : down[j];
+}
+
+// win: (stage B, branch-free form) the window's registers when every lane of the stage has
+// its window there already (LtS: the successor prefetch's), else v108.. and the v112 flag
+bool scan_bf_on() { return !(getenv("WB_TRIP_SCANBF") && getenv("WB_TRIP_SCANBF")[0] == '0'); }
+
 void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &sl, uint32_t U,
-                     int st, bool fall_in, const std::string &L, std::pair<int, int> slot) {
-  static const char *const T[kTripScan] = {"v108", "v109", "v110", "v111"};
+                     int st, bool fall_in, const std::string &L, std::pair<int, int> slot,
+                     const std::vector<std::string> *win = nullptr) {
+  const char *T[kTripScan];
+  for (uint32_t j = 0; j < kTripScan; j++) T[j] = win && j < win->size() ? (*win)[j].c_str() : scan_T(sl, j);
   const uint32_t x = sl.x, y = sl.y, fall = r.pc + 3;
   const DInstr &br = P.code[r.pc + 2];
   const int32_t tcnt = int32_t(int16_t(br.w2 >> 16));
@@ -2792,11 +2850,15 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
     return;
   }
   // stage B: the window lanes' exits in iteration order (s[82:83] = still looping)
-  e.l("v_cmp_ne_u32_e32 vcc, 0, v112");
-  e.l("s_andn2_b64 s[84:85], exec, vcc");        // plain lanes
-  e.l("s_and_b64 exec, exec, vcc");
-  e.l("s_cbranch_execz %s_sb", L.c_str());
-  if (!(getenv("WB_TRIP_SCANBF") && getenv("WB_TRIP_SCANBF")[0] == '0')) {
+  if (win) {
+    e.l("s_mov_b64 s[84:85], 0");                // (every lane has its window)
+  } else {
+    e.l("v_cmp_ne_u32_e32 vcc, 0, v112");
+    e.l("s_andn2_b64 s[84:85], exec, vcc");        // plain lanes
+    e.l("s_and_b64 exec, exec, vcc");
+    e.l("s_cbranch_execz %s_sb", L.c_str());
+  }
+  if (scan_bf_on()) {
     // Branch-free (WB_TRIP_SCANBF=0: the iteration-by-iteration form below): each lane's
     // exit iteration E (U + 1: none) and the word it ended on, from the last iteration to
     // the first; then x += d * min(E, U), the count min(E, U) * (cnt + tcnt) less the
@@ -2823,11 +2885,20 @@ void trip_scan_stage(Em &e, const Program &P, const JitRun &r, const ScanLoop &s
     e.l("v_mad_i32_i24 %s, %s, %s, %s", VCNT, Em, ck.c_str(), VCNT);
     e.l("v_cmp_lt_u32_e32 vcc, %u, %s", U, E);   // vcc = still going round
     if (tcnt) {
-      e.l("v_mov_b32 %s, 0x%x", tmp, uint32_t(-tcnt));
-      e.l("v_cndmask_b32_e64 %s, %s, 0, vcc", tmp, tmp);
+      if (-tcnt >= -16 && -tcnt <= 64) {
+        e.l("v_cndmask_b32_e64 %s, %d, 0, vcc", tmp, -tcnt);
+      } else {
+        e.l("v_mov_b32 %s, 0x%x", tmp, uint32_t(-tcnt));
+        e.l("v_cndmask_b32_e64 %s, %s, 0, vcc", tmp, tmp);
+      }
       e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, tmp);
     }
-    e.l("v_cndmask_b32_e32 %s, 0x%x, %s, vcc", VPC, fall, VPC);
+    if (fall <= 64) {   // (VCC is a constant-bus read already: no literal beside it)
+      e.l("v_cndmask_b32_e64 %s, %u, %s, vcc", VPC, fall, VPC);
+    } else {
+      e.l("v_mov_b32 %s, 0x%x", tmp, fall);
+      e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", VPC, tmp, VPC);
+    }
     if (slot.first >= 0) {   // (the load cache: the word that ended the scan, and its address)
       e.l("v_add_u32_e32 %s, 0x%x, %s", tmp, sl.off, e.v(x));
       e.l("v_cndmask_b32_e32 v%d, %s, v%d, vcc", slot.first, tmp, slot.first);
@@ -3013,10 +3084,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       if (!is_scan[q] || !start.count(runs[q].pc + 3)) continue;
       const uint32_t s = uint32_t(start[runs[q].pc + 3]);
       if (s == q || !is_scan[s] || pf_from[s] >= 0) continue;
-      if (next - scan_k < 128 + 2 * P.total_cells() + 16) break;   // (as the slots)
+      // (x in `next`, the window below it from an even register in address order: one
+      // 16-byte load can fill it, scan_window_loads)
+      const uint32_t lo = (next - scan_k) & ~1u;
+      if (lo < 128 + 2 * P.total_cells() + 16) break;   // (as the slots)
       pfr[q].x = next;
-      for (uint32_t j = 1; j <= scan_k; j++) pfr[q].v.push_back("v" + std::to_string(next - j));
-      next -= scan_k + 1;
+      for (uint32_t j = 0; j < scan_k; j++)
+        pfr[q].v.push_back("v" + std::to_string(scans[s].d < 0 ? lo + scan_k - 1 - j : lo + j));
+      next = lo - 1;
       pf_to[q] = int(s);
       pf_from[s] = int(q);
       inval.push_back(pfr[q].x);
@@ -3274,15 +3349,16 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     const uint32_t nbody = ends_run(lop) ? r.len - 1 : r.len;
     std::vector<int> lead;
     const std::vector<MemGroup> groups = jit_groups(P, r, &lead);
-    // the load cache's stage (LtF) enters with every lane's cached addresses equal to its
-    // loads' (and the scan windows that set them passed the bounds and alignment test): a
-    // group whose every access is a 32-bit access at such a (cell, offset), with the cell
-    // unwritten since the run's start, needs no test there (WB_TRIP_FWDCHK=0 keeps them)
-    std::vector<MemGroup> groups_f = groups;
-    if (fwd_ok[k] && !(getenv("WB_TRIP_FWDCHK") && getenv("WB_TRIP_FWDCHK")[0] == '0')) {
-      std::vector<std::pair<uint32_t, uint32_t>> ok;   // checked (cell, offset)
-      for (const auto &f : fwd[k]) ok.push_back({P.code[f.first].w1 & 0xFFFFu, P.code[f.first].w3});
-      std::vector<uint8_t> good(groups_f.size(), 1), written_c(TC_VF_CELLS + 8, 0);
+    // Groups a stage need not test (MemGroup::checked): every access of the group a 32-bit
+    // access at a (cell, offset) whose 32-bit access these lanes already passed the test
+    // for, with the cell unwritten since the run's start -- in the load cache's stage (LtF)
+    // the cached addresses (the scan windows that set them were tested), in stage B of a
+    // run with a stage A the stage-A accesses (C3's swap stores at the words its stage A
+    // loaded). WB_TRIP_FWDCHK=0 keeps every test.
+    const bool skip_on = !(getenv("WB_TRIP_FWDCHK") && getenv("WB_TRIP_FWDCHK")[0] == '0');
+    auto mark_checked = [&](std::vector<MemGroup> &gs, const std::vector<std::pair<uint32_t, uint32_t>> &ok,
+                            uint32_t from) {
+      std::vector<uint8_t> good(gs.size(), 1), written_c(TC_VF_CELLS + 8, 0);
       int cur = -1;
       std::vector<uint32_t> w;
       for (uint32_t i = 0; i < r.len; i++) {
@@ -3292,9 +3368,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         if (const uint32_t n = mem_bytes(op)) {
           const uint32_t a = I.w1 & 0xFFFFu;
           const bool hit = std::find(ok.begin(), ok.end(), std::make_pair(a, I.w3)) != ok.end();
-          if (cur < 0 || n != 4 || !hit || a >= written_c.size() || written_c[a]) {
-            if (cur >= 0) good[size_t(cur)] = 0;
-          }
+          if (cur >= 0 && (i < from || n != 4 || !hit || a >= written_c.size() || written_c[a]))
+            good[size_t(cur)] = 0;
         } else if (xmop(I)) {
           cur = -1;
         }
@@ -3302,7 +3377,21 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         for (uint32_t x : w)
           if (x < written_c.size()) written_c[x] = 1;
       }
-      for (size_t q = 0; q < groups_f.size(); q++) groups_f[q].checked = good[q] != 0;
+      for (size_t q = 0; q < gs.size(); q++) gs[q].checked = good[q] != 0;
+    };
+    std::vector<MemGroup> groups_f = groups, groups_b = groups;
+    if (skip_on && fwd_ok[k]) {
+      std::vector<std::pair<uint32_t, uint32_t>> ok;
+      for (const auto &f : fwd[k]) ok.push_back({P.code[f.first].w1 & 0xFFFFu, P.code[f.first].w3});
+      mark_checked(groups_f, ok, 0);
+    }
+    if (skip_on && split[k] && !is_scan[k]) {
+      std::vector<std::pair<uint32_t, uint32_t>> ok;
+      for (uint32_t i = 0; i < split[k]; i++) {
+        const DInstr &I = P.code[r.pc + i];
+        if (mem_bytes(op_of(I)) == 4) ok.push_back({I.w1 & 0xFFFFu, I.w3});
+      }
+      mark_checked(groups_b, ok, split[k]);
     }
     uint32_t done = 0, done_a = 0;
     // st 0: stage A, 1: stage B, 2: the whole run for the lanes the load cache serves (LtF),
@@ -3338,8 +3427,10 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         e.l("v_cmp_eq_u32_e32 vcc, v%u, %s", pf.x, e.v(scans[k].x));
         e.l("s_and_b64 exec, exec, vcc");
         e.l("s_cbranch_execz %s", e.stage_end.c_str());
-        for (uint32_t j = 0; j < scan_k; j++) e.l("v_mov_b32 v%u, %s", 108 + j, pf.v[j].c_str());
-        e.l("v_mov_b32 v112, 1");
+        if (!scan_bf_on()) {   // (the branch-free stage B reads the prefetch registers)
+          for (uint32_t j = 0; j < scan_k; j++) e.l("v_mov_b32 %s, %s", scan_T(scans[k], j), pf.v[j].c_str());
+          e.l("v_mov_b32 v112, 1");
+        }
       }
       if (st == 2) {   // the lanes whose every cached word is at its load's address
         // (the effective address is 33 bits: a lane whose x + offset carries, or lands on
@@ -3360,13 +3451,15 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         }
         e.l("s_cbranch_execz %s", e.stage_end.c_str());
       }
-      if (is_scan[k]) trip_scan_stage(e, P, r, scans[k], scan_k, sb, in_region(r.pc + 3), L, slot_of[k]);
+      if (is_scan[k])
+        trip_scan_stage(e, P, r, scans[k], scan_k, sb, in_region(r.pc + 3), L, slot_of[k],
+                        st == 3 && scan_bf_on() ? &pfr[size_t(pf_from[k])].v : nullptr);
       const size_t at = e.o.size();
       const uint32_t i0 = sb == 1 ? split[k] : 0, i1 = st == 0 ? split[k] : nbody;
       for (uint32_t i = i0; i < i1; i++) {
         const DInstr &I = P.code[r.pc + i];
         e.pc = r.pc + i;
-        e.group = lead[i] >= 0 ? &(st == 2 ? groups_f : groups)[size_t(lead[i])] : nullptr;
+        e.group = lead[i] >= 0 ? &(st == 2 ? groups_f : st == 1 ? groups_b : groups)[size_t(lead[i])] : nullptr;
         if (!emit(e, I)) return "";
         e.done += (I.w0 >> 16) & 0xFFu;
       }
