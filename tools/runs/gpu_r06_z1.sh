@@ -1,0 +1,13 @@
+# r06 z1: same-build profiles after the trip-mode changes: C3 (64K x 1 MiB) and mt19937
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06z1; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+export PROF_TIMEOUT=170
+step prof_mt 300 bash $R/tools/prof_bench.sh gpurun_out/r06z1/mt --workload mt
+step prof_c3 800 bash $R/tools/prof_bench.sh gpurun_out/r06z1/c3 --workload c3
+echo all done
