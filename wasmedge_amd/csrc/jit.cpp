@@ -3498,15 +3498,29 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         if (is_branch_op(lop) && lop != OP_JMP) {
           const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
           branch_cond(e, last);   // vcc = taken
-          e.l("v_mov_b32 %s, 0x%x", X0, fall);
-          e.l("v_mov_b32 %s, 0x%x", X1, tgt);
-          e.l("v_cndmask_b32_e32 %s, %s, %s, vcc", VPC, X0, X1);
+          // (VOP3 selects take inline constants, -16..64: the pcs and corrections of small
+          // modules need no moves)
+          auto inl = [](int64_t v) { return v >= -16 && v <= 64; };
+          std::string f = std::to_string(fall), t = std::to_string(tgt);
+          if (!inl(fall)) { e.l("v_mov_b32 %s, 0x%x", X0, fall); f = X0; }
+          if (!inl(tgt)) { e.l("v_mov_b32 %s, 0x%x", X1, tgt); t = X1; }
+          e.l("v_cndmask_b32_e64 %s, %s, %s, vcc", VPC, f.c_str(), t.c_str());
           if (tcnt) {
-            e.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));
-            e.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
-            e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+            if (inl(tcnt)) {
+              e.l("v_cndmask_b32_e64 %s, 0, %d, vcc", X0, tcnt);
+            } else {
+              e.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));
+              e.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
+            }
+            if (r.cnt && inl(r.cnt)) {   // (the run's count in the same add)
+              e.l("v_add3_u32 %s, %s, %s, %u", VCNT, VCNT, X0, r.cnt);
+            } else {
+              e.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+              add_cnt(r.cnt);
+            }
+          } else {
+            add_cnt(r.cnt);
           }
-          add_cnt(r.cnt);
           if (!in_region(tgt)) { e.l("s_and_b64 s[68:69], vcc, exec"); out_if("s[68:69]"); }
           if (!in_region(fall)) { e.l("s_andn2_b64 s[68:69], exec, vcc"); out_if("s[68:69]"); }
         } else if (lop == OP_JMP && brt_thread(tgt) >= 0) {
@@ -4545,12 +4559,20 @@ std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32
           e.l("s_cbranch_scc0 Lbs%s", K.c_str());
           Em x;
           x.l("Lbs%s:", K.c_str());
-          x.l("v_mov_b32 %s, 0x%x", X0, fall);
-          x.l("v_mov_b32 %s, 0x%x", X1, tgt);
-          x.l("v_cndmask_b32_e32 %s, %s, %s, vcc", VPC, X0, X1);
-          x.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));   // a taken branch's correction
-          x.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
-          x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+          {   // (inline constants where they fit: VOP3 selects take -16..64)
+            auto inl = [](int64_t v) { return v >= -16 && v <= 64; };
+            std::string f = std::to_string(fall), t = std::to_string(tgt);
+            if (!inl(fall)) { x.l("v_mov_b32 %s, 0x%x", X0, fall); f = X0; }
+            if (!inl(tgt)) { x.l("v_mov_b32 %s, 0x%x", X1, tgt); t = X1; }
+            x.l("v_cndmask_b32_e64 %s, %s, %s, vcc", VPC, f.c_str(), t.c_str());
+            if (inl(tcnt)) {   // a taken branch's correction
+              x.l("v_cndmask_b32_e64 %s, 0, %d, vcc", X0, int32_t(tcnt));
+            } else {
+              x.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));
+              x.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
+            }
+            x.l("v_add_u32_e32 %s, %s, %s", VCNT, VCNT, X0);
+          }
           x.l("s_add_u32 s65, s65, 0x%x", r.cnt);
           flush(x);
           if (fall != tgt && !hybrid && !depth_pick) {   // (hybrid: every split goes to Lsched, hence the trips)
