@@ -1,4 +1,5 @@
-# r06 z1: same-build profiles after the trip-mode changes: C3 (64K x 1 MiB) and mt19937
+# r06 z1: same-build profiles at HEAD after the trip-mode and branch-transfer changes:
+# C4, C1, C5, mt19937, C3 (64K x 1 MiB)
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r06z1; mkdir -p $O
 step() {  # name, timeout, command...
@@ -8,6 +9,9 @@ step() {  # name, timeout, command...
   if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
 }
 export PROF_TIMEOUT=170
+step prof_c4 200 bash $R/tools/prof_bench.sh gpurun_out/r06z1/c4 --workload c4
+step prof_c1 200 bash $R/tools/prof_bench.sh gpurun_out/r06z1/c1 --workload c1
+step prof_c5 200 bash $R/tools/prof_bench.sh gpurun_out/r06z1/c5 --workload c5 --steps 3 --warmup 1
 step prof_mt 300 bash $R/tools/prof_bench.sh gpurun_out/r06z1/mt --workload mt
 step prof_c3 800 bash $R/tools/prof_bench.sh gpurun_out/r06z1/c3 --workload c3
 echo all done
