@@ -1,0 +1,15 @@
+# r06 zc: vcc range guards + re-tests only for successor runs: parity, then C4, C3 4K, C3 1 MiB
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06zc; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+step tests 800 python -u -m pytest tests/test_tripcache.py tests/test_workloads.py tests/test_xmem_jit.py tests/test_jit.py -m gpu -v --timeout 300 --timeout-method thread
+step c4_in 200 python bench.py --workload c4 --no-cpu-baseline
+step c3k_in 200 python bench.py --workload c3 --elements 4096 --no-cpu-baseline
+step c3_in 300 python bench.py --workload c3 --no-cpu-baseline
+step c4_b 200 python bench.py --workload c4 --no-cpu-baseline
+echo all done

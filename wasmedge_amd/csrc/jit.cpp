@@ -3124,6 +3124,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // runs (VPC), so it recomputes the rest of its batch before it returns (stage end), and a
   // run with its own LtF / LtS tests ends a batch.
   const bool batch_on = !(getenv("WB_TRIP_BATCH") && getenv("WB_TRIP_BATCH")[0] == '0');
+  // Inline stages (WB_TRIP_INLINE=0 turns it off): a run's stage code sits in the test
+  // chain right after its test, which branches past it when no lane is there -- a stage
+  // that takes lanes costs no taken branch (out of line it costs two: there and back), one
+  // that takes none costs one. Taken branches are what the trips' scalar stream waits on (a
+  // taken branch refetches: ~20 cycles, tools/ubench/lat.hip); C3 1 MiB +6% with stage B
+  // inline (profiles/r06zb_bench_c3_*).
+  const bool inline_on = !(getenv("WB_TRIP_INLINE") && getenv("WB_TRIP_INLINE")[0] == '0');
+  const bool smask_on = !(getenv("WB_TRIP_SMASK") && getenv("WB_TRIP_SMASK")[0] == '0');
   // dst = (v == pc) per lane; VOP3 takes no literal, so a pc past the inline constants goes
   // through s68 / s69 (alternating: the compare has read one before the next is written)
   auto vcmp64 = [](Em &x, const char *dst, uint32_t pc, const char *v, uint32_t j) {
@@ -3151,7 +3159,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[a[j]].pc, TPC);
           h.l("s_and_b64 s[74:75], vcc, exec");
         }
-        h.l("s_cbranch_scc1 LtA%u", a[j]);
+        h.l("@@LtA%u@@", a[j]);   // (the test's branch and, inline, the stage-A code: below)
         h.l("LtAr%u:", a[j]);
       }
     }
@@ -3225,14 +3233,15 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   std::vector<std::pair<uint32_t, uint32_t>> gopen;   // (label id, last run) of blocks still open
   uint32_t nguard = 0;
   for (uint32_t k = 0; k < nr; k++) {
-    for (uint32_t e : gblk[k]) {   // lo <= VPC <= hi, else past the block
+    for (uint32_t e : gblk[k]) {   // lo <= VPC <= hi (VPC - lo <= hi - lo), else past the block
       const uint32_t lo = runs[k].pc, hi = runs[e].pc;
-      h.l("s_mov_b32 s68, 0x%x", lo);
-      h.l("s_mov_b32 s69, 0x%x", hi + 1);
-      h.l("v_cmp_le_u32_e64 s[80:81], s68, %s", VPC);
-      h.l("v_cmp_gt_u32_e64 s[86:87], s69, %s", VPC);
-      h.l("s_and_b64 s[80:81], s[80:81], s[86:87]");
-      h.l("s_cbranch_scc0 Lg%u", nguard);
+      if (lo) {
+        h.l("v_subrev_u32_e32 %s, 0x%x, %s", X0, lo, VPC);
+        h.l("v_cmp_ge_u32_e32 vcc, 0x%x, %s", hi - lo, X0);
+      } else {
+        h.l("v_cmp_ge_u32_e32 vcc, 0x%x, %s", hi, VPC);
+      }
+      h.l("s_cbranch_vccz Lg%u", nguard);
       gopen.push_back({nguard++, e});
     }
     if (batch_on && bfirst[k] == k)
@@ -3247,14 +3256,14 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
       h.l("s_and_b64 s[74:75], vcc, exec");
     }
-    h.l("s_cbranch_scc1 LtB%u", k);
+    h.l("@@LtB%u@@", k);   // (the test's branch and, inline, the stage-B code: below)
     h.l("LtBr%u:", k);
     if (fwd_ok[k]) {   // the lanes that arrived this trip (not at its start there): LtF
       h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, VPC);
       h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
       h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
       h.l("s_andn2_b64 s[74:75], s[74:75], vcc");
-      h.l("s_cbranch_scc1 LtF%u", k);
+      h.l("@@LtF%u@@", k);
       h.l("LtFr%u:", k);
     }
     if (pf_from[k] >= 0) {   // the lanes its prefetching scan moved here this trip: LtS
@@ -3262,7 +3271,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       h.l("s_andn2_b64 s[74:75], vcc, s[76:77]");
       h.l("v_cmp_eq_u32_e32 vcc, 0x%x, %s", runs[k].pc, TPC);
       h.l("s_andn2_b64 s[74:75], s[74:75], vcc");
-      h.l("s_cbranch_scc1 LtS%u", k);
+      h.l("@@LtS%u@@", k);
       h.l("LtSr%u:", k);
     }
     while (!gopen.empty() && gopen.back().second == k) {
@@ -3270,28 +3279,19 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       gopen.pop_back();
     }
   }
+  // ---- after the trip: go on while more lanes are in the runs than outside them (Ltnc;
+  // none in the runs implies more outside than in, since ALL is not empty). The common
+  // case -- every lane in the runs, at more than one pc -- falls through to the budget and
+  // takes one branch, back to Ltp.
+  h.l("s_cmp_eq_u64 s[76:77], 0");
+  h.l("s_cbranch_scc0 Ltnc");
   if (hybrid) {
-    // ---- every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL)
-    h.l("s_cmp_eq_u64 s[76:77], 0");
-    h.l("s_cbranch_scc0 Ltnc");
+    // every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL; Ltcv)
     h.l("v_readfirstlane_b32 s68, %s", VPC);
     h.l("s_nop 1");
     h.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
-    h.l("s_cbranch_vccnz Ltbud");   // (every lane in the runs: the trips go on)
-    long_jump(h, "Lsched", "Ltcq");
-    h.l("Ltnc:");
+    h.l("s_cbranch_vccz Ltcv");
   }
-  // ---- after the trip: go on while more lanes are in the runs than outside them
-  // (one branch: none in the runs implies more outside than in, since ALL is not empty)
-  if (!hybrid) {
-    h.l("s_cmp_eq_u64 s[76:77], 0");
-    h.l("s_cbranch_scc1 Ltbud");
-  }
-  h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
-  h.l("s_bcnt1_i32_b64 s68, s[80:81]");
-  h.l("s_bcnt1_i32_b64 s69, s[76:77]");
-  h.l("s_cmp_gt_u32 s69, s68");
-  h.l("s_cbranch_scc1 Ltx");
   h.l("Ltbud:");
   // (>= what one lane can retire in a trip: one run, or with chaining every run once)
   uint32_t trip_cost = 256, chained = 0;
@@ -3307,16 +3307,26 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     }
   }
   if (chain) trip_cost = std::max(trip_cost, chained + (uint32_t)kTripScan * 64u);
+  // (no borrow: go on -- a budget that reaches 0 exactly runs one more trip)
   h.l("s_sub_u32 s64, s64, 0x%x", trip_cost);
-  h.l("s_cselect_b32 s64, 0, s64");
-  h.l("s_cmp_eq_u32 s64, 0");
   h.l("s_cbranch_scc0 Ltp");
   // budget spent: back to the kernel with no group (reason 1)
+  h.l("s_mov_b32 s64, 0");
   h.l("s_mov_b64 exec, 0");
   h.l("s_mov_b32 s65, 0");
   h.l("s_add_u32 s68, s70, %u", TC_JIT_XS);
   h.l("s_addc_u32 s69, s71, 0");
   h.l("s_setpc_b64 s[68:69]");
+  if (hybrid) {
+    h.l("Ltcv:");
+    long_jump(h, "Lsched", "Ltcq");
+  }
+  h.l("Ltnc:");   // (some lanes outside the runs; more of them than in: Ltx)
+  h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
+  h.l("s_bcnt1_i32_b64 s68, s[80:81]");
+  h.l("s_bcnt1_i32_b64 s69, s[76:77]");
+  h.l("s_cmp_gt_u32 s69, s68");
+  h.l("s_cbranch_scc0 Ltbud");
   // ---- leaving the trips: escapes first (the C++ step executes their instruction: xh),
   // then the other lanes outside (their handlers, through the scheduler's pick)
   h.l("Ltx:");
@@ -3398,6 +3408,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     // 3: stage B for the lanes whose window a prefetching scan loaded this trip (LtS)
     static const char *const stage_name[4] = {"LtA", "LtB", "LtF", "LtS"};
     for (int st = 0; st < 4; st++) {
+      bool salu_moved = false;   // (the transfer joined its moved lanes to the batch: join_batch)
       if (st == 0 && !split[k]) continue;
       if (st == 2 && !fwd_ok[k]) continue;
       if (st == 3 && pf_from[k] < 0) continue;
@@ -3477,6 +3488,23 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         e.group = nullptr;
         auto out_if = [&](const char *m) { e.l("s_or_b64 s[76:77], s[76:77], %s", m); };
         auto add_cnt = [&](int64_t c) { if (c) e.l("v_add_u32_e32 %s, 0x%x, %s", VCNT, uint32_t(c), VCNT); };
+        // Lanes moved onto a later run of this run's test batch join that run's batch mask
+        // by scalar ops on the mask that moved them (`m` is this run's EXEC, or VCC / ~VCC
+        // under it: a "vcc" / "~vcc" in its place), instead of a compare the next test would
+        // wait on (VALU -> SALU, ~28 cycles: tools/ubench/lat.hip). WB_TRIP_SMASK=0: compares.
+        auto join_batch = [&](uint32_t to, const char *m) {
+          if (st != 1 || !batch_on || !smask_on || is_scan[k]) return;   // (a scan's stage moves lanes itself)
+          for (uint32_t j = k + 1; j <= blast[k]; j++) {
+            if (runs[j].pc != to || split[j] || !chain) continue;
+            const char *pr = PREG[j - bfirst[j]];
+            if (m[0] == 'e') {   // ("exec")
+              e.l("s_or_b64 %s, %s, exec", pr, pr);
+            } else {
+              e.l(m[0] == '~' ? "s_andn2_b64 s[68:69], exec, vcc" : "s_and_b64 s[68:69], vcc, exec");
+              e.l("s_or_b64 %s, %s, s[68:69]", pr, pr);
+            }
+          }
+        };
         // the run at pc when it is one br_table (a JMP onto it takes the table: WB_BRT_THREAD)
         auto brt_thread = [&](uint32_t pc) -> int {
           if (!brt_on || !start.count(pc)) return -1;
@@ -3523,6 +3551,13 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           }
           if (!in_region(tgt)) { e.l("s_and_b64 s[68:69], vcc, exec"); out_if("s[68:69]"); }
           if (!in_region(fall)) { e.l("s_andn2_b64 s[68:69], exec, vcc"); out_if("s[68:69]"); }
+          if (tgt == fall) {
+            join_batch(tgt, "exec");
+          } else {
+            join_batch(tgt, "vcc");
+            join_batch(fall, "~vcc");
+          }
+          salu_moved = true;
         } else if (lop == OP_JMP && brt_thread(tgt) >= 0) {
           // a jump onto a run that is one br_table (C4's `br $machine` back to its state
           // dispatch): the table's choice made here, so that a lane whose entry lies ahead
@@ -3547,6 +3582,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
             e.l("v_mov_b32 %s, 0x%x", VPC, t);
             add_cnt(int32_t(P.brtab[2 * (B.w3 + q) + 1]));
             if (!in_region(t)) out_if("exec");
+            join_batch(t, "exec");
+            salu_moved = true;
           } else {
             emit_br_table(e, B);
             e.l("v_mov_b32 %s, %s", VPC, Y0);
@@ -3557,6 +3594,8 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           e.l("v_mov_b32 %s, 0x%x", VPC, tgt);
           add_cnt(int64_t(r.cnt) + int16_t(last.w2 >> 16));
           if (!in_region(tgt)) out_if("exec");
+          join_batch(tgt, "exec");
+          salu_moved = true;
         } else if (lop == OP_BR_TABLE) {
           emit_br_table(e, last);   // Y0 = target, Y1 = correction
           e.l("v_mov_b32 %s, %s", VPC, Y0);
@@ -3607,18 +3646,61 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           e.l("v_mov_b32 %s, 0x%x", VPC, fall);
           add_cnt(r.cnt);
           if (!in_region(fall)) out_if("exec");
+          join_batch(fall, "exec");
+          salu_moved = true;
         }
         e.drain();
       }
       std::string code = sched_on ? e.o.substr(0, at) + schedule(e.o.substr(at)) : e.o;
       code += e.stage_end + ":\n";
       code += "s_mov_b64 exec, s[96:97]\n";
-      if (st == 1 && batch_on) {   // (this run may have moved lanes: the rest of its batch)
+      if (st == 1 && batch_on && !(smask_on && salu_moved && !is_scan[k])) {   // (moved lanes: the rest of its batch)
+        // Only the tests of runs its lanes can go to: a test on TPC (a run with a stage A)
+        // sees no move, and a run whose exits are known (a jump, a branch, falling through,
+        // a jump onto a br_table's run) moves lanes only onto those pcs.
+        std::vector<uint32_t> succ;
+        bool known = !is_scan[k] && !fwd_ok[k] && pf_from[k] < 0 && pf_to[k] < 0;
+        if (known) {
+          const uint32_t fall = r.pc + r.len;
+          if (lop == OP_JMP) {
+            const int q = brt_on && start.count(last.w3) && runs[start[last.w3]].len == 1 &&
+                                  op_of(P.code[last.w3]) == OP_BR_TABLE
+                              ? int(start[last.w3]) : -1;
+            if (q >= 0) {
+              const DInstr &B = P.code[last.w3];
+              for (uint32_t t = 0; t <= (B.w1 >> 16); t++) succ.push_back(P.brtab[2 * (B.w3 + t)]);
+            } else {
+              succ.push_back(last.w3);
+            }
+          } else if (is_branch_op(lop)) {
+            succ = {fall, last.w3};
+          } else if (!ends_run(lop)) {
+            succ.push_back(fall);
+          } else {
+            known = false;
+          }
+        }
         Em rb;
-        for (uint32_t j = k + 1; j <= blast[k]; j++) b_cmp(rb, j);
+        for (uint32_t j = k + 1; j <= blast[k]; j++) {
+          if (known && (split[j] || std::find(succ.begin(), succ.end(), runs[j].pc) == succ.end())) continue;
+          b_cmp(rb, j);
+        }
         code += rb.o;
       }
-      code += "s_branch " + std::string(stage_name[st]) + "r" + std::to_string(k) + "\n";
+      // the test's branch: past the stage inline (a stage short enough for the branch's
+      // reach, 2^15 dwords: <= 2,048 lines of at most 12 bytes), else to it out of line
+      const std::string mark = "@@" + L + "@@\n", ret = std::string(stage_name[st]) + "r" + std::to_string(k);
+      const size_t at_m = h.o.find(mark);
+      if (at_m == std::string::npos) return "";
+      if (inline_on && std::count(code.begin(), code.end(), '\n') <= 2048) {
+        const std::string al = ".p2align 2\n";   // (in the chain: no alignment)
+        if (code.compare(0, al.size(), al) == 0) code.erase(0, al.size());
+        h.o.replace(at_m, mark.size(), "s_cbranch_scc0 " + ret + "\n" + code);
+        oob += e.tail;
+        continue;
+      }
+      h.o.replace(at_m, mark.size(), "s_cbranch_scc1 " + L + "\n");
+      code += "s_branch " + ret + "\n";
       code += e.tail;
       (st ? oob : ooa) += code;
     }
