@@ -1,0 +1,16 @@
+# r06 zf: 32-bit granule addresses in trip stages (WB_TRIP_MAD): parity, then A/B on C3 4K, C3 1 MiB; C4
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06zf; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+step tests 900 python -u -m pytest tests/test_tripcache.py tests/test_workloads.py tests/test_xmem_jit.py tests/test_jit.py tests/test_memgrow.py tests/test_layout.py tests/test_bulk.py tests/test_scalar.py -m gpu -v --timeout 300 --timeout-method thread
+step c3k_on 200 python bench.py --workload c3 --elements 4096 --no-cpu-baseline
+step c3k_off 200 env WB_TRIP_MAD=0 python bench.py --workload c3 --elements 4096 --no-cpu-baseline
+step c3_on 300 python bench.py --workload c3 --no-cpu-baseline
+step c3_off 300 env WB_TRIP_MAD=0 python bench.py --workload c3 --no-cpu-baseline
+step c4 200 python bench.py --workload c4 --no-cpu-baseline
+echo all done

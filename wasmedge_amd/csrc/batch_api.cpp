@@ -80,7 +80,7 @@ void compile_runs(WasmEdge_BatchContext *C, std::vector<DInstr> &codepad, std::v
     std::vector<uint64_t> addr;
     const wb::JitCost jc{&C->cost_off_h, &C->cost_pool_h, C->cost_else};
     const std::string src = wb::jit_source(P, runs, C->mlog, C->conf.CostLimit ? &jc : nullptr, want_simt,
-                                           want_trip, &C->xinfo_h, C->xlog);
+                                           want_trip, &C->xinfo_h, C->xlog, C->mem_max_pages);
     const std::string err = src.empty() ? std::string("compiled runs: no source")
                                         : wb::jit_load(src, runs.size(), C->device, &addr);
     if (err.empty()) {

@@ -73,6 +73,10 @@ uint16_t xmop(const DInstr &I) {
 // at word xinfo[2 (k - 1)]), for the jit_source call that is compiling (null in dry runs)
 thread_local const std::vector<uint32_t> *g_xinfo = nullptr;
 thread_local uint32_t g_xlog = 0;   // (their granule: 4 << g_xlog bytes, KParams::xlog)
+// the first memory's page limit (jit_source's mem_pages): at most kMadPages, a lane's
+// granule address fits 32 bits (granule_addr)
+thread_local uint32_t g_mem_pages = 65536;
+constexpr uint32_t kMadPages = 1000;
 
 // compare ops: VOPC suffix (32-bit form; the 64-bit form appends "64" to the type)
 const char *cmp_kind(uint16_t k) {   // k: 0 EQ, 1 NE, 2 LT_S, 3 LT_U, 4 GT_S, 5 GT_U, 6 LE_S, 7 LE_U, 8 GE_S, 9 GE_U
@@ -354,6 +358,9 @@ struct Em {
   // escape (OUTSIDE s[76:77], ESC s[78:79]: the C++ step executes that instruction);
   // the other lanes go on (past the stage's end when none is left). Out of line.
   bool trip = false;
+  // (trip stages, memory 0 below kMadPages) a VGPR holding 63 << (2 + g): granule_addr's
+  // multiply-add form
+  const char *madk = nullptr;
   // Trip-mode load cache (trip_source): loads whose value a scan's exit left in a VGPR --
   // pc -> {the cache's address VGPR, its value VGPR}: the load becomes a move (the lanes
   // running this code matched the address first) -- and the address VGPRs every store
@@ -453,6 +460,24 @@ void group_check(Em &e, const MemGroup &G) {
   group_base(e, G);
 }
 
+// pr = base + the granule address of byte ea: rows of 256 << g bytes, (ea >> (2 + g)) of
+// them, + the byte in the granule. With e.madk (the lane's memory below 64 MiB: the offset
+// fits 32 bits) that offset is (ea >> s) * (63 << s) + ea, s = 2 + g: one multiply-add and
+// one 64-bit add instead of two 64-bit shifts and adds.
+void granule_addr(Em &e, const char *pr, const std::string &ea, const char *base) {
+  if (e.madk) {
+    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, ea.c_str());
+    e.l("v_mad_u32_u24 %s, %s, %s, %s", W0, W0, e.madk, ea.c_str());
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", pr, WP, base);
+    return;
+  }
+  e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, ea.c_str());
+  e.l("v_lshlrev_b64 %s, %u, %s", pr, 8 + e.g, WP);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", pr, pr, base);
+  e.l("v_bfe_u32 %s, %s, 0, %u", W0, ea.c_str(), 2 + e.g);
+  e.l("v_lshl_add_u64 %s, %s, 0, %s", pr, WP, pr);
+}
+
 // Address operand(s) of the access at offset imm (n bytes) of the current group: the
 // first word's "vaddr, off[ offset:k]" and, for n = 8, the second word's.
 void mem_ea(Em &e, uint32_t a, uint32_t imm, uint32_t n, std::string *w1, std::string *w2) {
@@ -472,19 +497,11 @@ void mem_ea(Em &e, uint32_t a, uint32_t imm, uint32_t n, std::string *w1, std::s
   // granule rows of 256 << g bytes, (ea >> (2 + g)) of them, + the byte in the granule
   std::string ea = e.V(a);
   if (imm) { e.l("v_add_u32_e32 %s, 0x%x, %s", Y0, imm, e.v(a)); ea = Y0; }
-  e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, ea.c_str());
-  e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
-  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-  e.l("v_bfe_u32 %s, %s, 0, %u", W0, ea.c_str(), 2 + e.g);
-  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  granule_addr(e, XP, ea, MEM);
   *w1 = std::string(XP) + ", off";
   if (n == 8) {   // ZP = address of the second word (ea + 4: maybe the next granule)
     e.l("v_add_u32_e32 %s, 4, %s", Y1, ea.c_str());
-    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y1);
-    e.l("v_lshlrev_b64 %s, %u, %s", ZP, 8 + e.g, WP);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, ZP, MEM);
-    e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y1, 2 + e.g);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", ZP, WP, ZP);
+    granule_addr(e, ZP, Y1, MEM);
     *w2 = std::string(ZP) + ", off";
   }
 }
@@ -510,11 +527,7 @@ void mem_ea16(Em &e, uint32_t a, uint32_t imm, std::string w[4]) {
     const std::string pr = WPAIR[q];
     const std::string lo = "v" + pr.substr(2, pr.find(':') - 2);
     e.l("v_add_u32_e32 %s, 0x%x, %s", Y1, imm + 4u * q, e.v(a));
-    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y1);
-    e.l("v_lshlrev_b64 %s, %u, %s", pr.c_str(), 8 + e.g, WP);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", pr.c_str(), pr.c_str(), MEM);
-    e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y1, 2 + e.g);
-    e.l("v_lshl_add_u64 %s, %s, 0, %s", pr.c_str(), WP, pr.c_str());
+    granule_addr(e, pr.c_str(), Y1, MEM);
     w[q] = pr + ", off";
   }
 }
@@ -2751,11 +2764,15 @@ void scan_window_loads(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<
   e.l("s_mov_b64 s[68:69], exec");
   e.l("s_and_b64 exec, exec, vcc");
   e.l("s_cbranch_execz Lx4a%s", id.c_str());
-  e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + g, Y0);
-  e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + g, WP);
-  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, base);
-  e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + g);
-  e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  if (!sl.mem) {
+    granule_addr(e, XP, Y0, MEM);
+  } else {
+    e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + g, Y0);
+    e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + g, WP);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, base);
+    e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + g);
+    e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+  }
   e.l("global_load_dwordx4 v[%d:%d], %s, off", r, r + 3, XP);
   e.l("Lx4a%s:", id.c_str());
   e.l("s_andn2_b64 exec, s[68:69], vcc");
@@ -2784,11 +2801,7 @@ void scan_window_words(Em &e, const ScanLoop &sl, uint32_t U, const std::vector<
       e.l("v_lshlrev_b64 %s, 6, %s", XP, WP);
       e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
     } else {
-      e.l("v_lshrrev_b32_e32 %s, %u, %s", W0, 2 + e.g, Y0);
-      e.l("v_lshlrev_b64 %s, %u, %s", XP, 8 + e.g, WP);
-      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, XP, MEM);
-      e.l("v_bfe_u32 %s, %s, 0, %u", W0, Y0, 2 + e.g);
-      e.l("v_lshl_add_u64 %s, %s, 0, %s", XP, WP, XP);
+      granule_addr(e, XP, Y0, MEM);
     }
     e.l("global_load_dword %s, %s, off", dst[j - 1].c_str(), XP);
   }
@@ -3005,13 +3018,18 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // stored), from its scan's stage A, and after any store of the lane (emit_store).
   const bool fwd_on = !(getenv("WB_TRIP_FWD") && getenv("WB_TRIP_FWD")[0] == '0');
   std::vector<std::pair<int, int>> slot_of(runs.size(), {-1, -1});
+  // granule_addr's constant (Em::madk) in v255 when the first memory stays below kMadPages
+  // (WB_TRIP_MAD=0: the 64-bit form); the slots below it
+  const bool mad_on = g_mem_pages <= kMadPages && P.has_mem && 128 + 2 * P.total_cells() + 16 < 255 &&
+                      !(getenv("WB_TRIP_MAD") && getenv("WB_TRIP_MAD")[0] == '0');
+  const uint32_t top = mad_on ? 254 : 255;
   std::vector<uint32_t> slot_regs;   // address VGPRs
   {
     uint32_t ns = 0;
     for (size_t k = 0; k < runs.size(); k++) {
       ScanLoop sl;
       if (!fwd_on || !scan_loop_of(P, runs[k], &sl)) continue;
-      const int a = 255 - 2 * int(ns), v = a - 1;
+      const int a = int(top) - 2 * int(ns), v = a - 1;
       // (above the frame, above what inlined callees may use of it, never the frame's)
       if (uint32_t(v) < 128 + 2 * P.total_cells() + 16) break;
       slot_of[k] = {a, v};
@@ -3079,7 +3097,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   std::vector<ScanPrefetch> pfr(nr);
   std::vector<uint32_t> inval = slot_regs;   // (what a store invalidates: Em::inval)
   {
-    uint32_t next = 255 - 2 * uint32_t(slot_regs.size());   // below the cache slots
+    uint32_t next = top - 2 * uint32_t(slot_regs.size());   // below the cache slots
     for (uint32_t q = 0; q < nr && pf_on && scan_k >= 2; q++) {
       if (!is_scan[q] || !start.count(runs[q].pc + 3)) continue;
       const uint32_t s = uint32_t(start[runs[q].pc + 3]);
@@ -3102,6 +3120,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_waitcnt lgkmcnt(0)");   // (a handler's bank-B prefetch must land: the batches use s[86:91])
   h.l("s_mov_b64 exec, s[96:97]");
   for (uint32_t r : inval) h.l("v_mov_b32 v%u, -1", r);
+  if (mad_on) h.l("v_mov_b32 v255, 0x%x", 63u << (2 + glog));
   h.l("s_mov_b64 s[76:77], s[96:97]");
   h.l("s_mov_b64 s[78:79], 0");
   for (const auto &r : runs) {
@@ -3415,6 +3434,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
       const int sb = st == 3 ? 1 : st;   // (the stage the code is)
       Em e;
       e.trip = true;
+      if (mad_on) e.madk = "v255";
       e.inval = inval;
       if (st == 2) e.fwd = fwd[k];
       if (!nob.empty()) e.nanobs = &nob;
@@ -3904,14 +3924,14 @@ bool recursive(const Program &P) {
 
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost, bool simt, bool trip, const std::vector<uint32_t> *xinfo,
-                       uint32_t xlog) {
+                       uint32_t xlog, uint32_t mem_pages) {
   if (cost) simt = false;
   // (extra memories: their accesses compile only against the context's word offsets)
   if (!P.xmems.empty() && (!xinfo || xinfo->size() < 2 * P.xmems.size())) return "";
   struct XinfoScope {
-    XinfoScope(const std::vector<uint32_t> *x, uint32_t lg) { g_xinfo = x; g_xlog = lg; }
-    ~XinfoScope() { g_xinfo = nullptr; g_xlog = 0; }
-  } xscope(xinfo, xlog);
+    XinfoScope(const std::vector<uint32_t> *x, uint32_t lg, uint32_t mp) { g_xinfo = x; g_xlog = lg; g_mem_pages = mp; }
+    ~XinfoScope() { g_xinfo = nullptr; g_xlog = 0; g_mem_pages = 65536; }
+  } xscope(xinfo, xlog, mem_pages);
   // trip mode beside SIMT scheduling (hybrid, the default) or alone (WB_HYBRID=0)
   const bool trips = trip && simt && runs.size() <= kTripMaxRuns;
   const bool hybrid = trips && !(getenv("WB_HYBRID") && getenv("WB_HYBRID")[0] == '0');
@@ -4934,8 +4954,11 @@ extern "C" __attribute__((visibility("default"))) int wb_jit_check(const uint8_t
       if (simt) runs = wb::jit_runs(P, tc, true, simt == 2);
       if (runs.empty()) continue;
       std::vector<char> obj;
+      // (a memory below kMadPages unless WB_JIT_CHECK_PAGES says otherwise: the 32-bit
+      // granule addresses of trip stages assembled too)
+      const char *cp = getenv("WB_JIT_CHECK_PAGES");
       const std::string src = wb::jit_source(P, runs, glog, nullptr, simt != 0, simt == 2, &xinfo,
-                                             P.divergent_xmem ? 5u : 0u);
+                                             P.divergent_xmem ? 5u : 0u, cp ? uint32_t(atoi(cp)) : wb::kMadPages);
       if (const char *dump = getenv(simt == 2 ? "WB_JIT_DUMP_TRIP" : simt ? "WB_JIT_DUMP_SIMT" : "WB_JIT_DUMP"))
         if (FILE *f = fopen(dump, "w")) { fputs(src.c_str(), f); fclose(f); }
       e = src.empty() ? "no source" : wb::jit_compile(src, &obj);

@@ -64,9 +64,12 @@ constexpr size_t kTripMaxRuns = 96;
 // offset in a lane's block at [2 (k - 1)] -- for the compiled XLD / XST (jit.cpp
 // emit_xmem, which address the wave's block through s[98:99], set by the kernel at every
 // core call); without it such a module gets no source. xlog: their granule (KParams::xlog).
+// mem_pages: the first memory's page limit (the context's mem_max_pages): trip stages of a
+// memory below 1,000 pages compute granule addresses in 32 bits (jit.cpp granule_addr).
 std::string jit_source(const Program &P, const std::vector<JitRun> &runs, uint32_t glog,
                        const JitCost *cost = nullptr, bool simt = false, bool trip = false,
-                       const std::vector<uint32_t> *xinfo = nullptr, uint32_t xlog = 0);
+                       const std::vector<uint32_t> *xinfo = nullptr, uint32_t xlog = 0,
+                       uint32_t mem_pages = 65536);
 
 // Whether trip mode pays for a module whose memory addresses do not depend on per-instance
 // data (Program::divergent_mem picks it for those): lanes part ways inside a loop on every
