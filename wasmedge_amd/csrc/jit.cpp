@@ -3151,6 +3151,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // inline (profiles/r06zb_bench_c3_*).
   const bool inline_on = !(getenv("WB_TRIP_INLINE") && getenv("WB_TRIP_INLINE")[0] == '0');
   const bool smask_on = !(getenv("WB_TRIP_SMASK") && getenv("WB_TRIP_SMASK")[0] == '0');
+  const bool cmpbr_on = !(getenv("WB_TRIP_CMPBR") && getenv("WB_TRIP_CMPBR")[0] == '0');
   // dst = (v == pc) per lane; VOP3 takes no literal, so a pc past the inline constants goes
   // through s68 / s69 (alternating: the compare has read one before the next is written)
   auto vcmp64 = [](Em &x, const char *dst, uint32_t pc, const char *v, uint32_t j) {
@@ -3545,20 +3546,40 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
         };
         if (is_branch_op(lop) && lop != OP_JMP) {
           const int32_t tcnt = int32_t(int16_t(last.w2 >> 16));
-          branch_cond(e, last);   // vcc = taken
+          // A br_if / br_unless on the cell the run's last instruction set from VCC (a
+          // compare: `v_cndmask cell, 0, 1, vcc` its last line, only waits after it) reads
+          // VCC itself -- no compare of the cell again; br_unless then selects the other
+          // way round (inv: VCC = not taken). WB_TRIP_CMPBR=0 compares again.
+          bool inv = false, reuse = false;
+          if ((lop == OP_BR_IF || lop == OP_BR_UNLESS) && cmpbr_on) {
+            size_t end = e.o.size();
+            while (end >= 2) {
+              const size_t b0 = e.o.rfind('\n', end - 2);
+              const size_t st0 = b0 == std::string::npos ? 0 : b0 + 1;
+              const std::string ln = e.o.substr(st0, end - st0);
+              if (ln.compare(0, 9, "s_waitcnt") == 0 || ln == "\n") { end = st0; continue; }
+              reuse = ln == "v_cndmask_b32_e64 " + std::string(e.v(last.w1 & 0xFFFFu)) + ", 0, 1, vcc\n";
+              break;
+            }
+          }
+          if (!reuse) branch_cond(e, last);   // vcc = taken
+          inv = reuse && lop == OP_BR_UNLESS;
           // (VOP3 selects take inline constants, -16..64: the pcs and corrections of small
           // modules need no moves)
           auto inl = [](int64_t v) { return v >= -16 && v <= 64; };
           std::string f = std::to_string(fall), t = std::to_string(tgt);
           if (!inl(fall)) { e.l("v_mov_b32 %s, 0x%x", X0, fall); f = X0; }
           if (!inl(tgt)) { e.l("v_mov_b32 %s, 0x%x", X1, tgt); t = X1; }
+          if (inv) std::swap(f, t);
           e.l("v_cndmask_b32_e64 %s, %s, %s, vcc", VPC, f.c_str(), t.c_str());
           if (tcnt) {
             if (inl(tcnt)) {
-              e.l("v_cndmask_b32_e64 %s, 0, %d, vcc", X0, tcnt);
+              if (inv) e.l("v_cndmask_b32_e64 %s, %d, 0, vcc", X0, tcnt);
+              else e.l("v_cndmask_b32_e64 %s, 0, %d, vcc", X0, tcnt);
             } else {
               e.l("v_mov_b32 %s, 0x%x", X1, uint32_t(tcnt));
-              e.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
+              if (inv) e.l("v_cndmask_b32_e64 %s, %s, 0, vcc", X0, X1);
+              else e.l("v_cndmask_b32_e32 %s, 0, %s, vcc", X0, X1);
             }
             if (r.cnt && inl(r.cnt)) {   // (the run's count in the same add)
               e.l("v_add3_u32 %s, %s, %s, %u", VCNT, VCNT, X0, r.cnt);
@@ -3569,13 +3590,15 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
           } else {
             add_cnt(r.cnt);
           }
-          if (!in_region(tgt)) { e.l("s_and_b64 s[68:69], vcc, exec"); out_if("s[68:69]"); }
-          if (!in_region(fall)) { e.l("s_andn2_b64 s[68:69], exec, vcc"); out_if("s[68:69]"); }
+          const char *taken_m = inv ? "s_andn2_b64 s[68:69], exec, vcc" : "s_and_b64 s[68:69], vcc, exec";
+          const char *fall_m = inv ? "s_and_b64 s[68:69], vcc, exec" : "s_andn2_b64 s[68:69], exec, vcc";
+          if (!in_region(tgt)) { e.l("%s", taken_m); out_if("s[68:69]"); }
+          if (!in_region(fall)) { e.l("%s", fall_m); out_if("s[68:69]"); }
           if (tgt == fall) {
             join_batch(tgt, "exec");
           } else {
-            join_batch(tgt, "vcc");
-            join_batch(fall, "~vcc");
+            join_batch(tgt, inv ? "~vcc" : "vcc");
+            join_batch(fall, inv ? "vcc" : "~vcc");
           }
           salu_moved = true;
         } else if (lop == OP_JMP && brt_thread(tgt) >= 0) {
