@@ -1,0 +1,15 @@
+# r06 zm: same-build profiles after the every-4th-trip convergence test: C4, mt19937, C3
+# address and compare-branch changes: C4, mt19937, C3 (64K x 1 MiB), C3 on memory 1, C3 grown
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06zm; mkdir -p $O
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "$n rc=$rc $(tail -1 $O/$n.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then echo "stopping after $n"; exit $rc; fi
+}
+export PROF_TIMEOUT=170
+step prof_c4 200 bash $R/tools/prof_bench.sh gpurun_out/r06zm/c4 --workload c4
+step prof_mt 300 bash $R/tools/prof_bench.sh gpurun_out/r06zm/mt --workload mt
+step prof_c3 800 bash $R/tools/prof_bench.sh gpurun_out/r06zm/c3 --workload c3
+echo all done

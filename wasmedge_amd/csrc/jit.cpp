@@ -3305,12 +3305,16 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // takes one branch, back to Ltp.
   h.l("s_cmp_eq_u64 s[76:77], 0");
   h.l("s_cbranch_scc0 Ltnc");
-  if (hybrid) {
-    // every lane in the runs and at one pc: back to SIMT scheduling (EXEC = ALL; Ltcv)
-    h.l("v_readfirstlane_b32 s68, %s", VPC);
-    h.l("s_nop 1");
-    h.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
-    h.l("s_cbranch_vccz Ltcv");
+  // every lane in the runs and at one pc: back to SIMT scheduling (hybrid; Ltck). The test
+  // (a VALU -> SGPR -> VALU -> branch chain) runs after every 4th trip only: CNT (s65, 0
+  // in the trips: nothing in them counts through it) counts trips in its top two bits and
+  // carries back to 0 on the 4th (WB_TRIP_CONV1=1: every trip)
+  const bool conv_every = getenv("WB_TRIP_CONV1") && getenv("WB_TRIP_CONV1")[0] == '1';
+  if (hybrid && !conv_every) {
+    h.l("s_add_u32 s65, s65, 0x40000000");
+    h.l("s_cbranch_scc1 Ltck");
+  } else if (hybrid) {
+    h.l("s_branch Ltck");
   }
   h.l("Ltbud:");
   // (>= what one lane can retire in a trip: one run, or with chaining every run once)
@@ -3338,7 +3342,12 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_addc_u32 s69, s71, 0");
   h.l("s_setpc_b64 s[68:69]");
   if (hybrid) {
-    h.l("Ltcv:");
+    h.l("Ltck:");
+    h.l("v_readfirstlane_b32 s68, %s", VPC);
+    h.l("s_nop 1");
+    h.l("v_cmp_ne_u32_e64 vcc, s68, %s", VPC);
+    h.l("s_cbranch_vccnz Ltbud");
+    h.l("s_mov_b32 s65, 0");   // (0 already unless WB_TRIP_CONV1)
     long_jump(h, "Lsched", "Ltcq");
   }
   h.l("Ltnc:");   // (some lanes outside the runs; more of them than in: Ltx)
@@ -3370,6 +3379,7 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_mov_b64 exec, s[74:75]");
   h.l("s_setpc_b64 s[70:71]");
   h.l("Ltq:");
+  h.l("s_mov_b32 s65, 0");   // (the trip count of Ltck)
   sched_block(h, "Ltq", "s[76:77]");
   // ---- the runs' stages
   for (uint32_t k = 0; k < nr; k++) {
