@@ -1,5 +1,5 @@
 # r06 zm: same-build profiles after the every-4th-trip convergence test: C4, mt19937, C3
-# address and compare-branch changes: C4, mt19937, C3 (64K x 1 MiB), C3 on memory 1, C3 grown
+
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r06zm; mkdir -p $O
 step() {  # name, timeout, command...

@@ -3310,8 +3310,11 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   // in the trips: nothing in them counts through it) counts trips in its top two bits and
   // carries back to 0 on the 4th (WB_TRIP_CONV1=1: every trip)
   const bool conv_every = getenv("WB_TRIP_CONV1") && getenv("WB_TRIP_CONV1")[0] == '1';
+  // (WB_TRIP_CONVP=k: every 2^k-th trip instead, k = 1..8)
+  const char *cpe = getenv("WB_TRIP_CONVP");
+  const uint32_t conv_log = cpe ? std::min(8u, std::max(1u, uint32_t(atoi(cpe)))) : 2u;
   if (hybrid && !conv_every) {
-    h.l("s_add_u32 s65, s65, 0x40000000");
+    h.l("s_add_u32 s65, s65, 0x%x", 1u << (32 - conv_log));
     h.l("s_cbranch_scc1 Ltck");
   } else if (hybrid) {
     h.l("s_branch Ltck");
