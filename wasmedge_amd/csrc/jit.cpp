@@ -3306,13 +3306,17 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
   h.l("s_cmp_eq_u64 s[76:77], 0");
   h.l("s_cbranch_scc0 Ltnc");
   // every lane in the runs and at one pc: back to SIMT scheduling (hybrid; Ltck). The test
-  // (a VALU -> SGPR -> VALU -> branch chain) runs after every 4th trip only: CNT (s65, 0
-  // in the trips: nothing in them counts through it) counts trips in its top two bits and
-  // carries back to 0 on the 4th (WB_TRIP_CONV1=1: every trip)
+  // (a VALU -> SGPR -> VALU -> branch chain) runs after every 16th trip only: CNT (s65, 0
+  // in the trips: nothing in them counts through it) counts trips in its top four bits and
+  // carries back to 0 on the 16th (WB_TRIP_CONV1=1: every trip; WB_TRIP_CONVP=k: every
+  // 2^k-th, k = 1..8). C4 kernel 1.36e12 (every trip) -> 1.60e12 (2nd) -> 1.69e12 (4th) ->
+  // 1.76e12 (8th) -> 1.82e12 (16th) -> 1.80e12 (64th); C3 and mt unchanged
+  // (`profiles/r06zl_*`, `r06zo_*`): a wave whose last lanes stand at one pc no longer
+  // leaves the trips for SIMT scheduling and re-enters them at the next split, trip
+  // after trip (each entry re-marks the lanes outside the runs, one compare per run).
   const bool conv_every = getenv("WB_TRIP_CONV1") && getenv("WB_TRIP_CONV1")[0] == '1';
-  // (WB_TRIP_CONVP=k: every 2^k-th trip instead, k = 1..8)
   const char *cpe = getenv("WB_TRIP_CONVP");
-  const uint32_t conv_log = cpe ? std::min(8u, std::max(1u, uint32_t(atoi(cpe)))) : 2u;
+  const uint32_t conv_log = cpe ? std::min(8u, std::max(1u, uint32_t(atoi(cpe)))) : 4u;
   if (hybrid && !conv_every) {
     h.l("s_add_u32 s65, s65, 0x%x", 1u << (32 - conv_log));
     h.l("s_cbranch_scc1 Ltck");
