@@ -3357,10 +3357,21 @@ std::string trip_source(const Program &P, const std::vector<JitRun> &runs, uint3
     h.l("s_mov_b32 s65, 0");   // (0 already unless WB_TRIP_CONV1)
     long_jump(h, "Lsched", "Ltcq");
   }
-  h.l("Ltnc:");   // (some lanes outside the runs; more of them than in: Ltx)
+  // Ltnc: some lanes outside the runs. The wave leaves the trips (Ltx) only when more
+  // than 64 times as many are outside as in -- i.e. when none is in: the lanes outside
+  // (C4's finished state machines at its trap tails) wait and then run their code together,
+  // instead of the wave leaving and re-entering the trips whenever they outnumber the rest
+  // (WB_TRIP_OUTSH=k: more than 2^k times as many, k = 0..6; C4 kernel 1.67e12 at k = 0 ->
+  // 1.79 (1) -> 1.83 (2) -> 1.86 (3) -> 1.91 (4) -> 2.03e12 (6) per step, C3 and mt
+  // unchanged: `profiles/r06zu_*`, `r06zv_*`). Lanes outside are never stranded: a budget
+  // exit hands the wave back to the kernel's scheduler, which picks among every lane.
+  const char *ose = getenv("WB_TRIP_OUTSH");
+  const int out_sh = ose ? std::max(0, std::min(6, atoi(ose))) : 6;
+  h.l("Ltnc:");
   h.l("s_andn2_b64 s[80:81], s[96:97], s[76:77]");
   h.l("s_bcnt1_i32_b64 s68, s[80:81]");
   h.l("s_bcnt1_i32_b64 s69, s[76:77]");
+  if (out_sh) h.l("s_lshl_b32 s68, s68, %d", out_sh);
   h.l("s_cmp_gt_u32 s69, s68");
   h.l("s_cbranch_scc0 Ltbud");
   // ---- leaving the trips: escapes first (the C++ step executes their instruction: xh),
